@@ -1,0 +1,160 @@
+/*
+ * c3hlac_mi355x.h -- C-ABI of the MI355X (gfx950) colour-voxel C3-HLAC recognition path.
+ *
+ * This is the drop-in boundary: plain pointers and sizes, no PCL/Eigen/torch types.
+ * Each entry point names the reference interface it replaces (paths relative to the
+ * reference root).  The C++ facade in mapping-private_amd/host/ re-exposes the
+ * reference's own names (getVoxelGrid, extractC3HLACSignature981/117, SearchObj,
+ * SearchObjMulti, SearchC3HLAC, PCA, Param) on top of these functions.
+ *
+ * Conventions:
+ *   - every function returns C3H_OK (0) or a negative C3H_ERR_* code; nothing calls exit();
+ *     c3h_last_error() describes the last failure of a context;
+ *   - output buffers are caller-owned; `on_device` selects whether a pointer is a HIP
+ *     device pointer (1) or host memory (0);
+ *   - one context = one device + one HIP stream; thread-compatible, not thread-safe
+ *     (the reference's SearchObj model).
+ */
+#ifndef C3HLAC_MI355X_H_
+#define C3HLAC_MI355X_H_
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define C3H_OK 0
+#define C3H_ERR_ARG -1       /* bad argument (null pointer, negative size, bad variant) */
+#define C3H_ERR_HIP -2       /* HIP runtime error (message in c3h_last_error) */
+#define C3H_ERR_STATE -3     /* call order: e.g. extract before voxelize */
+#define C3H_ERR_NOMEM -4     /* device allocation failed */
+#define C3H_ERR_RANGE -5     /* grid too large for int32 voxel indices */
+#define C3H_ERR_NOTFOUND -6  /* file could not be opened (PCA / param readers) */
+#define C3H_ERR_FORMAT -7    /* malformed file */
+
+#define C3H_VARIANT_981 981  /* C3HLAC981Estimation (rotation-variant) */
+#define C3H_VARIANT_117 117  /* C3HLAC117Estimation (rotation-invariant) */
+
+/* SearchMode (color_voxel_recognition/include/color_voxel_recognition/search.h:48) */
+enum { C3H_S_MODE_1 = 0, C3H_S_MODE_2, C3H_S_MODE_3, C3H_S_MODE_4, C3H_S_MODE_5, C3H_S_MODE_6 };
+
+typedef struct c3h_ctx c3h_ctx;
+
+/* pcl::VoxelGrid state after filter(): getNrDivisions / getMinBoxCoordinates /
+ * getMaxBoxCoordinates, plus the sizes of limitPoint's output and of the
+ * downsampled cloud. */
+typedef struct {
+  int32_t div_b[3];
+  int32_t min_b[3];
+  int32_t max_b[3];
+  int64_t n_valid;
+  int64_t n_occ;
+  float leaf;
+  float inv_leaf;
+} c3h_grid_info;
+
+/* extractC3HLACSignature981/117 arguments (c3_hlac/include/c3_hlac/c3_hlac_tools.h:75-86). */
+typedef struct {
+  int32_t variant;    /* 981 or 117 */
+  int32_t thr[3];     /* setColorThreshold r,g,b (c3_hlac.h:92) */
+  int32_t subdiv;     /* subdivision_size (0 = one vector for the whole grid) */
+  int32_t offset[3];  /* offset_x/y/z */
+  int32_t lut_double; /* setColor's sin/cos in double (1, default; v=255 -> 254) or float (0) */
+} c3h_extract_params;
+
+/* one ranked detection: maxDot/maxX/maxY/maxZ/maxMode (search.h:99-126) */
+typedef struct {
+  double score;
+  int32_t x, y, z, mode;
+} c3h_det;
+
+int c3h_version(void);
+
+/* context (one device, one stream) */
+int c3h_create(int hip_device, c3h_ctx** out);
+void c3h_destroy(c3h_ctx* ctx);
+int c3h_set_stream(c3h_ctx* ctx, void* hip_stream); /* NULL = the context's own stream */
+int c3h_synchronize(c3h_ctx* ctx);
+const char* c3h_last_error(const c3h_ctx* ctx);
+
+/* getVoxelGrid (c3_hlac/include/c3_hlac/c3_hlac_tools.hpp:124-130) preceded by
+ * limitPoint (color_voxel_recognition/test/detect_object.cpp:68-87): points with a
+ * non-finite coordinate or z >= z_limit are dropped (pass INFINITY for no limit).
+ * xyzrgb: n x 4 floats (x, y, z, rgb packed in the float bits as in PCL). */
+int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, float leaf,
+                 float z_limit, c3h_grid_info* info);
+/* VoxelGrid::getLeafLayout (setSaveLeafLayout(true)): div_b product int32, -1 = empty. */
+int c3h_get_leaf_layout(c3h_ctx* ctx, int32_t* out, int on_device);
+/* the downsampled cloud of getVoxelGrid: n_occ x 4 floats in ascending voxel index. */
+int c3h_get_downsampled(c3h_ctx* ctx, float* out_xyzrgb, int on_device);
+/* packed colour/occupancy grid, div_b product uint32: 0 = empty, else 1<<24 | rgb. */
+int c3h_get_grid(c3h_ctx* ctx, uint32_t* out, int on_device);
+/* use an externally produced packed grid (same encoding).  on_device=1 binds the
+ * pointer without copying; the caller keeps it alive until the next set/voxelize. */
+int c3h_set_grid(c3h_ctx* ctx, const uint32_t* words, const int32_t div_b[3],
+                 const int32_t min_b[3], float leaf, int on_device);
+int c3h_get_grid_info(c3h_ctx* ctx, c3h_grid_info* info);
+
+/* C3HLAC{981,117}Estimation::setVoxelFilter + compute (c3_hlac/src/c3_hlac.cpp:204-416),
+ * as called by extractC3HLACSignature981/117 (c3_hlac_tools.hpp:134-202).  Writes the
+ * subdivision counts (getSubdivNum) and the number of feature vectors (hist_num; 0 for
+ * the reference's silent-empty cases: offsets >= grid or a negative threshold). */
+int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3],
+                int64_t* hist_num);
+/* hist_num x variant floats of the last extract */
+int c3h_get_features(c3h_ctx* ctx, float* out, int on_device);
+/* exist_voxel_num of SearchC3HLAC::setC3HLAC
+ * (color_voxel_recognition/include/color_voxel_recognition/search_c3_hlac.h:60-61) */
+int c3h_get_exist(c3h_ctx* ctx, int32_t* out, int on_device);
+
+/* SearchObj configuration.
+ *   axis_p: D x F row-major projection (setSceneAxis, search.cpp:694-712); when var is
+ *           non-NULL row i is whitened by 1/sqrt(var[i]) exactly as setSceneAxis does.
+ *           NULL disables compression (compress_flg=false; then D must equal F).
+ *   axis_q: M x r x D model subspaces as readAxis leaves them (search.cpp:153-165,
+ *           819-837: transposed, MULTIPLE_SIMILARITY scaling already applied).
+ *   feature_max: setNormalizeVal values (search.cpp:742-748), NULL/0 = none. */
+int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_t D,
+                     int32_t F, const float* axis_q, int32_t M, int32_t r,
+                     const float* feature_max, int32_t feature_max_len);
+/* SearchObj::setRank / SearchObjMulti::setRank (search.cpp:130-143, 778-815):
+ * (re)allocates the per-model lists; modes start at S_MODE_1. */
+int c3h_set_rank(c3h_ctx* ctx, int32_t rank);
+/* cleanMax / cleanData list reset (search.cpp:683-690, 716-732): scores and x,y,z to 0,
+ * modes kept (the reference never resets them). */
+int c3h_clean_max(c3h_ctx* ctx);
+/* setData + search() (rotate=1) or searchWithoutRotation() (rotate=0)
+ * (search.cpp:384-480, 539-658, 915-968) on the features of the last extract; the
+ * lists continue from their current state.  Writes M x rank detections to `out` (host)
+ * and, when remove_overlap != 0, applies SearchObjMulti::removeOverlap
+ * (search.cpp:972-992) first.  Returns the number of scheduled modes (>0) or an error. */
+int c3h_search(c3h_ctx* ctx, const int32_t range[3], int32_t exist_threshold,
+               int32_t rotate, int32_t remove_overlap, c3h_det* out);
+/* Asynchronous variant for device-resident pipelines: no host sync; copies the M x rank
+ * lists into the device buffer d_out after the search (no removeOverlap). */
+int c3h_search_async(c3h_ctx* ctx, const int32_t range[3], int32_t exist_threshold,
+                     int32_t rotate, c3h_det* d_out);
+/* compressed features (setData before the summed-volume table): hist_num x D floats */
+int c3h_get_compressed(c3h_ctx* ctx, float* out, int on_device);
+/* per-position similarity of the last search, modes x M x P doubles (-1 = gated out).
+ * n_out receives the element count; pass out=NULL to query it. */
+int c3h_get_scores(c3h_ctx* ctx, double* out, int64_t* n_out, int on_device);
+/* SearchObjMulti::removeOverlap on host lists (pure host function, no context). */
+int c3h_remove_overlap(int32_t M, int32_t rank, const int32_t range[3], c3h_det* lists);
+
+/* PCA::read (color_voxel_recognition/src/pca.cpp:119-185): axis column-major dim x dim
+ * (eigenvector i contiguous), variances, optional mean.  Returns dim or an error. */
+int c3h_pca_read(const char* path, int32_t ascii, float* axis, float* var, float* mean,
+                 int32_t* has_mean, int32_t max_dim);
+
+/* per-kernel device time (ms) accumulated since the last reset with HIP events on the
+ * context stream; slots: 0 voxelize, 1 C3-HLAC, 2 compress, 3 score, 4 rank replay.
+ * counts_out receives the number of launches per slot.  Enabling adds event records. */
+#define C3H_NTIMERS 5
+int c3h_timing(c3h_ctx* ctx, int32_t enable);
+int c3h_kernel_times(c3h_ctx* ctx, float* ms_out, int32_t* counts_out, int32_t reset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

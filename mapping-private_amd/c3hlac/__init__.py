@@ -1,0 +1,235 @@
+"""MI355X-native colour-voxel C3-HLAC recognition (Python mirror of the C++ facade).
+
+Names follow the reference's API (c3_hlac/include/c3_hlac/c3_hlac_tools.h,
+color_voxel_recognition/include/color_voxel_recognition/search.h): every call goes
+through the C-ABI of libc3hlac_mi355x.so (HIP kernels for gfx950); there is no CPU
+fallback.  The C++ facade in host/ offers the same surface to C++ callers.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _capi
+from ._capi import DET_DTYPE, TIMER_NAMES, check, i32x3, ptr
+
+S_MODE = {"S_MODE_%d" % (i + 1): i for i in range(6)}
+DIM_C3HLAC_981_1_3_ALL = 981
+DIM_C3HLAC_117_1_3_ALL = 117
+
+
+class Context:
+    """One device + one HIP stream (c3h_create)."""
+
+    def __init__(self, device=0):
+        self.lib = _capi.load()
+        h = C.c_void_p()
+        rc = self.lib.c3h_create(int(device), C.byref(h))
+        if rc != 0:
+            raise _capi.C3HError("c3h_create(%d) failed: %s" % (device, _capi.ERRORS.get(rc, rc)))
+        self.h = h
+        self.device = device
+        self.info = None
+        self.hist_num = 0
+        self.subdiv = (0, 0, 0)
+        self.variant = None
+        self.M = 0
+        self.rank = 1
+        self.D = 0
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.c3h_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _chk(self, rc, what):
+        return check(rc, self.h, what)
+
+    def set_stream(self, stream_handle):
+        self._chk(self.lib.c3h_set_stream(self.h, C.c_void_p(stream_handle) if stream_handle else None), "set_stream")
+
+    def synchronize(self):
+        self._chk(self.lib.c3h_synchronize(self.h), "synchronize")
+
+    # --- voxel grid (getVoxelGrid + limitPoint) -------------------------------------
+    def voxelize(self, xyzrgb, leaf, z_limit=float("inf")):
+        """xyzrgb: (N,4) float32 host array or a device tensor (x,y,z, rgb bits)."""
+        on_dev = not isinstance(xyzrgb, np.ndarray)
+        if not on_dev:
+            xyzrgb = np.ascontiguousarray(xyzrgb, dtype=np.float32)
+            assert xyzrgb.ndim == 2 and xyzrgb.shape[1] == 4
+        n = xyzrgb.shape[0]
+        gi = _capi.GridInfo()
+        self._chk(self.lib.c3h_voxelize(self.h, ptr(xyzrgb), n, int(on_dev), float(leaf),
+                                        float(z_limit), C.byref(gi)), "voxelize")
+        self.info = gi
+        return gi
+
+    def set_grid(self, words, div_b, min_b=(0, 0, 0), leaf=0.01):
+        on_dev = not isinstance(words, np.ndarray)
+        if not on_dev:
+            words = np.ascontiguousarray(words, dtype=np.uint32)
+        self._chk(self.lib.c3h_set_grid(self.h, ptr(words), i32x3(div_b), i32x3(min_b),
+                                        float(leaf), int(on_dev)), "set_grid")
+        gi = _capi.GridInfo()
+        self._chk(self.lib.c3h_get_grid_info(self.h, C.byref(gi)), "get_grid_info")
+        self.info = gi
+        return gi
+
+    def nvox(self):
+        d = self.info.div_b
+        return int(d[0]) * int(d[1]) * int(d[2])
+
+    def grid(self):
+        out = np.zeros(self.nvox(), np.uint32)
+        if out.size:
+            self._chk(self.lib.c3h_get_grid(self.h, ptr(out), 0), "get_grid")
+        return out
+
+    def leaf_layout(self):
+        out = np.zeros(self.nvox(), np.int32)
+        if out.size:
+            self._chk(self.lib.c3h_get_leaf_layout(self.h, ptr(out), 0), "get_leaf_layout")
+        return out
+
+    def downsampled(self):
+        out = np.zeros((max(int(self.info.n_occ), 0), 4), np.float32)
+        if out.size:
+            self._chk(self.lib.c3h_get_downsampled(self.h, ptr(out), 0), "get_downsampled")
+        return out
+
+    # --- C3-HLAC ----------------------------------------------------------------------
+    def extract(self, variant, thr, subdiv=0, offset=(0, 0, 0), lut_double=True):
+        p = _capi.ExtractParams()
+        p.variant = int(variant)
+        p.thr = (C.c_int32 * 3)(*[int(t) for t in thr])
+        p.subdiv = int(subdiv)
+        p.offset = (C.c_int32 * 3)(*[int(o) for o in offset])
+        p.lut_double = int(bool(lut_double))
+        sb = (C.c_int32 * 3)()
+        hn = C.c_int64()
+        self._chk(self.lib.c3h_extract(self.h, C.byref(p), sb, C.byref(hn)), "extract")
+        self.hist_num = int(hn.value)
+        self.subdiv = tuple(int(x) for x in sb)
+        self.variant = int(variant)
+        return self.subdiv, self.hist_num
+
+    def features(self):
+        out = np.zeros((self.hist_num, self.variant), np.float32)
+        if out.size:
+            self._chk(self.lib.c3h_get_features(self.h, ptr(out), 0), "get_features")
+        return out
+
+    def exist(self):
+        out = np.zeros(self.hist_num, np.int32)
+        if out.size:
+            self._chk(self.lib.c3h_get_exist(self.h, ptr(out), 0), "get_exist")
+        return out
+
+    # --- search -----------------------------------------------------------------------
+    def search_setup(self, axis_p, var, axis_q, feature_max=None):
+        """axis_p: (D,F) or None; var: (D,) or None (whitening); axis_q: (M,r,D)."""
+        axis_q = np.ascontiguousarray(axis_q, dtype=np.float32)
+        M, r, D = axis_q.shape
+        if axis_p is not None:
+            axis_p = np.ascontiguousarray(axis_p, dtype=np.float32)
+            assert axis_p.shape[0] == D
+            F = axis_p.shape[1]
+        else:
+            F = D
+        if var is not None:
+            var = np.ascontiguousarray(var, dtype=np.float32)
+        fm = None if feature_max is None else np.ascontiguousarray(feature_max, dtype=np.float32)
+        self._chk(self.lib.c3h_search_setup(self.h, ptr(axis_p), ptr(var), D, F, ptr(axis_q), M, r,
+                                            ptr(fm), 0 if fm is None else fm.size), "search_setup")
+        self.M, self.D = M, D
+
+    def set_rank(self, rank):
+        self._chk(self.lib.c3h_set_rank(self.h, int(rank)), "set_rank")
+        self.rank = int(rank)
+
+    def clean_max(self):
+        self._chk(self.lib.c3h_clean_max(self.h), "clean_max")
+
+    def search(self, ranges, exist_threshold, rotate=True, remove_overlap=False):
+        out = np.zeros(max(self.M, 1) * self.rank, DET_DTYPE)
+        nm = self._chk(self.lib.c3h_search(self.h, i32x3(ranges), int(exist_threshold), int(bool(rotate)),
+                                           int(bool(remove_overlap)), ptr(out)), "search")
+        return out.reshape(max(self.M, 1), self.rank), nm
+
+    def search_async(self, ranges, exist_threshold, rotate=True, d_out=None):
+        return self._chk(self.lib.c3h_search_async(self.h, i32x3(ranges), int(exist_threshold),
+                                                   int(bool(rotate)), ptr(d_out)), "search_async")
+
+    def compressed(self):
+        out = np.zeros((self.hist_num, self.D), np.float32)
+        self._chk(self.lib.c3h_get_compressed(self.h, ptr(out), 0), "get_compressed")
+        return out
+
+    def scores(self):
+        n = C.c_int64()
+        self._chk(self.lib.c3h_get_scores(self.h, None, C.byref(n), 0), "get_scores")
+        out = np.zeros(n.value, np.float64)
+        if out.size:
+            self._chk(self.lib.c3h_get_scores(self.h, ptr(out), C.byref(n), 0), "get_scores")
+        return out
+
+    # --- timing -----------------------------------------------------------------------
+    def timing(self, enable=True):
+        self._chk(self.lib.c3h_timing(self.h, int(bool(enable))), "timing")
+
+    def kernel_times(self, reset=True):
+        ms = np.zeros(_capi.NTIMERS, np.float32)
+        cnt = np.zeros(_capi.NTIMERS, np.int32)
+        self._chk(self.lib.c3h_kernel_times(self.h, ptr(ms), ptr(cnt), int(bool(reset))), "kernel_times")
+        return {n: (float(ms[i]), int(cnt[i])) for i, n in enumerate(TIMER_NAMES)}
+
+
+def remove_overlap(lists, ranges):
+    """SearchObjMulti::removeOverlap on (M, rank) DET_DTYPE lists (host function)."""
+    lists = np.ascontiguousarray(lists, dtype=DET_DTYPE)
+    M, rank = lists.shape
+    check(_capi.load().c3h_remove_overlap(M, rank, i32x3(ranges), ptr(lists)), None, "remove_overlap")
+    return lists
+
+
+def pca_read(path, ascii=False, max_dim=4096):
+    """PCA::read -> (axis (dim,dim) with axis[:, i] = eigenvector i, variance, mean or None)."""
+    buf = np.zeros(max_dim * max_dim, np.float32)
+    var = np.zeros(max_dim, np.float32)
+    mean = np.zeros(max_dim, np.float32)
+    hm = C.c_int32()
+    dim = check(_capi.load().c3h_pca_read(str(path).encode(), int(bool(ascii)), ptr(buf), ptr(var),
+                                          ptr(mean), C.byref(hm), max_dim), None, "pca_read")
+    axis = buf[: dim * dim].reshape(dim, dim).T.copy()  # column i = eigenvector i
+    return axis, var[:dim].copy(), (mean[:dim].copy() if hm.value else None)
+
+
+def read_axis(axis, variance, dim, dim_model, multiple_similarity=True):
+    """SearchObj::readAxis transform (search.cpp:153-165): (dim_model, dim) float32."""
+    q = np.ascontiguousarray(axis[:, :dim_model].T, dtype=np.float32)
+    if multiple_similarity:
+        for i in range(1, dim_model):
+            q[i, :dim] = (q[i, :dim].astype(np.float64) * np.sqrt(np.float64(variance[i]))
+                          / np.sqrt(np.float64(variance[0]))).astype(np.float32)
+    return q
+
+
+def box_size(size_m, region_size):
+    """Sliding-box size in subdivisions (detect_object.cpp:254-266)."""
+    t = np.float32(size_m) / np.float32(region_size)
+    s = int(t)
+    if (t - s) >= 0.5 or s == 0:
+        s += 1
+    return s

@@ -1,0 +1,185 @@
+// c3h_internal.h -- context state and kernel-launcher declarations shared by the
+// HIP translation units of libc3hlac_mi355x.so.  gfx950 only; no dual code paths.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/c3hlac_mi355x.h"
+
+namespace c3h {
+
+// packed colour/occupancy voxel word: 0 = empty, else kOcc | r<<16 | g<<8 | b
+constexpr uint32_t kOcc = 1u << 24;
+constexpr uint32_t kEmptyKey = 0xffffffffu;
+constexpr int kBlock = 256;
+// largest centre-voxel extent of one C3 tile per axis; subdivisions wider than this
+// are split into several tiles whose exact integer partial sums are added in 64 bit.
+constexpr int kTileMax = 16;
+constexpr int kChunk = 64;  // list entries per packed-operand chunk (16 groups of 4)
+
+// reference constants (c3_hlac/src/c3_hlac.cpp:38-45), as float
+constexpr float kNorm0 = 1 / 255.0;
+constexpr float kNorm1 = 1 / 65025.0;
+constexpr float kNorm117_1 = 1 / 845325.0;
+constexpr float kNorm117_1Bin = 1 / 13.0;
+
+// ---- device buffers --------------------------------------------------------------
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;  // capacity in elements
+};
+
+struct SearchLists {  // SearchObjMulti max_*_multi state, host side
+  int rank = 0, M = 0;
+  std::vector<double> score;
+  std::vector<int32_t> x, y, z, mode;
+};
+
+struct Timer {
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[C3H_NTIMERS];
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
+  float ms[C3H_NTIMERS] = {0, 0, 0, 0, 0};
+  int count[C3H_NTIMERS] = {0, 0, 0, 0, 0};
+  bool enabled = false;
+};
+
+}  // namespace c3h
+
+struct c3h_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t own_stream = nullptr;
+  std::string err;
+
+  // voxel grid
+  bool have_grid = false;
+  c3h_grid_info info{};
+  c3h::DevBuf<uint32_t> grid;       // owned packed grid
+  const uint32_t* grid_ptr = nullptr;  // the grid in use (owned or bound)
+  c3h::DevBuf<float> pts;           // staging copy of host points
+  c3h::DevBuf<uint32_t> keys, cnt, sr, sg, sb;  // voxel hash table
+  c3h::DevBuf<float> sx, sy, sz;
+  uint64_t table_size = 0;          // power of two
+  c3h::DevBuf<uint32_t> scratch;    // minmax / counters
+  c3h::DevBuf<uint32_t> tmp_u32;    // leaf-layout block sums
+  c3h::DevBuf<int32_t> tmp_i32;     // leaf layout for host copies
+  uint32_t* h_small = nullptr;      // pinned host scratch (64 words)
+  bool table_valid = false;         // hash table matches the grid (voxelize path)
+
+  // features
+  bool have_feat = false;
+  c3h_extract_params last{};
+  int64_t hist_num = 0;
+  int32_t subdiv_b[3] = {0, 0, 0};
+  int feat_dim = 0;
+  c3h::DevBuf<float> feat;
+  c3h::DevBuf<int32_t> exist;
+  c3h::DevBuf<unsigned long long> acc64;
+  c3h::DevBuf<int32_t> segs;        // per-axis tile segment tables
+  std::vector<int32_t> h_segs;      // host copy (kept alive for the async upload)
+  c3h::DevBuf<uint32_t> lut;        // 256 packed (sin | cos<<8), two variants
+  bool lut_ready = false;
+
+  // search
+  bool have_setup = false;
+  int D = 0, F = 0, M = 0, r = 0, Dpad = 0;
+  bool compress = true;
+  c3h::DevBuf<float> axis_pt;       // F x Dpad (transposed, whitened)
+  c3h::DevBuf<float> axis_q;        // M x r x D
+  c3h::DevBuf<float> fmax;
+  int fmax_len = 0;
+  c3h::DevBuf<float> G;             // hist_num x D compressed features
+  bool g_valid = false;
+  c3h::DevBuf<double> scores;
+  int64_t scores_n = 0;
+  int rank = 1;
+  c3h::SearchLists lists;
+  std::vector<c3h_det> h_lists;     // host staging of the lists
+  c3h::DevBuf<c3h_det> d_lists;
+  bool lists_host_valid = true;     // host lists are current
+  bool lists_dev_valid = false;     // device lists are current
+  int32_t last_range[3] = {0, 0, 0};
+
+  c3h::Timer timer;
+};
+
+namespace c3h {
+
+// ---- launchers (defined in the .hip files) ----------------------------------------
+hipError_t launch_minmax(const float4* pts, int64_t n, float z_limit, uint32_t* out,
+                         hipStream_t s);
+hipError_t launch_voxel_accum(const float4* pts, int64_t n, float z_limit, float inv,
+                              const int32_t min_b[3], const int32_t div_b[3], uint32_t* keys,
+                              uint32_t* cnt, uint32_t* sr, uint32_t* sg, uint32_t* sb,
+                              float* sx, float* sy, float* sz, uint64_t table_size,
+                              uint32_t* overflow, hipStream_t s);
+hipError_t launch_voxel_scatter(const uint32_t* keys, const uint32_t* cnt, const uint32_t* sr,
+                                const uint32_t* sg, const uint32_t* sb, uint64_t table_size,
+                                uint32_t* grid, uint32_t* n_occ, hipStream_t s);
+hipError_t launch_leaf_layout(const uint32_t* grid, int64_t nvox, int32_t* leaf,
+                              uint32_t* block_sums, int64_t nblocks, hipStream_t s);
+hipError_t launch_downsampled(const int32_t* leaf, const uint32_t* grid, int64_t nvox,
+                              const int32_t div_b[3], const uint32_t* keys, const uint32_t* cnt,
+                              const float* sx, const float* sy, const float* sz,
+                              uint64_t table_size, float* out, hipStream_t s);
+
+struct C3Launch {
+  const uint32_t* grid;
+  int gx, gy, gz;
+  const int32_t* segs;  // [3][nseg_max][3] = start, len, subdiv
+  int nseg[3];
+  int seg_stride;
+  int sbx, sby;
+  int lmax[3];  // max segment length per axis (LDS tile dims)
+  int thr[3];
+  int variant;
+  int atomic;
+  const uint32_t* lut;  // 256 packed entries
+  float* feat;
+  int32_t* exist;
+  unsigned long long* acc64;
+  int64_t ntiles;
+};
+hipError_t launch_c3hlac(const C3Launch& a, hipStream_t s);
+hipError_t launch_c3_finalize(const unsigned long long* acc64, int64_t hist_num, int variant,
+                              float* feat, int32_t* exist, hipStream_t s);
+
+hipError_t launch_compress(const float* feat, int64_t H, int F, const float* axis_pt, int D,
+                           int Dpad, const float* fmax, int fmax_len, float* G, hipStream_t s);
+
+struct ScoreLaunch {
+  const float* G;
+  const int32_t* exist;
+  int D;
+  int xn, yn, zn;
+  int xr, yr, zr;
+  int xe, ye, ze;
+  int thr;
+  const float* axis_q;
+  int M, r;
+  double* scores;  // M x P for this mode
+};
+hipError_t launch_score(const ScoreLaunch& a, hipStream_t s);
+
+struct ReplayMode {
+  int64_t offset;  // into scores (M x P block)
+  int64_t P;
+  int xe, ye;
+  int mode;
+};
+struct ReplayModes {
+  ReplayMode m[6];
+  int n;
+};
+hipError_t launch_replay(const double* scores, const ReplayModes& modes, int M, int rank,
+                         int r1, int r2, int r3, c3h_det* lists, hipStream_t s);
+
+hipError_t launch_clean_lists(c3h_det* lists, int n, hipStream_t s);
+size_t c3hlac_lds_bytes(int tw_max, int list_max);
+int64_t leaf_layout_blocks(int64_t nvox);
+
+}  // namespace c3h

@@ -1,0 +1,979 @@
+// capi.hip -- C-ABI of libc3hlac_mi355x.so (see include/c3hlac_mi355x.h).
+//
+// Host-side sequencing of the voxeliser, C3-HLAC and search kernels, with the
+// reference's argument semantics: setVoxelFilter's float subdivision arithmetic
+// (c3_hlac/src/c3_hlac.cpp:204-231), the search mode schedule (search.cpp:384-427),
+// setSceneAxis whitening (search.cpp:701-712), setRank/cleanMax list state
+// (search.cpp:130-143, 683-732) and removeOverlap (search.cpp:972-992).
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "c3h_internal.h"
+
+using c3h::DevBuf;
+
+namespace {
+
+int fail(c3h_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+int hip_fail(c3h_ctx* ctx, const char* what, hipError_t e) {
+  return fail(ctx, C3H_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIPCHK(expr)                                     \
+  do {                                                   \
+    hipError_t e_ = (expr);                              \
+    if (e_ != hipSuccess) return hip_fail(ctx, #expr, e_); \
+  } while (0)
+
+template <class T>
+int ensure(c3h_ctx* ctx, DevBuf<T>& b, size_t n) {
+  if (n == 0) n = 1;
+  if (b.n >= n) return C3H_OK;
+  if (b.p) {
+    hipError_t e = hipFree(b.p);
+    b.p = nullptr;
+    b.n = 0;
+    if (e != hipSuccess) return hip_fail(ctx, "hipFree", e);
+  }
+  hipError_t e = hipMalloc(&b.p, n * sizeof(T));
+  if (e != hipSuccess) {
+    b.p = nullptr;
+    return fail(ctx, C3H_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  }
+  b.n = n;
+  return C3H_OK;
+}
+
+template <class T>
+void release(DevBuf<T>& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.n = 0;
+}
+
+#define ENSURE(buf, n)                          \
+  do {                                          \
+    int rc_ = ensure(ctx, buf, (size_t)(n));    \
+    if (rc_ != C3H_OK) return rc_;              \
+  } while (0)
+
+// ---- timing ------------------------------------------------------------------------
+struct Timed {
+  c3h_ctx* ctx;
+  int slot;
+  std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+  Timed(c3h_ctx* c, int s) : ctx(c), slot(s) {
+    if (!ctx->timer.enabled) return;
+    if (ctx->timer.pool.empty()) {
+      hipEvent_t a, b;
+      if (hipEventCreate(&a) != hipSuccess) return;
+      if (hipEventCreate(&b) != hipSuccess) {
+        (void)hipEventDestroy(a);
+        return;
+      }
+      ctx->timer.pool.push_back({a, b});
+    }
+    ev = ctx->timer.pool.back();
+    ctx->timer.pool.pop_back();
+    (void)hipEventRecord(ev.first, ctx->stream);
+  }
+  ~Timed() {
+    if (!ev.first) return;
+    (void)hipEventRecord(ev.second, ctx->stream);
+    ctx->timer.pending[slot].push_back(ev);
+  }
+};
+
+void host_lut(int lut_double, uint32_t* out) {
+  const float angle_norm = M_PI / 510;  // color_chlac/include/color_chlac/color_chlac.h:9
+  for (int v = 0; v < 256; ++v) {
+    const float a = v * angle_norm;
+    int s, c;
+    if (lut_double) {
+      s = (int)(255 * std::sin((double)a));
+      c = (int)(255 * std::cos((double)a));
+    } else {
+      s = (int)(255 * sinf(a));
+      c = (int)(255 * cosf(a));
+    }
+    out[v] = (uint32_t)s | ((uint32_t)c << 8);
+  }
+}
+
+float dec_f(uint32_t e) {
+  const uint32_t u = (e & 0x80000000u) ? (e & 0x7fffffffu) : ~e;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+// search.cpp:218-251
+void get_range(int mode, int r1, int r2, int r3, int* xr, int* yr, int* zr) {
+  switch (mode) {
+    case C3H_S_MODE_1: *xr = r1; *yr = r2; *zr = r3; break;
+    case C3H_S_MODE_2: *xr = r1; *yr = r3; *zr = r2; break;
+    case C3H_S_MODE_3: *xr = r2; *yr = r1; *zr = r3; break;
+    case C3H_S_MODE_4: *xr = r2; *yr = r3; *zr = r1; break;
+    case C3H_S_MODE_5: *xr = r3; *yr = r1; *zr = r2; break;
+    default: *xr = r3; *yr = r2; *zr = r1; break;
+  }
+}
+
+// search.cpp:384-427
+int mode_schedule(int r1, int r2, int r3, int rotate, int* modes) {
+  if (!rotate) {
+    modes[0] = C3H_S_MODE_1;
+    return 1;
+  }
+  if (r1 == r2) {
+    if (r2 == r3) {
+      modes[0] = C3H_S_MODE_1;
+      return 1;
+    }
+    modes[0] = C3H_S_MODE_1; modes[1] = C3H_S_MODE_2; modes[2] = C3H_S_MODE_5;
+    return 3;
+  }
+  if (r2 == r3) {
+    modes[0] = C3H_S_MODE_1; modes[1] = C3H_S_MODE_5; modes[2] = C3H_S_MODE_6;
+    return 3;
+  }
+  if (r1 == r3) {
+    modes[0] = C3H_S_MODE_1; modes[1] = C3H_S_MODE_5; modes[2] = C3H_S_MODE_3;
+    return 3;
+  }
+  for (int i = 0; i < 6; ++i) modes[i] = i;
+  return 6;
+}
+
+// checkOverlap of SearchObjMulti (search.cpp:862-891) on host lists
+int check_overlap(const c3h_det* L, int rank, int r1, int r2, int r3, int x, int y, int z,
+                  int mode) {
+  int xr, yr, zr, num;
+  get_range(mode, r1, r2, r3, &xr, &yr, &zr);
+  for (num = 0; num < rank - 1; num++) {
+    int oxr, oyr, ozr;
+    get_range(L[num].mode, r1, r2, r3, &oxr, &oyr, &ozr);
+    int v1 = L[num].x - x;
+    v1 = v1 < 0 ? -v1 - oxr : v1 - xr;
+    int v2 = L[num].y - y;
+    v2 = v2 < 0 ? -v2 - oyr : v2 - yr;
+    int v3 = L[num].z - z;
+    v3 = v3 < 0 ? -v3 - ozr : v3 - zr;
+    if (v1 <= 0 && v2 <= 0 && v3 <= 0) return num;
+  }
+  return num;
+}
+
+struct Segs {
+  std::vector<int32_t> start, len, sub;
+};
+
+// one axis of the tile decomposition.  mode1: the whole grid is one subdivision
+// (hist_num == 1: c3_hlac.cpp:258,350 ignore offsets); otherwise centre voxel t >= 0
+// (grid coordinate off + t) belongs to subdivision floor(t * inv_s) -- the reference's
+// float arithmetic, so irregular runs caused by float rounding are reproduced.
+Segs axis_segments(int div, int off, float inv_s, bool mode1, int sb, bool* covered,
+                   bool* split) {
+  Segs s;
+  std::vector<int> runs_per_sub(std::max(sb, 1), 0);
+  auto push = [&](int a0, int len, int sub) {
+    for (int p = 0; p < len; p += c3h::kTileMax) {
+      s.start.push_back(a0 + p);
+      s.len.push_back(std::min(c3h::kTileMax, len - p));
+      s.sub.push_back(sub);
+      if (sub >= 0 && sub < (int)runs_per_sub.size()) runs_per_sub[sub]++;
+    }
+  };
+  if (mode1) {
+    if (div > 0) push(0, div, 0);
+  } else {
+    int t0 = 0;
+    while (t0 < div - off) {
+      const int sub = (int)floorf((float)t0 * inv_s);
+      int t1 = t0 + 1;
+      while (t1 < div - off && (int)floorf((float)t1 * inv_s) == sub) ++t1;
+      push(off + t0, t1 - t0, sub);
+      t0 = t1;
+    }
+  }
+  *covered = true;
+  *split = false;
+  for (int v : runs_per_sub) {
+    if (v == 0) *covered = false;
+    if (v > 1) *split = true;
+  }
+  return s;
+}
+
+int upload_lists(c3h_ctx* ctx) {
+  auto& L = ctx->lists;
+  const size_t n = (size_t)L.M * L.rank;
+  ENSURE(ctx->d_lists, n);
+  ctx->h_lists.resize(n);
+  for (size_t i = 0; i < n; ++i)
+    ctx->h_lists[i] = c3h_det{L.score[i], L.x[i], L.y[i], L.z[i], L.mode[i]};
+  HIPCHK(hipMemcpyAsync(ctx->d_lists.p, ctx->h_lists.data(), n * sizeof(c3h_det),
+                        hipMemcpyHostToDevice, ctx->stream));
+  ctx->lists_dev_valid = true;
+  return C3H_OK;
+}
+
+int download_lists(c3h_ctx* ctx) {
+  auto& L = ctx->lists;
+  const size_t n = (size_t)L.M * L.rank;
+  ctx->h_lists.resize(n);
+  HIPCHK(hipMemcpyAsync(ctx->h_lists.data(), ctx->d_lists.p, n * sizeof(c3h_det),
+                        hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  for (size_t i = 0; i < n; ++i) {
+    L.score[i] = ctx->h_lists[i].score;
+    L.x[i] = ctx->h_lists[i].x;
+    L.y[i] = ctx->h_lists[i].y;
+    L.z[i] = ctx->h_lists[i].z;
+    L.mode[i] = ctx->h_lists[i].mode;
+  }
+  ctx->lists_host_valid = true;
+  return C3H_OK;
+}
+
+void init_lists(c3h_ctx* ctx) {  // setRank: dot = 0, modes S_MODE_1 (never-initialised there)
+  auto& L = ctx->lists;
+  L.M = std::max(ctx->M, 1);
+  L.rank = ctx->rank;
+  const size_t n = (size_t)L.M * L.rank;
+  L.score.assign(n, 0.0);
+  L.x.assign(n, 0);
+  L.y.assign(n, 0);
+  L.z.assign(n, 0);
+  L.mode.assign(n, C3H_S_MODE_1);
+  ctx->lists_host_valid = true;
+  ctx->lists_dev_valid = false;
+}
+
+int sync_host_lists(c3h_ctx* ctx) {
+  if (!ctx->lists_host_valid) return download_lists(ctx);
+  return C3H_OK;
+}
+
+// setData + searchPart for every scheduled mode; leaves the lists valid on the device
+int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate) {
+  if (!ctx->have_feat) return fail(ctx, C3H_ERR_STATE, "c3h_search: no features (call c3h_extract)");
+  if (!ctx->have_setup) return fail(ctx, C3H_ERR_STATE, "c3h_search: no axes (call c3h_search_setup)");
+  if (!range || range[0] < 1 || range[1] < 1 || range[2] < 1)
+    return fail(ctx, C3H_ERR_ARG, "c3h_search: ranges must be >= 1");
+  if (ctx->feat_dim != ctx->F)
+    return fail(ctx, C3H_ERR_ARG, "c3h_search: feature dimension differs from the scene axis");
+  const int xn = ctx->subdiv_b[0], yn = ctx->subdiv_b[1], zn = ctx->subdiv_b[2];
+  const int64_t H = (int64_t)xn * yn * zn;
+  if (ctx->lists.M != std::max(ctx->M, 1) || ctx->lists.rank != ctx->rank) init_lists(ctx);
+  if (H < 1 || H != ctx->hist_num) return 0;  // setData returns early; search is skipped
+  if (!ctx->g_valid) {
+    ENSURE(ctx->G, (size_t)H * ctx->D);
+    Timed t(ctx, 2);
+    HIPCHK(c3h::launch_compress(ctx->feat.p, H, ctx->F, ctx->axis_pt.p, ctx->D, ctx->Dpad,
+                                ctx->fmax.p, ctx->fmax_len, ctx->G.p, ctx->stream));
+    ctx->g_valid = true;
+  }
+  int modes[6];
+  const int nm = mode_schedule(range[0], range[1], range[2], rotate, modes);
+  c3h::ReplayModes rm{};
+  int64_t total = 0;
+  for (int i = 0; i < nm; ++i) {
+    int xr, yr, zr;
+    get_range(modes[i], range[0], range[1], range[2], &xr, &yr, &zr);
+    const int xe = xn - xr + 1, ye = yn - yr + 1, ze = zn - zr + 1;
+    if (!(xe > 0 && ye > 0 && ze > 0)) continue;
+    rm.m[rm.n] = c3h::ReplayMode{total, (int64_t)xe * ye * ze, xe, ye, modes[i]};
+    total += rm.m[rm.n].P * ctx->M;
+    rm.n++;
+  }
+  ENSURE(ctx->scores, total);
+  ctx->scores_n = total;
+  {
+    Timed t(ctx, 3);
+    for (int i = 0; i < rm.n; ++i) {
+      int xr, yr, zr;
+      get_range(rm.m[i].mode, range[0], range[1], range[2], &xr, &yr, &zr);
+      c3h::ScoreLaunch a;
+      a.G = ctx->G.p;
+      a.exist = ctx->exist.p;
+      a.D = ctx->D;
+      a.xn = xn;
+      a.yn = yn;
+      a.zn = zn;
+      a.xr = xr;
+      a.yr = yr;
+      a.zr = zr;
+      a.xe = rm.m[i].xe;
+      a.ye = rm.m[i].ye;
+      a.ze = (int)(rm.m[i].P / ((int64_t)rm.m[i].xe * rm.m[i].ye));
+      a.thr = thr;
+      a.axis_q = ctx->axis_q.p;
+      a.M = ctx->M;
+      a.r = ctx->r;
+      a.scores = ctx->scores.p + rm.m[i].offset;
+      HIPCHK(c3h::launch_score(a, ctx->stream));
+    }
+  }
+  if (!ctx->lists_dev_valid) {
+    int rc = upload_lists(ctx);
+    if (rc != C3H_OK) return rc;
+  }
+  {
+    Timed t(ctx, 4);
+    HIPCHK(c3h::launch_replay(ctx->scores.p, rm, ctx->M, ctx->rank, range[0], range[1],
+                              range[2], ctx->d_lists.p, ctx->stream));
+  }
+  ctx->lists_host_valid = false;
+  ctx->last_range[0] = range[0];
+  ctx->last_range[1] = range[1];
+  ctx->last_range[2] = range[2];
+  return nm;
+}
+
+}  // namespace
+
+extern "C" {
+
+int c3h_version(void) { return 10000; }
+
+int c3h_create(int hip_device, c3h_ctx** out) {
+  if (!out) return C3H_ERR_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return C3H_ERR_HIP;
+  if (hip_device < 0 || hip_device >= ndev) return C3H_ERR_ARG;
+  c3h_ctx* ctx = new c3h_ctx();
+  ctx->device = hip_device;
+  auto bail = [&](int rc) {
+    c3h_destroy(ctx);
+    return rc;
+  };
+  if (hipSetDevice(hip_device) != hipSuccess) return bail(C3H_ERR_HIP);
+  if (hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess)
+    return bail(C3H_ERR_HIP);
+  ctx->stream = ctx->own_stream;
+  if (hipHostMalloc(&ctx->h_small, 64 * sizeof(uint32_t)) != hipSuccess) return bail(C3H_ERR_HIP);
+  if (ensure(ctx, ctx->scratch, 64) != C3H_OK) return bail(C3H_ERR_NOMEM);
+  if (ensure(ctx, ctx->lut, 512) != C3H_OK) return bail(C3H_ERR_NOMEM);
+  uint32_t lut[512];
+  host_lut(1, lut);
+  host_lut(0, lut + 256);
+  if (hipMemcpy(ctx->lut.p, lut, sizeof(lut), hipMemcpyHostToDevice) != hipSuccess)
+    return bail(C3H_ERR_HIP);
+  ctx->rank = 1;
+  *out = ctx;
+  return C3H_OK;
+}
+
+void c3h_destroy(c3h_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  release(ctx->grid);
+  release(ctx->pts);
+  release(ctx->keys);
+  release(ctx->cnt);
+  release(ctx->sr);
+  release(ctx->sg);
+  release(ctx->sb);
+  release(ctx->sx);
+  release(ctx->sy);
+  release(ctx->sz);
+  release(ctx->scratch);
+  release(ctx->tmp_u32);
+  release(ctx->tmp_i32);
+  release(ctx->feat);
+  release(ctx->exist);
+  release(ctx->acc64);
+  release(ctx->segs);
+  release(ctx->lut);
+  release(ctx->axis_pt);
+  release(ctx->axis_q);
+  release(ctx->fmax);
+  release(ctx->G);
+  release(ctx->scores);
+  release(ctx->d_lists);
+  for (int s = 0; s < C3H_NTIMERS; ++s)
+    for (auto& e : ctx->timer.pending[s]) ctx->timer.pool.push_back(e);
+  for (auto& e : ctx->timer.pool) {
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  if (ctx->h_small) (void)hipHostFree(ctx->h_small);
+  if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+  delete ctx;
+}
+
+int c3h_set_stream(c3h_ctx* ctx, void* hip_stream) {
+  if (!ctx) return C3H_ERR_ARG;
+  ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own_stream;
+  return C3H_OK;
+}
+
+int c3h_synchronize(c3h_ctx* ctx) {
+  if (!ctx) return C3H_ERR_ARG;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return C3H_OK;
+}
+
+const char* c3h_last_error(const c3h_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, float leaf,
+                 float z_limit, c3h_grid_info* info) {
+  if (!ctx) return C3H_ERR_ARG;
+  if (n < 0 || (n > 0 && !xyzrgb) || !(leaf > 0))
+    return fail(ctx, C3H_ERR_ARG, "c3h_voxelize: bad arguments");
+  HIPCHK(hipSetDevice(ctx->device));
+  ctx->have_grid = false;
+  ctx->have_feat = false;
+  ctx->g_valid = false;
+  ctx->table_valid = false;
+  c3h_grid_info gi{};
+  gi.leaf = leaf;
+  gi.inv_leaf = 1.0f / leaf;
+  const float4* d_pts = nullptr;
+  if (n > 0) {
+    if (on_device) {
+      d_pts = reinterpret_cast<const float4*>(xyzrgb);
+    } else {
+      ENSURE(ctx->pts, (size_t)n * 4);
+      HIPCHK(hipMemcpyAsync(ctx->pts.p, xyzrgb, (size_t)n * 16, hipMemcpyHostToDevice, ctx->stream));
+      d_pts = reinterpret_cast<const float4*>(ctx->pts.p);
+    }
+  }
+  Timed t(ctx, 0);
+  uint32_t init[16] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  memcpy(ctx->h_small, init, sizeof(init));
+  HIPCHK(hipMemcpyAsync(ctx->scratch.p, ctx->h_small, sizeof(init), hipMemcpyHostToDevice, ctx->stream));
+  if (n > 0) HIPCHK(c3h::launch_minmax(d_pts, n, z_limit, ctx->scratch.p, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->h_small, ctx->scratch.p, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  uint64_t nvalid;
+  memcpy(&nvalid, ctx->h_small + 6, 8);
+  gi.n_valid = (int64_t)nvalid;
+  if (nvalid == 0) {
+    ctx->info = gi;
+    ctx->have_grid = true;
+    ctx->grid_ptr = nullptr;
+    if (info) *info = gi;
+    return C3H_OK;
+  }
+  int64_t nvox = 1;
+  for (int a = 0; a < 3; ++a) {
+    const float mn = dec_f(ctx->h_small[a]), mx = dec_f(ctx->h_small[3 + a]);
+    gi.min_b[a] = (int)floorf(mn * gi.inv_leaf);
+    gi.max_b[a] = (int)floorf(mx * gi.inv_leaf);
+    gi.div_b[a] = gi.max_b[a] - gi.min_b[a] + 1;
+    nvox *= gi.div_b[a];
+  }
+  if (nvox > 2147483647LL)
+    return fail(ctx, C3H_ERR_RANGE, "c3h_voxelize: leaf size too small for int32 voxel indices");
+  uint64_t ts = 1024;
+  while (ts < 2 * nvalid) ts <<= 1;
+  ctx->table_size = ts;
+  ENSURE(ctx->keys, ts);
+  ENSURE(ctx->cnt, ts);
+  ENSURE(ctx->sr, ts);
+  ENSURE(ctx->sg, ts);
+  ENSURE(ctx->sb, ts);
+  ENSURE(ctx->sx, ts);
+  ENSURE(ctx->sy, ts);
+  ENSURE(ctx->sz, ts);
+  ENSURE(ctx->grid, (size_t)nvox);
+  HIPCHK(hipMemsetAsync(ctx->keys.p, 0xff, ts * 4, ctx->stream));
+  HIPCHK(hipMemsetAsync(ctx->cnt.p, 0, ts * 4, ctx->stream));
+  HIPCHK(hipMemsetAsync(ctx->sr.p, 0, ts * 4, ctx->stream));
+  HIPCHK(hipMemsetAsync(ctx->sg.p, 0, ts * 4, ctx->stream));
+  HIPCHK(hipMemsetAsync(ctx->sb.p, 0, ts * 4, ctx->stream));
+  HIPCHK(hipMemsetAsync(ctx->sx.p, 0, ts * 4, ctx->stream));
+  HIPCHK(hipMemsetAsync(ctx->sy.p, 0, ts * 4, ctx->stream));
+  HIPCHK(hipMemsetAsync(ctx->sz.p, 0, ts * 4, ctx->stream));
+  HIPCHK(hipMemsetAsync(ctx->grid.p, 0, (size_t)nvox * 4, ctx->stream));
+  HIPCHK(c3h::launch_voxel_accum(d_pts, n, z_limit, gi.inv_leaf, gi.min_b, gi.div_b, ctx->keys.p,
+                                 ctx->cnt.p, ctx->sr.p, ctx->sg.p, ctx->sb.p, ctx->sx.p, ctx->sy.p,
+                                 ctx->sz.p, ts, ctx->scratch.p + 8, ctx->stream));
+  HIPCHK(c3h::launch_voxel_scatter(ctx->keys.p, ctx->cnt.p, ctx->sr.p, ctx->sg.p, ctx->sb.p, ts,
+                                   ctx->grid.p, ctx->scratch.p + 9, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->h_small + 8, ctx->scratch.p + 8, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (ctx->h_small[8]) return fail(ctx, C3H_ERR_HIP, "c3h_voxelize: hash table overflow");
+  gi.n_occ = ctx->h_small[9];
+  ctx->info = gi;
+  ctx->grid_ptr = ctx->grid.p;
+  ctx->have_grid = true;
+  ctx->table_valid = true;
+  if (info) *info = gi;
+  return C3H_OK;
+}
+
+int c3h_get_grid_info(c3h_ctx* ctx, c3h_grid_info* info) {
+  if (!ctx || !info) return C3H_ERR_ARG;
+  if (!ctx->have_grid) return fail(ctx, C3H_ERR_STATE, "no grid");
+  *info = ctx->info;
+  return C3H_OK;
+}
+
+static int64_t grid_voxels(const c3h_ctx* ctx) {
+  return (int64_t)ctx->info.div_b[0] * ctx->info.div_b[1] * ctx->info.div_b[2];
+}
+
+int c3h_get_grid(c3h_ctx* ctx, uint32_t* out, int on_device) {
+  if (!ctx || !out) return C3H_ERR_ARG;
+  if (!ctx->have_grid) return fail(ctx, C3H_ERR_STATE, "no grid");
+  HIPCHK(hipSetDevice(ctx->device));
+  const int64_t nvox = grid_voxels(ctx);
+  if (nvox == 0) return C3H_OK;
+  HIPCHK(hipMemcpyAsync(out, ctx->grid_ptr, (size_t)nvox * 4,
+                        on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return C3H_OK;
+}
+
+static int compute_leaf_layout(c3h_ctx* ctx, int32_t* d_out) {
+  const int64_t nvox = grid_voxels(ctx);
+  const int64_t nb = c3h::leaf_layout_blocks(nvox);
+  ENSURE(ctx->tmp_u32, (size_t)nb);
+  HIPCHK(c3h::launch_leaf_layout(ctx->grid_ptr, nvox, d_out, ctx->tmp_u32.p, nb, ctx->stream));
+  return C3H_OK;
+}
+
+int c3h_get_leaf_layout(c3h_ctx* ctx, int32_t* out, int on_device) {
+  if (!ctx || !out) return C3H_ERR_ARG;
+  if (!ctx->have_grid) return fail(ctx, C3H_ERR_STATE, "no grid");
+  HIPCHK(hipSetDevice(ctx->device));
+  const int64_t nvox = grid_voxels(ctx);
+  if (nvox == 0) return C3H_OK;
+  int32_t* dst = out;
+  if (!on_device) {
+    ENSURE(ctx->tmp_i32, (size_t)nvox);
+    dst = ctx->tmp_i32.p;
+  }
+  int rc = compute_leaf_layout(ctx, dst);
+  if (rc != C3H_OK) return rc;
+  if (!on_device)
+    HIPCHK(hipMemcpyAsync(out, dst, (size_t)nvox * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return C3H_OK;
+}
+
+int c3h_get_downsampled(c3h_ctx* ctx, float* out, int on_device) {
+  if (!ctx || !out) return C3H_ERR_ARG;
+  if (!ctx->have_grid) return fail(ctx, C3H_ERR_STATE, "no grid");
+  if (!ctx->table_valid)
+    return fail(ctx, C3H_ERR_STATE, "c3h_get_downsampled: grid was not produced by c3h_voxelize");
+  HIPCHK(hipSetDevice(ctx->device));
+  const int64_t nvox = grid_voxels(ctx);
+  if (nvox == 0 || ctx->info.n_occ == 0) return C3H_OK;
+  ENSURE(ctx->tmp_i32, (size_t)nvox);
+  int rc = compute_leaf_layout(ctx, ctx->tmp_i32.p);
+  if (rc != C3H_OK) return rc;
+  float* dst = out;
+  if (!on_device) {
+    ENSURE(ctx->pts, (size_t)ctx->info.n_occ * 4);
+    dst = ctx->pts.p;
+  }
+  HIPCHK(c3h::launch_downsampled(ctx->tmp_i32.p, ctx->grid_ptr, nvox, ctx->info.div_b, ctx->keys.p,
+                                 ctx->cnt.p, ctx->sx.p, ctx->sy.p, ctx->sz.p, ctx->table_size, dst,
+                                 ctx->stream));
+  if (!on_device)
+    HIPCHK(hipMemcpyAsync(out, dst, (size_t)ctx->info.n_occ * 16, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return C3H_OK;
+}
+
+int c3h_set_grid(c3h_ctx* ctx, const uint32_t* words, const int32_t div_b[3],
+                 const int32_t min_b[3], float leaf, int on_device) {
+  if (!ctx || !div_b || !min_b || !(leaf > 0)) return C3H_ERR_ARG;
+  int64_t nvox = 1;
+  for (int a = 0; a < 3; ++a) {
+    if (div_b[a] < 0) return fail(ctx, C3H_ERR_ARG, "c3h_set_grid: negative dims");
+    nvox *= div_b[a];
+  }
+  if (nvox > 2147483647LL) return fail(ctx, C3H_ERR_RANGE, "c3h_set_grid: grid too large");
+  if (nvox > 0 && !words) return C3H_ERR_ARG;
+  HIPCHK(hipSetDevice(ctx->device));
+  c3h_grid_info gi{};
+  for (int a = 0; a < 3; ++a) {
+    gi.div_b[a] = div_b[a];
+    gi.min_b[a] = min_b[a];
+    gi.max_b[a] = min_b[a] + div_b[a] - 1;
+  }
+  gi.leaf = leaf;
+  gi.inv_leaf = 1.0f / leaf;
+  gi.n_valid = -1;
+  gi.n_occ = -1;
+  if (on_device || nvox == 0) {
+    ctx->grid_ptr = words;
+  } else {
+    ENSURE(ctx->grid, (size_t)nvox);
+    HIPCHK(hipMemcpyAsync(ctx->grid.p, words, (size_t)nvox * 4, hipMemcpyHostToDevice, ctx->stream));
+    ctx->grid_ptr = ctx->grid.p;
+  }
+  ctx->info = gi;
+  ctx->have_grid = true;
+  ctx->table_valid = false;
+  ctx->have_feat = false;
+  ctx->g_valid = false;
+  return C3H_OK;
+}
+
+int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3],
+                int64_t* hist_num_out) {
+  if (!ctx || !p) return C3H_ERR_ARG;
+  if (p->variant != 981 && p->variant != 117)
+    return fail(ctx, C3H_ERR_ARG, "c3h_extract: variant must be 981 or 117");
+  if (!ctx->have_grid) return fail(ctx, C3H_ERR_STATE, "c3h_extract: no grid");
+  HIPCHK(hipSetDevice(ctx->device));
+  ctx->have_feat = false;
+  ctx->g_valid = false;
+  const int F = p->variant;
+  const int* div = ctx->info.div_b;
+  int32_t sb[3] = {0, 0, 0};
+  int64_t hist_num = 1;
+  float inv_s = 0.0f;
+  auto empty = [&](const char* why) {
+    ctx->err = why;
+    ctx->hist_num = 0;
+    ctx->feat_dim = F;
+    ctx->subdiv_b[0] = sb[0];
+    ctx->subdiv_b[1] = sb[1];
+    ctx->subdiv_b[2] = sb[2];
+    ctx->have_feat = true;
+    if (subdiv_out) memcpy(subdiv_out, sb, sizeof(sb));
+    if (hist_num_out) *hist_num_out = 0;
+    return C3H_OK;
+  };
+  // setVoxelFilter (c3_hlac.cpp:204-231)
+  if (p->subdiv > 0) {
+    inv_s = 1.0 / p->subdiv;
+    if (div[0] <= p->offset[0] || div[1] <= p->offset[1] || div[2] <= p->offset[2])
+      return empty("setVoxelFilter: offset values exceed voxel grid size (empty feature)");
+    for (int a = 0; a < 3; ++a) sb[a] = (int)ceilf((div[a] - p->offset[a]) * inv_s);
+    hist_num = (int64_t)sb[0] * sb[1] * sb[2];
+  } else if (p->subdiv < 0) {
+    return empty("setVoxelFilter: invalid subdivision size (empty feature)");
+  }
+  // computeFeature (c3_hlac.cpp:398-401): negative thresholds -> silent empty output
+  if (p->thr[0] < 0 || p->thr[1] < 0 || p->thr[2] < 0)
+    return empty("computeFeature: invalid color_threshold (empty feature)");
+  const bool mode1 = (hist_num == 1);
+  bool covered[3], split[3];
+  Segs s[3];
+  for (int a = 0; a < 3; ++a)
+    s[a] = axis_segments(div[a], mode1 ? 0 : p->offset[a], inv_s, mode1, mode1 ? 1 : sb[a],
+                         &covered[a], &split[a]);
+  const int64_t ntiles = (int64_t)s[0].start.size() * s[1].start.size() * s[2].start.size();
+  const bool atomic = split[0] || split[1] || split[2];
+  const bool all_covered = covered[0] && covered[1] && covered[2] && ntiles > 0;
+  ENSURE(ctx->feat, (size_t)hist_num * F);
+  ENSURE(ctx->exist, (size_t)hist_num);
+  if (!all_covered || atomic) {
+    HIPCHK(hipMemsetAsync(ctx->feat.p, 0, (size_t)hist_num * F * 4, ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->exist.p, 0, (size_t)hist_num * 4, ctx->stream));
+  }
+  if (ntiles > 0) {
+    int stride = 0, lmax[3] = {1, 1, 1};
+    for (int a = 0; a < 3; ++a) {
+      stride = std::max(stride, (int)s[a].start.size());
+      for (int l : s[a].len) lmax[a] = std::max(lmax[a], l);
+    }
+    ctx->h_segs.assign((size_t)3 * stride * 3, 0);
+    for (int a = 0; a < 3; ++a)
+      for (size_t i = 0; i < s[a].start.size(); ++i) {
+        int32_t* e = &ctx->h_segs[((size_t)a * stride + i) * 3];
+        e[0] = s[a].start[i];
+        e[1] = s[a].len[i];
+        e[2] = s[a].sub[i];
+      }
+    ENSURE(ctx->segs, ctx->h_segs.size());
+    HIPCHK(hipMemcpyAsync(ctx->segs.p, ctx->h_segs.data(), ctx->h_segs.size() * 4,
+                          hipMemcpyHostToDevice, ctx->stream));
+    if (atomic) {
+      ENSURE(ctx->acc64, (size_t)hist_num * 981);
+      HIPCHK(hipMemsetAsync(ctx->acc64.p, 0, (size_t)hist_num * 981 * 8, ctx->stream));
+    }
+    c3h::C3Launch l;
+    l.grid = ctx->grid_ptr;
+    l.gx = div[0];
+    l.gy = div[1];
+    l.gz = div[2];
+    l.segs = ctx->segs.p;
+    for (int a = 0; a < 3; ++a) {
+      l.nseg[a] = (int)s[a].start.size();
+      l.lmax[a] = lmax[a];
+      l.thr[a] = p->thr[a];
+    }
+    l.seg_stride = stride;
+    l.sbx = mode1 ? 1 : sb[0];
+    l.sby = mode1 ? 1 : sb[1];
+    l.variant = F;
+    l.atomic = atomic ? 1 : 0;
+    l.lut = ctx->lut.p + (p->lut_double ? 0 : 256);
+    l.feat = ctx->feat.p;
+    l.exist = ctx->exist.p;
+    l.acc64 = ctx->acc64.p;
+    l.ntiles = ntiles;
+    Timed t(ctx, 1);
+    HIPCHK(c3h::launch_c3hlac(l, ctx->stream));
+    if (atomic)
+      HIPCHK(c3h::launch_c3_finalize(ctx->acc64.p, hist_num, F, ctx->feat.p, ctx->exist.p, ctx->stream));
+  }
+  ctx->hist_num = hist_num;
+  ctx->feat_dim = F;
+  ctx->subdiv_b[0] = sb[0];
+  ctx->subdiv_b[1] = sb[1];
+  ctx->subdiv_b[2] = sb[2];
+  ctx->last = *p;
+  ctx->have_feat = true;
+  if (subdiv_out) memcpy(subdiv_out, sb, sizeof(sb));
+  if (hist_num_out) *hist_num_out = hist_num;
+  return C3H_OK;
+}
+
+int c3h_get_features(c3h_ctx* ctx, float* out, int on_device) {
+  if (!ctx || !out) return C3H_ERR_ARG;
+  if (!ctx->have_feat) return fail(ctx, C3H_ERR_STATE, "no features");
+  HIPCHK(hipSetDevice(ctx->device));
+  const size_t n = (size_t)ctx->hist_num * ctx->feat_dim;
+  if (n) HIPCHK(hipMemcpyAsync(out, ctx->feat.p, n * 4, on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return C3H_OK;
+}
+
+int c3h_get_exist(c3h_ctx* ctx, int32_t* out, int on_device) {
+  if (!ctx || !out) return C3H_ERR_ARG;
+  if (!ctx->have_feat) return fail(ctx, C3H_ERR_STATE, "no features");
+  HIPCHK(hipSetDevice(ctx->device));
+  const size_t n = (size_t)ctx->hist_num;
+  if (n) HIPCHK(hipMemcpyAsync(out, ctx->exist.p, n * 4, on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return C3H_OK;
+}
+
+int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_t D, int32_t F,
+                     const float* axis_q, int32_t M, int32_t r, const float* feature_max,
+                     int32_t feature_max_len) {
+  if (!ctx) return C3H_ERR_ARG;
+  if (D < 1 || F < 1 || M < 1 || r < 1 || !axis_q || feature_max_len < 0 ||
+      (feature_max_len > 0 && !feature_max))
+    return fail(ctx, C3H_ERR_ARG, "c3h_search_setup: bad arguments");
+  if (!axis_p && D != F)
+    return fail(ctx, C3H_ERR_ARG, "c3h_search_setup: without compression D must equal F");
+  HIPCHK(hipSetDevice(ctx->device));
+  const int Dpad = (D + 7) / 8 * 8;
+  std::vector<float> pt((size_t)F * Dpad, 0.0f);
+  for (int d = 0; d < D; ++d) {
+    // setSceneAxis with whitening: row d scaled by 1/sqrt(var(d)) (search.cpp:701-712)
+    const float w = var ? (float)(1 / std::sqrt((double)var[d])) : 1.0f;
+    for (int j = 0; j < F; ++j) {
+      float v;
+      if (axis_p) v = var ? w * axis_p[(size_t)d * F + j] : axis_p[(size_t)d * F + j];
+      else v = (d == j) ? 1.0f : 0.0f;
+      pt[(size_t)j * Dpad + d] = v;
+    }
+  }
+  ENSURE(ctx->axis_pt, pt.size());
+  HIPCHK(hipMemcpy(ctx->axis_pt.p, pt.data(), pt.size() * 4, hipMemcpyHostToDevice));
+  ENSURE(ctx->axis_q, (size_t)M * r * D);
+  HIPCHK(hipMemcpy(ctx->axis_q.p, axis_q, (size_t)M * r * D * 4, hipMemcpyHostToDevice));
+  ctx->fmax_len = feature_max_len;
+  if (feature_max_len > 0) {
+    ENSURE(ctx->fmax, (size_t)feature_max_len);
+    HIPCHK(hipMemcpy(ctx->fmax.p, feature_max, (size_t)feature_max_len * 4, hipMemcpyHostToDevice));
+  }
+  ctx->compress = axis_p != nullptr;
+  ctx->D = D;
+  ctx->F = F;
+  ctx->M = M;
+  ctx->r = r;
+  ctx->Dpad = Dpad;
+  ctx->have_setup = true;
+  ctx->g_valid = false;
+  if (ctx->lists.M != M) init_lists(ctx);
+  return C3H_OK;
+}
+
+int c3h_set_rank(c3h_ctx* ctx, int32_t rank) {
+  if (!ctx || rank < 1 || rank > 4096) return C3H_ERR_ARG;
+  ctx->rank = rank;
+  init_lists(ctx);
+  return C3H_OK;
+}
+
+int c3h_clean_max(c3h_ctx* ctx) {
+  if (!ctx) return C3H_ERR_ARG;
+  if (ctx->lists.M != std::max(ctx->M, 1) || ctx->lists.rank != ctx->rank) init_lists(ctx);
+  if (!ctx->lists_host_valid && ctx->lists_dev_valid) {  // device copy is authoritative
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(c3h::launch_clean_lists(ctx->d_lists.p, ctx->lists.M * ctx->lists.rank, ctx->stream));
+    return C3H_OK;
+  }
+  auto& L = ctx->lists;
+  std::fill(L.score.begin(), L.score.end(), 0.0);
+  std::fill(L.x.begin(), L.x.end(), 0);
+  std::fill(L.y.begin(), L.y.end(), 0);
+  std::fill(L.z.begin(), L.z.end(), 0);
+  ctx->lists_dev_valid = false;
+  return C3H_OK;
+}
+
+int c3h_search(c3h_ctx* ctx, const int32_t range[3], int32_t exist_threshold, int32_t rotate,
+               int32_t remove_overlap, c3h_det* out) {
+  if (!ctx) return C3H_ERR_ARG;
+  HIPCHK(hipSetDevice(ctx->device));
+  const int nm = run_search(ctx, range, exist_threshold, rotate);
+  if (nm < 0) return nm;
+  int rc = sync_host_lists(ctx);
+  if (rc != C3H_OK) return rc;
+  auto& L = ctx->lists;
+  const size_t n = (size_t)L.M * L.rank;
+  std::vector<c3h_det> recs(n);
+  for (size_t i = 0; i < n; ++i) recs[i] = c3h_det{L.score[i], L.x[i], L.y[i], L.z[i], L.mode[i]};
+  if (remove_overlap) {
+    c3h_remove_overlap(L.M, L.rank, range, recs.data());
+    for (size_t i = 0; i < n; ++i) {
+      L.score[i] = recs[i].score;
+      L.x[i] = recs[i].x;
+      L.y[i] = recs[i].y;
+      L.z[i] = recs[i].z;
+      L.mode[i] = recs[i].mode;
+    }
+    ctx->lists_dev_valid = false;
+  }
+  if (out) memcpy(out, recs.data(), n * sizeof(c3h_det));
+  return nm;
+}
+
+int c3h_search_async(c3h_ctx* ctx, const int32_t range[3], int32_t exist_threshold,
+                     int32_t rotate, c3h_det* d_out) {
+  if (!ctx) return C3H_ERR_ARG;
+  HIPCHK(hipSetDevice(ctx->device));
+  const int nm = run_search(ctx, range, exist_threshold, rotate);
+  if (nm < 0) return nm;
+  if (d_out && ctx->lists_dev_valid) {
+    const size_t n = (size_t)ctx->lists.M * ctx->lists.rank;
+    HIPCHK(hipMemcpyAsync(d_out, ctx->d_lists.p, n * sizeof(c3h_det), hipMemcpyDeviceToDevice, ctx->stream));
+  }
+  return nm;
+}
+
+int c3h_get_compressed(c3h_ctx* ctx, float* out, int on_device) {
+  if (!ctx || !out) return C3H_ERR_ARG;
+  if (!ctx->g_valid) return fail(ctx, C3H_ERR_STATE, "no compressed features (run a search)");
+  HIPCHK(hipSetDevice(ctx->device));
+  const size_t n = (size_t)ctx->hist_num * ctx->D;
+  HIPCHK(hipMemcpyAsync(out, ctx->G.p, n * 4, on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return C3H_OK;
+}
+
+int c3h_get_scores(c3h_ctx* ctx, double* out, int64_t* n_out, int on_device) {
+  if (!ctx) return C3H_ERR_ARG;
+  if (n_out) *n_out = ctx->scores_n;
+  if (!out) return C3H_OK;
+  HIPCHK(hipSetDevice(ctx->device));
+  if (ctx->scores_n)
+    HIPCHK(hipMemcpyAsync(out, ctx->scores.p, (size_t)ctx->scores_n * 8,
+                          on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return C3H_OK;
+}
+
+int c3h_remove_overlap(int32_t M, int32_t rank, const int32_t range[3], c3h_det* lists) {
+  if (M < 1 || rank < 1 || !range || !lists) return C3H_ERR_ARG;
+  const int r1 = range[0], r2 = range[1], r3 = range[2];
+  for (int m = 0; m < M; m++) {
+    for (int i = 0; i < 1; i++) {
+      for (int m2 = 0; m2 < M; m2++) {
+        if (m2 == m) continue;
+        c3h_det* Lm = lists + (size_t)m * rank;
+        c3h_det* Lm2 = lists + (size_t)m2 * rank;
+        const int ov = check_overlap(Lm2, rank, r1, r2, r3, Lm[i].x, Lm[i].y, Lm[i].z, Lm[i].mode);
+        if (Lm[i].score > Lm2[ov].score)
+          for (int j = ov; j < rank - 1; j++) Lm2[j] = Lm2[j + 1];
+        else
+          for (int j = i; j < rank - 1; j++) Lm[j] = Lm[j + 1];
+      }
+    }
+  }
+  return C3H_OK;
+}
+
+int c3h_pca_read(const char* path, int32_t ascii, float* axis, float* var, float* mean,
+                 int32_t* has_mean, int32_t max_dim) {
+  if (!path || !axis || !var) return C3H_ERR_ARG;
+  FILE* fp = fopen(path, ascii ? "r" : "rb");
+  if (!fp) return C3H_ERR_NOTFOUND;
+  int dim = -1;
+  const bool got_dim = ascii ? fscanf(fp, "%d\n", &dim) == 1 : fread(&dim, sizeof(int), 1, fp) == 1;
+  if (!got_dim || dim <= 0 || dim > max_dim) {
+    fclose(fp);
+    return C3H_ERR_FORMAT;
+  }
+  bool ok = true;
+  for (int i = 0; i < dim && ok; i++)
+    for (int j = 0; j < dim && ok; j++) {
+      float* dst = &axis[(size_t)i * dim + j];  // axis(j, i): eigenvector i contiguous
+      ok = ascii ? fscanf(fp, "%f ", dst) == 1 : fread(dst, sizeof(float), 1, fp) == 1;
+    }
+  for (int i = 0; i < dim && ok; i++)
+    ok = ascii ? fscanf(fp, "%f\n", &var[i]) == 1 : fread(&var[i], sizeof(float), 1, fp) == 1;
+  if (!ok) {
+    fclose(fp);
+    return C3H_ERR_FORMAT;
+  }
+  float t;
+  const bool got = ascii ? fscanf(fp, "%f\n", &t) == 1 : fread(&t, sizeof(float), 1, fp) == 1;
+  if (has_mean) *has_mean = got ? 1 : 0;
+  if (got && mean) {
+    mean[0] = t;
+    for (int i = 1; i < dim; i++) {
+      float v = 0;
+      if (ascii ? fscanf(fp, "%f\n", &v) != 1 : fread(&v, sizeof(float), 1, fp) != 1) break;
+      mean[i] = v;
+    }
+  }
+  fclose(fp);
+  return dim;
+}
+
+int c3h_timing(c3h_ctx* ctx, int32_t enable) {
+  if (!ctx) return C3H_ERR_ARG;
+  ctx->timer.enabled = enable != 0;
+  return C3H_OK;
+}
+
+int c3h_kernel_times(c3h_ctx* ctx, float* ms_out, int32_t* counts_out, int32_t reset) {
+  if (!ctx) return C3H_ERR_ARG;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  for (int s = 0; s < C3H_NTIMERS; ++s) {
+    for (auto& e : ctx->timer.pending[s]) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) {
+        ctx->timer.ms[s] += ms;
+        ctx->timer.count[s] += 1;
+      }
+      ctx->timer.pool.push_back(e);
+    }
+    ctx->timer.pending[s].clear();
+  }
+  for (int s = 0; s < C3H_NTIMERS; ++s) {
+    if (ms_out) ms_out[s] = ctx->timer.ms[s];
+    if (counts_out) counts_out[s] = ctx->timer.count[s];
+    if (reset) {
+      ctx->timer.ms[s] = 0;
+      ctx->timer.count[s] = 0;
+    }
+  }
+  return C3H_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,89 @@
+"""CPU checks of the drop-in boundary: the HIP library loads, exports every symbol the
+C header declares, and its host-only entry points agree with the oracle."""
+import ctypes as C
+import re
+
+import numpy as np
+import pytest
+
+import c3hlac
+import pyoracle as po
+from c3hlac import _capi
+from conftest import GOLDEN, ROOT
+
+
+def declared_symbols():
+    names = set()
+    for h in (ROOT / "include").glob("*.h"):
+        txt = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
+        names |= set(re.findall(r"\b(c3h_[a-z0-9_]+)\s*\(", txt))
+    return sorted(names)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _capi.load()
+    names = declared_symbols()
+    assert len(names) >= 25
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    # and the Python binding covers the whole header
+    assert sorted(_capi.exported_symbols()) == names
+
+
+def test_version():
+    assert _capi.load().c3h_version() >= 10000
+
+
+@pytest.mark.parametrize("rel", ["compress_axis", "000/pca_result", "002/pca_result"])
+def test_pca_read_product_equals_oracle(rel):
+    path = GOLDEN / "ref_fixtures" / "models_offline_r" / rel
+    a1, v1, m1 = c3hlac.pca_read(path)
+    a2, v2, m2 = po.pca_read(path)
+    assert np.array_equal(a1, a2) and np.array_equal(v1, v2) and (m1 is None) == (m2 is None)
+
+
+def test_pca_read_errors():
+    lib = _capi.load()
+    buf = np.zeros(16, np.float32)
+    hm = C.c_int32()
+    rc = lib.c3h_pca_read(b"/nonexistent/file", 0, _capi.ptr(buf), _capi.ptr(buf), None, C.byref(hm), 4)
+    assert rc == -6  # C3H_ERR_NOTFOUND
+    rc = lib.c3h_pca_read(str(GOLDEN / "ref_fixtures/models_offline_r/compress_axis").encode(), 0,
+                          _capi.ptr(buf), _capi.ptr(buf), None, C.byref(hm), 4)
+    assert rc == -7  # dim 137 > max_dim
+
+
+def test_remove_overlap_product_equals_oracle():
+    rng = np.random.default_rng(11)
+    for trial in range(20):
+        M, rank = int(rng.integers(2, 6)), int(rng.integers(1, 5))
+        r = tuple(int(v) for v in rng.integers(1, 4, 3))
+        L = po.Lists(M, rank)
+        L.score[:] = np.sort(rng.random(M * rank).reshape(M, rank), 1)[:, ::-1].ravel()
+        for arr in (L.x, L.y, L.z):
+            arr[:] = rng.integers(0, 8, M * rank)
+        L.mode[:] = rng.integers(0, 6, M * rank)
+        recs = np.zeros((M, rank), c3hlac.DET_DTYPE)
+        recs["score"] = L.score.reshape(M, rank)
+        recs["x"], recs["y"], recs["z"] = L.x.reshape(M, rank), L.y.reshape(M, rank), L.z.reshape(M, rank)
+        recs["mode"] = L.mode.reshape(M, rank)
+        out = c3hlac.remove_overlap(recs, r)
+        po.remove_overlap(L, r)
+        assert out["score"].ravel().tolist() == L.score.tolist()
+        assert out["x"].ravel().tolist() == L.x.tolist() and out["mode"].ravel().tolist() == L.mode.tolist()
+
+
+def test_box_size_rounding():
+    # detect_object.cpp:254-266: truncate, +1 when the fraction >= 0.5 or the result is 0
+    assert c3hlac.box_size(0.20, 0.2) == 1
+    assert c3hlac.box_size(0.35, 0.2) == 2
+    assert c3hlac.box_size(0.05, 0.2) == 1
+    assert c3hlac.box_size(0.40, 0.1) == 4
+
+
+def test_read_axis_transform():
+    axis, var, _ = c3hlac.pca_read(GOLDEN / "ref_fixtures/models_offline_r/000/pca_result")
+    q = c3hlac.read_axis(axis, var, 100, 20, multiple_similarity=True)
+    assert q.shape == (20, 100)
+    np.testing.assert_array_equal(q[0], axis[:, 0])
+    np.testing.assert_allclose(q[5], axis[:, 5] * np.sqrt(var[5]) / np.sqrt(var[0]), rtol=1e-6)

@@ -1,0 +1,346 @@
+"""GPU parity tests: the HIP path through the C-ABI against the oracle and the golden
+fixtures.  Integer/index outputs must be bit-exact; features are compared bit-exactly
+with the oracle's exact-integer mode and within 1e-4 relative with its fp32-faithful
+mode; scores within the tolerances stated per test."""
+import numpy as np
+import pytest
+
+import c3hlac
+import np_ref as npr
+import pyoracle as po
+from c3hlac import synth
+from conftest import GOLDEN_CASES, THR, load_golden
+
+pytestmark = pytest.mark.gpu
+
+SCORE_RTOL_F64 = 1e-5   # GPU (fp32, direct box sums) vs the float64 oracle
+SCORE_RTOL_F32 = 1e-4   # vs the reference-order fp32 oracle (summed-volume table error)
+
+
+def _words_xyz(ctx):
+    d = ctx.info.div_b
+    return ctx.grid().reshape(d[2], d[1], d[0])
+
+
+@pytest.mark.parametrize("name", GOLDEN_CASES)
+def test_golden_voxelize(ctx, name):
+    z = load_golden(name)
+    gi = ctx.voxelize(z["pts"], float(z["leaf"]), float(z["z_limit"]))
+    assert list(gi.div_b) == list(z["div_b"]) and list(gi.min_b) == list(z["min_b"])
+    assert gi.n_occ == z["cloud"].shape[0]
+    assert np.array_equal(ctx.grid(), z["grid_words"])
+    assert np.array_equal(ctx.leaf_layout(), z["leaf_layout"])
+    ds = ctx.downsampled()
+    assert np.array_equal(ds[:, 3].view(np.uint32), z["cloud"][:, 3].view(np.uint32))
+    np.testing.assert_allclose(ds[:, :3], z["cloud"][:, :3], rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("name", GOLDEN_CASES)
+@pytest.mark.parametrize("variant", [981, 117])
+def test_golden_extract(ctx, name, variant):
+    z = load_golden(name)
+    ctx.voxelize(z["pts"], float(z["leaf"]), float(z["z_limit"]))
+    sb, hn = ctx.extract(variant, tuple(z["thr"]), int(z["subdiv"]), tuple(z["offset"]))
+    assert tuple(sb) == tuple(z["subdiv_b"])
+    f = ctx.features()
+    assert np.array_equal(f, z["feat%d_exact" % variant])
+    np.testing.assert_allclose(f, z["feat%d_faithful" % variant], rtol=1e-4)
+    assert np.array_equal(ctx.exist(), z["exist"])
+
+
+@pytest.mark.parametrize("name", [n for n in GOLDEN_CASES if n != "kinect_32_whole"])
+def test_golden_search(ctx, name):
+    z = load_golden(name)
+    ctx.voxelize(z["pts"], float(z["leaf"]), float(z["z_limit"]))
+    ctx.extract(981, tuple(z["thr"]), int(z["subdiv"]), tuple(z["offset"]))
+    ctx.search_setup(z["axis_t"], z["var"], z["axis_q"])
+    ctx.set_rank(int(z["rank"]))
+    lists, nm = ctx.search(tuple(z["ranges"]), int(z["thr_exist"]), rotate=True)
+    sc = ctx.scores()
+    ref = z["scores_f64"]
+    assert sc.shape == ref.shape
+    assert np.array_equal(sc < 0, ref < 0)  # identical exist gate
+    ok = ref > 0
+    np.testing.assert_allclose(sc[ok], ref[ok], rtol=SCORE_RTOL_F64)
+    np.testing.assert_allclose(sc[ok], z["scores_f32"][ok], rtol=SCORE_RTOL_F32)
+    # the GPU's rank lists are exactly the reference replay of its own scores
+    _assert_replay_matches(ctx, tuple(z["ranges"]), int(z["rank"]), lists)
+    np.testing.assert_allclose(lists["score"], z["lists_f64"][:, :, 0], rtol=SCORE_RTOL_F64)
+
+
+def _assert_replay_matches(ctx, ranges, rank, lists, prior=None):
+    sc = ctx.scores()
+    M = lists.shape[0]
+    xn, yn, zn = ctx.subdiv
+    ms, off = [], 0
+    for mode in npr.mode_schedule(ranges, True):
+        xr, yr, zr = npr._ranges(mode, ranges)
+        xe, ye, ze = xn - xr + 1, yn - yr + 1, zn - zr + 1
+        if xe <= 0 or ye <= 0 or ze <= 0:
+            continue
+        P = xe * ye * ze
+        ms.append((mode, xe, ye, sc[off:off + M * P].reshape(M, P)))
+        off += M * P
+    nl = npr.replay(ms, ranges, rank, prior)
+    got = [[(float(e["score"]), int(e["x"]), int(e["y"]), int(e["z"]), int(e["mode"])) for e in m] for m in lists]
+    assert got == [[tuple(e) for e in m] for m in nl]
+
+
+@pytest.mark.parametrize("variant", [981, 117])
+@pytest.mark.parametrize("subdiv,offset", [(10, (0, 0, 0)), (7, (2, 1, 3)), (0, (0, 0, 0)), (3, (0, 0, 0)),
+                                           (20, (0, 0, 0)), (25, (1, 0, 2)), (16, (0, 0, 0)), (17, (0, 0, 0)),
+                                           (40, (1, 1, 1))])
+def test_extract_subdivision_cases(ctx, variant, subdiv, offset):
+    """Single-tile, multi-tile (64-bit partials), whole-grid and hist_num==1 paths."""
+    pts = synth.parity_cloud(9000, grid=30, leaf=0.01, seed=7)
+    g, layout, cloud = po.voxelize(pts, 0.01)
+    ctx.voxelize(pts, 0.01)
+    sb, hn = ctx.extract(variant, THR, subdiv, offset)
+    fe, sbo, hno = po.c3hlac(g, layout, cloud, variant, THR, 0.01, subdiv, offset, exact=True)
+    assert tuple(sb) == tuple(sbo) and hn == hno
+    assert np.array_equal(ctx.features(), fe)
+    fa, _, _ = po.c3hlac(g, layout, cloud, 981, THR, 0.01, subdiv, offset, exact=False)
+    assert np.array_equal(ctx.exist(), po.exist(fa))
+
+
+@pytest.mark.parametrize("k", range(13))
+def test_kat_pair_per_offset(ctx, k):
+    rel = npr.REL[k]
+    words = np.zeros((3, 3, 3), np.uint32)
+    c1, c2 = (200, 30, 149), (10, 250, 147)
+    words[1, 1, 1] = (1 << 24) | (c1[0] << 16) | (c1[1] << 8) | c1[2]
+    words[1 + rel[2], 1 + rel[1], 1 + rel[0]] = (1 << 24) | (c2[0] << 16) | (c2[1] << 8) | c2[2]
+    ctx.set_grid(words.reshape(-1), (3, 3, 3))
+    for variant in (981, 117):
+        ctx.extract(variant, THR, 0)
+        fn, ex, _ = npr.c3hlac(words, variant, THR, 0)
+        assert np.array_equal(ctx.features(), fn)
+
+
+@pytest.mark.parametrize("lut_double", [True, False])
+def test_colour_255_lut_flag(ctx, lut_double):
+    words = synth.random_words(12, 0.5, seed=5, colour_max=255)
+    words[words != 0] |= np.uint32(0xFF0000)  # force r = 255
+    ctx.set_grid(words.reshape(-1), (12, 12, 12))
+    for variant in (981, 117):
+        ctx.extract(variant, THR, 4, lut_double=lut_double)
+        fn, ex, _ = npr.c3hlac(words, variant, THR, 4, lut_double=lut_double)
+        assert np.array_equal(ctx.features(), fn)
+
+
+@pytest.mark.parametrize("occ", [0.02, 0.3, 1.0])
+def test_random_grids_vs_numpy(ctx, occ):
+    words = synth.random_words((37, 29, 23), occ, seed=int(occ * 100) + 1, colour_max=255)
+    ctx.set_grid(words.reshape(-1), (37, 29, 23))
+    for variant, S, off in ((981, 10, (0, 0, 0)), (117, 6, (1, 2, 3)), (981, 0, (0, 0, 0))):
+        ctx.extract(variant, (100, 200, 50), S, off)
+        fn, ex, _ = npr.c3hlac(words, variant, (100, 200, 50), S, off)
+        assert np.array_equal(ctx.features(), fn)
+        assert np.array_equal(ctx.exist(), ex)
+
+
+def test_edge_cases(ctx):
+    # empty cloud / all NaN: empty grid; subdiv > 0 -> setVoxelFilter fails -> no features
+    nan = np.full((10, 4), np.nan, np.float32)
+    gi = ctx.voxelize(nan, 0.01)
+    assert gi.n_valid == 0 and gi.n_occ == 0
+    sb, hn = ctx.extract(981, THR, 10)
+    assert hn == 0
+    sb, hn = ctx.extract(981, THR, 0)
+    assert hn == 1 and not ctx.features().any()
+    # single point
+    one = np.array([[0.123, -0.456, 0.789, synth.pack_rgb(10, 200, 30)]], np.float32)
+    gi = ctx.voxelize(one, 0.01)
+    assert gi.n_occ == 1 and list(gi.div_b) == [1, 1, 1]
+    ctx.extract(981, THR, 0)
+    g, layout, cloud = po.voxelize(one, 0.01)
+    fe, _, _ = po.c3hlac(g, layout, cloud, 981, THR, 0.01, 0, exact=True)
+    assert np.array_equal(ctx.features(), fe)
+    # offsets >= grid and negative thresholds: the reference's silent empty output
+    pts = synth.parity_cloud(500, grid=8, leaf=0.01, seed=3)
+    ctx.voxelize(pts, 0.01)
+    assert ctx.extract(981, THR, 4, (8, 0, 0))[1] == 0
+    assert ctx.extract(981, (-1, 0, 0), 4)[1] == 0
+    # z limit drops points
+    gi = ctx.voxelize(pts, 0.01, z_limit=0.04)
+    g, layout, cloud = po.voxelize(pts, 0.01, 0.04)
+    assert gi.n_valid == g.n_valid and np.array_equal(ctx.leaf_layout(), layout)
+
+
+def test_multipoint_voxel_colour_mean(ctx):
+    rng = np.random.default_rng(5)
+    n = 20000
+    cells = rng.integers(0, 6, (n, 3))
+    xyz = ((cells + 0.1 + 0.8 * rng.random((n, 3))) * 0.01).astype(np.float32)
+    col = rng.integers(0, 256, (n, 3))
+    pts = np.concatenate([xyz, synth.pack_rgb(col[:, 0], col[:, 1], col[:, 2])[:, None]], 1).astype(np.float32)
+    ctx.voxelize(pts, 0.01)
+    g, layout, cloud = po.voxelize(pts, 0.01)
+    d = g.div_b
+    assert np.array_equal(ctx.leaf_layout(), layout)
+    words = ctx.grid()
+    occ = layout >= 0
+    exp = (1 << 24) | cloud[layout[occ], 3].view(np.uint32)
+    assert np.array_equal(words[occ], exp) and not words[~occ].any()
+    ds = ctx.downsampled()
+    np.testing.assert_allclose(ds[:, :3], cloud[:, :3], rtol=2e-6)
+
+
+def test_config2_kinect_128(ctx):
+    """Config 2: 1M-pt Kinect-style scene, 128^3, C3-HLAC-981 + 1-model search."""
+    pts = synth.kinect_scene(1_000_000, grid=128, leaf=0.02, seed=synth.BASE_SEED)
+    g, layout, cloud = po.voxelize(pts, 0.02)
+    gi = ctx.voxelize(pts, 0.02)
+    assert list(gi.div_b) == [128, 128, 128] and gi.n_occ == g.n_occ
+    assert np.array_equal(ctx.leaf_layout(), layout)
+    sb, hn = ctx.extract(981, THR, 10)
+    fe, sbo, _ = po.c3hlac(g, layout, cloud, 981, THR, 0.02, 10, exact=True)
+    ff, _, _ = po.c3hlac(g, layout, cloud, 981, THR, 0.02, 10, exact=False)
+    f = ctx.features()
+    assert np.array_equal(f, fe)
+    np.testing.assert_allclose(f, ff, rtol=1e-4)
+    ex = ctx.exist()
+    assert np.array_equal(ex, po.exist(ff))
+    axis_t, var, axis_q = synth.random_bases(981, 100, 1, 20, seed=1)
+    ctx.search_setup(axis_t, var, axis_q)
+    ctx.set_rank(1)
+    ctx.clean_max()
+    lists, nm = ctx.search((2, 2, 2), 100)
+    Ld, _, scd = po.search(sb, ff, ex, synth.whiten(axis_t, var), axis_q, (2, 2, 2), 1, 100, dbl=True,
+                           want_scores=True)
+    L32, _, sc32 = po.search(sb, ff, ex, synth.whiten(axis_t, var), axis_q, (2, 2, 2), 1, 100, dbl=False,
+                             want_scores=True)
+    sc = ctx.scores()
+    assert np.array_equal(sc < 0, scd < 0)
+    ok = scd > 0
+    np.testing.assert_allclose(sc[ok], scd[ok], rtol=SCORE_RTOL_F64)
+    np.testing.assert_allclose(sc[ok], sc32[ok], rtol=SCORE_RTOL_F32)
+    best = Ld.records()[0][0]
+    assert (int(lists[0, 0]["x"]), int(lists[0, 0]["y"]), int(lists[0, 0]["z"])) == best[1:4]
+    _assert_replay_matches(ctx, (2, 2, 2), 1, lists)
+
+
+def test_config3_kinect_256_ri117_multimodel(ctx):
+    """Config 3: 256^3, RI-117, compress 117->100, 10 models x r=20, v2-style rank = M."""
+    pts = synth.kinect_scene(1_000_000, grid=256, leaf=0.01, seed=synth.BASE_SEED + 1)
+    g, layout, cloud = po.voxelize(pts, 0.01)
+    gi = ctx.voxelize(pts, 0.01)
+    assert list(gi.div_b) == [256, 256, 256]
+    sb, hn = ctx.extract(117, THR, 10)
+    assert sb == (26, 26, 26)
+    fe, _, _ = po.c3hlac(g, layout, cloud, 117, THR, 0.01, 10, exact=True)
+    f = ctx.features()
+    assert np.array_equal(f, fe)
+    f981, _, _ = po.c3hlac(g, layout, cloud, 981, THR, 0.01, 10, exact=False)
+    ex = po.exist(f981)
+    assert np.array_equal(ctx.exist(), ex)
+    M = 10
+    axis_t, var, axis_q = synth.random_bases(117, 100, M, 20, seed=2)
+    ctx.search_setup(axis_t, var, axis_q)
+    ctx.set_rank(M)
+    ctx.clean_max()
+    lists, nm = ctx.search((2, 2, 2), 100)
+    Ld, _, scd = po.search(sb, f, ex, synth.whiten(axis_t, var), axis_q, (2, 2, 2), M, 100, dbl=True,
+                           want_scores=True)
+    sc = ctx.scores()
+    assert np.array_equal(sc < 0, scd < 0)
+    ok = scd > 0
+    np.testing.assert_allclose(sc[ok], scd[ok], rtol=SCORE_RTOL_F64)
+    _assert_replay_matches(ctx, (2, 2, 2), M, lists)
+    # same detections as the float64 oracle (top entry of every model)
+    for m in range(M):
+        assert (int(lists[m, 0]["x"]), int(lists[m, 0]["y"]), int(lists[m, 0]["z"])) == Ld.records()[m][0][1:4]
+
+
+@pytest.mark.parametrize("ranges", [(1, 2, 1), (1, 2, 3), (2, 1, 1), (3, 3, 1)])
+def test_rotation_modes_and_rank(ctx, ranges):
+    pts = synth.kinect_scene(300_000, grid=96, leaf=0.02, seed=77)
+    ctx.voxelize(pts, 0.02)
+    sb, hn = ctx.extract(981, THR, 8)
+    f = ctx.features()
+    ex = ctx.exist()
+    axis_t, var, axis_q = synth.random_bases(981, 40, 3, 8, seed=9)
+    ctx.search_setup(axis_t, var, axis_q)
+    ctx.set_rank(4)
+    lists, nm = ctx.search(ranges, 50)
+    assert nm == len(npr.mode_schedule(ranges, True))
+    _assert_replay_matches(ctx, ranges, 4, lists)
+    Ld, _, scd = po.search(sb, f, ex, synth.whiten(axis_t, var), axis_q, ranges, 4, 50, dbl=True, want_scores=True)
+    sc = ctx.scores()
+    ok = scd > 0
+    np.testing.assert_allclose(sc[ok], scd[ok], rtol=SCORE_RTOL_F64)
+    # a second search continues from the current lists (no cleanMax): same semantics
+    prior = [[(float(e["score"]), int(e["x"]), int(e["y"]), int(e["z"]), int(e["mode"])) for e in m] for m in lists]
+    lists2, _ = ctx.search(ranges, 50)
+    _assert_replay_matches(ctx, ranges, 4, lists2, prior=[[list(e) for e in m] for m in prior])
+    # removeOverlap on the lists (SearchObjMulti) equals the host function
+    ctx.clean_max()
+    l3, _ = ctx.search(ranges, 50, remove_overlap=True)
+    ctx.clean_max()
+    l4, _ = ctx.search(ranges, 50, remove_overlap=False)
+    assert np.array_equal(c3hlac.remove_overlap(l4, ranges), l3)
+
+
+def test_search_without_rotation_and_feature_max(ctx):
+    pts = synth.kinect_scene(200_000, grid=64, leaf=0.02, seed=5)
+    ctx.voxelize(pts, 0.02)
+    sb, hn = ctx.extract(117, THR, 5)
+    f = ctx.features()
+    ex = ctx.exist()
+    fmax = f.max(0) * np.float32(0.75)
+    fmax[3] = 0
+    axis_t, var, axis_q = synth.random_bases(117, 30, 2, 6, seed=3)
+    ctx.search_setup(axis_t, var, axis_q, feature_max=fmax)
+    ctx.set_rank(2)
+    lists, nm = ctx.search((1, 2, 3), 30, rotate=False)
+    assert nm == 1
+    Ld, _, scd = po.search(sb, f, ex, synth.whiten(axis_t, var), axis_q, (1, 2, 3), 2, 30, rotate=False,
+                           dbl=True, fmax=fmax, want_scores=True)
+    sc = ctx.scores()
+    ok = scd > 0
+    np.testing.assert_allclose(sc[ok], scd[ok], rtol=SCORE_RTOL_F64)
+    _assert_replay_matches(ctx, (1, 2, 3), 2, lists)
+
+
+def test_no_compression_path(ctx):
+    pts = synth.kinect_scene(100_000, grid=48, leaf=0.02, seed=6)
+    ctx.voxelize(pts, 0.02)
+    sb, hn = ctx.extract(117, THR, 6)
+    f = ctx.features()
+    ex = ctx.exist()
+    rng = np.random.default_rng(0)
+    axis_q = rng.standard_normal((2, 5, 117)).astype(np.float32)
+    ctx.search_setup(None, None, axis_q)
+    ctx.set_rank(1)
+    lists, nm = ctx.search((2, 2, 2), 20)
+    Ld, _, scd = po.search(sb, f, ex, None, axis_q, (2, 2, 2), 1, 20, dbl=True, want_scores=True)
+    sc = ctx.scores()
+    ok = scd > 0
+    np.testing.assert_allclose(sc[ok], scd[ok], rtol=SCORE_RTOL_F64)
+
+
+def test_dense_grid_512_style_small(ctx):
+    """Config-5 style dense occupancy (100 %) on a small grid: exact vs numpy."""
+    words = synth.dense_words(40, seed=8)
+    ctx.set_grid(words.reshape(-1), (40, 40, 40))
+    for variant in (981, 117):
+        ctx.extract(variant, THR, 10)
+        fn, ex, _ = npr.c3hlac(words, variant, THR, 10)
+        assert np.array_equal(ctx.features(), fn)
+        assert np.array_equal(ctx.exist(), ex)
+
+
+def test_dense_256_bin_block_linearity(ctx):
+    """Size-independent property at full size: the binary-count bins (normalised by 1)
+    are exact integers, and summing them over subdivisions must give the whole-grid
+    (subdivision_size 0) histogram; checked on a dense 256^3 grid the oracle would take
+    minutes on."""
+    words = synth.dense_words(256, seed=12)
+    ctx.set_grid(words.reshape(-1), (256, 256, 256))
+    ctx.extract(981, THR, 16)
+    parts = ctx.features()[:, 495:].astype(np.float64).sum(0)
+    ctx.extract(981, THR, 0)
+    whole = ctx.features()[0, 495:].astype(np.float64)
+    # per-subdivision counts are exact in float32; the whole-grid ones are float(exact int)
+    np.testing.assert_array_equal(parts.astype(np.float32), whole.astype(np.float32))
+    assert whole[:6].sum() == 3 * 256 ** 3  # each voxel adds beta_c + (1-beta_c) per colour
