@@ -94,6 +94,9 @@ int c3h_get_grid(c3h_ctx* ctx, uint32_t* out, int on_device);
 int c3h_set_grid(c3h_ctx* ctx, const uint32_t* words, const int32_t div_b[3],
                  const int32_t min_b[3], float leaf, int on_device);
 int c3h_get_grid_info(c3h_ctx* ctx, c3h_grid_info* info);
+/* device pointer of the packed grid in use (for zero-copy c3h_set_grid into another
+ * context on the same device); valid until the next voxelize / set_grid. */
+int c3h_grid_device_ptr(c3h_ctx* ctx, const uint32_t** out);
 
 /* C3HLAC{981,117}Estimation::setVoxelFilter + compute (c3_hlac/src/c3_hlac.cpp:204-416),
  * as called by extractC3HLACSignature981/117 (c3_hlac_tools.hpp:134-202).  Writes the
@@ -134,6 +137,13 @@ int c3h_search(c3h_ctx* ctx, const int32_t range[3], int32_t exist_threshold,
  * lists into the device buffer d_out after the search (no removeOverlap). */
 int c3h_search_async(c3h_ctx* ctx, const int32_t range[3], int32_t exist_threshold,
                      int32_t rotate, c3h_det* d_out);
+/* Batch driver for device-resident frames (configs 3-5): for each frame i, bind
+ * d_grids[i] (same dims/min_b/leaf), cleanMax, extract with *p, and search (async) into
+ * d_out + i * M * rank.  One host call, no host synchronisation. */
+int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes,
+                   const int32_t div_b[3], const int32_t min_b[3], float leaf,
+                   const c3h_extract_params* p, const int32_t range[3], int32_t exist_threshold,
+                   int32_t rotate, c3h_det* d_out);
 /* compressed features (setData before the summed-volume table): hist_num x D floats */
 int c3h_get_compressed(c3h_ctx* ctx, float* out, int on_device);
 /* per-position similarity of the last search, modes x M x P doubles (-1 = gated out).

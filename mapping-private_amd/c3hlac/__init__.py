@@ -172,6 +172,22 @@ class Context:
         return self._chk(self.lib.c3h_search_async(self.h, i32x3(ranges), int(exist_threshold),
                                                    int(bool(rotate)), ptr(d_out)), "search_async")
 
+    def run_frames(self, grid_ptrs, div_b, min_b, leaf, variant, thr, subdiv, ranges, exist_threshold,
+                   rotate=True, d_out=None, offset=(0, 0, 0), lut_double=True):
+        """c3h_run_frames: grid_ptrs = uint64 numpy array of device pointers."""
+        gp = np.ascontiguousarray(grid_ptrs, dtype=np.uint64)
+        p = _capi.ExtractParams()
+        p.variant = int(variant)
+        p.thr = (C.c_int32 * 3)(*[int(t) for t in thr])
+        p.subdiv = int(subdiv)
+        p.offset = (C.c_int32 * 3)(*[int(o) for o in offset])
+        p.lut_double = int(bool(lut_double))
+        nm = self._chk(self.lib.c3h_run_frames(self.h, ptr(gp), gp.size, i32x3(div_b), i32x3(min_b), float(leaf),
+                                               C.byref(p), i32x3(ranges), int(exist_threshold),
+                                               int(bool(rotate)), ptr(d_out)), "run_frames")
+        self.variant = int(variant)
+        return nm
+
     def compressed(self):
         out = np.zeros((self.hist_num, self.D), np.float32)
         self._chk(self.lib.c3h_get_compressed(self.h, ptr(out), 0), "get_compressed")

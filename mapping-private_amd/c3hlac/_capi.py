@@ -56,6 +56,7 @@ _SIGS = {
     "c3h_get_grid": (C.c_int, [_P, _P, C.c_int]),
     "c3h_set_grid": (C.c_int, [_P, _P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_float, C.c_int]),
     "c3h_get_grid_info": (C.c_int, [_P, C.POINTER(GridInfo)]),
+    "c3h_grid_device_ptr": (C.c_int, [_P, C.POINTER(_P)]),
     "c3h_extract": (C.c_int, [_P, C.POINTER(ExtractParams), C.POINTER(C.c_int32), C.POINTER(C.c_int64)]),
     "c3h_get_features": (C.c_int, [_P, _P, C.c_int]),
     "c3h_get_exist": (C.c_int, [_P, _P, C.c_int]),
@@ -64,6 +65,8 @@ _SIGS = {
     "c3h_clean_max": (C.c_int, [_P]),
     "c3h_search": (C.c_int, [_P, C.POINTER(C.c_int32), C.c_int32, C.c_int32, C.c_int32, _P]),
     "c3h_search_async": (C.c_int, [_P, C.POINTER(C.c_int32), C.c_int32, C.c_int32, _P]),
+    "c3h_run_frames": (C.c_int, [_P, _P, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_float,
+                                 C.POINTER(ExtractParams), C.POINTER(C.c_int32), C.c_int32, C.c_int32, _P]),
     "c3h_get_compressed": (C.c_int, [_P, _P, C.c_int]),
     "c3h_get_scores": (C.c_int, [_P, _P, C.POINTER(C.c_int64), C.c_int]),
     "c3h_remove_overlap": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(C.c_int32), _P]),

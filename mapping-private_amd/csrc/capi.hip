@@ -520,6 +520,13 @@ int c3h_get_grid_info(c3h_ctx* ctx, c3h_grid_info* info) {
   return C3H_OK;
 }
 
+int c3h_grid_device_ptr(c3h_ctx* ctx, const uint32_t** out) {
+  if (!ctx || !out) return C3H_ERR_ARG;
+  if (!ctx->have_grid) return fail(ctx, C3H_ERR_STATE, "no grid");
+  *out = ctx->grid_ptr;
+  return C3H_OK;
+}
+
 static int64_t grid_voxels(const c3h_ctx* ctx) {
   return (int64_t)ctx->info.div_b[0] * ctx->info.div_b[1] * ctx->info.div_b[2];
 }
@@ -684,17 +691,20 @@ int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3]
       stride = std::max(stride, (int)s[a].start.size());
       for (int l : s[a].len) lmax[a] = std::max(lmax[a], l);
     }
-    ctx->h_segs.assign((size_t)3 * stride * 3, 0);
+    std::vector<int32_t> segs((size_t)3 * stride * 3, 0);
     for (int a = 0; a < 3; ++a)
       for (size_t i = 0; i < s[a].start.size(); ++i) {
-        int32_t* e = &ctx->h_segs[((size_t)a * stride + i) * 3];
+        int32_t* e = &segs[((size_t)a * stride + i) * 3];
         e[0] = s[a].start[i];
         e[1] = s[a].len[i];
         e[2] = s[a].sub[i];
       }
-    ENSURE(ctx->segs, ctx->h_segs.size());
-    HIPCHK(hipMemcpyAsync(ctx->segs.p, ctx->h_segs.data(), ctx->h_segs.size() * 4,
-                          hipMemcpyHostToDevice, ctx->stream));
+    if (segs != ctx->h_segs || !ctx->segs.p) {  // frames of one geometry reuse the table
+      ctx->h_segs.swap(segs);
+      ENSURE(ctx->segs, ctx->h_segs.size());
+      HIPCHK(hipMemcpyAsync(ctx->segs.p, ctx->h_segs.data(), ctx->h_segs.size() * 4,
+                            hipMemcpyHostToDevice, ctx->stream));
+    }
     if (atomic) {
       ENSURE(ctx->acc64, (size_t)hist_num * 981);
       HIPCHK(hipMemsetAsync(ctx->acc64.p, 0, (size_t)hist_num * 981 * 8, ctx->stream));
@@ -864,6 +874,27 @@ int c3h_search_async(c3h_ctx* ctx, const int32_t range[3], int32_t exist_thresho
   return nm;
 }
 
+int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes,
+                   const int32_t div_b[3], const int32_t min_b[3], float leaf,
+                   const c3h_extract_params* p, const int32_t range[3], int32_t exist_threshold,
+                   int32_t rotate, c3h_det* d_out) {
+  if (!ctx || !d_grids || nframes < 0 || !div_b || !min_b || !p || !range || !d_out)
+    return C3H_ERR_ARG;
+  int nm = 0;
+  for (int32_t i = 0; i < nframes; ++i) {
+    int rc = c3h_set_grid(ctx, d_grids[i], div_b, min_b, leaf, 1);
+    if (rc != C3H_OK) return rc;
+    rc = c3h_clean_max(ctx);
+    if (rc != C3H_OK) return rc;
+    rc = c3h_extract(ctx, p, nullptr, nullptr);
+    if (rc != C3H_OK) return rc;
+    nm = c3h_search_async(ctx, range, exist_threshold, rotate,
+                          d_out + (size_t)i * std::max(ctx->M, 1) * ctx->rank);
+    if (nm < 0) return nm;
+  }
+  return nm;
+}
+
 int c3h_get_compressed(c3h_ctx* ctx, float* out, int on_device) {
   if (!ctx || !out) return C3H_ERR_ARG;
   if (!ctx->g_valid) return fail(ctx, C3H_ERR_STATE, "no compressed features (run a search)");
@@ -947,6 +978,15 @@ int c3h_pca_read(const char* path, int32_t ascii, float* axis, float* var, float
 int c3h_timing(c3h_ctx* ctx, int32_t enable) {
   if (!ctx) return C3H_ERR_ARG;
   ctx->timer.enabled = enable != 0;
+  if (enable) {  // pre-create event pairs so no hipEventCreate lands in a timed region
+    HIPCHK(hipSetDevice(ctx->device));
+    while (ctx->timer.pool.size() < 2048) {
+      hipEvent_t a, b;
+      HIPCHK(hipEventCreate(&a));
+      HIPCHK(hipEventCreate(&b));
+      ctx->timer.pool.push_back({a, b});
+    }
+  }
   return C3H_OK;
 }
 
