@@ -153,14 +153,23 @@ int c3h_get_scores(c3h_ctx* ctx, double* out, int64_t* n_out, int on_device);
 int c3h_remove_overlap(int32_t M, int32_t rank, const int32_t range[3], c3h_det* lists);
 
 /* PCA::read (color_voxel_recognition/src/pca.cpp:119-185): axis column-major dim x dim
- * (eigenvector i contiguous), variances, optional mean.  Returns dim or an error. */
+ * (eigenvector i contiguous), variances, optional mean.  Returns dim or an error.
+ * axis = var = NULL queries the dimension (header only; max_dim ignored). */
 int c3h_pca_read(const char* path, int32_t ascii, float* axis, float* var, float* mean,
                  int32_t* has_mean, int32_t max_dim);
 
 /* per-kernel device time (ms) accumulated since the last reset with HIP events on the
  * context stream; slots: 0 voxelize, 1 C3-HLAC, 2 compress, 3 score, 4 rank replay.
- * counts_out receives the number of launches per slot.  Enabling adds event records. */
+ * counts_out receives the number of launches per slot.  Enabling adds event records.
+ * enable: 0 = off, 1 = every slot, otherwise a mask of C3H_TIMING_* bits (the slots
+ * bracketed by events; fewer events = less perturbation of back-to-back launches). */
 #define C3H_NTIMERS 5
+#define C3H_TIMING_VOXELIZE 0x2
+#define C3H_TIMING_C3HLAC 0x4
+#define C3H_TIMING_COMPRESS 0x8
+#define C3H_TIMING_SCORE 0x10
+#define C3H_TIMING_REPLAY 0x20
+#define C3H_TIMING_ALL 0x3e
 int c3h_timing(c3h_ctx* ctx, int32_t enable);
 int c3h_kernel_times(c3h_ctx* ctx, float* ms_out, int32_t* counts_out, int32_t reset);
 

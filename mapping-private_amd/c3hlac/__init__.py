@@ -203,7 +203,9 @@ class Context:
 
     # --- timing -----------------------------------------------------------------------
     def timing(self, enable=True):
-        self._chk(self.lib.c3h_timing(self.h, int(bool(enable))), "timing")
+        """True/False: all slots / off; an int: C3H_TIMING_* mask (e.g. timing_mask("c3hlac"))."""
+        v = int(enable) if not isinstance(enable, bool) else int(enable)
+        self._chk(self.lib.c3h_timing(self.h, v), "timing")
 
     def kernel_times(self, reset=True):
         ms = np.zeros(_capi.NTIMERS, np.float32)
@@ -230,6 +232,11 @@ def pca_read(path, ascii=False, max_dim=4096):
                                           ptr(mean), C.byref(hm), max_dim), None, "pca_read")
     axis = buf[: dim * dim].reshape(dim, dim).T.copy()  # column i = eigenvector i
     return axis, var[:dim].copy(), (mean[:dim].copy() if hm.value else None)
+
+
+def timing_mask(*slots):
+    """C3H_TIMING_* mask for the named slots (TIMER_NAMES)."""
+    return sum(2 << TIMER_NAMES.index(n) for n in slots)
 
 
 def read_axis(axis, variance, dim, dim_model, multiple_similarity=True):

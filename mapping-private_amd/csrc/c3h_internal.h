@@ -39,12 +39,17 @@ struct SearchLists {  // SearchObjMulti max_*_multi state, host side
   std::vector<int32_t> x, y, z, mode;
 };
 
+struct ScorePartial {
+  double score;
+  int64_t order;  // (mode index << 40) | position, -1 = none
+};
+
 struct Timer {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[C3H_NTIMERS];
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
   float ms[C3H_NTIMERS] = {0, 0, 0, 0, 0};
   int count[C3H_NTIMERS] = {0, 0, 0, 0, 0};
-  bool enabled = false;
+  uint32_t mask = 0;  // slots being timed
 };
 
 }  // namespace c3h
@@ -80,6 +85,16 @@ struct c3h_ctx {
   c3h::DevBuf<int32_t> exist;
   c3h::DevBuf<unsigned long long> acc64;
   c3h::DevBuf<int32_t> segs;        // per-axis tile segment tables
+  c3h::DevBuf<int16_t> axmap;       // per-axis coordinate -> segment (pass-1 tile lookup)
+  std::vector<int16_t> h_axmap;
+  c3h::DevBuf<uint32_t> tileflags;  // [2] row-list counters | [ntiles] epoch stamps
+  uint32_t tile_epoch = 0;
+  c3h::DevBuf<int32_t> rows;        // non-empty subdivisions of the last extract (direct mode)
+  bool rows_valid = false;          // rows/epoch describe the current features
+  bool g_sparse = false;            // G holds only the listed rows (others stale)
+  c3h::DevBuf<long long> glist;     // sparse search: gate list
+  c3h::DevBuf<uint32_t> gcnt;       // [2] gate-list counters by search epoch parity
+  uint32_t search_epoch = 0;
   std::vector<int32_t> h_segs;      // host copy (kept alive for the async upload)
   c3h::DevBuf<uint32_t> lut;        // 256 packed (sin | cos<<8), two variants
   bool lut_ready = false;
@@ -96,6 +111,10 @@ struct c3h_ctx {
   bool g_valid = false;
   c3h::DevBuf<double> scores;
   int64_t scores_n = 0;
+  c3h::DevBuf<float> qt;            // D x Opad transposed model basis (fast score path)
+  int Opad = 0;
+  c3h::DevBuf<c3h::ScorePartial> partials;
+  bool pending_clean = false;       // cleanMax requested while the device lists are current
   int rank = 1;
   c3h::SearchLists lists;
   std::vector<c3h_det> h_lists;     // host staging of the lists
@@ -142,14 +161,23 @@ struct C3Launch {
   float* feat;
   int32_t* exist;
   unsigned long long* acc64;
+  const int16_t* axmap;   // per-axis centre coordinate -> segment index (-1 = none)
+  uint32_t* flags;        // ntiles epoch stamps
+  int32_t* rows;          // direct mode: non-empty subdivision list output (nullable)
+  uint32_t* rowcnt;       // [2] row-list counters by epoch parity
+  uint32_t epoch;
+  int zero_empty;
   int64_t ntiles;
+  int debug;
 };
 hipError_t launch_c3hlac(const C3Launch& a, hipStream_t s);
 hipError_t launch_c3_finalize(const unsigned long long* acc64, int64_t hist_num, int variant,
                               float* feat, int32_t* exist, hipStream_t s);
 
+// rows/nrows (device): compress only the listed rows (sparse mode), else all H rows
 hipError_t launch_compress(const float* feat, int64_t H, int F, const float* axis_pt, int D,
-                           int Dpad, const float* fmax, int fmax_len, float* G, hipStream_t s);
+                           int Dpad, const float* fmax, int fmax_len, float* G,
+                           const int32_t* rows, const uint32_t* nrows, hipStream_t s);
 
 struct ScoreLaunch {
   const float* G;
@@ -159,11 +187,41 @@ struct ScoreLaunch {
   int xr, yr, zr;
   int xe, ye, ze;
   int thr;
-  const float* axis_q;
-  int M, r;
-  double* scores;  // M x P for this mode
+  const float* axis_q;  // M x r x D (generic path)
+  const float* qt;      // D x Opad transposed basis (fast path)
+  int M, r, Opad;
+  double* scores;       // M x P for this mode
+  ScorePartial* partials;  // per-block per-model best (nullable)
+  int64_t order_base;
 };
 hipError_t launch_score(const ScoreLaunch& a, hipStream_t s);
+bool score_fast_ok(int D, int Opad);
+int64_t score_blocks(const ScoreLaunch& a);
+
+// sparse search (fast path): gate every position of every mode, project the list
+struct ModeGeom {
+  int64_t offset;  // into scores (M x P block)
+  int64_t P;
+  int xe, ye, xr, yr, zr;
+};
+struct SparseSearch {
+  const float* G;
+  const int32_t* exist;
+  int D, xn, yn, zn, thr;
+  const float* qt;
+  int M, r, Opad;
+  double* scores;
+  ModeGeom md[6];
+  int nmodes;
+  int64_t pstart[7];      // prefix of P over modes
+  int64_t order_base[6];  // mode index << 40
+  long long* list;        // gate list entries (mode << 40 | position)
+  uint32_t* cnt;          // [2] list counters by epoch parity
+  uint32_t epoch;
+  ScorePartial* partials;  // per block per model (nullable)
+};
+hipError_t launch_sparse_search(const SparseSearch& a, hipStream_t s);
+int64_t sparse_score_blocks(const SparseSearch& a);
 
 struct ReplayMode {
   int64_t offset;  // into scores (M x P block)
@@ -176,7 +234,11 @@ struct ReplayModes {
   int n;
 };
 hipError_t launch_replay(const double* scores, const ReplayModes& modes, int M, int rank,
-                         int r1, int r2, int r3, c3h_det* lists, hipStream_t s);
+                         int r1, int r2, int r3, int clean, c3h_det* lists, c3h_det* out2,
+                         hipStream_t s);
+hipError_t launch_argmax_replay(const ScorePartial* partials, int64_t nparts, const uint32_t* nlist,
+                                const ReplayModes& modes, int M, int clean, c3h_det* lists,
+                                c3h_det* out2, hipStream_t s);
 
 hipError_t launch_clean_lists(c3h_det* lists, int n, hipStream_t s);
 size_t c3hlac_lds_bytes(int tw_max, int list_max);

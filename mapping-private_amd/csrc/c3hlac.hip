@@ -33,6 +33,8 @@
 //   5. scatter the 981 integer bins to LDS, fold/normalise, coalesced store
 // Tiles are enumerated x-fastest and dealt to XCDs in contiguous ranges so neighbouring
 // tiles (which share halo lines) run on the same L2.
+#include <algorithm>
+
 #include "c3h_internal.h"
 
 namespace c3h {
@@ -98,11 +100,91 @@ __device__ __forceinline__ int32_t exist_from(float s0, float s1) {
   return (int32_t)((double)t + 0.001);
 }
 
+__device__ __forceinline__ int xcd_remap32(int b, int n) {
+  const int q = n >> 3, r = n & 7, xcd = b & 7, loc = b >> 3;
+  return xcd < r ? xcd * (q + 1) + loc : r * (q + 1) + (xcd - r) * q + loc;
+}
+
 __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t n) {
   const int64_t q = n / 8, r = n % 8, xcd = b % 8, loc = b / 8;
   return xcd < r ? xcd * (q + 1) + loc : r * (q + 1) + (xcd - r) * q + loc;
 }
 
+// ---------------------------------------------------------------- pass 1: occupancy
+// Streams the packed grid once (16-B loads, x-rows of 4 voxels when gx % 4 == 0) and
+// flags every tile (subdivision or <=16^3 piece of one) holding an occupied centre
+// voxel; the first flagger appends the tile to the work list.  axmap_[xyz][c] gives the
+// tile segment of centre coordinate c along that axis (-1 when c is no centre, e.g.
+// below the subdivision offset): the reference's float subdivision arithmetic is baked
+// into these host-built tables.
+constexpr int kOccUnroll = 4;  // 16-B loads per thread in flight per iteration
+
+// Flags are epoch stamps: tile t is non-empty in this frame iff flags[t] == epoch, so
+// nothing is reset between frames and the stores need no atomics (same value from every
+// writer).
+__device__ __forceinline__ void flag_tile(int t, uint32_t epoch, uint32_t* flags) {
+  flags[t] = epoch;
+}
+
+template <bool kVec>
+__global__ __launch_bounds__(kBlock) void c3_occupancy_kernel(
+    const uint32_t* __restrict__ grid, int gx, int gy, int gz, const int16_t* __restrict__ axmap,
+    int ns0, int ns1, uint32_t epoch, uint32_t* __restrict__ flags) {
+  const int64_t nvox = (int64_t)gx * gy * gz;
+  const int16_t* mx = axmap;
+  const int16_t* my = axmap + gx;
+  const int16_t* mz = axmap + gx + gy;
+  int last = -1;
+  const int64_t nthr = (int64_t)gridDim.x * kBlock;
+  if (kVec) {
+    const int64_t n4 = nvox >> 2;
+    const uint4* g4 = reinterpret_cast<const uint4*>(grid);
+    for (int64_t i0 = blockIdx.x * (int64_t)kBlock + threadIdx.x; i0 < n4; i0 += kOccUnroll * nthr) {
+      uint4 w[kOccUnroll];
+#pragma unroll
+      for (int j = 0; j < kOccUnroll; ++j) {  // all loads first: bytes in flight, not latency
+        const int64_t i = i0 + j * nthr;
+        w[j] = i < n4 ? g4[i] : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < kOccUnroll; ++j) {
+        if ((w[j].x | w[j].y | w[j].z | w[j].w) == 0) continue;
+        const uint32_t v = (uint32_t)((i0 + j * nthr) << 2);  // nvox < 2^32 (host-checked)
+        const uint32_t row = v / (uint32_t)gx;
+        const int x = (int)(v - row * (uint32_t)gx);
+        const int y = (int)(row % (uint32_t)gy), z = (int)(row / (uint32_t)gy);
+        const int ty = my[y], tz = mz[z];
+        if (ty < 0 || tz < 0) continue;
+        const uint32_t ws[4] = {w[j].x, w[j].y, w[j].z, w[j].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!ws[k]) continue;
+          const int tx = mx[x + k];
+          if (tx < 0) continue;
+          const int t = tx + ns0 * (ty + ns1 * tz);
+          if (t == last) continue;
+          last = t;
+          flag_tile(t, epoch, flags);
+        }
+      }
+    }
+  } else {
+    for (int64_t v = blockIdx.x * (int64_t)kBlock + threadIdx.x; v < nvox; v += nthr) {
+      if (!grid[v]) continue;
+      const uint32_t row = (uint32_t)v / (uint32_t)gx;
+      const int x = (int)((uint32_t)v - row * (uint32_t)gx);
+      const int y = (int)(row % (uint32_t)gy), z = (int)(row / (uint32_t)gy);
+      const int tx = mx[x], ty = my[y], tz = mz[z];
+      if (tx < 0 || ty < 0 || tz < 0) continue;
+      const int t = tx + ns0 * (ty + ns1 * tz);
+      if (t == last) continue;
+      last = t;
+      flag_tile(t, epoch, flags);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- pass 2: features
 struct KArgs {
   const uint32_t* grid;
   int gx, gy, gz;
@@ -116,164 +198,270 @@ struct KArgs {
   float* feat;
   int32_t* exist;
   unsigned long long* acc64;
-  int64_t ntiles;
+  const uint32_t* flags;  // tile epoch stamps of pass 1
+  int32_t* rows;          // direct mode: non-empty subdivisions of this frame (nullable)
+  uint32_t* rowcnt;       // [2] row-list counters by epoch parity
+  uint32_t epoch;
+  int ntiles;
+  int zero_empty;         // direct mode with every subdivision one tile (h == tile): zero
+                          // the rows of unflagged tiles here
+  int debug;  // diagnostics only (C3H_C3_DEBUG): 1 stop after the loads, 2 after compaction,
+             // 3 skip the tile kernel
 };
 
+constexpr int kMaxLoads = 4;  // uint4 tile loads per thread kept in flight together
+constexpr int kSegLds = 64;   // segment tables up to 64 segments per axis live in LDS
+
+// Persistent workgroups.  Phase Z zero-fills the feature rows of the tiles pass 1 left
+// unflagged (direct mode); phase T walks the work list: stage the (lx+2)x(ly+2)x(lz+1)
+// halo in LDS (all loads issued before the first LDS store), compact the occupied
+// centres, build the packed dot4 operands and accumulate exactly (see the header).
 __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint32_t* s_lut = smem;                       // 256
-  uint32_t* s_tile = s_lut + 256;               // tw_max
+  uint32_t* s_tile = s_lut + 256;               // tw_max (16-B aligned)
   uint16_t* s_list = reinterpret_cast<uint16_t*>(s_tile + a.tw_max);  // list_max (u16)
   uint32_t* s_arr = s_tile + a.tw_max + ((a.list_max + 7) / 8) * 4;   // kGroups*kArrStride
-  uint32_t* s_misc = s_arr + kGroups * kArrStride;                  // counter
+  uint32_t* s_misc = s_arr + kGroups * kArrStride;                  // counters [4]
+  uint32_t* s_work = s_misc + 4;                                     // kBlock tile ids
+  int32_t* s_segs = reinterpret_cast<int32_t*>(s_work + kBlock);    // segment table copy
   uint32_t* s_hist = s_arr;                                          // epilogue alias
-
-  const int tid = threadIdx.x;
-  const int64_t tile = xcd_remap(blockIdx.x, a.ntiles);
-  const int ix = (int)(tile % a.ns0);
-  const int iy = (int)((tile / a.ns0) % a.ns1);
-  const int iz = (int)(tile / ((int64_t)a.ns0 * a.ns1));
-  const int32_t* sx = a.segs + 3 * ix;
-  const int32_t* sy = a.segs + 3 * (a.seg_stride + iy);
-  const int32_t* sz = a.segs + 3 * (2 * a.seg_stride + iz);
-  const int x0 = sx[0], lx = sx[1], y0 = sy[0], ly = sy[1], z0 = sz[0], lz = sz[1];
-  const int64_t h = sx[2] + (int64_t)sy[2] * a.sbx + (int64_t)sz[2] * a.sbx * a.sby;
-  const int TX = lx + 2, TY = ly + 2, TXY = TX * TY;
-  const int TW = TXY * (lz + 1);
-
-  s_lut[tid] = a.lut[tid];
-  if (tid == 0) s_misc[0] = 0;
-  // 1. halo tile: x in [x0-1, x0+lx], y in [y0-1, y0+ly], z in [z0-1, z0+lz-1]
-  for (int i = tid; i < TW; i += kBlock) {
-    const int tz = i / TXY, rem = i - tz * TXY, ty = rem / TX, tx = rem - ty * TX;
-    const int gx = x0 - 1 + tx, gy = y0 - 1 + ty, gz = z0 - 1 + tz;
-    uint32_t w = 0;
-    if ((unsigned)gx < (unsigned)a.gx && (unsigned)gy < (unsigned)a.gy && (unsigned)gz < (unsigned)a.gz)
-      w = a.grid[((int64_t)gz * a.gy + gy) * a.gx + gx];
-    s_tile[i] = w;
-  }
-  __syncthreads();
-
-  // 2. compact occupied centres (tile index) into the list
-  const int V = lx * ly * lz, lxy = lx * ly;
-  const int lane = tid & 63;
-  for (int v0 = 0; v0 < V; v0 += kBlock) {
-    const int v = v0 + tid;
-    int ti = 0;
-    bool occ = false;
-    if (v < V) {
-      const int cz = v / lxy, rem = v - cz * lxy, cy = rem / lx, cx = rem - cy * lx;
-      ti = (cx + 1) + (cy + 1) * TX + (cz + 1) * TXY;
-      occ = s_tile[ti] != 0;
-    }
-    const unsigned long long m = __ballot(occ);
-    const int tot = __popcll(m);
-    uint32_t base = 0;
-    if (lane == 0 && tot) base = atomicAdd(&s_misc[0], (uint32_t)tot);
-    base = __shfl(base, 0, 64);
-    if (occ) s_list[base + __popcll(m & ((1ull << lane) - 1))] = (uint16_t)ti;
-  }
-  __syncthreads();
-  const int nlist = (int)s_misc[0];
+  const int tid = threadIdx.x, lane = tid & 63;
   const int F = a.variant;
-
-  if (nlist == 0) {  // empty subdivision: zero feature
-    if (!a.atomic) {
-      for (int i = tid; i < F; i += kBlock) a.feat[h * F + i] = 0.0f;
-      if (tid == 0) a.exist[h] = 0;
-    }
-    return;
-  }
-
-  // per-thread roles
+  if (blockIdx.x == 0 && tid == 0) a.rowcnt[(a.epoch + 1) & 1] = 0;  // next frame's row counter
+  if (a.debug == 3) return;  // diagnostics: occupancy pass only
+  s_lut[tid] = a.lut[tid];
+  const bool segs_lds = a.seg_stride <= kSegLds;
+  const int32_t* segs = segs_lds ? s_segs : a.segs;
+  if (segs_lds)
+    for (int e = tid; e < 9 * a.seg_stride; e += kBlock) s_segs[e] = a.segs[e];
   const int bg = tid / 15, bk = tid - bg * 15;  // build job (group, k), tid < 240
-  int delta = 0;
-  if (tid < 240 && bk < 13) delta = kRel[bk][0] + kRel[bk][1] * TX + kRel[bk][2] * TXY;
   const int at = tid / 90, arem = tid - at * 90, ak = arem / 6, an = arem - ak * 6;
-  uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
 
-  for (int c0 = 0; c0 < nlist; c0 += kChunk) {
-    // 3. build packed operands for list entries [c0, c0+64)
-    if (tid < 240) {
-      uint32_t nb[6] = {0, 0, 0, 0, 0, 0}, bb[6] = {0, 0, 0, 0, 0, 0};
+  // this workgroup owns tiles blockIdx.x + i * gridDim.x (spreads clustered surfaces)
+  const int per = (a.ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  for (int c0 = 0; c0 < per; c0 += kBlock) {
+    const int i = c0 + tid;
+    const int t = (int)blockIdx.x + i * (int)gridDim.x;
+    const bool valid = i < per;
+    const bool flagged = valid && a.flags[t] == a.epoch;
+    if (a.zero_empty) {  // rows of empty tiles (h == t here), one wave-wide store per 64 floats
+      unsigned long long m = __ballot(valid && !flagged);
+      while (m) {
+        const int j = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const int tj = __shfl(t, j, 64);
+        float* row = a.feat + (int64_t)tj * F;
+        for (int q = lane; q < F; q += 64) row[q] = 0.0f;
+        if (lane == 0) a.exist[tj] = 0;
+      }
+    }
+    if (tid == 0) s_misc[1] = 0;
+    __syncthreads();
+    {
+      const unsigned long long m = __ballot(flagged);
+      if (m) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&s_misc[1], (uint32_t)__popcll(m));
+        base = __shfl(base, 0, 64);
+        if (flagged) s_work[base + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)t;
+      }
+    }
+    __syncthreads();
+    const int nw = (int)s_misc[1];
+  for (int wi = 0; wi < nw; ++wi) {
+    const int tile = (int)s_work[wi];
+    const int ix = tile % a.ns0, iy = (tile / a.ns0) % a.ns1, iz = tile / (a.ns0 * a.ns1);
+    const int32_t* sx = segs + 3 * ix;
+    const int32_t* sy = segs + 3 * (a.seg_stride + iy);
+    const int32_t* sz = segs + 3 * (2 * a.seg_stride + iz);
+    const int x0 = sx[0], lx = sx[1], y0 = sy[0], ly = sy[1], z0 = sz[0], lz = sz[1];
+    const int64_t h = sx[2] + (int64_t)sy[2] * a.sbx + (int64_t)sz[2] * a.sbx * a.sby;
+    const bool vec = (a.gx & 3) == 0 && x0 >= 1 && ((x0 + lx + 1 + 3) & ~3) <= a.gx;
+    const int xs = vec ? ((x0 - 1) & ~3) : x0 - 1;
+    const int TX = vec ? (((x0 + lx + 1 - xs) + 3) & ~3) : lx + 2;
+    const int TY = ly + 2, TXY = TX * TY;
+    const int nrows = TY * (lz + 1);
+    if (tid == 0) s_misc[0] = 0;
+
+    // 1. halo tile; every load of a thread is issued before its first LDS store
+    if (vec) {
+      const int q4 = TX >> 2, n = nrows * q4;
+      uint4 w[kMaxLoads];
+      int idx[kMaxLoads];
+      int q = tid / q4, r = tid - q * q4;
+      const int sq = kBlock / q4, sr = kBlock - sq * q4;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int e = c0 + bg * 4 + j;
-        if (e >= nlist) break;
-        const int ti = s_list[e];
-        const uint32_t w = s_tile[ti + delta];
-        if (!w) continue;
-        const int sh = 8 * j;
-        if (bk == 14) {
-#pragma unroll
-          for (int n = 0; n < 6; ++n) {
-            nb[n] |= 1u << sh;
-            bb[n] |= 1u << sh;
-          }
-          continue;
+      for (int j = 0; j < kMaxLoads; ++j) {
+        const int e = tid + j * kBlock;
+        idx[j] = e;
+        w[j] = make_uint4(0, 0, 0, 0);
+        if (e < n) {
+          const int ty = q % TY, tz = q / TY;
+          const int gy = y0 - 1 + ty, gz = z0 - 1 + tz;
+          if ((unsigned)gy < (unsigned)a.gy && (unsigned)gz < (unsigned)a.gz)
+            w[j] = *reinterpret_cast<const uint4*>(a.grid + ((int64_t)gz * a.gy + gy) * a.gx + xs + 4 * r);
         }
-        const uint32_t r = (w >> 16) & 0xffu, g = (w >> 8) & 0xffu, b = w & 0xffu;
-        const uint32_t lr = s_lut[r], lg = s_lut[g], lb = s_lut[b];
-        nb[0] |= (lr & 0xffu) << sh;
-        nb[1] |= (lr >> 8) << sh;
-        nb[2] |= (lg & 0xffu) << sh;
-        nb[3] |= (lg >> 8) << sh;
-        nb[4] |= (lb & 0xffu) << sh;
-        nb[5] |= (lb >> 8) << sh;
-        const uint32_t br = (int)r > a.thr_r, bgn = (int)g > a.thr_g, bbl = (int)b > a.thr_b;
-        bb[0] |= br << sh;
-        bb[1] |= (br ^ 1u) << sh;
-        bb[2] |= bgn << sh;
-        bb[3] |= (bgn ^ 1u) << sh;
-        bb[4] |= bbl << sh;
-        bb[5] |= (bbl ^ 1u) << sh;
+        q += sq;
+        r += sr;
+        if (r >= q4) {
+          r -= q4;
+          ++q;
+        }
       }
-      uint32_t* dst = s_arr + bg * kArrStride + bk * 6;
 #pragma unroll
-      for (int n = 0; n < 6; ++n) {
-        dst[n] = nb[n];
-        dst[90 + n] = bb[n];
+      for (int j = 0; j < kMaxLoads; ++j)
+        if (idx[j] < n) *reinterpret_cast<uint4*>(&s_tile[4 * idx[j]]) = w[j];
+      for (int e = tid + kMaxLoads * kBlock; e < n; e += kBlock) {  // larger tiles
+        const int qq = e / q4, rr = e - qq * q4;
+        const int gy = y0 - 1 + qq % TY, gz = z0 - 1 + qq / TY;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if ((unsigned)gy < (unsigned)a.gy && (unsigned)gz < (unsigned)a.gz)
+          v = *reinterpret_cast<const uint4*>(a.grid + ((int64_t)gz * a.gy + gy) * a.gx + xs + 4 * rr);
+        *reinterpret_cast<uint4*>(&s_tile[4 * e]) = v;
+      }
+    } else {
+      const int n = nrows * TX;
+      for (int e = tid; e < n; e += kBlock) {
+        const int qq = e / TX, rr = e - qq * TX;
+        const int gy = y0 - 1 + qq % TY, gz = z0 - 1 + qq / TY, gxx = xs + rr;
+        s_tile[e] = ((unsigned)gy < (unsigned)a.gy && (unsigned)gz < (unsigned)a.gz &&
+                     (unsigned)gxx < (unsigned)a.gx)
+                        ? a.grid[((int64_t)gz * a.gy + gy) * a.gx + gxx] : 0u;
       }
     }
     __syncthreads();
-    // 4. exact integer accumulation: acc[c] += sum_g dot4(A_c[g], N_{k,n}[g])
-    if (tid < 180) {
-      const int ng = (min(nlist - c0, kChunk) + 3) >> 2;
-      const uint32_t* col = s_arr + at * 90 + ak * 6 + an;
-      const uint32_t* ctr = s_arr + at * 90 + 13 * 6;
-      for (int g = 0; g < ng; ++g) {
-        const uint32_t nv = col[g * kArrStride];
-#pragma unroll
-        for (int c = 0; c < 6; ++c)
-          acc[c] = __builtin_amdgcn_udot4(ctr[g * kArrStride + c], nv, acc[c], false);
-      }
+    if (a.debug == 1) {
+      if (tid == 0 && s_tile[0] == 0xdeadbeefu) a.exist[0] = 1;  // keep the loads live
+      __syncthreads();
+      continue;
     }
-    __syncthreads();
-  }
 
-  // 5. epilogue: integer bins -> LDS, then fold / normalise / store
-  if (tid < 180) {
+    // 2. compact the occupied centres (tile index) into the list
+    {
+      const int V = lx * ly * lz;
+      int cx = tid % lx, rq = tid / lx;  // v = tid + kBlock*i -> (cx, rq = cy + ly*cz)
+      const int sq = kBlock / lx, sr = kBlock - sq * lx;
+      for (int v0 = 0; v0 < V; v0 += kBlock) {
+        const int v = v0 + tid;
+        int ti = 0;
+        bool occ = false;
+        if (v < V) {
+          const int cy = rq % ly, cz = rq / ly;
+          ti = (x0 - xs + cx) + (cy + 1) * TX + (cz + 1) * TXY;
+          occ = s_tile[ti] != 0;
+        }
+        const unsigned long long m = __ballot(occ);
+        if (m) {
+          uint32_t base = 0;
+          if (lane == 0) base = atomicAdd(&s_misc[0], (uint32_t)__popcll(m));
+          base = __shfl(base, 0, 64);
+          if (occ) s_list[base + __popcll(m & ((1ull << lane) - 1))] = (uint16_t)ti;
+        }
+        cx += sr;
+        rq += sq;
+        if (cx >= lx) {
+          cx -= lx;
+          ++rq;
+        }
+      }
+    }
+    __syncthreads();
+    const int nlist = (int)s_misc[0];
+    if (a.debug == 2) {
+      if (tid == 0 && nlist == 0x7fffffff) a.exist[0] = 1;
+      __syncthreads();
+      continue;
+    }
+
+    int delta = 0;
+    if (tid < 240 && bk < 13) delta = kRel[bk][0] + kRel[bk][1] * TX + kRel[bk][2] * TXY;
+    uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
+    for (int c0 = 0; c0 < nlist; c0 += kChunk) {
+      // 3. build packed operands for list entries [c0, c0+64)
+      if (tid < 240) {
+        uint32_t nb[6] = {0, 0, 0, 0, 0, 0}, bb[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int c = 0; c < 6; ++c) {
-      const int bi = bin_of(at, ak, an, c);
-      if (bi >= 0) s_hist[bi] = acc[c];
+        for (int j = 0; j < 4; ++j) {
+          const int e = c0 + bg * 4 + j;
+          if (e >= nlist) break;
+          const uint32_t w = s_tile[s_list[e] + delta];
+          if (!w) continue;
+          const int sh = 8 * j;
+          if (bk == 14) {
+#pragma unroll
+            for (int n = 0; n < 6; ++n) {
+              nb[n] |= 1u << sh;
+              bb[n] |= 1u << sh;
+            }
+            continue;
+          }
+          const uint32_t r = (w >> 16) & 0xffu, g = (w >> 8) & 0xffu, b = w & 0xffu;
+          const uint32_t lr = s_lut[r], lg = s_lut[g], lb = s_lut[b];
+          nb[0] |= (lr & 0xffu) << sh;
+          nb[1] |= (lr >> 8) << sh;
+          nb[2] |= (lg & 0xffu) << sh;
+          nb[3] |= (lg >> 8) << sh;
+          nb[4] |= (lb & 0xffu) << sh;
+          nb[5] |= (lb >> 8) << sh;
+          const uint32_t br = (int)r > a.thr_r, bgn = (int)g > a.thr_g, bbl = (int)b > a.thr_b;
+          bb[0] |= br << sh;
+          bb[1] |= (br ^ 1u) << sh;
+          bb[2] |= bgn << sh;
+          bb[3] |= (bgn ^ 1u) << sh;
+          bb[4] |= bbl << sh;
+          bb[5] |= (bbl ^ 1u) << sh;
+        }
+        uint32_t* dst = s_arr + bg * kArrStride + bk * 6;
+#pragma unroll
+        for (int n = 0; n < 6; ++n) {
+          dst[n] = nb[n];
+          dst[90 + n] = bb[n];
+        }
+      }
+      __syncthreads();
+      // 4. exact integer accumulation: acc[c] += sum_g dot4(A_c[g], N_{k,n}[g])
+      if (tid < 180) {
+        const int ng = (min(nlist - c0, kChunk) + 3) >> 2;
+        const uint32_t* col = s_arr + at * 90 + ak * 6 + an;
+        const uint32_t* ctr = s_arr + at * 90 + 13 * 6;
+        for (int g = 0; g < ng; ++g) {
+          const uint32_t nv = col[g * kArrStride];
+#pragma unroll
+          for (int c = 0; c < 6; ++c)
+            acc[c] = __builtin_amdgcn_udot4(ctr[g * kArrStride + c], nv, acc[c], false);
+        }
+      }
+      __syncthreads();
     }
-  }
-  __syncthreads();
-  if (a.atomic) {
-    for (int i = tid; i < 981; i += kBlock) {
-      const uint32_t v = s_hist[i];
-      if (v) atomicAdd(&a.acc64[h * 981 + i], (unsigned long long)v);
+    // 5. epilogue: integer bins -> LDS, then fold / normalise / store
+    if (tid < 180) {
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const int bi = bin_of(at, ak, an, c);
+        if (bi >= 0) s_hist[bi] = acc[c];
+      }
     }
-    return;
+    __syncthreads();
+    if (a.atomic) {
+      for (int i = tid; i < 981; i += kBlock) {
+        const uint32_t v = s_hist[i];
+        if (v) atomicAdd(&a.acc64[h * 981 + i], (unsigned long long)v);
+      }
+    } else {
+      float* out = a.feat + h * F;
+      if (F == 981) {
+        for (int i = tid; i < 981; i += kBlock) out[i] = (float)s_hist[i] * norm981(i);
+      } else {
+        for (int i = tid; i < 117; i += kBlock) out[i] = (float)fold117(s_hist, i) * norm117(i);
+      }
+      if (tid == 0) a.exist[h] = exist_from((float)s_hist[0], (float)s_hist[1]);
+    }
+    if (a.rows && tid == 0) a.rows[atomicAdd(&a.rowcnt[a.epoch & 1], 1u)] = (int32_t)h;
+    __syncthreads();  // LDS is reused by the next tile
   }
-  float* out = a.feat + h * F;
-  if (F == 981) {
-    for (int i = tid; i < 981; i += kBlock) out[i] = (float)s_hist[i] * norm981(i);
-  } else {
-    for (int i = tid; i < 117; i += kBlock) out[i] = (float)fold117(s_hist, i) * norm117(i);
+    __syncthreads();  // s_work / s_misc[1] are rewritten by the next chunk
   }
-  if (tid == 0) a.exist[h] = exist_from((float)s_hist[0], (float)s_hist[1]);
 }
 
 // multi-tile subdivisions: 64-bit exact partial sums -> features
@@ -294,10 +482,23 @@ __global__ __launch_bounds__(kBlock) void c3_finalize_kernel(const unsigned long
 }  // namespace
 
 size_t c3hlac_lds_bytes(int tw_max, int list_max) {
-  return sizeof(uint32_t) * (256 + tw_max + ((list_max + 7) / 8) * 4 + kGroups * kArrStride + 4);
+  return sizeof(uint32_t) * (256 + tw_max + ((list_max + 7) / 8) * 4 + kGroups * kArrStride + 4 + kBlock +
+                             9 * kSegLds);
 }
 
 hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
+  // pass 1: occupancy flags + work list (flags/work zeroed by the caller)
+  const int64_t nvox = (int64_t)l.gx * l.gy * l.gz;
+  const bool vec = (l.gx & 3) == 0;
+  const int64_t items = vec ? nvox / 4 : nvox;
+  int g1 = (int)std::min<int64_t>((items + kBlock * kOccUnroll - 1) / (kBlock * kOccUnroll), 256 * 32);
+  if (g1 < 1) g1 = 1;
+  if (vec)
+    c3_occupancy_kernel<true><<<g1, kBlock, 0, s>>>(l.grid, l.gx, l.gy, l.gz, l.axmap, l.nseg[0],
+                                                    l.nseg[1], l.epoch, l.flags);
+  else
+    c3_occupancy_kernel<false><<<g1, kBlock, 0, s>>>(l.grid, l.gx, l.gy, l.gz, l.axmap, l.nseg[0],
+                                                     l.nseg[1], l.epoch, l.flags);
   KArgs a;
   a.grid = l.grid;
   a.gx = l.gx;
@@ -310,7 +511,8 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
   a.seg_stride = l.seg_stride;
   a.sbx = l.sbx;
   a.sby = l.sby;
-  a.tw_max = (l.lmax[0] + 2) * (l.lmax[1] + 2) * (l.lmax[2] + 1);
+  const int tx_max = ((l.lmax[0] + 2) + 3 + 3) & ~3;
+  a.tw_max = tx_max * (l.lmax[1] + 2) * (l.lmax[2] + 1);
   a.list_max = l.lmax[0] * l.lmax[1] * l.lmax[2];
   a.thr_r = l.thr[0];
   a.thr_g = l.thr[1];
@@ -321,9 +523,18 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
   a.feat = l.feat;
   a.exist = l.exist;
   a.acc64 = l.acc64;
-  a.ntiles = l.ntiles;
+  a.flags = l.flags;
+  a.rows = l.rows;
+  a.rowcnt = l.rowcnt;
+  a.epoch = l.epoch;
+  a.zero_empty = l.zero_empty;
+  a.ntiles = (int)l.ntiles;
+  a.debug = l.debug;
   const size_t lds = c3hlac_lds_bytes(a.tw_max, a.list_max);
-  c3hlac_tile_kernel<<<(unsigned)l.ntiles, kBlock, lds, s>>>(a);
+  // persistent grid: enough resident workgroups to cover the chip several times over
+  const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / lds)));
+  const int grid = (int)std::min<int64_t>(l.ntiles, 256 * per_cu);
+  c3hlac_tile_kernel<<<std::max(grid, 1), kBlock, lds, s>>>(a);
   return hipGetLastError();
 }
 

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "c3h_internal.h"
@@ -68,7 +69,7 @@ struct Timed {
   int slot;
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
   Timed(c3h_ctx* c, int s) : ctx(c), slot(s) {
-    if (!ctx->timer.enabled) return;
+    if (!(ctx->timer.mask >> (s + 1) & 1)) return;
     if (ctx->timer.pool.empty()) {
       hipEvent_t a, b;
       if (hipEventCreate(&a) != hipSuccess) return;
@@ -253,15 +254,29 @@ void init_lists(c3h_ctx* ctx) {  // setRank: dot = 0, modes S_MODE_1 (never-init
   L.mode.assign(n, C3H_S_MODE_1);
   ctx->lists_host_valid = true;
   ctx->lists_dev_valid = false;
+  ctx->pending_clean = false;
 }
 
 int sync_host_lists(c3h_ctx* ctx) {
-  if (!ctx->lists_host_valid) return download_lists(ctx);
+  if (!ctx->lists_host_valid) {
+    int rc = download_lists(ctx);
+    if (rc != C3H_OK) return rc;
+  }
+  if (ctx->pending_clean) {  // a cleanMax recorded while the device copy was current
+    auto& L = ctx->lists;
+    std::fill(L.score.begin(), L.score.end(), 0.0);
+    std::fill(L.x.begin(), L.x.end(), 0);
+    std::fill(L.y.begin(), L.y.end(), 0);
+    std::fill(L.z.begin(), L.z.end(), 0);
+    ctx->pending_clean = false;
+    ctx->lists_dev_valid = false;
+  }
   return C3H_OK;
 }
 
 // setData + searchPart for every scheduled mode; leaves the lists valid on the device
-int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate) {
+int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate,
+               c3h_det* d_out) {
   if (!ctx->have_feat) return fail(ctx, C3H_ERR_STATE, "c3h_search: no features (call c3h_extract)");
   if (!ctx->have_setup) return fail(ctx, C3H_ERR_STATE, "c3h_search: no axes (call c3h_search_setup)");
   if (!range || range[0] < 1 || range[1] < 1 || range[2] < 1)
@@ -275,9 +290,16 @@ int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate
   if (!ctx->g_valid) {
     ENSURE(ctx->G, (size_t)H * ctx->D);
     Timed t(ctx, 2);
+    // sparse: only the non-empty rows of the extract's list (the rest stay stale and are
+    // gated on exist by every consumer)
+    const bool sparse = ctx->rows_valid && c3h::score_fast_ok(ctx->D, ctx->Opad);
     HIPCHK(c3h::launch_compress(ctx->feat.p, H, ctx->F, ctx->axis_pt.p, ctx->D, ctx->Dpad,
-                                ctx->fmax.p, ctx->fmax_len, ctx->G.p, ctx->stream));
+                                ctx->fmax.p, ctx->fmax_len, ctx->G.p,
+                                sparse ? ctx->rows.p : nullptr,
+                                sparse ? ctx->tileflags.p + (ctx->tile_epoch & 1) : nullptr,
+                                ctx->stream));
     ctx->g_valid = true;
+    ctx->g_sparse = sparse;
   }
   int modes[6];
   const int nm = mode_schedule(range[0], range[1], range[2], rotate, modes);
@@ -294,31 +316,85 @@ int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate
   }
   ENSURE(ctx->scores, total);
   ctx->scores_n = total;
-  {
-    Timed t(ctx, 3);
+  // per-mode score launches; rank 1 uses the per-block partials (fast path only)
+  bool all_fast = c3h::score_fast_ok(ctx->D, ctx->Opad);
+  int64_t nparts = 0;
+  std::vector<c3h::ScoreLaunch> launches;
+  for (int i = 0; i < rm.n; ++i) {
+    int xr, yr, zr;
+    get_range(rm.m[i].mode, range[0], range[1], range[2], &xr, &yr, &zr);
+    c3h::ScoreLaunch a{};
+    a.G = ctx->G.p;
+    a.exist = ctx->exist.p;
+    a.D = ctx->D;
+    a.xn = xn;
+    a.yn = yn;
+    a.zn = zn;
+    a.xr = xr;
+    a.yr = yr;
+    a.zr = zr;
+    a.xe = rm.m[i].xe;
+    a.ye = rm.m[i].ye;
+    a.ze = (int)(rm.m[i].P / ((int64_t)rm.m[i].xe * rm.m[i].ye));
+    a.thr = thr;
+    a.axis_q = ctx->axis_q.p;
+    a.qt = ctx->qt.p;
+    a.M = ctx->M;
+    a.r = ctx->r;
+    a.Opad = ctx->Opad;
+    a.scores = ctx->scores.p + rm.m[i].offset;
+    a.order_base = (int64_t)i << 40;
+    launches.push_back(a);
+    nparts += c3h::score_blocks(a);
+  }
+  const bool use_argmax = all_fast && ctx->rank == 1;
+  const uint32_t* nlist = nullptr;
+  if (all_fast) {  // sparse: gate every position, project the passing ones
+    c3h::SparseSearch q{};
+    q.G = ctx->G.p;
+    q.exist = ctx->exist.p;
+    q.D = ctx->D;
+    q.xn = xn;
+    q.yn = yn;
+    q.zn = zn;
+    q.thr = thr;
+    q.qt = ctx->qt.p;
+    q.M = ctx->M;
+    q.r = ctx->r;
+    q.Opad = ctx->Opad;
+    q.scores = ctx->scores.p;
+    q.nmodes = rm.n;
+    q.pstart[0] = 0;
     for (int i = 0; i < rm.n; ++i) {
-      int xr, yr, zr;
-      get_range(rm.m[i].mode, range[0], range[1], range[2], &xr, &yr, &zr);
-      c3h::ScoreLaunch a;
-      a.G = ctx->G.p;
-      a.exist = ctx->exist.p;
-      a.D = ctx->D;
-      a.xn = xn;
-      a.yn = yn;
-      a.zn = zn;
-      a.xr = xr;
-      a.yr = yr;
-      a.zr = zr;
-      a.xe = rm.m[i].xe;
-      a.ye = rm.m[i].ye;
-      a.ze = (int)(rm.m[i].P / ((int64_t)rm.m[i].xe * rm.m[i].ye));
-      a.thr = thr;
-      a.axis_q = ctx->axis_q.p;
-      a.M = ctx->M;
-      a.r = ctx->r;
-      a.scores = ctx->scores.p + rm.m[i].offset;
-      HIPCHK(c3h::launch_score(a, ctx->stream));
+      const auto& a = launches[i];
+      q.md[i] = c3h::ModeGeom{rm.m[i].offset, rm.m[i].P, a.xe, a.ye, a.xr, a.yr, a.zr};
+      q.pstart[i + 1] = q.pstart[i] + rm.m[i].P;
+      q.order_base[i] = (int64_t)i << 40;
     }
+    const int64_t ptot = q.pstart[rm.n];
+    ENSURE(ctx->glist, (size_t)std::max<int64_t>(ptot, 1));
+    if (!ctx->gcnt.p) {
+      ENSURE(ctx->gcnt, 2);
+      HIPCHK(hipMemsetAsync(ctx->gcnt.p, 0, 8, ctx->stream));
+      ctx->search_epoch = 0;
+    }
+    ++ctx->search_epoch;
+    q.list = ctx->glist.p;
+    q.cnt = ctx->gcnt.p;
+    q.epoch = ctx->search_epoch;
+    nparts = c3h::sparse_score_blocks(q);
+    if (use_argmax) {
+      ENSURE(ctx->partials, (size_t)std::max<int64_t>(nparts, 1) * ctx->M);
+      q.partials = ctx->partials.p;
+      nlist = ctx->gcnt.p + (q.epoch & 1);
+    }
+    Timed t(ctx, 3);
+    HIPCHK(c3h::launch_sparse_search(q, ctx->stream));
+  } else {
+    if (ctx->g_sparse)
+      return fail(ctx, C3H_ERR_STATE, "c3h_search: internal: sparse G on the dense score path");
+    Timed t(ctx, 3);
+    for (auto& a : launches) HIPCHK(c3h::launch_score(a, ctx->stream));
   }
   if (!ctx->lists_dev_valid) {
     int rc = upload_lists(ctx);
@@ -326,8 +402,14 @@ int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate
   }
   {
     Timed t(ctx, 4);
-    HIPCHK(c3h::launch_replay(ctx->scores.p, rm, ctx->M, ctx->rank, range[0], range[1],
-                              range[2], ctx->d_lists.p, ctx->stream));
+    const int clean = ctx->pending_clean ? 1 : 0;
+    if (use_argmax)
+      HIPCHK(c3h::launch_argmax_replay(ctx->partials.p, nparts, nlist, rm, ctx->M, clean, ctx->d_lists.p,
+                                       d_out, ctx->stream));
+    else
+      HIPCHK(c3h::launch_replay(ctx->scores.p, rm, ctx->M, ctx->rank, range[0], range[1],
+                                range[2], clean, ctx->d_lists.p, d_out, ctx->stream));
+    ctx->pending_clean = false;
   }
   ctx->lists_host_valid = false;
   ctx->last_range[0] = range[0];
@@ -392,12 +474,19 @@ void c3h_destroy(c3h_ctx* ctx) {
   release(ctx->exist);
   release(ctx->acc64);
   release(ctx->segs);
+  release(ctx->axmap);
+  release(ctx->tileflags);
+  release(ctx->rows);
+  release(ctx->glist);
+  release(ctx->gcnt);
   release(ctx->lut);
   release(ctx->axis_pt);
   release(ctx->axis_q);
   release(ctx->fmax);
   release(ctx->G);
   release(ctx->scores);
+  release(ctx->qt);
+  release(ctx->partials);
   release(ctx->d_lists);
   for (int s = 0; s < C3H_NTIMERS; ++s)
     for (auto& e : ctx->timer.pending[s]) ctx->timer.pool.push_back(e);
@@ -640,6 +729,7 @@ int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3]
   HIPCHK(hipSetDevice(ctx->device));
   ctx->have_feat = false;
   ctx->g_valid = false;
+  ctx->rows_valid = false;
   const int F = p->variant;
   const int* div = ctx->info.div_b;
   int32_t sb[3] = {0, 0, 0};
@@ -677,6 +767,11 @@ int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3]
     s[a] = axis_segments(div[a], mode1 ? 0 : p->offset[a], inv_s, mode1, mode1 ? 1 : sb[a],
                          &covered[a], &split[a]);
   const int64_t ntiles = (int64_t)s[0].start.size() * s[1].start.size() * s[2].start.size();
+  for (int a = 0; a < 3; ++a)
+    if (s[a].start.size() > 32767) {
+      ctx->err = "c3h_extract: more than 32767 tile segments along one axis";
+      return C3H_ERR_RANGE;
+    }
   const bool atomic = split[0] || split[1] || split[2];
   const bool all_covered = covered[0] && covered[1] && covered[2] && ntiles > 0;
   ENSURE(ctx->feat, (size_t)hist_num * F);
@@ -699,11 +794,31 @@ int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3]
         e[1] = s[a].len[i];
         e[2] = s[a].sub[i];
       }
-    if (segs != ctx->h_segs || !ctx->segs.p) {  // frames of one geometry reuse the table
+    if (segs != ctx->h_segs || !ctx->segs.p) {  // frames of one geometry reuse the tables
       ctx->h_segs.swap(segs);
       ENSURE(ctx->segs, ctx->h_segs.size());
       HIPCHK(hipMemcpyAsync(ctx->segs.p, ctx->h_segs.data(), ctx->h_segs.size() * 4,
                             hipMemcpyHostToDevice, ctx->stream));
+      // centre coordinate -> segment index per axis, for the occupancy pass
+      ctx->h_axmap.assign((size_t)div[0] + div[1] + div[2], (int16_t)-1);
+      int16_t* m = ctx->h_axmap.data();
+      for (int a = 0; a < 3; ++a) {
+        for (size_t i = 0; i < s[a].start.size(); ++i)
+          for (int c = s[a].start[i]; c < s[a].start[i] + s[a].len[i]; ++c) m[c] = (int16_t)i;
+        m += div[a];
+      }
+      ENSURE(ctx->axmap, ctx->h_axmap.size());
+      HIPCHK(hipMemcpyAsync(ctx->axmap.p, ctx->h_axmap.data(), ctx->h_axmap.size() * 2,
+                            hipMemcpyHostToDevice, ctx->stream));
+    }
+    Timed t(ctx, 1);  // the whole C3 stage: flag reset, occupancy pass, tile kernel
+    // [2] row-list counters | [ntiles] epoch stamps; zeroed only when (re)allocated or
+    // when the epoch wraps
+    const size_t tf_n = (size_t)ntiles + 2;
+    if (ctx->tileflags.n < tf_n || ++ctx->tile_epoch == 0) {
+      ENSURE(ctx->tileflags, tf_n);
+      HIPCHK(hipMemsetAsync(ctx->tileflags.p, 0, ctx->tileflags.n * 4, ctx->stream));
+      ctx->tile_epoch = 1;
     }
     if (atomic) {
       ENSURE(ctx->acc64, (size_t)hist_num * 981);
@@ -729,8 +844,20 @@ int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3]
     l.feat = ctx->feat.p;
     l.exist = ctx->exist.p;
     l.acc64 = ctx->acc64.p;
+    l.axmap = ctx->axmap.p;
+    l.rowcnt = ctx->tileflags.p;
+    l.flags = ctx->tileflags.p + 2;
+    l.rows = nullptr;
+    if (!atomic) {  // the non-empty rows feed the sparse compress of the search
+      ENSURE(ctx->rows, (size_t)hist_num);
+      l.rows = ctx->rows.p;
+    }
+    ctx->rows_valid = !atomic;
+    l.epoch = ctx->tile_epoch;
+    l.zero_empty = (!atomic && all_covered) ? 1 : 0;
     l.ntiles = ntiles;
-    Timed t(ctx, 1);
+    l.debug = 0;
+    if (const char* dbg = getenv("C3H_C3_DEBUG")) l.debug = atoi(dbg);  // diagnostics only
     HIPCHK(c3h::launch_c3hlac(l, ctx->stream));
     if (atomic)
       HIPCHK(c3h::launch_c3_finalize(ctx->acc64.p, hist_num, F, ctx->feat.p, ctx->exist.p, ctx->stream));
@@ -793,6 +920,15 @@ int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_
   HIPCHK(hipMemcpy(ctx->axis_pt.p, pt.data(), pt.size() * 4, hipMemcpyHostToDevice));
   ENSURE(ctx->axis_q, (size_t)M * r * D);
   HIPCHK(hipMemcpy(ctx->axis_q.p, axis_q, (size_t)M * r * D * 4, hipMemcpyHostToDevice));
+  // transposed basis for the fast score path: qt[d][m*r + i] = axis_q[m][i][d]
+  const int Opad = (M * r + 15) / 16 * 16;
+  std::vector<float> qt((size_t)D * Opad, 0.0f);
+  for (int m = 0; m < M; ++m)
+    for (int i = 0; i < r; ++i)
+      for (int d = 0; d < D; ++d) qt[(size_t)d * Opad + m * r + i] = axis_q[((size_t)m * r + i) * D + d];
+  ENSURE(ctx->qt, qt.size());
+  HIPCHK(hipMemcpy(ctx->qt.p, qt.data(), qt.size() * 4, hipMemcpyHostToDevice));
+  ctx->Opad = Opad;
   ctx->fmax_len = feature_max_len;
   if (feature_max_len > 0) {
     ENSURE(ctx->fmax, (size_t)feature_max_len);
@@ -820,9 +956,8 @@ int c3h_set_rank(c3h_ctx* ctx, int32_t rank) {
 int c3h_clean_max(c3h_ctx* ctx) {
   if (!ctx) return C3H_ERR_ARG;
   if (ctx->lists.M != std::max(ctx->M, 1) || ctx->lists.rank != ctx->rank) init_lists(ctx);
-  if (!ctx->lists_host_valid && ctx->lists_dev_valid) {  // device copy is authoritative
-    HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(c3h::launch_clean_lists(ctx->d_lists.p, ctx->lists.M * ctx->lists.rank, ctx->stream));
+  if (!ctx->lists_host_valid && ctx->lists_dev_valid) {  // device copy is authoritative:
+    ctx->pending_clean = true;  // applied by the next replay kernel (or the next download)
     return C3H_OK;
   }
   auto& L = ctx->lists;
@@ -838,7 +973,7 @@ int c3h_search(c3h_ctx* ctx, const int32_t range[3], int32_t exist_threshold, in
                int32_t remove_overlap, c3h_det* out) {
   if (!ctx) return C3H_ERR_ARG;
   HIPCHK(hipSetDevice(ctx->device));
-  const int nm = run_search(ctx, range, exist_threshold, rotate);
+  const int nm = run_search(ctx, range, exist_threshold, rotate, nullptr);
   if (nm < 0) return nm;
   int rc = sync_host_lists(ctx);
   if (rc != C3H_OK) return rc;
@@ -865,9 +1000,13 @@ int c3h_search_async(c3h_ctx* ctx, const int32_t range[3], int32_t exist_thresho
                      int32_t rotate, c3h_det* d_out) {
   if (!ctx) return C3H_ERR_ARG;
   HIPCHK(hipSetDevice(ctx->device));
-  const int nm = run_search(ctx, range, exist_threshold, rotate);
+  const int nm = run_search(ctx, range, exist_threshold, rotate, d_out);
   if (nm < 0) return nm;
-  if (d_out && ctx->lists_dev_valid) {
+  if (nm == 0 && d_out) {  // no search ran: hand out the current lists
+    int rc = sync_host_lists(ctx);
+    if (rc != C3H_OK) return rc;
+    rc = upload_lists(ctx);
+    if (rc != C3H_OK) return rc;
     const size_t n = (size_t)ctx->lists.M * ctx->lists.rank;
     HIPCHK(hipMemcpyAsync(d_out, ctx->d_lists.p, n * sizeof(c3h_det), hipMemcpyDeviceToDevice, ctx->stream));
   }
@@ -900,8 +1039,25 @@ int c3h_get_compressed(c3h_ctx* ctx, float* out, int on_device) {
   if (!ctx->g_valid) return fail(ctx, C3H_ERR_STATE, "no compressed features (run a search)");
   HIPCHK(hipSetDevice(ctx->device));
   const size_t n = (size_t)ctx->hist_num * ctx->D;
-  HIPCHK(hipMemcpyAsync(out, ctx->G.p, n * 4, on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, ctx->stream));
+  if (!ctx->g_sparse) {
+    HIPCHK(hipMemcpyAsync(out, ctx->G.p, n * 4, on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return C3H_OK;
+  }
+  // sparse compress: rows of empty subdivisions (exist == 0) were not written; they are 0
+  std::vector<float> g(n);
+  std::vector<int32_t> ex((size_t)ctx->hist_num);
+  HIPCHK(hipMemcpyAsync(g.data(), ctx->G.p, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ex.data(), ctx->exist.p, ex.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  for (size_t h = 0; h < ex.size(); ++h)
+    if (!ex[h]) std::fill(g.begin() + h * ctx->D, g.begin() + (h + 1) * ctx->D, 0.0f);
+  if (on_device) {
+    HIPCHK(hipMemcpyAsync(out, g.data(), n * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  } else {
+    memcpy(out, g.data(), n * 4);
+  }
   return C3H_OK;
 }
 
@@ -939,11 +1095,16 @@ int c3h_remove_overlap(int32_t M, int32_t rank, const int32_t range[3], c3h_det*
 
 int c3h_pca_read(const char* path, int32_t ascii, float* axis, float* var, float* mean,
                  int32_t* has_mean, int32_t max_dim) {
-  if (!path || !axis || !var) return C3H_ERR_ARG;
+  const bool query = !axis && !var;  // size query: read the header only
+  if (!path || (!query && (!axis || !var))) return C3H_ERR_ARG;
   FILE* fp = fopen(path, ascii ? "r" : "rb");
   if (!fp) return C3H_ERR_NOTFOUND;
   int dim = -1;
   const bool got_dim = ascii ? fscanf(fp, "%d\n", &dim) == 1 : fread(&dim, sizeof(int), 1, fp) == 1;
+  if (query) {
+    fclose(fp);
+    return got_dim && dim > 0 ? dim : C3H_ERR_FORMAT;
+  }
   if (!got_dim || dim <= 0 || dim > max_dim) {
     fclose(fp);
     return C3H_ERR_FORMAT;
@@ -977,7 +1138,7 @@ int c3h_pca_read(const char* path, int32_t ascii, float* axis, float* var, float
 
 int c3h_timing(c3h_ctx* ctx, int32_t enable) {
   if (!ctx) return C3H_ERR_ARG;
-  ctx->timer.enabled = enable != 0;
+  ctx->timer.mask = enable == 1 ? C3H_TIMING_ALL : (uint32_t)enable & C3H_TIMING_ALL;
   if (enable) {  // pre-create event pairs so no hipEventCreate lands in a timed region
     HIPCHK(hipSetDevice(ctx->device));
     while (ctx->timer.pool.size() < 2048) {

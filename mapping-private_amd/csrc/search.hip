@@ -21,75 +21,164 @@ namespace c3h {
 namespace {
 
 // ---------------------------------------------------------------- compress (GEMM)
-constexpr int kCM = 64, kCN = 128, kCK = 16;
+// G[h][d] = sum_j f'[h][j] * P[j][d] (P = whitened axis_p transposed, F x Dpad).
+// 512-thread block: 64 rows x 128 columns; lane = row (f staged k-major in LDS, read
+// conflict-free), wave = 16 columns whose P values are wave-uniform scalar loads.
+// fma chain in ascending j (the reference's GEMV order).
+constexpr int kCM = 64, kCN = 128, kCK = 128, kCT = 512, kCW = 16;
 
-__global__ __launch_bounds__(kBlock) void compress_kernel(
+__global__ __launch_bounds__(kCT) void compress_kernel(
     const float* __restrict__ feat, int64_t H, int F, const float* __restrict__ PT, int D,
-    int Dpad, const float* __restrict__ fmax, int fmax_len, float* __restrict__ G) {
-  __shared__ float fs[kCK][kCM + 4];
-  __shared__ float ps[kCK][kCN];
+    int Dpad, const float* __restrict__ fmax, int fmax_len, float* __restrict__ G,
+    const int32_t* __restrict__ rows, const uint32_t* __restrict__ nrows) {
+  __shared__ float fs[kCK * (kCM + 1)];
+  __shared__ int64_t s_row[kCM];
   const int tid = threadIdx.x;
-  const int th = tid & 15, td = tid >> 4;
+  const int row = tid & (kCM - 1);
+  const int cg = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t h0 = blockIdx.x * (int64_t)kCM;
-  const int d0 = blockIdx.y * kCN;
-  float acc[4][8];
+  // sparse mode: this block's rows are rows[h0 .. h0+63] of the non-empty-row list
+  // (G rows of empty subdivisions are left untouched; consumers gate them on exist)
+  const int64_t nr = rows ? (int64_t)*nrows : H;
+  if (h0 >= nr) return;
+  if (tid < kCM) s_row[tid] = h0 + tid < nr ? (rows ? (int64_t)rows[h0 + tid] : h0 + tid) : -1;
+  __syncthreads();
+  const int c0 = blockIdx.y * kCN + cg * kCW;
+  const bool active = c0 < D;
+  float acc[kCW];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = 0.0f;
-
+  for (int j = 0; j < kCW; ++j) acc[j] = 0.0f;
   for (int j0 = 0; j0 < F; j0 += kCK) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = tid + kBlock * q, row = e >> 4, col = e & 15;
-      const int64_t hh = h0 + row;
-      const int jj = j0 + col;
+    const int kn = min(kCK, F - j0);
+    int r = tid / kn, c = tid - (tid / kn) * kn;  // e = tid + kCT*i -> (r, c), no division in the loop
+    const int sr = kCT / kn, sc = kCT - (kCT / kn) * kn;
+    for (int e = tid; e < kCM * kn; e += kCT) {
+      const int64_t hh = s_row[r];
+      const int jj = j0 + c;
       float v = 0.0f;
-      if (hh < H && jj < F) {
+      if (hh >= 0) {
         v = feat[hh * F + jj];
-        if (jj < fmax_len) {  // SearchObj::setData histogram normalisation
+        if (jj < fmax_len) {  // SearchObj::setData histogram normalisation (search.cpp:563-570)
           const float mx = fmax[jj];
           if (mx == 0.0f) v = 0.0f;
           else if (v == mx) v = 1.0f;
           else v = __fdiv_rn(v, mx);
         }
       }
-      fs[col][row] = v;
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int e = tid + kBlock * q, row = e >> 7, col = e & 127;
-      ps[row][col] = (j0 + row < F && d0 + col < Dpad) ? PT[(int64_t)(j0 + row) * Dpad + d0 + col] : 0.0f;
+      fs[c * (kCM + 1) + r] = v;
+      r += sr;
+      c += sc;
+      if (c >= kn) {
+        c -= kn;
+        ++r;
+      }
     }
     __syncthreads();
+    if (active) {
+      const float* __restrict__ pk = PT + (int64_t)j0 * Dpad + c0;
+      for (int k = 0; k < kn; ++k) {
+        const float fv = fs[k * (kCM + 1) + row];
+        const float* __restrict__ p = pk + (int64_t)k * Dpad;
 #pragma unroll
-    for (int kk = 0; kk < kCK; ++kk) {
-      float av[4], bv[8];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) av[i] = fs[kk][th * 4 + i];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) bv[j] = ps[kk][td * 8 + j];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_fmaf(av[i], bv[j], acc[i][j]);
+        for (int j = 0; j < kCW; ++j) acc[j] = __builtin_fmaf(fv, p[j], acc[j]);
+      }
     }
     __syncthreads();
   }
+  const int64_t hh = s_row[row];
+  if (active && hh >= 0) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t hh = h0 + th * 4 + i;
-    if (hh >= H) continue;
+    for (int j = 0; j < kCW; ++j)
+      if (c0 + j < D) G[hh * D + c0 + j] = acc[j];
+  }
+}
+
+// Sparse compress (row list from the extract): 16 listed rows per workgroup x all
+// columns (Dpad <= 128).  The 16 feature rows (max-normalised) and 32-row chunks of P
+// are staged in LDS, P prefetched one chunk ahead into registers so only the first
+// load's latency is exposed; thread = (row, 8 columns); the fma chain per output runs
+// in ascending j exactly like compress_kernel, so both paths give identical G rows.
+constexpr int kRR = 16, kRK = 32;
+
+__global__ __launch_bounds__(kBlock) void compress_rows_kernel(
+    const float* __restrict__ feat, int F, const float* __restrict__ PT, int D, int Dpad,
+    const float* __restrict__ fmax, int fmax_len, float* __restrict__ G,
+    const int32_t* __restrict__ rows, const uint32_t* __restrict__ nrows) {
+  extern __shared__ __attribute__((aligned(16))) float csm[];
+  float* pc = csm;                 // kRK x Dpad
+  float* fs = csm + kRK * Dpad;    // kRR x F
+  const int tid = threadIdx.x;
+  const int n = (int)*nrows;
+  const int r0 = blockIdx.x * kRR;
+  if (r0 >= n) return;
+  const int nq4 = kRK * Dpad / 4, tot4 = F * Dpad / 4;
+  const float4* P4 = reinterpret_cast<const float4*>(PT);
+  float4 pre[4];
+  auto load_chunk = [&](int c) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int d = d0 + td * 8 + j;
-      if (d < D) G[hh * D + d] = acc[i][j];
+    for (int j = 0; j < 4; ++j) {
+      const int e = tid + j * kBlock, g = c * nq4 + e;
+      pre[j] = (e < nq4 && g < tot4) ? P4[g] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+  };
+  load_chunk(0);
+  for (int e = tid; e < kRR * F; e += kBlock) {
+    const int r = e / F, j = e - r * F;
+    float v = 0.0f;
+    if (r0 + r < n) {
+      v = feat[(int64_t)rows[r0 + r] * F + j];
+      if (j < fmax_len) {  // setData max-normalisation (search.cpp:563-570)
+        const float mx = fmax[j];
+        if (mx == 0.0f) v = 0.0f;
+        else if (v == mx) v = 1.0f;
+        else v = __fdiv_rn(v, mx);
+      }
+    }
+    fs[e] = v;
+  }
+  const int row = tid >> 4, cg = tid & 15;
+  const bool active = 8 * cg < Dpad;
+  float acc[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) acc[q] = 0.0f;
+  const int nch = (F + kRK - 1) / kRK;
+  for (int c = 0; c < nch; ++c) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = tid + j * kBlock;
+      if (e < nq4) reinterpret_cast<float4*>(pc)[e] = pre[j];
+    }
+    if (c + 1 < nch) load_chunk(c + 1);
+    __syncthreads();
+    if (active) {
+      const int kn = min(kRK, F - c * kRK);
+      const float* fr = fs + row * F + c * kRK;
+      for (int k = 0; k < kn; ++k) {
+        const float fv = fr[k];
+        const float4 p0 = *reinterpret_cast<const float4*>(&pc[k * Dpad + 8 * cg]);
+        const float4 p1 = *reinterpret_cast<const float4*>(&pc[k * Dpad + 8 * cg + 4]);
+        acc[0] = __builtin_fmaf(fv, p0.x, acc[0]);
+        acc[1] = __builtin_fmaf(fv, p0.y, acc[1]);
+        acc[2] = __builtin_fmaf(fv, p0.z, acc[2]);
+        acc[3] = __builtin_fmaf(fv, p0.w, acc[3]);
+        acc[4] = __builtin_fmaf(fv, p1.x, acc[4]);
+        acc[5] = __builtin_fmaf(fv, p1.y, acc[5]);
+        acc[6] = __builtin_fmaf(fv, p1.z, acc[6]);
+        acc[7] = __builtin_fmaf(fv, p1.w, acc[7]);
+      }
+    }
+  }
+  if (active && r0 + row < n) {
+    const int64_t h = rows[r0 + row];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (8 * cg + q < D) G[h * D + 8 * cg + q] = acc[q];
   }
 }
 
 // ---------------------------------------------------------------- score
-// SP positions per workgroup (64, or 16 when the box vectors are wide: no compression)
+// Generic path (any D, any M*r): SP positions per workgroup, basis through the scalar path.
 template <int SP>
 __global__ __launch_bounds__(kBlock) void score_kernel(ScoreLaunch a, int64_t P) {
   extern __shared__ __attribute__((aligned(16))) float ssm[];
@@ -137,7 +226,6 @@ __global__ __launch_bounds__(kBlock) void score_kernel(ScoreLaunch a, int64_t P)
   }
   constexpr int kRowsPerPass = kBlock / SP;
   const int pp = tid & (SP - 1);
-  // wave-uniform model row -> the basis is read through the scalar cache
   const int i0 = __builtin_amdgcn_readfirstlane(tid / SP);
   for (int m = 0; m < a.M; ++m) {
     const float* __restrict__ Q = a.axis_q + (int64_t)m * a.r * a.D;
@@ -165,6 +253,240 @@ __global__ __launch_bounds__(kBlock) void score_kernel(ScoreLaunch a, int64_t P)
   }
 }
 
+// Fast path (D <= 256, D % 4 == 0, M*r <= 256) = the sparse search below: 32 list
+// entries per workgroup.  Box features are summed with float4 loads and staged k-major in
+// LDS (lanes = positions: conflict-free); the projection onto all M*r basis rows is a
+// 32 x Opad x D fp32 GEMM with a 2-position x 16-row register tile per thread (one
+// ds_read_b64 of box features + four ds_read_b128 of basis rows feed 32 FMAs), the basis
+// streamed through LDS in 16-row chunks prefetched one chunk ahead into registers;
+// |Q_m f|^2 is summed per (position, model) in a fixed order.  The block also emits its
+// per-model best (score, scan order) so rank-1 searches need no second pass.
+constexpr int kFP = 32;
+
+// ---------------------------------------------------------------- sparse search
+// The exist gate passes few positions on surface scenes (a depth camera sees a 2-D
+// manifold), so the gate runs first over every position of every mode and compacts the
+// passing ones into a list; the projection then runs over the list only.  Entries are
+// (mode index << 40) | position; list order is irrelevant: scores are per position and
+// the per-block partials break ties on the scan order explicitly.
+__device__ __forceinline__ int find_mode(const SparseSearch& a, int64_t g) {
+  int mi = 0;
+  while (mi + 1 < a.nmodes && g >= a.pstart[mi + 1]) ++mi;
+  return mi;
+}
+
+__global__ __launch_bounds__(kBlock) void gate_kernel(SparseSearch a) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (blockIdx.x == 0 && tid == 0) a.cnt[(a.epoch + 1) & 1] = 0;  // next search's counter
+  const int64_t g = blockIdx.x * (int64_t)kBlock + tid;
+  bool pass = false;
+  int64_t entry = 0;
+  if (g < a.pstart[a.nmodes]) {
+    const int mi = find_mode(a, g);
+    const ModeGeom& md = a.md[mi];
+    const int64_t p = g - a.pstart[mi];
+    const int64_t xye = (int64_t)md.xe * md.ye;
+    const int x = (int)(p % md.xe), y = (int)((p / md.xe) % md.ye), z = (int)(p / xye);
+    const int xyn = a.xn * a.yn;
+    const int h = z * xyn + y * a.xn + x;
+    int e = 0;  // SearchObj::clipValue<int> on exist_voxel_num (search.cpp:484-535), exact
+    for (int dz = 0; dz < md.zr; ++dz)
+      for (int dy = 0; dy < md.yr; ++dy)
+        for (int dx = 0; dx < md.xr; ++dx) e += a.exist[h + dz * xyn + dy * a.xn + dx];
+    pass = e > a.thr;
+    entry = ((int64_t)mi << 40) | p;
+    if (!pass)
+      for (int m = 0; m < a.M; ++m) a.scores[md.offset + (int64_t)m * md.P + p] = -1.0;
+  }
+  const unsigned long long m = __ballot(pass);
+  if (m) {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&a.cnt[a.epoch & 1], (uint32_t)__popcll(m));
+    base = __shfl(base, 0, 64);
+    if (pass) a.list[base + __popcll(m & ((1ull << lane) - 1))] = entry;
+  }
+}
+
+// Fast-path projection over the gate list:
+// kFP entries per workgroup; box rows of empty subdivisions are skipped (their G rows
+// may be stale: the sparse compress only writes non-empty rows; an all-zero row adds
+// nothing to a sum that starts at +0).
+__global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch a) {
+  extern __shared__ __attribute__((aligned(16))) float ssm[];
+  const int D = a.D, Opad = a.Opad, D4 = a.D >> 2;
+  const int n = (int)a.cnt[a.epoch & 1];
+  const int64_t e0 = blockIdx.x * (int64_t)kFP;
+  if (e0 >= n) return;
+  float* fT = ssm;
+  float* qc = fT + D * kFP;
+  float* qv = ssm;
+  const int region = max(D * kFP + 16 * Opad, kFP * (Opad + 1));
+  float* ffv = ssm + region;
+  int* gate = reinterpret_cast<int*>(ffv + kFP);
+  int* hrow = gate + kFP;
+  int* rng = hrow + kFP;                       // packed xr | yr << 10 | zr << 20
+  long long* ent = reinterpret_cast<long long*>(rng + kFP + (kFP & 1));
+  double* bsc = reinterpret_cast<double*>(ent + kFP);  // kFP * M
+  const int tid = threadIdx.x;
+  const int xyn = a.xn * a.yn;
+  // basis chunk c = rows [16c, 16c+16) of qt (D x Opad row-major, contiguous); chunk 0
+  // is requested now so its latency overlaps the list / exist / G loads
+  const int D16 = (D + 15) >> 4, nq4 = 4 * Opad, tot4 = D * Opad / 4;
+  const float4* qt4 = reinterpret_cast<const float4*>(a.qt);
+  float4 pre[4];
+  auto load_chunk = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = tid + j * kBlock, g = c * nq4 + e;
+      pre[j] = (e < nq4 && g < tot4) ? qt4[g] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  load_chunk(0);
+
+  if (tid < kFP) {
+    const int64_t e = e0 + tid;
+    int ok = 0, h = 0, rr = 0;
+    long long en = -1;
+    if (e < n) {
+      en = a.list[e];
+      const int mi = (int)(en >> 40);
+      const int64_t p = en & ((1ll << 40) - 1);
+      const ModeGeom& md = a.md[mi];
+      const int64_t xye = (int64_t)md.xe * md.ye;
+      const int x = (int)(p % md.xe), y = (int)((p / md.xe) % md.ye), z = (int)(p / xye);
+      h = z * xyn + y * a.xn + x;
+      rr = md.xr | (md.yr << 10) | (md.zr << 20);
+      ok = 1;
+    }
+    gate[tid] = ok;
+    hrow[tid] = h;
+    rng[tid] = rr;
+    ent[tid] = en;
+  }
+  __syncthreads();
+  {  // box sums in the fixed (dz, dy, dx) order over non-empty rows; lane = position
+    const int pp = tid & (kFP - 1), dg = tid / kFP;
+    const bool ok = gate[pp];
+    const int h = hrow[pp], rr = rng[pp];
+    const int xr = rr & 1023, yr = (rr >> 10) & 1023, zr = rr >> 20;
+    const float4* G4 = reinterpret_cast<const float4*>(a.G);
+    unsigned long long live = 0;  // occupancy of the first 64 box cells
+    const int ncell = xr * yr * zr;
+    if (ok) {
+      int c = 0;
+      for (int dz = 0; dz < zr; ++dz)
+        for (int dy = 0; dy < yr; ++dy)
+          for (int dx = 0; dx < xr && c < 64; ++dx, ++c)
+            if (a.exist[h + dz * xyn + dy * a.xn + dx]) live |= 1ull << c;
+    }
+    for (int d4 = dg; d4 < D4; d4 += kBlock / kFP) {
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ok) {
+        int c = 0;
+        for (int dz = 0; dz < zr; ++dz)
+          for (int dy = 0; dy < yr; ++dy)
+            for (int dx = 0; dx < xr; ++dx, ++c) {
+              const int hh = h + dz * xyn + dy * a.xn + dx;
+              const bool use = c < 64 ? (live >> c & 1) : (a.exist[hh] != 0);
+              if (!use) continue;
+              const float4 g = G4[(int64_t)hh * D4 + d4];
+              s.x += g.x;
+              s.y += g.y;
+              s.z += g.z;
+              s.w += g.w;
+            }
+      }
+      fT[(4 * d4 + 0) * kFP + pp] = s.x;
+      fT[(4 * d4 + 1) * kFP + pp] = s.y;
+      fT[(4 * d4 + 2) * kFP + pp] = s.z;
+      fT[(4 * d4 + 3) * kFP + pp] = s.w;
+    }
+    (void)ncell;
+  }
+  __syncthreads();
+  if (tid < kFP) {
+    float s = 0.0f;
+    for (int d = 0; d < D; ++d) s = __builtin_fmaf(fT[d * kFP + tid], fT[d * kFP + tid], s);
+    ffv[tid] = s;
+  }
+  const int tp = tid & 15, to = tid >> 4;
+  const bool active = to * 16 < Opad;
+  float acc[2][16];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[i][j] = 0.0f;
+  for (int c = 0; c < D16; ++c) {
+    const int d0 = 16 * c, dn = min(16, D - d0);
+    __syncthreads();  // fT complete / the previous chunk's readers done
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = tid + j * kBlock;
+      if (e < nq4) reinterpret_cast<float4*>(qc)[e] = pre[j];
+    }
+    if (c + 1 < D16) load_chunk(c + 1);
+    __syncthreads();
+    if (active) {
+      for (int dd = 0; dd < dn; ++dd) {
+        const float2 f = *reinterpret_cast<const float2*>(&fT[(d0 + dd) * kFP + 2 * tp]);
+        const float4* qrow = reinterpret_cast<const float4*>(&qc[dd * Opad + 16 * to]);
+#pragma unroll
+        for (int j4 = 0; j4 < 4; ++j4) {
+          const float4 q = qrow[j4];
+          acc[0][4 * j4 + 0] = __builtin_fmaf(f.x, q.x, acc[0][4 * j4 + 0]);
+          acc[0][4 * j4 + 1] = __builtin_fmaf(f.x, q.y, acc[0][4 * j4 + 1]);
+          acc[0][4 * j4 + 2] = __builtin_fmaf(f.x, q.z, acc[0][4 * j4 + 2]);
+          acc[0][4 * j4 + 3] = __builtin_fmaf(f.x, q.w, acc[0][4 * j4 + 3]);
+          acc[1][4 * j4 + 0] = __builtin_fmaf(f.y, q.x, acc[1][4 * j4 + 0]);
+          acc[1][4 * j4 + 1] = __builtin_fmaf(f.y, q.y, acc[1][4 * j4 + 1]);
+          acc[1][4 * j4 + 2] = __builtin_fmaf(f.y, q.z, acc[1][4 * j4 + 2]);
+          acc[1][4 * j4 + 3] = __builtin_fmaf(f.y, q.w, acc[1][4 * j4 + 3]);
+        }
+      }
+    }
+  }
+  __syncthreads();  // qv aliases fT / qc
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) qv[(2 * tp + i) * (Opad + 1) + 16 * to + j] = acc[i][j];
+  }
+  __syncthreads();
+  for (int e = tid; e < kFP * a.M; e += kBlock) {
+    const int m = e / kFP, pp = e - m * kFP;
+    double sc = -2.0;
+    if (gate[pp]) {
+      float q2 = 0.0f;
+      const float* q = qv + pp * (Opad + 1) + m * a.r;
+      for (int i = 0; i < a.r; ++i) q2 = __builtin_fmaf(q[i], q[i], q2);
+      sc = sqrt((double)q2) / sqrt((double)ffv[pp]);
+      const long long en = ent[pp];
+      const ModeGeom& md = a.md[(int)(en >> 40)];
+      a.scores[md.offset + (int64_t)m * md.P + (en & ((1ll << 40) - 1))] = sc;
+    }
+    bsc[e] = sc;
+  }
+  if (a.partials) {
+    __syncthreads();
+    for (int m = tid; m < a.M; m += kBlock) {  // (score desc, scan order asc)
+      double best = -2.0;
+      long long bo = -1;
+      for (int pp = 0; pp < kFP; ++pp) {
+        if (!gate[pp]) continue;
+        const double sc = bsc[m * kFP + pp];
+        const long long en = ent[pp];
+        const long long o = a.order_base[(int)(en >> 40)] + (en & ((1ll << 40) - 1));
+        if (sc > best || (sc == best && o < bo)) {
+          best = sc;
+          bo = o;
+        }
+      }
+      a.partials[(int64_t)blockIdx.x * a.M + m] = ScorePartial{best, bo};
+    }
+  }
+}
+
 // ---------------------------------------------------------------- rank replay
 __device__ __forceinline__ void get_range(int mode, int r1, int r2, int r3, int& xr, int& yr,
                                           int& zr) {
@@ -178,92 +500,169 @@ __device__ __forceinline__ void get_range(int mode, int r1, int r2, int r3, int&
   }
 }
 
+// rank update of searchPart (search.cpp:464-474) incl. checkOverlap (:327-356)
+__device__ void rank_update(c3h_det* L, int rank, double cs, int x, int y, int z, int mode,
+                            int xr, int yr, int zr, int r1, int r2, int r3) {
+  for (int i = 0; i < rank; i++) {
+    if (cs > L[i].score) {
+      int num;
+      for (num = 0; num < rank - 1; num++) {
+        int oxr, oyr, ozr;
+        get_range(L[num].mode, r1, r2, r3, oxr, oyr, ozr);
+        int v1 = L[num].x - x;
+        v1 = v1 < 0 ? -v1 - oxr : v1 - xr;
+        int v2 = L[num].y - y;
+        v2 = v2 < 0 ? -v2 - oyr : v2 - yr;
+        int v3 = L[num].z - z;
+        v3 = v3 < 0 ? -v3 - ozr : v3 - zr;
+        if (v1 <= 0 && v2 <= 0 && v3 <= 0) break;
+      }
+      for (int q = 0; q < num - i; q++) L[num - q] = L[num - 1 - q];
+      if (i <= num) {
+        L[i].score = cs;
+        L[i].x = x;
+        L[i].y = y;
+        L[i].z = z;
+        L[i].mode = mode;
+      }
+      break;
+    }
+  }
+}
+
+// general rank: one wave per model scans the scores in (mode, z, y, x) order, eight
+// 64-position chunks per load batch; only candidates above the current rank-th score
+// (lists only grow) reach the serial update.
 __global__ __launch_bounds__(64) void replay_kernel(const double* __restrict__ scores,
                                                     ReplayModes modes, int rank, int r1,
-                                                    int r2, int r3,
-                                                    c3h_det* __restrict__ lists) {
+                                                    int r2, int r3, int clean,
+                                                    c3h_det* __restrict__ lists,
+                                                    c3h_det* __restrict__ out2) {
   extern __shared__ __attribute__((aligned(16))) c3h_det L[];
   const int m = blockIdx.x, lane = threadIdx.x;
   c3h_det* gl = lists + (int64_t)m * rank;
-  for (int i = lane; i < rank; i += 64) L[i] = gl[i];
+  for (int i = lane; i < rank; i += 64) {
+    c3h_det e = gl[i];
+    if (clean) {
+      e.score = 0.0;
+      e.x = e.y = e.z = 0;
+    }
+    L[i] = e;
+  }
   __syncthreads();
   for (int mi = 0; mi < modes.n; ++mi) {
     const ReplayMode md = modes.m[mi];
     int xr, yr, zr;
     get_range(md.mode, r1, r2, r3, xr, yr, zr);
     const double* sc = scores + md.offset + (int64_t)m * md.P;
-    for (int64_t base = 0; base < md.P; base += 64) {
-      const int64_t p = base + lane;
-      const double s = p < md.P ? sc[p] : -1.0;
-      double T = L[rank - 1].score;
-      unsigned long long mask = __ballot(s > T);
-      while (mask) {
-        const int j = __ffsll((long long)mask) - 1;
-        const double cs = __shfl(s, j, 64);
-        if (lane == 0) {
-          const int64_t pc = base + j;
-          const int x = (int)(pc % md.xe), y = (int)((pc / md.xe) % md.ye),
-                    z = (int)(pc / ((int64_t)md.xe * md.ye));
-          for (int i = 0; i < rank; i++) {
-            if (cs > L[i].score) {
-              // checkOverlap (search.cpp:327-356)
-              int num;
-              for (num = 0; num < rank - 1; num++) {
-                int oxr, oyr, ozr;
-                get_range(L[num].mode, r1, r2, r3, oxr, oyr, ozr);
-                int v1 = L[num].x - x;
-                v1 = v1 < 0 ? -v1 - oxr : v1 - xr;
-                int v2 = L[num].y - y;
-                v2 = v2 < 0 ? -v2 - oyr : v2 - yr;
-                int v3 = L[num].z - z;
-                v3 = v3 < 0 ? -v3 - ozr : v3 - zr;
-                if (v1 <= 0 && v2 <= 0 && v3 <= 0) break;
-              }
-              for (int q = 0; q < num - i; q++) L[num - q] = L[num - 1 - q];
-              if (i <= num) {
-                L[i].score = cs;
-                L[i].x = x;
-                L[i].y = y;
-                L[i].z = z;
-                L[i].mode = md.mode;
-              }
-              break;
-            }
+    for (int64_t b0 = 0; b0 < md.P; b0 += 512) {
+      double s[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t p = b0 + 64 * j + lane;
+        s[j] = p < md.P ? sc[p] : -1.0;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t base = b0 + 64 * j;
+        double T = L[rank - 1].score;
+        unsigned long long mask = __ballot(s[j] > T);
+        while (mask) {
+          const int jl = __ffsll((long long)mask) - 1;
+          const double cs = __shfl(s[j], jl, 64);
+          if (lane == 0) {
+            const int64_t pc = base + jl;
+            rank_update(L, rank, cs, (int)(pc % md.xe), (int)((pc / md.xe) % md.ye),
+                        (int)(pc / ((int64_t)md.xe * md.ye)), md.mode, xr, yr, zr, r1, r2, r3);
           }
+          __syncthreads();
+          T = L[rank - 1].score;
+          const unsigned long long later = jl >= 63 ? 0ull : (~0ull << (jl + 1));
+          mask = __ballot(s[j] > T) & later;
         }
-        __syncthreads();
-        T = L[rank - 1].score;
-        const unsigned long long later = j >= 63 ? 0ull : (~0ull << (j + 1));
-        mask = __ballot(s > T) & later;
       }
     }
   }
   __syncthreads();
-  for (int i = lane; i < rank; i += 64) gl[i] = L[i];
+  for (int i = lane; i < rank; i += 64) {
+    gl[i] = L[i];
+    if (out2) out2[(int64_t)m * rank + i] = L[i];
+  }
 }
 
-// cleanMax on the device copy of the lists: score and x,y,z to 0, modes kept
-__global__ void clean_lists_kernel(c3h_det* __restrict__ L, int n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) {
-    L[i].score = 0.0;
-    L[i].x = 0;
-    L[i].y = 0;
-    L[i].z = 0;
+// rank 1: the update reduces to "first strictly greater maximum in scan order"
+// (checkOverlap returns slot 0 when rank_num == 1), so the per-block partials of the
+// score kernel are reduced with (score desc, scan order asc) and applied to slot 0.
+__global__ __launch_bounds__(kBlock) void argmax_replay_kernel(
+    const ScorePartial* __restrict__ partials, int64_t nparts, const uint32_t* __restrict__ nlist,
+    ReplayModes modes, int M, int clean, c3h_det* __restrict__ lists,
+    c3h_det* __restrict__ out2) {
+  if (nlist) nparts = ((int64_t)*nlist + kFP - 1) / kFP;  // sparse search: blocks that ran
+  __shared__ double s_sc[kBlock / 64];
+  __shared__ long long s_or[kBlock / 64];
+  const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  double best = -2.0;
+  long long bo = -1;
+  for (int64_t i = tid; i < nparts; i += kBlock) {
+    const ScorePartial q = partials[i * M + m];
+    if (q.order >= 0 && (q.score > best || (q.score == best && q.order < bo))) {
+      best = q.score;
+      bo = q.order;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double os = __shfl_xor(best, o, 64);
+    const long long oo = __shfl_xor(bo, o, 64);
+    if (oo >= 0 && (os > best || (os == best && (bo < 0 || oo < bo)))) {
+      best = os;
+      bo = oo;
+    }
+  }
+  if (lane == 0) {
+    s_sc[w] = best;
+    s_or[w] = bo;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int i = 1; i < kBlock / 64; ++i)
+      if (s_or[i] >= 0 && (s_sc[i] > best || (s_sc[i] == best && (bo < 0 || s_or[i] < bo)))) {
+        best = s_sc[i];
+        bo = s_or[i];
+      }
+    c3h_det e = lists[m];
+    if (clean) {
+      e.score = 0.0;
+      e.x = e.y = e.z = 0;
+    }
+    if (bo >= 0 && best > e.score) {
+      const int mi = (int)(bo >> 40);
+      const int64_t p = bo & ((1ll << 40) - 1);
+      const ReplayMode md = modes.m[mi];
+      e.score = best;
+      e.x = (int)(p % md.xe);
+      e.y = (int)((p / md.xe) % md.ye);
+      e.z = (int)(p / ((int64_t)md.xe * md.ye));
+      e.mode = md.mode;
+    }
+    lists[m] = e;
+    if (out2) out2[m] = e;
   }
 }
 
 }  // namespace
 
-hipError_t launch_clean_lists(c3h_det* lists, int n, hipStream_t s) {
-  clean_lists_kernel<<<(n + 255) / 256, 256, 0, s>>>(lists, n);
-  return hipGetLastError();
-}
-
 hipError_t launch_compress(const float* feat, int64_t H, int F, const float* axis_pt, int D,
-                           int Dpad, const float* fmax, int fmax_len, float* G, hipStream_t s) {
+                           int Dpad, const float* fmax, int fmax_len, float* G,
+                           const int32_t* rows, const uint32_t* nrows, hipStream_t s) {
+  if (rows && Dpad <= 128 && ((size_t)kRK * Dpad + (size_t)kRR * F) * 4 <= 65536) {  // sparse list
+    const size_t lds = sizeof(float) * ((size_t)kRK * Dpad + (size_t)kRR * F);
+    compress_rows_kernel<<<(unsigned)((H + kRR - 1) / kRR), kBlock, lds, s>>>(
+        feat, F, axis_pt, D, Dpad, fmax, fmax_len, G, rows, nrows);
+    return hipGetLastError();
+  }
   dim3 grid((unsigned)((H + kCM - 1) / kCM), (unsigned)((Dpad + kCN - 1) / kCN));
-  compress_kernel<<<grid, kBlock, 0, s>>>(feat, H, F, axis_pt, D, Dpad, fmax, fmax_len, G);
+  compress_kernel<<<grid, kCT, 0, s>>>(feat, H, F, axis_pt, D, Dpad, fmax, fmax_len, G, rows, nrows);
   return hipGetLastError();
 }
 
@@ -271,10 +670,20 @@ size_t score_lds_bytes(int D, int r, int SP) {
   return sizeof(float) * ((size_t)SP * (D + 1) + (size_t)r * SP + SP) + sizeof(int) * SP;
 }
 
+bool score_fast_ok(int D, int Opad) { return D <= 256 && (D & 3) == 0 && Opad <= 256; }
+
+int64_t score_blocks(const ScoreLaunch& a) {
+  const int64_t P = (int64_t)a.xe * a.ye * a.ze;
+  if (score_fast_ok(a.D, a.Opad)) return (P + kFP - 1) / kFP;
+  return a.D <= 256 ? (P + 63) / 64 : (P + 15) / 16;
+}
+
 hipError_t launch_score(const ScoreLaunch& a, hipStream_t s) {
   const int64_t P = (int64_t)a.xe * a.ye * a.ze;
   if (P <= 0) return hipSuccess;
-  if (a.D <= 256) {
+  if (score_fast_ok(a.D, a.Opad)) {
+    return hipErrorInvalidValue;  // the fast path is the sparse search (launch_sparse_search)
+  } else if (a.D <= 256) {
     score_kernel<64><<<(unsigned)((P + 63) / 64), kBlock, score_lds_bytes(a.D, a.r, 64), s>>>(a, P);
   } else {
     score_kernel<16><<<(unsigned)((P + 15) / 16), kBlock, score_lds_bytes(a.D, a.r, 16), s>>>(a, P);
@@ -282,9 +691,31 @@ hipError_t launch_score(const ScoreLaunch& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+int64_t sparse_score_blocks(const SparseSearch& a) { return (a.pstart[a.nmodes] + kFP - 1) / kFP; }
+
+hipError_t launch_sparse_search(const SparseSearch& a, hipStream_t s) {
+  const int64_t ptot = a.pstart[a.nmodes];
+  if (ptot <= 0) return hipSuccess;
+  gate_kernel<<<(unsigned)((ptot + kBlock - 1) / kBlock), kBlock, 0, s>>>(a);
+  const size_t region = std::max((size_t)a.D * kFP + 16 * (size_t)a.Opad, (size_t)kFP * (a.Opad + 1));
+  const size_t lds = sizeof(float) * (region + kFP) + sizeof(int) * 4 * kFP + sizeof(long long) * kFP +
+                     sizeof(double) * kFP * a.M + 16;
+  score_list_kernel<<<(unsigned)sparse_score_blocks(a), kBlock, lds, s>>>(a);
+  return hipGetLastError();
+}
+
 hipError_t launch_replay(const double* scores, const ReplayModes& modes, int M, int rank,
-                         int r1, int r2, int r3, c3h_det* lists, hipStream_t s) {
-  replay_kernel<<<M, 64, sizeof(c3h_det) * rank, s>>>(scores, modes, rank, r1, r2, r3, lists);
+                         int r1, int r2, int r3, int clean, c3h_det* lists, c3h_det* out2,
+                         hipStream_t s) {
+  replay_kernel<<<M, 64, sizeof(c3h_det) * rank, s>>>(scores, modes, rank, r1, r2, r3, clean,
+                                                      lists, out2);
+  return hipGetLastError();
+}
+
+hipError_t launch_argmax_replay(const ScorePartial* partials, int64_t nparts,
+                                const uint32_t* nlist, const ReplayModes& modes, int M, int clean,
+                                c3h_det* lists, c3h_det* out2, hipStream_t s) {
+  argmax_replay_kernel<<<M, kBlock, 0, s>>>(partials, nparts, nlist, modes, M, clean, lists, out2);
   return hipGetLastError();
 }
 

@@ -60,13 +60,31 @@ __global__ __launch_bounds__(kBlock) void minmax_kernel(const float4* __restrict
     mx[a] = wave_reduce(mx[a], umax);
   }
   cnt = wave_reduce(cnt, uadd);
+  // block reduction in LDS, then one set of atomics per block (same-address atomics
+  // from every wave serialise at the memory side)
+  __shared__ uint32_t red[kBlock / 64][7];
+  const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
-#pragma unroll
     for (int a = 0; a < 3; ++a) {
-      atomicMin(&out[a], mn[a]);
-      atomicMax(&out[3 + a], mx[a]);
+      red[w][a] = mn[a];
+      red[w][3 + a] = mx[a];
     }
-    atomicAdd(reinterpret_cast<unsigned long long*>(out + 6), (unsigned long long)cnt);
+    red[w][6] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < kBlock / 64; ++i) {
+      for (int a = 0; a < 3; ++a) {
+        red[0][a] = umin(red[0][a], red[i][a]);
+        red[0][3 + a] = umax(red[0][3 + a], red[i][3 + a]);
+      }
+      red[0][6] += red[i][6];
+    }
+    for (int a = 0; a < 3; ++a) {
+      atomicMin(&out[a], red[0][a]);
+      atomicMax(&out[3 + a], red[0][3 + a]);
+    }
+    atomicAdd(reinterpret_cast<unsigned long long*>(out + 6), (unsigned long long)red[0][6]);
   }
 }
 
@@ -252,7 +270,7 @@ int grid_for(int64_t n, int cap = 4096) {
 
 hipError_t launch_minmax(const float4* pts, int64_t n, float z_limit, uint32_t* out,
                          hipStream_t s) {
-  minmax_kernel<<<grid_for(n), kBlock, 0, s>>>(pts, n, z_limit, out);
+  minmax_kernel<<<grid_for(n, 512), kBlock, 0, s>>>(pts, n, z_limit, out);
   return hipGetLastError();
 }
 

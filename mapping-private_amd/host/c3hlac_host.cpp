@@ -1,0 +1,468 @@
+// c3hlac_host.cpp -- the reference-named C++ facade over the C-ABI (see c3hlac_host.h).
+#include "c3hlac_host.h"
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+
+namespace c3hlac {
+
+namespace {
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void grid_info(const Context& ctx, c3h_grid_info* info) {
+  ctx.check(c3h_get_grid_info(ctx.get(), info), "c3h_get_grid_info");
+}
+
+Vector3i v3(const int32_t* p) {
+  Vector3i v;
+  v[0] = p[0];
+  v[1] = p[1];
+  v[2] = p[2];
+  return v;
+}
+
+// extractC3HLACSignature{981,117} body (c3_hlac_tools.hpp:134-160, 169-195): the silent
+// empty cases of setVoxelFilter / computeFeature leave `feature` empty and still return
+// getSubdivNum().
+Vector3i extract(VoxelGrid& grid, int variant, std::vector<std::vector<float> >& feature, int thr_r,
+                 int thr_g, int thr_b, float voxel_size, int subdiv, int ox, int oy, int oz,
+                 bool lut_double) {
+  feature.resize(0);
+  if (grid.leaf() != 0.0f && voxel_size != grid.leaf())
+    throw Error(C3H_ERR_ARG, "extractC3HLACSignature: voxel_size differs from the grid's leaf size");
+  c3h_extract_params p;
+  p.variant = variant;
+  p.thr[0] = thr_r;
+  p.thr[1] = thr_g;
+  p.thr[2] = thr_b;
+  p.subdiv = subdiv;
+  p.offset[0] = ox;
+  p.offset[1] = oy;
+  p.offset[2] = oz;
+  p.lut_double = lut_double ? 1 : 0;
+  int32_t sb[3];
+  int64_t hist_num = 0;
+  const Context& ctx = grid.context();
+  ctx.check(c3h_extract(ctx.get(), &p, sb, &hist_num), "c3h_extract");
+  if (hist_num > 0) {
+    std::vector<float> flat((size_t)hist_num * variant);
+    ctx.check(c3h_get_features(ctx.get(), flat.data(), 0), "c3h_get_features");
+    feature.resize((size_t)hist_num);
+    for (int64_t h = 0; h < hist_num; ++h)
+      feature[h].assign(flat.begin() + h * variant, flat.begin() + (h + 1) * variant);
+  }
+  return v3(sb);
+}
+
+// Param::readParam (param.cpp:200-222): first "key value" pair whose key matches.
+template <typename T>
+bool read_param(const char* filename, const char* key, T& val) {
+  std::ifstream in(filename);
+  if (!in) return false;
+  std::string tok;
+  while (in >> tok) {
+    if (tok == key) {
+      std::string v;
+      if (!(in >> v)) return false;
+      std::istringstream vs(v);
+      return (bool)(vs >> val);
+    }
+  }
+  return false;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------- Context
+Context::Context(int hip_device) {
+  c3h_ctx* c = nullptr;
+  const int rc = c3h_create(hip_device, &c);
+  if (rc != C3H_OK) throw Error(rc, "c3h_create failed (no HIP device or library not built?)");
+  ctx_.reset(c, c3h_destroy);
+}
+
+void Context::check(int rc, const char* what) const {
+  if (rc < 0) {
+    const char* m = c3h_last_error(ctx_.get());
+    throw Error(rc, std::string(what) + ": " + (m ? m : ""));
+  }
+}
+
+void Context::setStream(void* s) { check(c3h_set_stream(get(), s), "c3h_set_stream"); }
+void Context::synchronize() { check(c3h_synchronize(get()), "c3h_synchronize"); }
+
+// ------------------------------------------------------------------------- VoxelGrid
+void VoxelGrid::setLeafSize(float lx, float ly, float lz) {
+  if (lx != ly || ly != lz) throw Error(C3H_ERR_ARG, "VoxelGrid: anisotropic leaves are not supported");
+  leaf_ = lx;
+}
+
+Vector3i VoxelGrid::getNrDivisions() const {
+  c3h_grid_info i;
+  grid_info(ctx_, &i);
+  return v3(i.div_b);
+}
+Vector3i VoxelGrid::getMinBoxCoordinates() const {
+  c3h_grid_info i;
+  grid_info(ctx_, &i);
+  return v3(i.min_b);
+}
+Vector3i VoxelGrid::getMaxBoxCoordinates() const {
+  c3h_grid_info i;
+  grid_info(ctx_, &i);
+  return v3(i.max_b);
+}
+
+std::vector<int> VoxelGrid::getLeafLayout() const {
+  const Vector3i d = getNrDivisions();
+  std::vector<int> out((size_t)d[0] * d[1] * d[2]);
+  ctx_.check(c3h_get_leaf_layout(ctx_.get(), out.data(), 0), "c3h_get_leaf_layout");
+  return out;
+}
+
+void VoxelGrid::setPackedGrid(const uint32_t* words, const Vector3i& div_b, const Vector3i& min_b,
+                              float leaf, bool on_device) {
+  ctx_.check(c3h_set_grid(ctx_.get(), words, div_b.v, min_b.v, leaf, on_device ? 1 : 0), "c3h_set_grid");
+  leaf_ = leaf;
+}
+
+std::vector<uint32_t> VoxelGrid::getPackedGrid() const {
+  const Vector3i d = getNrDivisions();
+  std::vector<uint32_t> out((size_t)d[0] * d[1] * d[2]);
+  ctx_.check(c3h_get_grid(ctx_.get(), out.data(), 0), "c3h_get_grid");
+  return out;
+}
+
+void getVoxelGrid(VoxelGrid& grid, const std::vector<PointXYZRGB>& input,
+                  std::vector<PointXYZRGB>& output, float voxel_size, float z_limit) {
+  static_assert(sizeof(PointXYZRGB) == 16, "xyzrgb record must be 4 floats");
+  grid.leaf_ = voxel_size;
+  c3h_grid_info info;
+  grid.ctx_.check(c3h_voxelize(grid.ctx_.get(), reinterpret_cast<const float*>(input.data()),
+                               (int64_t)input.size(), 0, voxel_size, z_limit, &info),
+                  "c3h_voxelize");
+  output.resize((size_t)info.n_occ);
+  if (info.n_occ > 0)
+    grid.ctx_.check(c3h_get_downsampled(grid.ctx_.get(), reinterpret_cast<float*>(output.data()), 0),
+                    "c3h_get_downsampled");
+}
+
+Vector3i extractC3HLACSignature981(VoxelGrid& grid, std::vector<std::vector<float> >& feature, int r,
+                                   int g, int b, float voxel_size, int subdiv, int ox, int oy, int oz,
+                                   bool lut_double) {
+  return extract(grid, C3H_VARIANT_981, feature, r, g, b, voxel_size, subdiv, ox, oy, oz, lut_double);
+}
+void extractC3HLACSignature981(VoxelGrid& grid, std::vector<float>& feature, int r, int g, int b,
+                               float voxel_size, bool lut_double) {
+  std::vector<std::vector<float> > tmp;
+  extract(grid, C3H_VARIANT_981, tmp, r, g, b, voxel_size, 0, 0, 0, 0, lut_double);
+  feature = tmp.empty() ? std::vector<float>() : tmp[0];
+}
+Vector3i extractC3HLACSignature117(VoxelGrid& grid, std::vector<std::vector<float> >& feature, int r,
+                                   int g, int b, float voxel_size, int subdiv, int ox, int oy, int oz,
+                                   bool lut_double) {
+  return extract(grid, C3H_VARIANT_117, feature, r, g, b, voxel_size, subdiv, ox, oy, oz, lut_double);
+}
+void extractC3HLACSignature117(VoxelGrid& grid, std::vector<float>& feature, int r, int g, int b,
+                               float voxel_size, bool lut_double) {
+  std::vector<std::vector<float> > tmp;
+  extract(grid, C3H_VARIANT_117, tmp, r, g, b, voxel_size, 0, 0, 0, 0, lut_double);
+  feature = tmp.empty() ? std::vector<float>() : tmp[0];
+}
+
+// ------------------------------------------------------------------------- PCA
+void PCA::read(const char* filename, bool ascii) {
+  // c3h_pca_read returns the axis column-major (eigenvector i contiguous), as the file
+  int32_t has_mean = 0;
+  int dim = c3h_pca_read(filename, ascii ? 1 : 0, nullptr, nullptr, nullptr, &has_mean, 0);
+  if (dim < 0) throw Error(dim, std::string("PCA::read: cannot read ") + filename);
+  std::vector<float> col((size_t)dim * dim), var(dim), mean(dim);
+  dim = c3h_pca_read(filename, ascii ? 1 : 0, col.data(), var.data(), mean.data(), &has_mean, dim);
+  if (dim < 0) throw Error(dim, std::string("PCA::read: malformed ") + filename);
+  axis_ = MatrixXf(dim, dim);
+  for (int i = 0; i < dim; ++i)
+    for (int j = 0; j < dim; ++j) axis_(j, i) = col[(size_t)i * dim + j];
+  variance_ = var;
+  mean_flg_ = has_mean != 0;
+  if (mean_flg_) mean_ = mean;
+  else mean_.clear();
+}
+
+const std::vector<float>& PCA::getMean() const {
+  if (!mean_flg_) throw Error(C3H_ERR_STATE, "PCA::getMean: no mean vector in the file");
+  return mean_;
+}
+
+// ------------------------------------------------------------------------- Param
+float Param::readVoxelSize(const char* f) {
+  float v;
+  return read_param(f, "voxel_size:", v) && v > 0 ? v : -1.0f;
+}
+int Param::readDim(const char* f) {
+  int v;
+  return read_param(f, "dim:", v) && v >= 1 ? v : -1;
+}
+int Param::readBoxSizeScene(const char* f) {
+  int v;
+  return read_param(f, "box_size(scene):", v) && v >= 1 ? v : -1;
+}
+int Param::readBoxSizeModel(const char* f) {
+  int v;
+  return read_param(f, "box_size(model):", v) && v >= 1 ? v : -1;
+}
+int Param::readRotateNum(const char* f) {
+  int v;
+  return read_param(f, "rotate_num:", v) && v >= 1 ? v : -1;
+}
+int Param::readC3HLACFlag(const char* f) {
+  int v;
+  return read_param(f, "c3_hlac_flg:", v) ? v : -1;
+}
+void Param::readColorThreshold(int& r, int& g, int& b, const char* f) {
+  std::ifstream in(f);
+  if (!in || !(in >> r >> g >> b)) throw Error(C3H_ERR_NOTFOUND, std::string("Param::readColorThreshold: ") + f);
+}
+
+// ------------------------------------------------------------------------- SearchObj
+void SearchObj::setRange(int r1, int r2, int r3) {
+  range_[0] = r1;
+  range_[1] = r2;
+  range_[2] = r3;
+}
+
+void SearchObj::setRank(int rank_num) {
+  rank_ = rank_num;
+  ctx_.check(c3h_set_rank(ctx_.get(), rank_num), "c3h_set_rank");
+  dets_.assign((size_t)model_num_ * rank_, c3h_det{0.0, 0, 0, 0, C3H_S_MODE_1});
+}
+
+// readAxis (search.cpp:153-165): the first dim_model eigenvectors as rows; rows i >= 1
+// scaled by sqrt(var_i)/sqrt(var_0) over the first `dim` columns (double arithmetic).
+static MatrixXf read_model_axis(const char* filename, int dim, int dim_model, bool ascii, bool ms) {
+  PCA pca;
+  pca.read(filename, ascii);
+  const MatrixXf& a = pca.getAxis();
+  if (dim_model > a.cols) throw Error(C3H_ERR_ARG, "readAxis: dim_model exceeds the PCA dimension");
+  MatrixXf q(dim_model, a.rows);
+  for (int i = 0; i < dim_model; ++i)
+    for (int j = 0; j < a.rows; ++j) q(i, j) = a(j, i);
+  if (ms) {
+    const std::vector<float>& v = pca.getVariance();
+    for (int i = 1; i < dim_model; ++i)
+      for (int j = 0; j < dim && j < a.rows; ++j)
+        q(i, j) = (float)((double)q(i, j) * std::sqrt((double)v[i]) / std::sqrt((double)v[0]));
+  }
+  return q;
+}
+
+void SearchObj::readAxis(const char* filename, int dim, int dim_model, bool ascii, bool ms) {
+  axis_q_.assign(1, read_model_axis(filename, dim, dim_model, ascii, ms));
+  model_dim_ = dim_model;
+  setup_dirty_ = true;
+}
+
+void SearchObj::getRange(int& xr, int& yr, int& zr, SearchMode mode) const {
+  xr = xRange(mode);
+  yr = yRange(mode);
+  zr = zRange(mode);
+}
+
+// xRange / yRange / zRange (search.cpp:260-317)
+int SearchObj::xRange(SearchMode m) const {
+  switch (m) {
+    case S_MODE_1: case S_MODE_2: return range_[0];
+    case S_MODE_3: case S_MODE_4: return range_[1];
+    case S_MODE_5: case S_MODE_6: return range_[2];
+  }
+  return 0;
+}
+int SearchObj::yRange(SearchMode m) const {
+  switch (m) {
+    case S_MODE_3: case S_MODE_5: return range_[0];
+    case S_MODE_1: case S_MODE_6: return range_[1];
+    case S_MODE_2: case S_MODE_4: return range_[2];
+  }
+  return 0;
+}
+int SearchObj::zRange(SearchMode m) const {
+  switch (m) {
+    case S_MODE_4: case S_MODE_6: return range_[0];
+    case S_MODE_2: case S_MODE_5: return range_[1];
+    case S_MODE_1: case S_MODE_3: return range_[2];
+  }
+  return 0;
+}
+
+const c3h_det& SearchObj::det(int m, int num) const {
+  const size_t i = (size_t)m * rank_ + num;
+  if (m < 0 || m >= model_num_ || num < 0 || num >= rank_ || i >= dets_.size())
+    throw Error(C3H_ERR_ARG, "SearchObj: detection index out of range");
+  return dets_[i];
+}
+
+void SearchObj::setSceneAxis(const MatrixXf& axis) {
+  axis_p_ = axis;
+  compress_ = true;
+  setup_dirty_ = true;
+}
+
+// setSceneAxis with whitening (search.cpp:701-712): row i scaled by float(1/sqrt(var_i))
+void SearchObj::setSceneAxis(const MatrixXf& axis, const std::vector<float>& var, int dim) {
+  (void)dim;
+  if ((int)var.size() < axis.rows) throw Error(C3H_ERR_ARG, "setSceneAxis: variance shorter than the axis");
+  axis_p_ = axis;
+  for (int i = 0; i < axis.rows; ++i) {
+    const float s = (float)(1 / std::sqrt((double)var[i]));
+    for (int j = 0; j < axis.cols; ++j) axis_p_(i, j) = s * axis_p_(i, j);
+  }
+  compress_ = true;
+  setup_dirty_ = true;
+}
+
+void SearchObj::setNormalizeVal(const char* filename) {
+  std::ifstream in(filename);
+  if (!in) throw Error(C3H_ERR_NOTFOUND, std::string("setNormalizeVal: ") + filename);
+  float v;
+  while (in >> v) feature_max_.push_back(v);
+  setup_dirty_ = true;
+}
+
+void SearchObj::cleanMax() {
+  ctx_.check(c3h_clean_max(ctx_.get()), "c3h_clean_max");
+  for (auto& d : dets_) {
+    d.score = 0.0;
+    d.x = d.y = d.z = 0;
+  }
+}
+
+void SearchObj::cleanData() {
+  xn_ = yn_ = zn_ = 0;
+  cleanMax();
+}
+
+void SearchObj::ensureSetup(int F) {
+  if (!setup_dirty_) return;
+  if (axis_q_.empty()) throw Error(C3H_ERR_STATE, "SearchObj: readAxis has not been called");
+  const int M = (int)axis_q_.size(), r = model_dim_;
+  const int D = compress_ ? axis_p_.rows : F;
+  if (compress_ && axis_p_.cols != F)
+    throw Error(C3H_ERR_ARG, "SearchObj: scene axis width differs from the feature dimension");
+  std::vector<float> q((size_t)M * r * D, 0.0f);
+  for (int m = 0; m < M; ++m) {
+    if (axis_q_[m].cols < D) throw Error(C3H_ERR_ARG, "SearchObj: model axis narrower than D");
+    for (int i = 0; i < r; ++i)
+      for (int d = 0; d < D; ++d) q[((size_t)m * r + i) * D + d] = axis_q_[m](i, d);
+  }
+  ctx_.check(c3h_search_setup(ctx_.get(), compress_ ? axis_p_.data.data() : nullptr, nullptr, D, F,
+                              q.data(), M, r, feature_max_.empty() ? nullptr : feature_max_.data(),
+                              (int)feature_max_.size()),
+             "c3h_search_setup");
+  if (rank_ < 1) setRank(1);
+  else ctx_.check(c3h_set_rank(ctx_.get(), rank_), "c3h_set_rank");
+  dets_.assign((size_t)model_num_ * rank_, c3h_det{0.0, 0, 0, 0, C3H_S_MODE_1});
+  setup_dirty_ = false;
+}
+
+void SearchObj::setDataFromContext(const Vector3i& subdiv_b) {
+  xn_ = subdiv_b[0];
+  yn_ = subdiv_b[1];
+  zn_ = subdiv_b[2];
+}
+
+void SearchObj::run(bool rotate, bool remove_overlap) {
+  const double t0 = now_s();
+  const int M = (int)axis_q_.size();
+  std::vector<c3h_det> out((size_t)std::max(M, 1) * std::max(rank_, 1));
+  const int rc = c3h_search(ctx_.get(), range_, threshold_, rotate ? 1 : 0, remove_overlap ? 1 : 0,
+                            out.data());
+  ctx_.check(rc, "c3h_search");
+  if (rc > 0) dets_ = out;
+  search_time = now_s() - t0;
+}
+
+void SearchObj::search() { run(true, false); }
+void SearchObj::searchWithoutRotation() { run(false, false); }
+
+// writeResult (search.cpp:662-679)
+void SearchObj::writeResult(const char* filename, int box_size) {
+  FILE* fp = fopen(filename, "w");
+  if (!fp) throw Error(C3H_ERR_NOTFOUND, std::string("writeResult: ") + filename);
+  for (int r = 0; r < rank_; ++r) {
+    const c3h_det& d = det(0, r);
+    if (d.score == 0) break;
+    int xr, yr, zr;
+    getRange(xr, yr, zr, (SearchMode)d.mode);
+    fprintf(fp, "%d %d %d %d %d %d %f\n", d.x * box_size, xr * box_size, d.y * box_size,
+            yr * box_size, d.z * box_size, zr * box_size, d.score);
+  }
+  fprintf(fp, "time: %f\n", search_time);
+  fclose(fp);
+}
+
+// ------------------------------------------------------------------------- SearchObjMulti
+void SearchObjMulti::setRank(int rank_num) { SearchObj::setRank(rank_num); }
+
+void SearchObjMulti::readAxis(char** filename, int dim, int dim_model, bool ascii, bool ms) {
+  axis_q_.clear();
+  for (int m = 0; m < model_num_; ++m)
+    axis_q_.push_back(read_model_axis(filename[m], dim, dim_model, ascii, ms));
+  model_dim_ = dim_model;
+  setup_dirty_ = true;
+}
+
+// removeOverlap (search.cpp:972-992) on the lists of the last search
+void SearchObjMulti::removeOverlap() {
+  if (dets_.empty()) return;
+  ctx_.check(c3h_remove_overlap(model_num_, rank_, range_, dets_.data()), "c3h_remove_overlap");
+}
+
+// SearchObjMulti::cleanData (search.cpp:760-770) keeps the lists
+void SearchObjMulti::cleanData() { xn_ = yn_ = zn_ = 0; }
+
+// ------------------------------------------------------------------------- setC3HLAC
+static void set_c3hlac(SearchObj& so, int F, int thr_r, int thr_g, int thr_b, const VoxelGrid& grid,
+                       double voxel_size, int subdiv) {
+  const Context& ctx = so.context();
+  // bind the grid's device buffer into the search context without a copy
+  const uint32_t* words = nullptr;
+  grid.context().check(c3h_grid_device_ptr(grid.context().get(), &words), "c3h_grid_device_ptr");
+  c3h_grid_info gi;
+  grid_info(grid.context(), &gi);
+  if ((float)voxel_size != gi.leaf)
+    throw Error(C3H_ERR_ARG, "setC3HLAC: voxel_size differs from the grid's leaf size");
+  ctx.check(c3h_set_grid(ctx.get(), words, gi.div_b, gi.min_b, gi.leaf, 1), "c3h_set_grid");
+  c3h_extract_params p;
+  p.variant = F;
+  p.thr[0] = thr_r;
+  p.thr[1] = thr_g;
+  p.thr[2] = thr_b;
+  p.subdiv = subdiv;
+  p.offset[0] = p.offset[1] = p.offset[2] = 0;
+  p.lut_double = 1;
+  int32_t sb[3];
+  int64_t hist_num = 0;
+  ctx.check(c3h_extract(ctx.get(), &p, sb, &hist_num), "c3h_extract");
+  so.setDataFromContext(v3(sb));
+}
+
+void SearchC3HLAC::setC3HLAC(int dim, int r, int g, int b, const VoxelGrid& grid, double voxel_size,
+                             int subdiv) {
+  (void)dim;
+  ensureSetup(C3H_VARIANT_981);
+  set_c3hlac(*this, C3H_VARIANT_981, r, g, b, grid, voxel_size, subdiv);
+}
+
+void SearchC3HLACMulti::setC3HLAC(int dim, int r, int g, int b, const VoxelGrid& grid,
+                                  double voxel_size, int subdiv) {
+  (void)dim;
+  ensureSetup(C3H_VARIANT_981);
+  set_c3hlac(*this, C3H_VARIANT_981, r, g, b, grid, voxel_size, subdiv);
+}
+
+}  // namespace c3hlac

@@ -1,0 +1,250 @@
+// c3hlac_host.h -- C++ facade with the reference's API names over the C-ABI
+// (include/c3hlac_mi355x.h).  A caller of the reference's
+//   getVoxelGrid / extractC3HLACSignature981/117   (c3_hlac/include/c3_hlac/c3_hlac_tools.h:53-89)
+//   SearchObj / SearchObjMulti                     (color_voxel_recognition/include/color_voxel_recognition/search.h:53-270)
+//   SearchC3HLAC / SearchC3HLACMulti               (.../search_c3_hlac.h:44-88)
+//   PCA::read                                      (.../pca.h:60-72, src/pca.cpp:119-185)
+//   Param                                          (.../param.h, src/param.cpp:43-222)
+// switches by replacing the PCL/Eigen types with the small value types below.
+//
+// Differences that are deliberate (documented in INTEGRATION.md):
+//   - the voxel grid lives on the GPU: `VoxelGrid` owns a device context, and the
+//     downsampled cloud is only materialised when asked for (getVoxelGrid's `output`);
+//   - errors raise c3hlac::Error instead of exit()/stderr, except where the reference
+//     reports through a return value (setVoxelFilter's bool -> empty features, Param's -1);
+//   - SearchObj::search_time is measured on the host around the whole search call.
+#ifndef C3HLAC_HOST_H_
+#define C3HLAC_HOST_H_
+
+#include <cmath>
+#include <limits>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "c3hlac_mi355x.h"
+
+namespace c3hlac {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& what) : std::runtime_error(what), code(c) {}
+};
+
+// pcl::PointXYZRGB as stored in binary PCD files: rgb is the packed 0x00RRGGBB in the
+// float's bits (pcl_cloud layout minus the SSE padding).
+struct PointXYZRGB {
+  float x, y, z, rgb;
+};
+
+struct Vector3i {  // Eigen::Vector3i
+  int v[3] = {0, 0, 0};
+  int& operator[](int i) { return v[i]; }
+  int operator[](int i) const { return v[i]; }
+  int x() const { return v[0]; }
+  int y() const { return v[1]; }
+  int z() const { return v[2]; }
+};
+
+// Row-major dense float matrix (stand-in for Eigen::MatrixXf in the search API).
+struct MatrixXf {
+  int rows = 0, cols = 0;
+  std::vector<float> data;
+  MatrixXf() = default;
+  MatrixXf(int r, int c) : rows(r), cols(c), data((size_t)r * c, 0.0f) {}
+  float& operator()(int r, int c) { return data[(size_t)r * cols + c]; }
+  float operator()(int r, int c) const { return data[(size_t)r * cols + c]; }
+};
+
+// One device + one HIP stream (c3h_ctx); shared by the objects bound to it.
+class Context {
+ public:
+  explicit Context(int hip_device = 0);
+  c3h_ctx* get() const { return ctx_.get(); }
+  void check(int rc, const char* what) const;
+  void setStream(void* hip_stream);
+  void synchronize();
+
+ private:
+  std::shared_ptr<c3h_ctx> ctx_;
+};
+
+// pcl::VoxelGrid<PointXYZRGB> after filter(): the packed colour/occupancy grid on the GPU.
+class VoxelGrid {
+ public:
+  explicit VoxelGrid(int hip_device = 0) : ctx_(hip_device) {}
+  explicit VoxelGrid(const Context& ctx) : ctx_(ctx) {}
+  void setLeafSize(float lx, float ly, float lz);
+  void setSaveLeafLayout(bool) {}  // the leaf layout is always derivable (getLeafLayout)
+  Vector3i getNrDivisions() const;
+  Vector3i getMinBoxCoordinates() const;
+  Vector3i getMaxBoxCoordinates() const;
+  std::vector<int> getLeafLayout() const;
+  // the grid of an external producer (same packing as c3h_get_grid)
+  void setPackedGrid(const uint32_t* words, const Vector3i& div_b, const Vector3i& min_b, float leaf,
+                     bool on_device);
+  std::vector<uint32_t> getPackedGrid() const;
+  const Context& context() const { return ctx_; }
+  float leaf() const { return leaf_; }
+
+ private:
+  friend void getVoxelGrid(VoxelGrid&, const std::vector<PointXYZRGB>&, std::vector<PointXYZRGB>&,
+                           float, float);
+  Context ctx_;
+  float leaf_ = 0.0f;
+};
+
+// getVoxelGrid (c3_hlac_tools.hpp:124-130), with detect_object.cpp's limitPoint
+// (z >= z_limit or non-finite points dropped) folded in.
+void getVoxelGrid(VoxelGrid& grid, const std::vector<PointXYZRGB>& input,
+                  std::vector<PointXYZRGB>& output, float voxel_size,
+                  float z_limit = std::numeric_limits<float>::infinity());
+
+// extractC3HLACSignature981/117 (c3_hlac_tools.hpp:134-202).  `lut_double` selects the
+// setColor sin/cos evaluation (true = double, the reference build's default).
+Vector3i extractC3HLACSignature981(VoxelGrid& grid, std::vector<std::vector<float> >& feature,
+                                   int color_threshold_r, int color_threshold_g,
+                                   int color_threshold_b, float voxel_size,
+                                   int subdivision_size = 0, int offset_x = 0, int offset_y = 0,
+                                   int offset_z = 0, bool lut_double = true);
+void extractC3HLACSignature981(VoxelGrid& grid, std::vector<float>& feature, int color_threshold_r,
+                               int color_threshold_g, int color_threshold_b, float voxel_size,
+                               bool lut_double = true);
+Vector3i extractC3HLACSignature117(VoxelGrid& grid, std::vector<std::vector<float> >& feature,
+                                   int color_threshold_r, int color_threshold_g,
+                                   int color_threshold_b, float voxel_size,
+                                   int subdivision_size = 0, int offset_x = 0, int offset_y = 0,
+                                   int offset_z = 0, bool lut_double = true);
+void extractC3HLACSignature117(VoxelGrid& grid, std::vector<float>& feature, int color_threshold_r,
+                               int color_threshold_g, int color_threshold_b, float voxel_size,
+                               bool lut_double = true);
+
+// PCA file reader (pca.cpp:119-185).  getAxis() is dim x dim with eigenvector i in
+// column i, as Eigen holds it.
+class PCA {
+ public:
+  explicit PCA(bool mean_flg = true) : mean_flg_(mean_flg) {}
+  void read(const char* filename, bool ascii = false);
+  const MatrixXf& getAxis() const { return axis_; }
+  const std::vector<float>& getVariance() const { return variance_; }
+  const std::vector<float>& getMean() const;
+  int dim() const { return axis_.rows; }
+
+ private:
+  bool mean_flg_;
+  MatrixXf axis_;
+  std::vector<float> variance_, mean_;
+};
+
+// Param (param.h): the same keys, defaults and -1 error returns.
+struct Param {
+  static float readVoxelSize(const char* filename = "param/parameters.txt");
+  static int readDim(const char* filename = "param/parameters.txt");
+  static int readBoxSizeScene(const char* filename = "param/parameters.txt");
+  static int readBoxSizeModel(const char* filename = "param/parameters.txt");
+  static int readRotateNum(const char* filename = "param/parameters.txt");
+  static int readC3HLACFlag(const char* filename = "param/parameters.txt");
+  static void readColorThreshold(int& r, int& g, int& b,
+                                 const char* filename = "param/color_threshold.txt");
+};
+
+enum SearchMode { S_MODE_1, S_MODE_2, S_MODE_3, S_MODE_4, S_MODE_5, S_MODE_6 };
+
+// SearchObj (search.h:53-176): single-model sliding-box search.  The integral table and
+// scores live on the device; setC3HLAC extracts and binds the features in one call.
+class SearchObj {
+ public:
+  double search_time = 0.0;
+  explicit SearchObj(int hip_device = 0) : ctx_(hip_device) {}
+  explicit SearchObj(const Context& ctx) : ctx_(ctx) {}
+  virtual ~SearchObj() = default;
+
+  void setRange(int range1, int range2, int range3);
+  virtual void setRank(int rank_num);
+  void setThreshold(int exist_voxel_num_threshold) { threshold_ = exist_voxel_num_threshold; }
+  virtual void readAxis(const char* filename, int dim, int dim_model, bool ascii,
+                        bool multiple_similarity);
+  void getRange(int& xrange, int& yrange, int& zrange, SearchMode mode) const;
+  void search();
+  void searchWithoutRotation();
+  void writeResult(const char* filename, int box_size);
+  virtual void cleanMax();
+  void setSceneAxis(const MatrixXf& axis);
+  void setSceneAxis(const MatrixXf& axis, const std::vector<float>& var, int dim);
+  virtual void cleanData();
+  int XYnum() const { return xn_ * yn_; }
+  int Znum() const { return zn_; }
+  virtual int maxX(int num) const { return det(0, num).x; }
+  virtual int maxY(int num) const { return det(0, num).y; }
+  virtual int maxZ(int num) const { return det(0, num).z; }
+  virtual SearchMode maxMode(int num) const { return (SearchMode)det(0, num).mode; }
+  virtual double maxDot(int num) const { return det(0, num).score; }
+  virtual int maxXrange(int num) const { return xRange(maxMode(num)); }
+  virtual int maxYrange(int num) const { return yRange(maxMode(num)); }
+  virtual int maxZrange(int num) const { return zRange(maxMode(num)); }
+  void setNormalizeVal(const char* filename);
+
+  // setData (search.cpp:539-658) on features already extracted into this context
+  void setDataFromContext(const Vector3i& subdiv_b);
+  const Context& context() const { return ctx_; }
+  // all M x rank detections of the last search (model-major)
+  const std::vector<c3h_det>& detections() const { return dets_; }
+
+ protected:
+  Context ctx_;
+  int range_[3] = {1, 1, 1};
+  int rank_ = 0, threshold_ = 0, model_num_ = 1;
+  int xn_ = 0, yn_ = 0, zn_ = 0;
+  int model_dim_ = 0;                 // r
+  std::vector<MatrixXf> axis_q_;      // per model r x D
+  MatrixXf axis_p_;                   // D x F (already whitened when var given)
+  bool compress_ = false, setup_dirty_ = true;
+  std::vector<float> feature_max_;
+  std::vector<c3h_det> dets_;
+  int xRange(SearchMode m) const;
+  int yRange(SearchMode m) const;
+  int zRange(SearchMode m) const;
+  const c3h_det& det(int m, int num) const;
+  void ensureSetup(int F);
+  void run(bool rotate, bool remove_overlap);
+};
+
+// SearchObjMulti (search.h:181-270): M models scored per position, one list per model.
+class SearchObjMulti : public SearchObj {
+ public:
+  using SearchObj::SearchObj;
+  void setModelNum(int model_num) { model_num_ = model_num; }
+  void setRank(int rank_num) override;
+  void readAxis(char** filename, int dim, int dim_model, bool ascii, bool multiple_similarity);
+  int maxX(int m, int num) const { return det(m, num).x; }
+  int maxY(int m, int num) const { return det(m, num).y; }
+  int maxZ(int m, int num) const { return det(m, num).z; }
+  SearchMode maxMode(int m, int num) const { return (SearchMode)det(m, num).mode; }
+  double maxDot(int m, int num) const { return det(m, num).score; }
+  int maxXrange(int m, int num) const { return xRange(maxMode(m, num)); }
+  int maxYrange(int m, int num) const { return yRange(maxMode(m, num)); }
+  int maxZrange(int m, int num) const { return zRange(maxMode(m, num)); }
+  void removeOverlap();
+  void cleanData() override;
+};
+
+// SearchC3HLAC{,Multi}::setC3HLAC (search_c3_hlac.h:53-88): C3-HLAC-981 of the grid,
+// exist counts and setData, all on the device.  `cloud_downsampled` is not needed: the
+// packed grid carries each voxel's colour.
+class SearchC3HLAC : public SearchObj {
+ public:
+  using SearchObj::SearchObj;
+  void setC3HLAC(int dim, int color_threshold_r, int color_threshold_g, int color_threshold_b,
+                 const VoxelGrid& grid, double voxel_size, int subdivision_size);
+};
+class SearchC3HLACMulti : public SearchObjMulti {
+ public:
+  using SearchObjMulti::SearchObjMulti;
+  void setC3HLAC(int dim, int color_threshold_r, int color_threshold_g, int color_threshold_b,
+                 const VoxelGrid& grid, double voxel_size, int subdivision_size);
+};
+
+}  // namespace c3hlac
+
+#endif  // C3HLAC_HOST_H_

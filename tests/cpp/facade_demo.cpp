@@ -1,0 +1,121 @@
+// Drives the reference-named C++ facade (mapping-private_amd/host/c3hlac_host.h) the way
+// color_voxel_recognition/test/detect_object.cpp and detect_object_vosch_multi.cpp drive
+// the reference: Param -> PCA/readAxis/setSceneAxis -> getVoxelGrid -> setC3HLAC ->
+// search -> maxX/maxY/maxZ/maxDot.  Prints one JSON object on stdout.
+//   facade_demo params <param_dir> <models_dir>       (host only: Param + PCA readers)
+//   facade_demo run <xyzrgb.bin> <out_features.bin>   (GPU: the detection pipeline)
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <string>
+#include <vector>
+
+#include "c3hlac_host.h"
+
+using namespace c3hlac;
+
+static int params(const std::string& pdir, const std::string& mdir) {
+  const std::string pf = pdir + "/parameters.txt", cf = pdir + "/color_threshold.txt";
+  int r = 0, g = 0, b = 0;
+  Param::readColorThreshold(r, g, b, cf.c_str());
+  PCA pca_scene;
+  pca_scene.read((mdir + "/compress_axis").c_str(), false);
+  PCA pca_model;
+  pca_model.read((mdir + "/000/pca_result").c_str(), false);
+  printf("{\"voxel_size\": %.9g, \"dim\": %d, \"box_scene\": %d, \"box_model\": %d, \"rotate_num\": %d, "
+         "\"c3_hlac_flg\": %d, \"missing_key\": %d, \"thr\": [%d, %d, %d], \"scene_dim\": %d, "
+         "\"scene_axis_00\": %.9g, \"scene_axis_10\": %.9g, \"scene_var0\": %.9g, \"model_dim\": %d}\n",
+         Param::readVoxelSize(pf.c_str()), Param::readDim(pf.c_str()), Param::readBoxSizeScene(pf.c_str()),
+         Param::readBoxSizeModel(pf.c_str()), Param::readRotateNum(pf.c_str()),
+         Param::readC3HLACFlag(pf.c_str()), Param::readDim(cf.c_str()), r, g, b, pca_scene.dim(),
+         pca_scene.getAxis()(0, 0), pca_scene.getAxis()(1, 0), pca_scene.getVariance()[0], pca_model.dim());
+  return 0;
+}
+
+// synthetic models: identity-like bases written as PCA files so readAxis parses them
+static void write_pca(const char* path, int dim, unsigned seed) {
+  std::vector<float> axis((size_t)dim * dim, 0.0f), var(dim);
+  unsigned s = seed;
+  for (int i = 0; i < dim; ++i) {
+    for (int j = 0; j < dim; ++j) {
+      s = s * 1664525u + 1013904223u;
+      axis[(size_t)i * dim + j] = ((s >> 8) & 0xffff) / 65536.0f - 0.5f;  // column i
+    }
+    var[i] = 1.0f / (1 + i);
+  }
+  FILE* fp = fopen(path, "wb");
+  fwrite(&dim, 4, 1, fp);
+  fwrite(axis.data(), 4, axis.size(), fp);
+  fwrite(var.data(), 4, var.size(), fp);
+  fclose(fp);
+}
+
+static int run(const std::string& cloud_path, const std::string& feat_path) {
+  std::ifstream in(cloud_path, std::ios::binary);
+  std::vector<PointXYZRGB> cloud;
+  PointXYZRGB p;
+  while (in.read(reinterpret_cast<char*>(&p), sizeof(p))) cloud.push_back(p);
+
+  VoxelGrid grid(0);
+  std::vector<PointXYZRGB> down;
+  getVoxelGrid(grid, cloud, down, 0.01f);
+  const Vector3i div = grid.getNrDivisions();
+
+  std::vector<std::vector<float> > f981;
+  const Vector3i sb = extractC3HLACSignature981(grid, f981, 147, 146, 148, 0.01f, 8);
+  std::vector<float> whole117;
+  extractC3HLACSignature117(grid, whole117, 147, 146, 148, 0.01f);
+  {
+    std::ofstream out(feat_path, std::ios::binary);
+    for (auto& row : f981) out.write(reinterpret_cast<const char*>(row.data()), row.size() * 4);
+    out.write(reinterpret_cast<const char*>(whole117.data()), whole117.size() * 4);
+  }
+
+  // detect_object_vosch_multi-style search: 2 models, r = 4, compression 981 -> 16
+  const int D = 16, r = 4, M = 2;
+  std::string m0 = feat_path + ".m0", m1 = feat_path + ".m1";
+  write_pca(m0.c_str(), D, 7);
+  write_pca(m1.c_str(), D, 11);
+  MatrixXf axis(D, 981);
+  std::vector<float> var(D);
+  unsigned s = 3;
+  for (int i = 0; i < D; ++i) {
+    var[i] = 1.0f + i;
+    for (int j = 0; j < 981; ++j) {
+      s = s * 1664525u + 1013904223u;
+      axis(i, j) = ((s >> 8) & 0xffff) / 65536.0f - 0.5f;
+    }
+  }
+  SearchC3HLACMulti search(grid.context());
+  search.setModelNum(M);
+  search.setRank(1);
+  search.setThreshold(10);
+  search.setRange(2, 2, 1);
+  char* names[2] = {&m0[0], &m1[0]};
+  search.readAxis(names, D, r, false, true);
+  search.setSceneAxis(axis, var, D);
+  search.cleanData();
+  search.setC3HLAC(D, 147, 146, 148, grid, 0.01, 8);
+  search.search();
+  printf("{\"n_points\": %zu, \"n_occ\": %zu, \"div\": [%d, %d, %d], \"subdiv\": [%d, %d, %d], "
+         "\"hist_num\": %zu, \"n117\": %zu, \"xy\": %d, \"z\": %d, \"dets\": [",
+         cloud.size(), down.size(), div[0], div[1], div[2], sb[0], sb[1], sb[2], f981.size(),
+         whole117.size(), search.XYnum(), search.Znum());
+  for (int m = 0; m < M; ++m)
+    printf("%s[%.17g, %d, %d, %d, %d, %d]", m ? ", " : "", search.maxDot(m, 0), search.maxX(m, 0),
+           search.maxY(m, 0), search.maxZ(m, 0), (int)search.maxMode(m, 0), search.maxXrange(m, 0));
+  printf("]}\n");
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  try {
+    if (argc == 4 && !strcmp(argv[1], "params")) return params(argv[2], argv[3]);
+    if (argc == 4 && !strcmp(argv[1], "run")) return run(argv[2], argv[3]);
+  } catch (const Error& e) {
+    fprintf(stderr, "c3hlac::Error %d: %s\n", e.code, e.what());
+    return 2;
+  }
+  fprintf(stderr, "usage: facade_demo params <param_dir> <models_dir> | run <cloud.bin> <out.bin>\n");
+  return 1;
+}

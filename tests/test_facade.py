@@ -1,0 +1,108 @@
+"""The reference-named C++ facade (mapping-private_amd/host/c3hlac_host.h), driven by
+tests/cpp/facade_demo.cpp the way detect_object*.cpp drive the reference.
+
+CPU: the facade compiles and links against the C-ABI library; Param / PCA readers agree
+with the reference's files (param.cpp:43-222, pca.cpp:119-185) and with the oracle.
+GPU: getVoxelGrid -> extractC3HLACSignature981/117 -> SearchC3HLACMulti through the
+facade equals the same pipeline through the Python binding and the oracle.
+"""
+import json
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT as REPO
+
+import pyoracle as po
+import c3hlac
+from c3hlac import synth
+
+PKG = REPO / "mapping-private_amd"
+FIX = GOLDEN / "ref_fixtures"
+
+
+@pytest.fixture(scope="module")
+def demo(tmp_path_factory):
+    if not (PKG / "lib" / "libc3hlac_host.so").exists():
+        pytest.fail("libc3hlac_host.so not built (make -C mapping-private_amd)")
+    exe = tmp_path_factory.mktemp("facade") / "facade_demo"
+    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-Werror", "-I", str(REPO / "include"), "-I", str(PKG / "host"),
+           str(REPO / "tests" / "cpp" / "facade_demo.cpp"), "-L", str(PKG / "lib"), "-lc3hlac_host",
+           "-lc3hlac_mi355x", "-Wl,-rpath," + str(PKG / "lib"), "-o", str(exe)]
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    subprocess.run(cmd, check=True, capture_output=True, text=True)
+    return exe
+
+
+def test_facade_params_and_pca(demo):
+    out = subprocess.run([str(demo), "params", str(FIX / "param_v1"), str(FIX / "models_offline_r")],
+                         check=True, capture_output=True, text=True).stdout
+    j = json.loads(out)
+    assert j["voxel_size"] == pytest.approx(0.02, rel=1e-7)
+    assert (j["dim"], j["box_scene"], j["box_model"], j["rotate_num"], j["c3_hlac_flg"]) == (100, 10, 10, 1, 1)
+    assert j["missing_key"] == -1  # Param::readDim on a file without "dim:" returns -1
+    assert j["thr"] == [147, 146, 148]
+    axis, var, _ = po.pca_read(FIX / "models_offline_r" / "compress_axis")
+    assert j["scene_dim"] == axis.shape[0] == 137
+    # getAxis()(i, 0) = eigenvector 0, component i
+    assert np.float32(j["scene_axis_00"]) == axis[0, 0] and np.float32(j["scene_axis_10"]) == axis[1, 0]
+    assert np.float32(j["scene_var0"]) == var[0]
+    assert j["model_dim"] == 100
+
+
+def _lcg(seed, n):
+    s = np.uint64(seed)
+    out = np.empty(n, np.float32)
+    for i in range(n):
+        s = (s * np.uint64(1664525) + np.uint64(1013904223)) & np.uint64(0xFFFFFFFF)
+        out[i] = np.float32(int((s >> np.uint64(8)) & np.uint64(0xFFFF)) / 65536.0) - np.float32(0.5)
+    return out, s
+
+
+@pytest.mark.gpu
+def test_facade_pipeline_matches_binding(demo, tmp_path, ctx):
+    pts = synth.kinect_scene(40_000, grid=40, leaf=0.01, seed=synth.BASE_SEED + 5)
+    cloud = tmp_path / "cloud.bin"
+    pts.astype(np.float32).tofile(cloud)
+    feat = tmp_path / "feat.bin"
+    r = subprocess.run([str(demo), "run", str(cloud), str(feat)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    j = json.loads(r.stdout)
+
+    # the same pipeline through the Python binding (same context type, same kernels) and the oracle
+    gi = ctx.voxelize(pts, 0.01)
+    assert j["div"] == list(gi.div_b) and j["n_occ"] == gi.n_occ
+    sb, hn = ctx.extract(981, (147, 146, 148), 8)
+    f981 = ctx.features()
+    ctx.extract(117, (147, 146, 148), 0)
+    f117 = ctx.features()
+    got = np.fromfile(feat, np.float32)
+    assert j["hist_num"] == hn and j["subdiv"] == list(sb)
+    np.testing.assert_array_equal(got[:hn * 981].reshape(hn, 981), f981)
+    np.testing.assert_array_equal(got[hn * 981:], f117.reshape(-1))
+    g, layout, cl = po.voxelize(pts, 0.01)
+    fo, _, _ = po.c3hlac(g, layout, cl, 981, (147, 146, 148), 0.01, 8, exact=True)
+    np.testing.assert_array_equal(f981, fo)
+
+    # search: the PCA files the demo wrote, its LCG scene axis, readAxis + setSceneAxis
+    D, rdim, M = 16, 4, 2
+    qs = []
+    for m in range(M):
+        a, v, _ = c3hlac.pca_read(str(feat) + ".m%d" % m)
+        qs.append(c3hlac.read_axis(a, v, D, rdim, multiple_similarity=True))
+    vals, _ = _lcg(3, D * 981)
+    axis = vals.reshape(D, 981)
+    var = np.arange(1, D + 1, dtype=np.float32)
+    ctx.search_setup(axis, var, np.stack(qs))
+    ctx.set_rank(1)
+    ctx.extract(981, (147, 146, 148), 8)
+    det, _ = ctx.search((2, 2, 1), 10, rotate=True)
+    det = det[:, 0]
+    assert j["xy"] == sb[0] * sb[1] and j["z"] == sb[2]
+    for m in range(M):
+        s, x, y, z, mode, xr = j["dets"][m]
+        assert (s, x, y, z, mode) == (det["score"][m], det["x"][m], det["y"][m], det["z"][m], det["mode"][m])
+        assert xr == (2 if mode in (0, 1) else (2 if mode in (2, 3) else 1))
