@@ -144,6 +144,10 @@ int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes
                    const int32_t div_b[3], const int32_t min_b[3], float leaf,
                    const c3h_extract_params* p, const int32_t range[3], int32_t exist_threshold,
                    int32_t rotate, c3h_det* d_out);
+/* Frames in flight in c3h_run_frames (default 4): frame lanes are child contexts with
+ * their own streams, so the latency-bound search of one frame overlaps the HBM stream of
+ * the next.  Lane 0 (this context) takes the last frame.  1 = strictly sequential. */
+int c3h_set_lanes(c3h_ctx* ctx, int32_t lanes);
 /* compressed features (setData before the summed-volume table): hist_num x D floats */
 int c3h_get_compressed(c3h_ctx* ctx, float* out, int on_device);
 /* per-position similarity of the last search, modes x M x P doubles (-1 = gated out).

@@ -188,6 +188,10 @@ class Context:
         self.variant = int(variant)
         return nm
 
+    def set_lanes(self, n):
+        """Frames in flight in run_frames (child contexts on their own streams)."""
+        self._chk(self.lib.c3h_set_lanes(self.h, int(n)), "set_lanes")
+
     def compressed(self):
         out = np.zeros((self.hist_num, self.D), np.float32)
         self._chk(self.lib.c3h_get_compressed(self.h, ptr(out), 0), "get_compressed")

@@ -60,6 +60,17 @@ struct c3h_ctx {
   hipStream_t own_stream = nullptr;
   std::string err;
 
+  // frame lanes of c3h_run_frames: child contexts on their own streams (frames are
+  // independent, so K frames are in flight at once); children time into the parent
+  c3h_ctx* parent = nullptr;
+  std::vector<c3h_ctx*> lanes;
+  std::vector<hipEvent_t> lane_ev;
+  hipEvent_t fork_ev = nullptr;
+  int nlanes = 4;
+  // host copy of the search setup, replayed into the lanes
+  uint64_t setup_version = 0;
+  std::vector<float> h_axis_p, h_var, h_axis_q, h_fmax;
+
   // voxel grid
   bool have_grid = false;
   c3h_grid_info info{};
@@ -87,7 +98,8 @@ struct c3h_ctx {
   c3h::DevBuf<int32_t> segs;        // per-axis tile segment tables
   c3h::DevBuf<int16_t> axmap;       // per-axis coordinate -> segment (pass-1 tile lookup)
   std::vector<int16_t> h_axmap;
-  c3h::DevBuf<uint32_t> tileflags;  // [2] row-list counters | [ntiles] epoch stamps
+  c3h::DevBuf<uint32_t> tileflags;  // [2] row counters | [2] work counters | [ntiles] stamps
+  c3h::DevBuf<int32_t> work;        // non-empty tiles of the last extract
   uint32_t tile_epoch = 0;
   c3h::DevBuf<int32_t> rows;        // non-empty subdivisions of the last extract (direct mode)
   bool rows_valid = false;          // rows/epoch describe the current features
@@ -95,6 +107,7 @@ struct c3h_ctx {
   c3h::DevBuf<long long> glist;     // sparse search: gate list
   c3h::DevBuf<uint32_t> gcnt;       // [2] gate-list counters by search epoch parity
   uint32_t search_epoch = 0;
+  c3h::DevBuf<long long> prof;      // diagnostics (C3H_PROF)
   std::vector<int32_t> h_segs;      // host copy (kept alive for the async upload)
   c3h::DevBuf<uint32_t> lut;        // 256 packed (sin | cos<<8), two variants
   bool lut_ready = false;
@@ -127,6 +140,13 @@ struct c3h_ctx {
 };
 
 namespace c3h {
+
+// Workgroup barrier for LDS-only hand-offs: waits for this wave's LDS (and scalar) ops
+// but not for its outstanding global loads/stores, so prefetches issued before the
+// barrier stay in flight (__syncthreads() also drains vmcnt on gfx9).
+__device__ __forceinline__ void lds_barrier() {
+  __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 
 // ---- launchers (defined in the .hip files) ----------------------------------------
 hipError_t launch_minmax(const float4* pts, int64_t n, float z_limit, uint32_t* out,
@@ -163,13 +183,17 @@ struct C3Launch {
   unsigned long long* acc64;
   const int16_t* axmap;   // per-axis centre coordinate -> segment index (-1 = none)
   uint32_t* flags;        // ntiles epoch stamps
+  int32_t* work;          // ntiles: non-empty tiles (pass 1 output)
+  uint32_t* workcnt;      // [2] work-list counters by epoch parity
   int32_t* rows;          // direct mode: non-empty subdivision list output (nullable)
   uint32_t* rowcnt;       // [2] row-list counters by epoch parity
   uint32_t epoch;
   int zero_empty;
   int64_t ntiles;
+  long long* prof;  // diagnostics (C3H_PROF)
   int debug;
 };
+int64_t c3hlac_grid(const C3Launch& a);  // persistent grid of the tile kernel
 hipError_t launch_c3hlac(const C3Launch& a, hipStream_t s);
 hipError_t launch_c3_finalize(const unsigned long long* acc64, int64_t hist_num, int variant,
                               float* feat, int32_t* exist, hipStream_t s);
@@ -195,7 +219,7 @@ struct ScoreLaunch {
   int64_t order_base;
 };
 hipError_t launch_score(const ScoreLaunch& a, hipStream_t s);
-bool score_fast_ok(int D, int Opad);
+bool score_fast_ok(int D, int r);  // the sparse list path applies
 int64_t score_blocks(const ScoreLaunch& a);
 
 // sparse search (fast path): gate every position of every mode, project the list
@@ -208,8 +232,9 @@ struct SparseSearch {
   const float* G;
   const int32_t* exist;
   int D, xn, yn, zn, thr;
-  const float* qt;
+  const float* qt;        // D x Opad (row stride), zero-padded past M*r
   int M, r, Opad;
+  int mpg;                // models per workgroup (whole models, mpg*r <= 64)
   double* scores;
   ModeGeom md[6];
   int nmodes;
@@ -219,6 +244,7 @@ struct SparseSearch {
   uint32_t* cnt;          // [2] list counters by epoch parity
   uint32_t epoch;
   ScorePartial* partials;  // per block per model (nullable)
+  long long* prof;         // diagnostics (C3H_PROF): [blocks][8]
 };
 hipError_t launch_sparse_search(const SparseSearch& a, hipStream_t s);
 int64_t sparse_score_blocks(const SparseSearch& a);

@@ -34,6 +34,7 @@
 // Tiles are enumerated x-fastest and dealt to XCDs in contiguous ranges so neighbouring
 // tiles (which share halo lines) run on the same L2.
 #include <algorithm>
+#include <cstdlib>
 
 #include "c3h_internal.h"
 
@@ -117,39 +118,66 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t n) {
 // tile segment of centre coordinate c along that axis (-1 when c is no centre, e.g.
 // below the subdivision offset): the reference's float subdivision arithmetic is baked
 // into these host-built tables.
-constexpr int kOccUnroll = 4;  // 16-B loads per thread in flight per iteration
+constexpr int kOccUnroll = 4;  // 16-B loads per thread in flight per chunk
+constexpr int kOccSet = 256;   // LDS set of tiles touched by one workgroup
 
 // Flags are epoch stamps: tile t is non-empty in this frame iff flags[t] == epoch, so
-// nothing is reset between frames and the stores need no atomics (same value from every
-// writer).
-__device__ __forceinline__ void flag_tile(int t, uint32_t epoch, uint32_t* flags) {
-  flags[t] = epoch;
+// nothing is reset between frames.  Each workgroup streams contiguous 16-KB chunks
+// (4096 voxels: coalesced 16-B loads, all issued before use), collects the tiles of its
+// occupied centre voxels in an LDS set, and only then stamps them: one global atomic
+// per (workgroup, tile), off the streaming path; the first stamper of a tile appends it
+// to the work list.  The set overflows only for tiny subdivisions (then tiles are
+// stamped directly).
+__device__ __forceinline__ void stamp_tile(int t, uint32_t epoch, uint32_t* flags, uint32_t* cnt,
+                                           int32_t* work) {
+  if (atomicExch(&flags[t], epoch) != epoch) work[atomicAdd(cnt, 1u)] = t;
+}
+
+__device__ __forceinline__ void set_insert(int* s_set, int t, uint32_t epoch, uint32_t* flags,
+                                           uint32_t* cnt, int32_t* work) {
+  int h = (int)(((uint32_t)t * 0x9E3779B1u) >> 24);  // 8-bit hash
+  static_assert(kOccSet == 256 && kBlock == 256, "set slot per thread");
+  for (int probe = 0; probe < kOccSet; ++probe, h = (h + 1) & (kOccSet - 1)) {
+    const int cur = s_set[h];
+    if (cur == t) return;
+    if (cur == -1) {
+      const int old = atomicCAS(&s_set[h], -1, t);
+      if (old == -1 || old == t) return;
+    }
+  }
+  stamp_tile(t, epoch, flags, cnt, work);  // set full
 }
 
 template <bool kVec>
 __global__ __launch_bounds__(kBlock) void c3_occupancy_kernel(
     const uint32_t* __restrict__ grid, int gx, int gy, int gz, const int16_t* __restrict__ axmap,
-    int ns0, int ns1, uint32_t epoch, uint32_t* __restrict__ flags) {
+    int ns0, int ns1, uint32_t epoch, uint32_t* __restrict__ flags, uint32_t* __restrict__ cnt,
+    int32_t* __restrict__ work) {
+  __shared__ int s_set[kOccSet];
+  const int tid = threadIdx.x, lane = tid & 63;
   const int64_t nvox = (int64_t)gx * gy * gz;
   const int16_t* mx = axmap;
   const int16_t* my = axmap + gx;
   const int16_t* mz = axmap + gx + gy;
+  cnt += epoch & 1;
+  s_set[tid] = -1;
+  __syncthreads();
   int last = -1;
-  const int64_t nthr = (int64_t)gridDim.x * kBlock;
   if (kVec) {
     const int64_t n4 = nvox >> 2;
     const uint4* g4 = reinterpret_cast<const uint4*>(grid);
-    for (int64_t i0 = blockIdx.x * (int64_t)kBlock + threadIdx.x; i0 < n4; i0 += kOccUnroll * nthr) {
+    constexpr int kChunk4 = kBlock * kOccUnroll;
+    for (int64_t c0 = blockIdx.x * (int64_t)kChunk4; c0 < n4; c0 += (int64_t)gridDim.x * kChunk4) {
       uint4 w[kOccUnroll];
 #pragma unroll
       for (int j = 0; j < kOccUnroll; ++j) {  // all loads first: bytes in flight, not latency
-        const int64_t i = i0 + j * nthr;
+        const int64_t i = c0 + j * kBlock + tid;
         w[j] = i < n4 ? g4[i] : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
       for (int j = 0; j < kOccUnroll; ++j) {
         if ((w[j].x | w[j].y | w[j].z | w[j].w) == 0) continue;
-        const uint32_t v = (uint32_t)((i0 + j * nthr) << 2);  // nvox < 2^32 (host-checked)
+        const uint32_t v = (uint32_t)((c0 + j * kBlock + tid) << 2);  // nvox < 2^32 (host-checked)
         const uint32_t row = v / (uint32_t)gx;
         const int x = (int)(v - row * (uint32_t)gx);
         const int y = (int)(row % (uint32_t)gy), z = (int)(row / (uint32_t)gy);
@@ -164,12 +192,12 @@ __global__ __launch_bounds__(kBlock) void c3_occupancy_kernel(
           const int t = tx + ns0 * (ty + ns1 * tz);
           if (t == last) continue;
           last = t;
-          flag_tile(t, epoch, flags);
+          set_insert(s_set, t, epoch, flags, cnt, work);
         }
       }
     }
   } else {
-    for (int64_t v = blockIdx.x * (int64_t)kBlock + threadIdx.x; v < nvox; v += nthr) {
+    for (int64_t v = blockIdx.x * (int64_t)kBlock + tid; v < nvox; v += (int64_t)gridDim.x * kBlock) {
       if (!grid[v]) continue;
       const uint32_t row = (uint32_t)v / (uint32_t)gx;
       const int x = (int)((uint32_t)v - row * (uint32_t)gx);
@@ -179,8 +207,20 @@ __global__ __launch_bounds__(kBlock) void c3_occupancy_kernel(
       const int t = tx + ns0 * (ty + ns1 * tz);
       if (t == last) continue;
       last = t;
-      flag_tile(t, epoch, flags);
+      set_insert(s_set, t, epoch, flags, cnt, work);
     }
+  }
+  __syncthreads();
+  // flush: one stamp per (workgroup, tile); new tiles appended with one add per wave
+  const int t = s_set[tid];
+  bool fresh = false;
+  if (t >= 0) fresh = atomicExch(&flags[t], epoch) != epoch;
+  const unsigned long long m = __ballot(fresh);
+  if (m) {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(cnt, (uint32_t)__popcll(m));
+    base = __shfl(base, 0, 64);
+    if (fresh) work[base + __popcll(m & ((1ull << lane) - 1))] = t;
   }
 }
 
@@ -199,12 +239,15 @@ struct KArgs {
   int32_t* exist;
   unsigned long long* acc64;
   const uint32_t* flags;  // tile epoch stamps of pass 1
+  const int32_t* work;    // non-empty tiles of pass 1
+  uint32_t* workcnt;      // [2] work-list counters by epoch parity
   int32_t* rows;          // direct mode: non-empty subdivisions of this frame (nullable)
   uint32_t* rowcnt;       // [2] row-list counters by epoch parity
   uint32_t epoch;
   int ntiles;
   int zero_empty;         // direct mode with every subdivision one tile (h == tile): zero
                           // the rows of unflagged tiles here
+  long long* prof;  // diagnostics only (C3H_PROF): per-block phase timestamps [grid][8]
   int debug;  // diagnostics only (C3H_C3_DEBUG): 1 stop after the loads, 2 after compaction,
              // 3 skip the tile kernel
 };
@@ -216,6 +259,9 @@ constexpr int kSegLds = 64;   // segment tables up to 64 segments per axis live 
 // unflagged (direct mode); phase T walks the work list: stage the (lx+2)x(ly+2)x(lz+1)
 // halo in LDS (all loads issued before the first LDS store), compact the occupied
 // centres, build the packed dot4 operands and accumulate exactly (see the header).
+#define C3H_PROF(k, cond) \
+  if (a.prof && tid == 0 && (cond)) a.prof[blockIdx.x * 8 + (k)] = (long long)wall_clock64()
+
 __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint32_t* s_lut = smem;                       // 256
@@ -223,12 +269,28 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
   uint16_t* s_list = reinterpret_cast<uint16_t*>(s_tile + a.tw_max);  // list_max (u16)
   uint32_t* s_arr = s_tile + a.tw_max + ((a.list_max + 7) / 8) * 4;   // kGroups*kArrStride
   uint32_t* s_misc = s_arr + kGroups * kArrStride;                  // counters [4]
-  uint32_t* s_work = s_misc + 4;                                     // kBlock tile ids
-  int32_t* s_segs = reinterpret_cast<int32_t*>(s_work + kBlock);    // segment table copy
+  int32_t* s_segs = reinterpret_cast<int32_t*>(s_misc + 4);         // segment table copy
   uint32_t* s_hist = s_arr;                                          // epilogue alias
   const int tid = threadIdx.x, lane = tid & 63;
   const int F = a.variant;
-  if (blockIdx.x == 0 && tid == 0) a.rowcnt[(a.epoch + 1) & 1] = 0;  // next frame's row counter
+  C3H_PROF(0, true);
+  // issued together: the work count, this workgroup's first work item, its phase-Z flags
+  const int G = (int)gridDim.x;
+  int wi = (int)blockIdx.x;
+  int tile_next = wi < a.ntiles ? a.work[wi] : 0;  // speculative; used only if wi < nwork
+  const int nwork = (int)a.workcnt[a.epoch & 1];
+  const int per = (a.ntiles - (int)blockIdx.x + G - 1) / G;  // phase-Z tiles of this block
+  uint32_t zflag[2];
+  int zt[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    zt[j] = (int)blockIdx.x + (tid + j * kBlock) * G;
+    zflag[j] = (a.zero_empty && tid + j * kBlock < per) ? a.flags[zt[j]] : a.epoch;
+  }
+  if (blockIdx.x == 0 && tid == 0) {  // the next frame's counters
+    a.rowcnt[(a.epoch + 1) & 1] = 0;
+    a.workcnt[(a.epoch + 1) & 1] = 0;
+  }
   if (a.debug == 3) return;  // diagnostics: occupancy pass only
   s_lut[tid] = a.lut[tid];
   const bool segs_lds = a.seg_stride <= kSegLds;
@@ -237,40 +299,13 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
     for (int e = tid; e < 9 * a.seg_stride; e += kBlock) s_segs[e] = a.segs[e];
   const int bg = tid / 15, bk = tid - bg * 15;  // build job (group, k), tid < 240
   const int at = tid / 90, arem = tid - at * 90, ak = arem / 6, an = arem - ak * 6;
+  lds_barrier();
+  C3H_PROF(1, true);
 
-  // this workgroup owns tiles blockIdx.x + i * gridDim.x (spreads clustered surfaces)
-  const int per = (a.ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-  for (int c0 = 0; c0 < per; c0 += kBlock) {
-    const int i = c0 + tid;
-    const int t = (int)blockIdx.x + i * (int)gridDim.x;
-    const bool valid = i < per;
-    const bool flagged = valid && a.flags[t] == a.epoch;
-    if (a.zero_empty) {  // rows of empty tiles (h == t here), one wave-wide store per 64 floats
-      unsigned long long m = __ballot(valid && !flagged);
-      while (m) {
-        const int j = __ffsll((long long)m) - 1;
-        m &= m - 1;
-        const int tj = __shfl(t, j, 64);
-        float* row = a.feat + (int64_t)tj * F;
-        for (int q = lane; q < F; q += 64) row[q] = 0.0f;
-        if (lane == 0) a.exist[tj] = 0;
-      }
-    }
-    if (tid == 0) s_misc[1] = 0;
-    __syncthreads();
-    {
-      const unsigned long long m = __ballot(flagged);
-      if (m) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&s_misc[1], (uint32_t)__popcll(m));
-        base = __shfl(base, 0, 64);
-        if (flagged) s_work[base + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)t;
-      }
-    }
-    __syncthreads();
-    const int nw = (int)s_misc[1];
-  for (int wi = 0; wi < nw; ++wi) {
-    const int tile = (int)s_work[wi];
+  // the work list is dense: workgroup b takes items b, b + G, ... (balanced)
+  for (; wi < (a.debug == 4 ? 0 : nwork); wi += G) {
+    const int tile = tile_next;
+    if (wi + G < nwork) tile_next = a.work[wi + G];
     const int ix = tile % a.ns0, iy = (tile / a.ns0) % a.ns1, iz = tile / (a.ns0 * a.ns1);
     const int32_t* sx = segs + 3 * ix;
     const int32_t* sy = segs + 3 * (a.seg_stride + iy);
@@ -330,10 +365,11 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
                         ? a.grid[((int64_t)gz * a.gy + gy) * a.gx + gxx] : 0u;
       }
     }
-    __syncthreads();
+    lds_barrier();
+    C3H_PROF(3, wi == (int)blockIdx.x);
     if (a.debug == 1) {
       if (tid == 0 && s_tile[0] == 0xdeadbeefu) a.exist[0] = 1;  // keep the loads live
-      __syncthreads();
+      lds_barrier();
       continue;
     }
 
@@ -366,11 +402,12 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
+    C3H_PROF(4, wi == (int)blockIdx.x);
     const int nlist = (int)s_misc[0];
     if (a.debug == 2) {
       if (tid == 0 && nlist == 0x7fffffff) a.exist[0] = 1;
-      __syncthreads();
+      lds_barrier();
       continue;
     }
 
@@ -419,7 +456,7 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
           dst[90 + n] = bb[n];
         }
       }
-      __syncthreads();
+      lds_barrier();
       // 4. exact integer accumulation: acc[c] += sum_g dot4(A_c[g], N_{k,n}[g])
       if (tid < 180) {
         const int ng = (min(nlist - c0, kChunk) + 3) >> 2;
@@ -432,8 +469,9 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
             acc[c] = __builtin_amdgcn_udot4(ctr[g * kArrStride + c], nv, acc[c], false);
         }
       }
-      __syncthreads();
+      lds_barrier();
     }
+    C3H_PROF(5, wi == (int)blockIdx.x);
     // 5. epilogue: integer bins -> LDS, then fold / normalise / store
     if (tid < 180) {
 #pragma unroll
@@ -442,7 +480,7 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
         if (bi >= 0) s_hist[bi] = acc[c];
       }
     }
-    __syncthreads();
+    lds_barrier();
     if (a.atomic) {
       for (int i = tid; i < 981; i += kBlock) {
         const uint32_t v = s_hist[i];
@@ -458,10 +496,33 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
       if (tid == 0) a.exist[h] = exist_from((float)s_hist[0], (float)s_hist[1]);
     }
     if (a.rows && tid == 0) a.rows[atomicAdd(&a.rowcnt[a.epoch & 1], 1u)] = (int32_t)h;
-    __syncthreads();  // LDS is reused by the next tile
+    lds_barrier();  // LDS is reused by the next tile
+    C3H_PROF(6, wi == (int)blockIdx.x);
   }
-    __syncthreads();  // s_work / s_misc[1] are rewritten by the next chunk
+  // phase Z (direct mode, every subdivision one tile: h == tile): rows of the tiles pass 1
+  // left unstamped, one wave-wide store per 64 floats
+  if (a.zero_empty) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      unsigned long long m = __ballot(zflag[j] != a.epoch);
+      while (m) {
+        const int q = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const int tj = __shfl(zt[j], q, 64);
+        float* row = a.feat + (int64_t)tj * F;
+        for (int c = lane; c < F; c += 64) row[c] = 0.0f;
+        if (lane == 0) a.exist[tj] = 0;
+      }
+    }
+    for (int i = tid + 2 * kBlock; i < per; i += kBlock) {  // > 512 tiles per workgroup
+      const int t = (int)blockIdx.x + i * G;
+      if (a.flags[t] != a.epoch) {
+        for (int c = 0; c < F; ++c) a.feat[(int64_t)t * F + c] = 0.0f;
+        a.exist[t] = 0;
+      }
+    }
   }
+  C3H_PROF(7, true);
 }
 
 // multi-tile subdivisions: 64-bit exact partial sums -> features
@@ -482,8 +543,32 @@ __global__ __launch_bounds__(kBlock) void c3_finalize_kernel(const unsigned long
 }  // namespace
 
 size_t c3hlac_lds_bytes(int tw_max, int list_max) {
-  return sizeof(uint32_t) * (256 + tw_max + ((list_max + 7) / 8) * 4 + kGroups * kArrStride + 4 + kBlock +
-                             9 * kSegLds);
+  return sizeof(uint32_t) * (256 + tw_max + ((list_max + 7) / 8) * 4 + kGroups * kArrStride + 4 + 9 * kSegLds);
+}
+
+// persistent grid: every workgroup resident at once (occupancy from LDS and VGPRs)
+int64_t c3hlac_grid(const C3Launch& l) {
+  const int tx_max = ((l.lmax[0] + 2) + 3 + 3) & ~3;
+  const size_t lds = c3hlac_lds_bytes(tx_max * (l.lmax[1] + 2) * (l.lmax[2] + 1), l.lmax[0] * l.lmax[1] * l.lmax[2]);
+  static thread_local size_t c_lds = 0;
+  static thread_local int c_per_cu = 0, c_ncu = 0, c_dev = -1;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (lds != c_lds || dev != c_dev) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c3hlac_tile_kernel, kBlock, lds) != hipSuccess ||
+        per_cu < 1)
+      per_cu = 1;
+    int n_cu = 256;
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    c_lds = lds;
+    c_per_cu = per_cu;
+    c_ncu = n_cu;
+    c_dev = dev;
+  }
+  int64_t grid = std::min<int64_t>(l.ntiles, (int64_t)c_ncu * c_per_cu);
+  if (const char* g = getenv("C3H_TILE_GRID")) grid = std::max<int64_t>(1, std::min<int64_t>(grid, atoi(g)));
+  return std::max<int64_t>(grid, 1);
 }
 
 hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
@@ -495,10 +580,10 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
   if (g1 < 1) g1 = 1;
   if (vec)
     c3_occupancy_kernel<true><<<g1, kBlock, 0, s>>>(l.grid, l.gx, l.gy, l.gz, l.axmap, l.nseg[0],
-                                                    l.nseg[1], l.epoch, l.flags);
+                                                    l.nseg[1], l.epoch, l.flags, l.workcnt, l.work);
   else
     c3_occupancy_kernel<false><<<g1, kBlock, 0, s>>>(l.grid, l.gx, l.gy, l.gz, l.axmap, l.nseg[0],
-                                                     l.nseg[1], l.epoch, l.flags);
+                                                     l.nseg[1], l.epoch, l.flags, l.workcnt, l.work);
   KArgs a;
   a.grid = l.grid;
   a.gx = l.gx;
@@ -524,17 +609,18 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
   a.exist = l.exist;
   a.acc64 = l.acc64;
   a.flags = l.flags;
+  a.work = l.work;
+  a.workcnt = l.workcnt;
   a.rows = l.rows;
   a.rowcnt = l.rowcnt;
   a.epoch = l.epoch;
   a.zero_empty = l.zero_empty;
   a.ntiles = (int)l.ntiles;
   a.debug = l.debug;
+  a.prof = l.prof;
   const size_t lds = c3hlac_lds_bytes(a.tw_max, a.list_max);
-  // persistent grid: enough resident workgroups to cover the chip several times over
-  const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / lds)));
-  const int grid = (int)std::min<int64_t>(l.ntiles, 256 * per_cu);
-  c3hlac_tile_kernel<<<std::max(grid, 1), kBlock, lds, s>>>(a);
+  const int grid = (int)c3hlac_grid(l);
+  c3hlac_tile_kernel<<<grid, kBlock, lds, s>>>(a);
   return hipGetLastError();
 }
 

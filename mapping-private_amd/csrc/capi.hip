@@ -6,6 +6,7 @@
 // setSceneAxis whitening (search.cpp:701-712), setRank/cleanMax list state
 // (search.cpp:130-143, 683-732) and removeOverlap (search.cpp:972-992).
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -66,27 +67,28 @@ void release(DevBuf<T>& b) {
 // ---- timing ------------------------------------------------------------------------
 struct Timed {
   c3h_ctx* ctx;
+  c3h::Timer* T;
   int slot;
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
-  Timed(c3h_ctx* c, int s) : ctx(c), slot(s) {
-    if (!(ctx->timer.mask >> (s + 1) & 1)) return;
-    if (ctx->timer.pool.empty()) {
+  Timed(c3h_ctx* c, int s) : ctx(c), T(c->parent ? &c->parent->timer : &c->timer), slot(s) {
+    if (!(T->mask >> (s + 1) & 1)) return;
+    if (T->pool.empty()) {
       hipEvent_t a, b;
       if (hipEventCreate(&a) != hipSuccess) return;
       if (hipEventCreate(&b) != hipSuccess) {
         (void)hipEventDestroy(a);
         return;
       }
-      ctx->timer.pool.push_back({a, b});
+      T->pool.push_back({a, b});
     }
-    ev = ctx->timer.pool.back();
-    ctx->timer.pool.pop_back();
-    (void)hipEventRecord(ev.first, ctx->stream);
+    ev = T->pool.back();
+    T->pool.pop_back();
+    (void)hipEventRecord(ev.first, ctx->stream);  // on the stream the kernels run on
   }
   ~Timed() {
     if (!ev.first) return;
     (void)hipEventRecord(ev.second, ctx->stream);
-    ctx->timer.pending[slot].push_back(ev);
+    T->pending[slot].push_back(ev);
   }
 };
 
@@ -211,6 +213,63 @@ Segs axis_segments(int div, int off, float inv_s, bool mode1, int sb, bool* cove
   return s;
 }
 
+// diagnostics (env C3H_PROF=<file>): per-block phase timestamps of the tile / score
+// kernels; after each instrumented launch one line per kernel is appended to the file:
+// for each probe k, median over blocks of (t_k - t_0) and max over blocks of
+// (t_k - min_b t_0), in microseconds (wall_clock64: 100 MHz).  Synchronises: never on.
+const char* prof_path() {
+  static const char* p = getenv("C3H_PROF");
+  return p && *p ? p : nullptr;
+}
+
+int prof_prepare(c3h_ctx* ctx, int64_t nblocks, long long** out) {
+  *out = nullptr;
+  if (!prof_path()) return C3H_OK;
+  ENSURE(ctx->prof, (size_t)nblocks * 8);
+  HIPCHK(hipMemsetAsync(ctx->prof.p, 0, (size_t)nblocks * 8 * 8, ctx->stream));
+  *out = ctx->prof.p;
+  return C3H_OK;
+}
+
+int prof_dump(c3h_ctx* ctx, const char* name, int64_t nblocks) {
+  if (!prof_path()) return C3H_OK;
+  std::vector<long long> t((size_t)nblocks * 8);
+  HIPCHK(hipMemcpyAsync(t.data(), ctx->prof.p, t.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  long long t0min = LLONG_MAX;
+  int64_t nb = 0;
+  for (int64_t b = 0; b < nblocks; ++b)
+    if (t[b * 8]) {
+      t0min = std::min(t0min, t[b * 8]);
+      ++nb;
+    }
+  FILE* f = fopen(prof_path(), "a");
+  if (!f) return C3H_OK;
+  fprintf(f, "%s blocks=%lld started=%lld", name, (long long)nblocks, (long long)nb);
+  for (int k = 1; k < 8; ++k) {
+    std::vector<double> d;
+    double mx = 0;
+    for (int64_t b = 0; b < nblocks; ++b)
+      if (t[b * 8] && t[b * 8 + k]) {
+        d.push_back((t[b * 8 + k] - t[b * 8]) * 0.01);
+        mx = std::max(mx, (t[b * 8 + k] - t0min) * 0.01);
+      }
+    if (d.empty()) continue;
+    std::nth_element(d.begin(), d.begin() + d.size() / 2, d.end());
+    fprintf(f, " p%d[n=%zu med=%.2f max=%.2f]", k, d.size(), d[d.size() / 2], mx);
+  }
+  long long s0 = LLONG_MAX;  // start spread
+  long long s1 = 0;
+  for (int64_t b = 0; b < nblocks; ++b)
+    if (t[b * 8]) {
+      s0 = std::min(s0, t[b * 8]);
+      s1 = std::max(s1, t[b * 8]);
+    }
+  fprintf(f, " start_spread=%.2f\n", nb ? (s1 - s0) * 0.01 : 0.0);
+  fclose(f);
+  return C3H_OK;
+}
+
 int upload_lists(c3h_ctx* ctx) {
   auto& L = ctx->lists;
   const size_t n = (size_t)L.M * L.rank;
@@ -292,7 +351,7 @@ int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate
     Timed t(ctx, 2);
     // sparse: only the non-empty rows of the extract's list (the rest stay stale and are
     // gated on exist by every consumer)
-    const bool sparse = ctx->rows_valid && c3h::score_fast_ok(ctx->D, ctx->Opad);
+    const bool sparse = ctx->rows_valid && c3h::score_fast_ok(ctx->D, ctx->r);
     HIPCHK(c3h::launch_compress(ctx->feat.p, H, ctx->F, ctx->axis_pt.p, ctx->D, ctx->Dpad,
                                 ctx->fmax.p, ctx->fmax_len, ctx->G.p,
                                 sparse ? ctx->rows.p : nullptr,
@@ -317,7 +376,7 @@ int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate
   ENSURE(ctx->scores, total);
   ctx->scores_n = total;
   // per-mode score launches; rank 1 uses the per-block partials (fast path only)
-  bool all_fast = c3h::score_fast_ok(ctx->D, ctx->Opad);
+  bool all_fast = c3h::score_fast_ok(ctx->D, ctx->r);
   int64_t nparts = 0;
   std::vector<c3h::ScoreLaunch> launches;
   for (int i = 0; i < rm.n; ++i) {
@@ -362,6 +421,7 @@ int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate
     q.M = ctx->M;
     q.r = ctx->r;
     q.Opad = ctx->Opad;
+    q.mpg = std::max(1, 64 / ctx->r);
     q.scores = ctx->scores.p;
     q.nmodes = rm.n;
     q.pstart[0] = 0;
@@ -388,8 +448,18 @@ int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate
       q.partials = ctx->partials.p;
       nlist = ctx->gcnt.p + (q.epoch & 1);
     }
-    Timed t(ctx, 3);
-    HIPCHK(c3h::launch_sparse_search(q, ctx->stream));
+    {
+      int rc = prof_prepare(ctx, nparts, &q.prof);
+      if (rc != C3H_OK) return rc;
+    }
+    {
+      Timed t(ctx, 3);
+      HIPCHK(c3h::launch_sparse_search(q, ctx->stream));
+    }
+    if (q.prof) {
+      int rc = prof_dump(ctx, "score_list_kernel", nparts);
+      if (rc != C3H_OK) return rc;
+    }
   } else {
     if (ctx->g_sparse)
       return fail(ctx, C3H_ERR_STATE, "c3h_search: internal: sparse G on the dense score path");
@@ -456,6 +526,9 @@ int c3h_create(int hip_device, c3h_ctx** out) {
 void c3h_destroy(c3h_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+  for (c3h_ctx* l : ctx->lanes) c3h_destroy(l);
+  for (hipEvent_t e : ctx->lane_ev) (void)hipEventDestroy(e);
+  if (ctx->fork_ev) (void)hipEventDestroy(ctx->fork_ev);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   release(ctx->grid);
   release(ctx->pts);
@@ -477,6 +550,7 @@ void c3h_destroy(c3h_ctx* ctx) {
   release(ctx->axmap);
   release(ctx->tileflags);
   release(ctx->rows);
+  release(ctx->work);
   release(ctx->glist);
   release(ctx->gcnt);
   release(ctx->lut);
@@ -812,9 +886,9 @@ int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3]
                             hipMemcpyHostToDevice, ctx->stream));
     }
     Timed t(ctx, 1);  // the whole C3 stage: flag reset, occupancy pass, tile kernel
-    // [2] row-list counters | [ntiles] epoch stamps; zeroed only when (re)allocated or
-    // when the epoch wraps
-    const size_t tf_n = (size_t)ntiles + 2;
+    // [2] row-list counters | [2] work-list counters | [ntiles] epoch stamps; zeroed only
+    // when (re)allocated or when the epoch wraps
+    const size_t tf_n = (size_t)ntiles + 4;
     if (ctx->tileflags.n < tf_n || ++ctx->tile_epoch == 0) {
       ENSURE(ctx->tileflags, tf_n);
       HIPCHK(hipMemsetAsync(ctx->tileflags.p, 0, ctx->tileflags.n * 4, ctx->stream));
@@ -845,8 +919,11 @@ int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3]
     l.exist = ctx->exist.p;
     l.acc64 = ctx->acc64.p;
     l.axmap = ctx->axmap.p;
+    ENSURE(ctx->work, (size_t)ntiles);
     l.rowcnt = ctx->tileflags.p;
-    l.flags = ctx->tileflags.p + 2;
+    l.workcnt = ctx->tileflags.p + 2;
+    l.flags = ctx->tileflags.p + 4;
+    l.work = ctx->work.p;
     l.rows = nullptr;
     if (!atomic) {  // the non-empty rows feed the sparse compress of the search
       ENSURE(ctx->rows, (size_t)hist_num);
@@ -857,8 +934,18 @@ int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3]
     l.zero_empty = (!atomic && all_covered) ? 1 : 0;
     l.ntiles = ntiles;
     l.debug = 0;
+    l.prof = nullptr;
     if (const char* dbg = getenv("C3H_C3_DEBUG")) l.debug = atoi(dbg);  // diagnostics only
+    const int64_t tgrid = c3h::c3hlac_grid(l);
+    {
+      int rc = prof_prepare(ctx, tgrid, &l.prof);
+      if (rc != C3H_OK) return rc;
+    }
     HIPCHK(c3h::launch_c3hlac(l, ctx->stream));
+    if (l.prof) {
+      int rc = prof_dump(ctx, "c3hlac_tile_kernel", tgrid);
+      if (rc != C3H_OK) return rc;
+    }
     if (atomic)
       HIPCHK(c3h::launch_c3_finalize(ctx->acc64.p, hist_num, F, ctx->feat.p, ctx->exist.p, ctx->stream));
   }
@@ -921,7 +1008,8 @@ int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_
   ENSURE(ctx->axis_q, (size_t)M * r * D);
   HIPCHK(hipMemcpy(ctx->axis_q.p, axis_q, (size_t)M * r * D * 4, hipMemcpyHostToDevice));
   // transposed basis for the fast score path: qt[d][m*r + i] = axis_q[m][i][d]
-  const int Opad = (M * r + 15) / 16 * 16;
+  // + 16 zero columns: a score workgroup's window of whole models may run past M*r
+  const int Opad = (M * r + 15) / 16 * 16 + 16;
   std::vector<float> qt((size_t)D * Opad, 0.0f);
   for (int m = 0; m < M; ++m)
     for (int i = 0; i < r; ++i)
@@ -934,6 +1022,12 @@ int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_
     ENSURE(ctx->fmax, (size_t)feature_max_len);
     HIPCHK(hipMemcpy(ctx->fmax.p, feature_max, (size_t)feature_max_len * 4, hipMemcpyHostToDevice));
   }
+  ctx->h_axis_p.assign(axis_p ? axis_p : nullptr, axis_p ? axis_p + (size_t)D * F : nullptr);
+  ctx->h_var.assign(var ? var : nullptr, var ? var + D : nullptr);
+  ctx->h_axis_q.assign(axis_q, axis_q + (size_t)M * r * D);
+  ctx->h_fmax.assign(feature_max ? feature_max : nullptr,
+                     feature_max ? feature_max + feature_max_len : nullptr);
+  ++ctx->setup_version;
   ctx->compress = axis_p != nullptr;
   ctx->D = D;
   ctx->F = F;
@@ -1013,23 +1107,69 @@ int c3h_search_async(c3h_ctx* ctx, const int32_t range[3], int32_t exist_thresho
   return nm;
 }
 
+int c3h_set_lanes(c3h_ctx* ctx, int32_t lanes) {
+  if (!ctx || lanes < 1 || lanes > 16) return C3H_ERR_ARG;
+  ctx->nlanes = lanes;
+  return C3H_OK;
+}
+
 int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes,
                    const int32_t div_b[3], const int32_t min_b[3], float leaf,
                    const c3h_extract_params* p, const int32_t range[3], int32_t exist_threshold,
                    int32_t rotate, c3h_det* d_out) {
   if (!ctx || !d_grids || nframes < 0 || !div_b || !min_b || !p || !range || !d_out)
     return C3H_ERR_ARG;
+  if (!ctx->have_setup) return fail(ctx, C3H_ERR_STATE, "c3h_run_frames: no axes (call c3h_search_setup)");
+  HIPCHK(hipSetDevice(ctx->device));
+  const size_t per_frame = (size_t)std::max(ctx->M, 1) * ctx->rank;
+  // lanes: lane 0 is the context itself and takes the last frame, so afterwards the
+  // context holds that frame's features, scores and lists as a sequential run would
+  const int K = std::max(1, std::min<int>(ctx->nlanes, std::max<int32_t>(nframes, 1)));
+  while ((int)ctx->lanes.size() < K - 1) {
+    c3h_ctx* c = nullptr;
+    int rc = c3h_create(ctx->device, &c);
+    if (rc != C3H_OK) return fail(ctx, rc, "c3h_run_frames: lane context");
+    c->parent = ctx;
+    ctx->lanes.push_back(c);
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ctx->lane_ev.push_back(e);
+  }
+  if (!ctx->fork_ev) HIPCHK(hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming));
+  for (int l = 0; l < K - 1; ++l) {  // lanes take the context's setup and rank
+    c3h_ctx* c = ctx->lanes[l];
+    if (c->setup_version != ctx->setup_version || !c->have_setup) {
+      int rc = c3h_search_setup(c, ctx->h_axis_p.empty() ? nullptr : ctx->h_axis_p.data(),
+                                ctx->h_var.empty() ? nullptr : ctx->h_var.data(), ctx->D, ctx->F,
+                                ctx->h_axis_q.data(), ctx->M, ctx->r,
+                                ctx->h_fmax.empty() ? nullptr : ctx->h_fmax.data(), (int)ctx->h_fmax.size());
+      if (rc != C3H_OK) return fail(ctx, rc, std::string("c3h_run_frames: lane setup: ") + c->err);
+      c->setup_version = ctx->setup_version;
+    }
+    if (c->rank != ctx->rank) {
+      int rc = c3h_set_rank(c, ctx->rank);
+      if (rc != C3H_OK) return rc;
+    }
+  }
+  HIPCHK(hipEventRecord(ctx->fork_ev, ctx->stream));  // inputs were produced on ctx's stream
+  for (int l = 0; l < K - 1; ++l) HIPCHK(hipStreamWaitEvent(ctx->lanes[l]->stream, ctx->fork_ev, 0));
   int nm = 0;
   for (int32_t i = 0; i < nframes; ++i) {
-    int rc = c3h_set_grid(ctx, d_grids[i], div_b, min_b, leaf, 1);
+    const int lane = (int)((nframes - 1 - i) % K);
+    c3h_ctx* c = lane == 0 ? ctx : ctx->lanes[lane - 1];
+    int rc = c3h_set_grid(c, d_grids[i], div_b, min_b, leaf, 1);
     if (rc != C3H_OK) return rc;
-    rc = c3h_clean_max(ctx);
+    rc = c3h_clean_max(c);
     if (rc != C3H_OK) return rc;
-    rc = c3h_extract(ctx, p, nullptr, nullptr);
-    if (rc != C3H_OK) return rc;
-    nm = c3h_search_async(ctx, range, exist_threshold, rotate,
-                          d_out + (size_t)i * std::max(ctx->M, 1) * ctx->rank);
-    if (nm < 0) return nm;
+    rc = c3h_extract(c, p, nullptr, nullptr);
+    if (rc != C3H_OK) return lane ? fail(ctx, rc, c->err) : rc;
+    const int r = c3h_search_async(c, range, exist_threshold, rotate, d_out + (size_t)i * per_frame);
+    if (r < 0) return lane ? fail(ctx, r, c->err) : r;
+    if (lane == 0) nm = r;
+  }
+  for (int l = 0; l < K - 1; ++l) {  // join
+    HIPCHK(hipEventRecord(ctx->lane_ev[l], ctx->lanes[l]->stream));
+    HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[l], 0));
   }
   return nm;
 }

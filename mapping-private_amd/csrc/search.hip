@@ -143,14 +143,14 @@ __global__ __launch_bounds__(kBlock) void compress_rows_kernel(
   for (int q = 0; q < 8; ++q) acc[q] = 0.0f;
   const int nch = (F + kRK - 1) / kRK;
   for (int c = 0; c < nch; ++c) {
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int e = tid + j * kBlock;
       if (e < nq4) reinterpret_cast<float4*>(pc)[e] = pre[j];
     }
     if (c + 1 < nch) load_chunk(c + 1);
-    __syncthreads();
+    lds_barrier();
     if (active) {
       const int kn = min(kRK, F - c * kRK);
       const float* fr = fs + row * F + c * kRK;
@@ -262,6 +262,7 @@ __global__ __launch_bounds__(kBlock) void score_kernel(ScoreLaunch a, int64_t P)
 // |Q_m f|^2 is summed per (position, model) in a fixed order.  The block also emits its
 // per-model best (score, scan order) so rank-1 searches need no second pass.
 constexpr int kFP = 32;
+constexpr int kOC = 64;  // basis rows per workgroup (whole models)
 
 // ---------------------------------------------------------------- sparse search
 // The exist gate passes few positions on surface scenes (a depth camera sees a 2-D
@@ -313,32 +314,37 @@ __global__ __launch_bounds__(kBlock) void gate_kernel(SparseSearch a) {
 // nothing to a sum that starts at +0).
 __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch a) {
   extern __shared__ __attribute__((aligned(16))) float ssm[];
-  const int D = a.D, Opad = a.Opad, D4 = a.D >> 2;
+  const int D = a.D, D4 = a.D >> 2, Qs = a.Opad;  // qt row stride
+#define C3H_SPROF(k) \
+  if (a.prof && threadIdx.x == 0 && blockIdx.y == 0) a.prof[blockIdx.x * 8 + (k)] = (long long)wall_clock64()
+  C3H_SPROF(0);
   const int n = (int)a.cnt[a.epoch & 1];
   const int64_t e0 = blockIdx.x * (int64_t)kFP;
   if (e0 >= n) return;
-  float* fT = ssm;
-  float* qc = fT + D * kFP;
-  float* qv = ssm;
-  const int region = max(D * kFP + 16 * Opad, kFP * (Opad + 1));
+  // model group of this workgroup: models [m0, m1), basis rows [m0*r, m1*r) padded to oc
+  const int m0 = blockIdx.y * a.mpg, m1 = min(a.M, m0 + a.mpg);
+  const int row0 = m0 * a.r, oc = ((m1 - m0) * a.r + 15) & ~15;  // <= kOC
+  float* fT = ssm;                    // D x kFP (k-major box features)
+  float* qc = fT + D * kFP;           // 16 x kOC basis chunk
+  float* qv = ssm;                    // kFP x (kOC+1), aliases fT/qc after the GEMM
+  const int region = max(D * kFP + 16 * kOC, kFP * (kOC + 1));
   float* ffv = ssm + region;
   int* gate = reinterpret_cast<int*>(ffv + kFP);
   int* hrow = gate + kFP;
   int* rng = hrow + kFP;                       // packed xr | yr << 10 | zr << 20
   long long* ent = reinterpret_cast<long long*>(rng + kFP + (kFP & 1));
-  double* bsc = reinterpret_cast<double*>(ent + kFP);  // kFP * M
+  double* bsc = reinterpret_cast<double*>(ent + kFP);  // kFP * mpg
   const int tid = threadIdx.x;
   const int xyn = a.xn * a.yn;
-  // basis chunk c = rows [16c, 16c+16) of qt (D x Opad row-major, contiguous); chunk 0
-  // is requested now so its latency overlaps the list / exist / G loads
-  const int D16 = (D + 15) >> 4, nq4 = 4 * Opad, tot4 = D * Opad / 4;
-  const float4* qt4 = reinterpret_cast<const float4*>(a.qt);
-  float4 pre[4];
+  // basis chunk c = qt rows [16c, 16c+16), columns [row0, row0+oc): one float4 per thread;
+  // chunk 0 is requested now so its latency overlaps the list / exist / G loads
+  const int D16 = (D + 15) >> 4;
+  float pre[4];  // 16 x oc floats per chunk, <= 4 per thread
   auto load_chunk = [&](int c) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int e = tid + j * kBlock, g = c * nq4 + e;
-      pre[j] = (e < nq4 && g < tot4) ? qt4[g] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int e = tid + j * kBlock, dd = e / oc, o = e - dd * oc, d = 16 * c + dd;
+      pre[j] = (dd < 16 && d < D) ? a.qt[(int64_t)d * Qs + row0 + o] : 0.0f;
     }
   };
   load_chunk(0);
@@ -363,118 +369,135 @@ __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch a) {
     rng[tid] = rr;
     ent[tid] = en;
   }
-  __syncthreads();
-  {  // box sums in the fixed (dz, dy, dx) order over non-empty rows; lane = position
+  lds_barrier();
+  C3H_SPROF(1);
+  {  // box sums in the fixed (dz, dy, dx) order over non-empty rows; lane = position.
+     // Cells go in batches of 4 x (this thread's d4 slots): every load of a batch is in
+     // flight together.  Rows of empty subdivisions read as 0 (their G rows may be stale;
+     // +0 added to a sum that starts at +0 changes nothing).
     const int pp = tid & (kFP - 1), dg = tid / kFP;
+    constexpr int kDG = kBlock / kFP;  // d4 stride
     const bool ok = gate[pp];
     const int h = hrow[pp], rr = rng[pp];
     const int xr = rr & 1023, yr = (rr >> 10) & 1023, zr = rr >> 20;
+    const int ncell = ok ? xr * yr * zr : 0;
     const float4* G4 = reinterpret_cast<const float4*>(a.G);
-    unsigned long long live = 0;  // occupancy of the first 64 box cells
-    const int ncell = xr * yr * zr;
-    if (ok) {
-      int c = 0;
-      for (int dz = 0; dz < zr; ++dz)
-        for (int dy = 0; dy < yr; ++dy)
-          for (int dx = 0; dx < xr && c < 64; ++dx, ++c)
-            if (a.exist[h + dz * xyn + dy * a.xn + dx]) live |= 1ull << c;
-    }
-    for (int d4 = dg; d4 < D4; d4 += kBlock / kFP) {
-      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ok) {
-        int c = 0;
-        for (int dz = 0; dz < zr; ++dz)
-          for (int dy = 0; dy < yr; ++dy)
-            for (int dx = 0; dx < xr; ++dx, ++c) {
-              const int hh = h + dz * xyn + dy * a.xn + dx;
-              const bool use = c < 64 ? (live >> c & 1) : (a.exist[hh] != 0);
-              if (!use) continue;
-              const float4 g = G4[(int64_t)hh * D4 + d4];
-              s.x += g.x;
-              s.y += g.y;
-              s.z += g.z;
-              s.w += g.w;
+    constexpr int kSlots = 4;  // d4 values per thread handled together (D4 <= 64)
+    float4 s[kSlots];
+#pragma unroll
+    for (int q = 0; q < kSlots; ++q) s[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int d4b = 0; d4b < D4; d4b += kSlots * kDG) {
+      for (int c0 = 0; c0 < ncell; c0 += 4) {
+        float4 g[4][kSlots];
+        bool lv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int c = c0 + k;
+          const int dx = c % xr, dy = (c / xr) % yr, dz = c / (xr * yr);
+          const int hh = h + dz * xyn + dy * a.xn + dx;
+          lv[k] = c < ncell && a.exist[c < ncell ? hh : h] != 0;
+#pragma unroll
+          for (int q = 0; q < kSlots; ++q) {
+            const int d4 = d4b + dg + q * kDG;
+            g[k][q] = (c < ncell && d4 < D4) ? G4[(int64_t)hh * D4 + d4] : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int q = 0; q < kSlots; ++q)
+            if (lv[k]) {
+              s[q].x += g[k][q].x;
+              s[q].y += g[k][q].y;
+              s[q].z += g[k][q].z;
+              s[q].w += g[k][q].w;
             }
       }
-      fT[(4 * d4 + 0) * kFP + pp] = s.x;
-      fT[(4 * d4 + 1) * kFP + pp] = s.y;
-      fT[(4 * d4 + 2) * kFP + pp] = s.z;
-      fT[(4 * d4 + 3) * kFP + pp] = s.w;
+#pragma unroll
+      for (int q = 0; q < kSlots; ++q) {
+        const int d4 = d4b + dg + q * kDG;
+        if (d4 < D4) {
+          fT[(4 * d4 + 0) * kFP + pp] = s[q].x;
+          fT[(4 * d4 + 1) * kFP + pp] = s[q].y;
+          fT[(4 * d4 + 2) * kFP + pp] = s[q].z;
+          fT[(4 * d4 + 3) * kFP + pp] = s[q].w;
+        }
+        s[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
-    (void)ncell;
   }
-  __syncthreads();
+  lds_barrier();
+  C3H_SPROF(2);
   if (tid < kFP) {
     float s = 0.0f;
     for (int d = 0; d < D; ++d) s = __builtin_fmaf(fT[d * kFP + tid], fT[d * kFP + tid], s);
     ffv[tid] = s;
   }
+  // GEMM: thread (tp, to): positions 2*tp, 2*tp+1; basis rows 4*to .. 4*to+3 of the group
   const int tp = tid & 15, to = tid >> 4;
-  const bool active = to * 16 < Opad;
-  float acc[2][16];
+  const bool active = 4 * to < oc;
+  float acc[2][4];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 16; ++j) acc[i][j] = 0.0f;
+    for (int q = 0; q < 4; ++q) acc[i][q] = 0.0f;
   for (int c = 0; c < D16; ++c) {
     const int d0 = 16 * c, dn = min(16, D - d0);
-    __syncthreads();  // fT complete / the previous chunk's readers done
+    lds_barrier();  // fT complete / the previous chunk's readers done
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int e = tid + j * kBlock;
-      if (e < nq4) reinterpret_cast<float4*>(qc)[e] = pre[j];
-    }
+    for (int j = 0; j < 4; ++j)  // [dd][oc] row-major
+      if (tid + j * kBlock < 16 * oc) qc[tid + j * kBlock] = pre[j];
     if (c + 1 < D16) load_chunk(c + 1);
-    __syncthreads();
+    lds_barrier();
     if (active) {
+#pragma unroll 4
       for (int dd = 0; dd < dn; ++dd) {
         const float2 f = *reinterpret_cast<const float2*>(&fT[(d0 + dd) * kFP + 2 * tp]);
-        const float4* qrow = reinterpret_cast<const float4*>(&qc[dd * Opad + 16 * to]);
-#pragma unroll
-        for (int j4 = 0; j4 < 4; ++j4) {
-          const float4 q = qrow[j4];
-          acc[0][4 * j4 + 0] = __builtin_fmaf(f.x, q.x, acc[0][4 * j4 + 0]);
-          acc[0][4 * j4 + 1] = __builtin_fmaf(f.x, q.y, acc[0][4 * j4 + 1]);
-          acc[0][4 * j4 + 2] = __builtin_fmaf(f.x, q.z, acc[0][4 * j4 + 2]);
-          acc[0][4 * j4 + 3] = __builtin_fmaf(f.x, q.w, acc[0][4 * j4 + 3]);
-          acc[1][4 * j4 + 0] = __builtin_fmaf(f.y, q.x, acc[1][4 * j4 + 0]);
-          acc[1][4 * j4 + 1] = __builtin_fmaf(f.y, q.y, acc[1][4 * j4 + 1]);
-          acc[1][4 * j4 + 2] = __builtin_fmaf(f.y, q.z, acc[1][4 * j4 + 2]);
-          acc[1][4 * j4 + 3] = __builtin_fmaf(f.y, q.w, acc[1][4 * j4 + 3]);
-        }
+        const float4 q = *reinterpret_cast<const float4*>(&qc[dd * oc + 4 * to]);
+        acc[0][0] = __builtin_fmaf(f.x, q.x, acc[0][0]);
+        acc[0][1] = __builtin_fmaf(f.x, q.y, acc[0][1]);
+        acc[0][2] = __builtin_fmaf(f.x, q.z, acc[0][2]);
+        acc[0][3] = __builtin_fmaf(f.x, q.w, acc[0][3]);
+        acc[1][0] = __builtin_fmaf(f.y, q.x, acc[1][0]);
+        acc[1][1] = __builtin_fmaf(f.y, q.y, acc[1][1]);
+        acc[1][2] = __builtin_fmaf(f.y, q.z, acc[1][2]);
+        acc[1][3] = __builtin_fmaf(f.y, q.w, acc[1][3]);
       }
     }
   }
-  __syncthreads();  // qv aliases fT / qc
+  lds_barrier();  // qv aliases fT / qc
+  C3H_SPROF(3);
   if (active) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 16; ++j) qv[(2 * tp + i) * (Opad + 1) + 16 * to + j] = acc[i][j];
+      for (int q = 0; q < 4; ++q) qv[(2 * tp + i) * (kOC + 1) + 4 * to + q] = acc[i][q];
   }
-  __syncthreads();
-  for (int e = tid; e < kFP * a.M; e += kBlock) {
-    const int m = e / kFP, pp = e - m * kFP;
+  lds_barrier();
+  const int nm = m1 - m0;
+  for (int e = tid; e < kFP * nm; e += kBlock) {
+    const int mm = e / kFP, pp = e - mm * kFP;
     double sc = -2.0;
     if (gate[pp]) {
       float q2 = 0.0f;
-      const float* q = qv + pp * (Opad + 1) + m * a.r;
+      const float* q = qv + pp * (kOC + 1) + mm * a.r;
       for (int i = 0; i < a.r; ++i) q2 = __builtin_fmaf(q[i], q[i], q2);
       sc = sqrt((double)q2) / sqrt((double)ffv[pp]);
       const long long en = ent[pp];
       const ModeGeom& md = a.md[(int)(en >> 40)];
-      a.scores[md.offset + (int64_t)m * md.P + (en & ((1ll << 40) - 1))] = sc;
+      a.scores[md.offset + (int64_t)(m0 + mm) * md.P + (en & ((1ll << 40) - 1))] = sc;
     }
     bsc[e] = sc;
   }
+  C3H_SPROF(4);
   if (a.partials) {
-    __syncthreads();
-    for (int m = tid; m < a.M; m += kBlock) {  // (score desc, scan order asc)
+    lds_barrier();
+    for (int mm = tid; mm < nm; mm += kBlock) {  // (score desc, scan order asc)
       double best = -2.0;
       long long bo = -1;
       for (int pp = 0; pp < kFP; ++pp) {
         if (!gate[pp]) continue;
-        const double sc = bsc[m * kFP + pp];
+        const double sc = bsc[mm * kFP + pp];
         const long long en = ent[pp];
         const long long o = a.order_base[(int)(en >> 40)] + (en & ((1ll << 40) - 1));
         if (sc > best || (sc == best && o < bo)) {
@@ -482,9 +505,10 @@ __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch a) {
           bo = o;
         }
       }
-      a.partials[(int64_t)blockIdx.x * a.M + m] = ScorePartial{best, bo};
+      a.partials[(int64_t)blockIdx.x * a.M + m0 + mm] = ScorePartial{best, bo};
     }
   }
+  C3H_SPROF(7);
 }
 
 // ---------------------------------------------------------------- rank replay
@@ -670,18 +694,18 @@ size_t score_lds_bytes(int D, int r, int SP) {
   return sizeof(float) * ((size_t)SP * (D + 1) + (size_t)r * SP + SP) + sizeof(int) * SP;
 }
 
-bool score_fast_ok(int D, int Opad) { return D <= 256 && (D & 3) == 0 && Opad <= 256; }
+bool score_fast_ok(int D, int r) { return D <= 256 && (D & 3) == 0 && r <= kOC; }
 
 int64_t score_blocks(const ScoreLaunch& a) {
   const int64_t P = (int64_t)a.xe * a.ye * a.ze;
-  if (score_fast_ok(a.D, a.Opad)) return (P + kFP - 1) / kFP;
+  if (score_fast_ok(a.D, a.r)) return (P + kFP - 1) / kFP;
   return a.D <= 256 ? (P + 63) / 64 : (P + 15) / 16;
 }
 
 hipError_t launch_score(const ScoreLaunch& a, hipStream_t s) {
   const int64_t P = (int64_t)a.xe * a.ye * a.ze;
   if (P <= 0) return hipSuccess;
-  if (score_fast_ok(a.D, a.Opad)) {
+  if (score_fast_ok(a.D, a.r)) {
     return hipErrorInvalidValue;  // the fast path is the sparse search (launch_sparse_search)
   } else if (a.D <= 256) {
     score_kernel<64><<<(unsigned)((P + 63) / 64), kBlock, score_lds_bytes(a.D, a.r, 64), s>>>(a, P);
@@ -697,10 +721,11 @@ hipError_t launch_sparse_search(const SparseSearch& a, hipStream_t s) {
   const int64_t ptot = a.pstart[a.nmodes];
   if (ptot <= 0) return hipSuccess;
   gate_kernel<<<(unsigned)((ptot + kBlock - 1) / kBlock), kBlock, 0, s>>>(a);
-  const size_t region = std::max((size_t)a.D * kFP + 16 * (size_t)a.Opad, (size_t)kFP * (a.Opad + 1));
+  const size_t region = std::max((size_t)a.D * kFP + 16 * (size_t)kOC, (size_t)kFP * (kOC + 1));
   const size_t lds = sizeof(float) * (region + kFP) + sizeof(int) * 4 * kFP + sizeof(long long) * kFP +
-                     sizeof(double) * kFP * a.M + 16;
-  score_list_kernel<<<(unsigned)sparse_score_blocks(a), kBlock, lds, s>>>(a);
+                     sizeof(double) * kFP * a.mpg + 16;
+  const unsigned groups = (unsigned)((a.M + a.mpg - 1) / a.mpg);
+  score_list_kernel<<<dim3((unsigned)sparse_score_blocks(a), groups), kBlock, lds, s>>>(a);
   return hipGetLastError();
 }
 

@@ -344,3 +344,40 @@ def test_dense_256_bin_block_linearity(ctx):
     # per-subdivision counts are exact in float32; the whole-grid ones are float(exact int)
     np.testing.assert_array_equal(parts.astype(np.float32), whole.astype(np.float32))
     assert whole[:6].sum() == 3 * 256 ** 3  # each voxel adds beta_c + (1-beta_c) per colour
+
+
+@pytest.mark.parametrize("lanes", [1, 3, 4])
+def test_run_frames_lanes_match_sequential(ctx, lanes):
+    """c3h_run_frames with frames in flight on lane contexts == frame-by-frame
+    cleanMax / extract / search on one context; the context ends with the last frame."""
+    import torch
+    G, S, rng_box = 64, 8, (2, 2, 1)
+    frames = [synth.kinect_scene(60_000, grid=G, leaf=0.01, seed=synth.BASE_SEED + 40 + i) for i in range(7)]
+    words = []
+    for pts in frames:
+        gi = ctx.voxelize(pts, 0.01)
+        assert list(gi.div_b) == [G] * 3
+        words.append(ctx.grid().reshape(-1).astype(np.uint32))
+    axis_t, var, axis_q = synth.random_bases(117, 24, 4, 6, seed=3)
+    ctx.search_setup(axis_t, var, axis_q)
+    ctx.set_rank(2)
+    ref = []
+    for w in words:
+        ctx.set_grid(w, (G, G, G))
+        ctx.clean_max()
+        ctx.extract(117, THR, S)
+        det, _ = ctx.search(rng_box, 20)
+        ref.append(det.copy())
+    last_feat = ctx.features()
+    dev = torch.device("cuda", 0)
+    d_grids = [torch.from_numpy(w.view(np.int32)).to(dev) for w in words]
+    d_out = torch.zeros((len(words), 4 * 2 * 3), dtype=torch.int64, device=dev)
+    ctx.set_lanes(lanes)
+    ctx.run_frames(np.array([g.data_ptr() for g in d_grids], np.uint64), (G, G, G), (0, 0, 0), 0.01, 117,
+                   THR, S, rng_box, 20, True, d_out.data_ptr())
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy().view(c3hlac.DET_DTYPE).reshape(len(words), 4, 2)
+    for i in range(len(words)):
+        np.testing.assert_array_equal(got[i], ref[i])
+    np.testing.assert_array_equal(ctx.features(), last_feat)
+    ctx.set_lanes(4)

@@ -1,0 +1,39 @@
+"""Diagnostics: host enqueue time vs device time of c3h_run_frames for 1..4 lanes."""
+import sys
+import time
+
+sys.path[:0] = ["mapping-private_amd"]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import c3hlac  # noqa: E402
+from c3hlac import synth  # noqa: E402
+
+G, LEAF = 256, 0.01
+dev = torch.device("cuda", 0)
+with c3hlac.Context(0) as ctx:
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    grids = []
+    for s in range(3):
+        pts = synth.kinect_scene(1_000_000, grid=G, leaf=LEAF, seed=synth.BASE_SEED + s)
+        ctx.voxelize(pts, LEAF)
+        w = torch.empty(G ** 3, dtype=torch.int32, device=dev)
+        ctx.lib.c3h_get_grid(ctx.h, c3hlac.ptr(w), 1)
+        grids += [w, torch.roll(w.view(G, G, G), 37, 2).reshape(-1).contiguous()]
+    axis_t, var, axis_q = synth.random_bases(117, 100, 10, 20, seed=synth.BASE_SEED)
+    ctx.search_setup(axis_t, var, axis_q)
+    ctx.set_rank(1)
+    N = 200
+    gptr = np.array([grids[i % 6].data_ptr() for i in range(N)], np.uint64)
+    dets = torch.zeros((N, 30), dtype=torch.int64, device=dev)
+    for lanes in (1, 2, 3, 4, 6, 8):
+        ctx.set_lanes(lanes)
+        for rep in range(2):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ctx.run_frames(gptr, (G,) * 3, (0, 0, 0), LEAF, 117, (147, 146, 148), 10, (2, 2, 2), 100, True,
+                           dets.data_ptr())
+            t1 = time.perf_counter()
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+        print("lanes=%d host_enqueue_us_per_frame=%.1f total_us_per_frame=%.1f" %
+              (lanes, (t1 - t0) / N * 1e6, (t2 - t0) / N * 1e6), flush=True)
