@@ -85,6 +85,14 @@ def load(path=None):
     if _lib is not None and path is None:
         return _lib
     p = Path(path) if path else Path(os.environ.get("C3HLAC_LIB", LIB_PATH))
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7 (same SONAME as
+    # /opt/rocm's).  Loading torch first makes this library bind to that already-loaded
+    # runtime; loading it first would leave torch to start a second runtime, which
+    # cannot open the device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not p.exists():
         raise RuntimeError(
             "libc3hlac_mi355x.so not found at %s: build it with `make -C mapping-private_amd` "

@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <string>
+#include <mutex>
 #include <vector>
 
 #include "../../include/c3hlac_mi355x.h"
@@ -45,6 +46,7 @@ struct ScorePartial {
 };
 
 struct Timer {
+  std::mutex mu;  // lanes enqueue from their own host threads
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[C3H_NTIMERS];
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
   float ms[C3H_NTIMERS] = {0, 0, 0, 0, 0};
@@ -66,7 +68,7 @@ struct c3h_ctx {
   std::vector<c3h_ctx*> lanes;
   std::vector<hipEvent_t> lane_ev;
   hipEvent_t fork_ev = nullptr;
-  int nlanes = 4;
+  int nlanes = 3;
   // host copy of the search setup, replayed into the lanes
   uint64_t setup_version = 0;
   std::vector<float> h_axis_p, h_var, h_axis_q, h_fmax;
@@ -108,6 +110,7 @@ struct c3h_ctx {
   c3h::DevBuf<uint32_t> gcnt;       // [2] gate-list counters by search epoch parity
   uint32_t search_epoch = 0;
   c3h::DevBuf<long long> prof;      // diagnostics (C3H_PROF)
+
   std::vector<int32_t> h_segs;      // host copy (kept alive for the async upload)
   c3h::DevBuf<uint32_t> lut;        // 256 packed (sin | cos<<8), two variants
   bool lut_ready = false;
@@ -193,6 +196,7 @@ struct C3Launch {
   long long* prof;  // diagnostics (C3H_PROF)
   int debug;
 };
+
 int64_t c3hlac_grid(const C3Launch& a);  // persistent grid of the tile kernel
 hipError_t launch_c3hlac(const C3Launch& a, hipStream_t s);
 hipError_t launch_c3_finalize(const unsigned long long* acc64, int64_t hist_num, int variant,
@@ -227,6 +231,7 @@ struct ModeGeom {
   int64_t offset;  // into scores (M x P block)
   int64_t P;
   int xe, ye, xr, yr, zr;
+  int mode;        // SearchMode id
 };
 struct SparseSearch {
   const float* G;
@@ -244,9 +249,25 @@ struct SparseSearch {
   uint32_t* cnt;          // [2] list counters by epoch parity
   uint32_t epoch;
   ScorePartial* partials;  // per block per model (nullable)
+  uint32_t* done;          // [2] finished-workgroup counters by epoch parity
+  c3h_det* lists;          // rank 1 fused replay: M lists (nullable = no fused replay)
+  c3h_det* out2;           // copy of the lists after the update (nullable)
+  int clean;               // apply a pending cleanMax first
   long long* prof;         // diagnostics (C3H_PROF): [blocks][8]
 };
-hipError_t launch_sparse_search(const SparseSearch& a, hipStream_t s);
+// sparse compress fused into the gate launch (nullable in launch_sparse_search)
+struct SparseCompress {
+  const float* feat;
+  const float* PT;
+  const float* fmax;
+  float* G;
+  const int32_t* rows;
+  const uint32_t* nrows;
+  int F, D, Dpad, fmax_len;
+  int64_t H;
+};
+bool compress_rows_ok(int F, int Dpad);
+hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc, hipStream_t s);
 int64_t sparse_score_blocks(const SparseSearch& a);
 
 struct ReplayMode {
@@ -262,9 +283,6 @@ struct ReplayModes {
 hipError_t launch_replay(const double* scores, const ReplayModes& modes, int M, int rank,
                          int r1, int r2, int r3, int clean, c3h_det* lists, c3h_det* out2,
                          hipStream_t s);
-hipError_t launch_argmax_replay(const ScorePartial* partials, int64_t nparts, const uint32_t* nlist,
-                                const ReplayModes& modes, int M, int clean, c3h_det* lists,
-                                c3h_det* out2, hipStream_t s);
 
 hipError_t launch_clean_lists(c3h_det* lists, int n, hipStream_t s);
 size_t c3hlac_lds_bytes(int tw_max, int list_max);

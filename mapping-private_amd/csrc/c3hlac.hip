@@ -118,8 +118,8 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t n) {
 // tile segment of centre coordinate c along that axis (-1 when c is no centre, e.g.
 // below the subdivision offset): the reference's float subdivision arithmetic is baked
 // into these host-built tables.
-constexpr int kOccUnroll = 4;  // 16-B loads per thread in flight per chunk
-constexpr int kOccSet = 256;   // LDS set of tiles touched by one workgroup
+constexpr int kOccUnroll = 8;  // 16-B loads per thread in flight per chunk
+constexpr int kOccSet = 1024;  // LDS set of tiles touched by one workgroup (4 KB)
 
 // Flags are epoch stamps: tile t is non-empty in this frame iff flags[t] == epoch, so
 // nothing is reset between frames.  Each workgroup streams contiguous 16-KB chunks
@@ -135,8 +135,8 @@ __device__ __forceinline__ void stamp_tile(int t, uint32_t epoch, uint32_t* flag
 
 __device__ __forceinline__ void set_insert(int* s_set, int t, uint32_t epoch, uint32_t* flags,
                                            uint32_t* cnt, int32_t* work) {
-  int h = (int)(((uint32_t)t * 0x9E3779B1u) >> 24);  // 8-bit hash
-  static_assert(kOccSet == 256 && kBlock == 256, "set slot per thread");
+  int h = (int)(((uint32_t)t * 0x9E3779B1u) >> 22);  // 10-bit hash
+  static_assert(kOccSet == 1024 && kOccSet % kBlock == 0, "set slots per thread");
   for (int probe = 0; probe < kOccSet; ++probe, h = (h + 1) & (kOccSet - 1)) {
     const int cur = s_set[h];
     if (cur == t) return;
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(kBlock) void c3_occupancy_kernel(
   const int16_t* my = axmap + gx;
   const int16_t* mz = axmap + gx + gy;
   cnt += epoch & 1;
-  s_set[tid] = -1;
+  for (int i = tid; i < kOccSet; i += kBlock) s_set[i] = -1;
   __syncthreads();
   int last = -1;
   if (kVec) {
@@ -212,15 +212,22 @@ __global__ __launch_bounds__(kBlock) void c3_occupancy_kernel(
   }
   __syncthreads();
   // flush: one stamp per (workgroup, tile); new tiles appended with one add per wave
-  const int t = s_set[tid];
-  bool fresh = false;
-  if (t >= 0) fresh = atomicExch(&flags[t], epoch) != epoch;
-  const unsigned long long m = __ballot(fresh);
-  if (m) {
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(cnt, (uint32_t)__popcll(m));
-    base = __shfl(base, 0, 64);
-    if (fresh) work[base + __popcll(m & ((1ull << lane) - 1))] = t;
+  int ts[kOccSet / kBlock];
+  bool fresh[kOccSet / kBlock];
+#pragma unroll
+  for (int j = 0; j < kOccSet / kBlock; ++j) {  // all exchanges in flight together
+    ts[j] = s_set[tid + j * kBlock];
+    fresh[j] = ts[j] >= 0 && atomicExch(&flags[ts[j]], epoch) != epoch;
+  }
+#pragma unroll
+  for (int j = 0; j < kOccSet / kBlock; ++j) {
+    const unsigned long long m = __ballot(fresh[j]);
+    if (m) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(cnt, (uint32_t)__popcll(m));
+      base = __shfl(base, 0, 64);
+      if (fresh[j]) work[base + __popcll(m & ((1ull << lane) - 1))] = ts[j];
+    }
   }
 }
 
@@ -245,8 +252,8 @@ struct KArgs {
   uint32_t* rowcnt;       // [2] row-list counters by epoch parity
   uint32_t epoch;
   int ntiles;
-  int zero_empty;         // direct mode with every subdivision one tile (h == tile): zero
-                          // the rows of unflagged tiles here
+  int zblocks;            // leading workgroups that zero the rows of unstamped tiles
+                          // (direct mode, every subdivision one tile: h == tile), else 0
   long long* prof;  // diagnostics only (C3H_PROF): per-block phase timestamps [grid][8]
   int debug;  // diagnostics only (C3H_C3_DEBUG): 1 stop after the loads, 2 after compaction,
              // 3 skip the tile kernel
@@ -275,22 +282,32 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
   const int F = a.variant;
   C3H_PROF(0, true);
   // issued together: the work count, this workgroup's first work item, its phase-Z flags
-  const int G = (int)gridDim.x;
-  int wi = (int)blockIdx.x;
-  int tile_next = wi < a.ntiles ? a.work[wi] : 0;  // speculative; used only if wi < nwork
-  const int nwork = (int)a.workcnt[a.epoch & 1];
-  const int per = (a.ntiles - (int)blockIdx.x + G - 1) / G;  // phase-Z tiles of this block
-  uint32_t zflag[2];
-  int zt[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    zt[j] = (int)blockIdx.x + (tid + j * kBlock) * G;
-    zflag[j] = (a.zero_empty && tid + j * kBlock < per) ? a.flags[zt[j]] : a.epoch;
-  }
   if (blockIdx.x == 0 && tid == 0) {  // the next frame's counters
     a.rowcnt[(a.epoch + 1) & 1] = 0;
     a.workcnt[(a.epoch + 1) & 1] = 0;
   }
+  if ((int)blockIdx.x < a.zblocks) {
+    // zero role (direct mode, every subdivision one tile: h == tile): rows of the tiles
+    // pass 1 left unstamped, one wave-wide store per 64 floats
+    for (int t0 = (int)blockIdx.x * kBlock; t0 < a.ntiles; t0 += a.zblocks * kBlock) {
+      const int t = t0 + tid;
+      unsigned long long m = __ballot(t < a.ntiles && a.flags[t] != a.epoch);
+      while (m) {
+        const int q = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const int tj = (t0 + (tid & ~63)) + q;
+        float* row = a.feat + (int64_t)tj * F;
+        for (int c = lane; c < F; c += 64) row[c] = 0.0f;
+        if (lane == 0) a.exist[tj] = 0;
+      }
+    }
+    return;
+  }
+  // work role: workgroup b takes items b, b + G, ... of the dense work list (balanced)
+  const int G = (int)gridDim.x - a.zblocks;
+  int wi = (int)blockIdx.x - a.zblocks;
+  int tile_next = wi < a.ntiles ? a.work[wi] : 0;  // speculative; used only if wi < nwork
+  const int nwork = (int)a.workcnt[a.epoch & 1];
   if (a.debug == 3) return;  // diagnostics: occupancy pass only
   s_lut[tid] = a.lut[tid];
   const bool segs_lds = a.seg_stride <= kSegLds;
@@ -302,7 +319,6 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
   lds_barrier();
   C3H_PROF(1, true);
 
-  // the work list is dense: workgroup b takes items b, b + G, ... (balanced)
   for (; wi < (a.debug == 4 ? 0 : nwork); wi += G) {
     const int tile = tile_next;
     if (wi + G < nwork) tile_next = a.work[wi + G];
@@ -499,29 +515,6 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
     lds_barrier();  // LDS is reused by the next tile
     C3H_PROF(6, wi == (int)blockIdx.x);
   }
-  // phase Z (direct mode, every subdivision one tile: h == tile): rows of the tiles pass 1
-  // left unstamped, one wave-wide store per 64 floats
-  if (a.zero_empty) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      unsigned long long m = __ballot(zflag[j] != a.epoch);
-      while (m) {
-        const int q = __ffsll((long long)m) - 1;
-        m &= m - 1;
-        const int tj = __shfl(zt[j], q, 64);
-        float* row = a.feat + (int64_t)tj * F;
-        for (int c = lane; c < F; c += 64) row[c] = 0.0f;
-        if (lane == 0) a.exist[tj] = 0;
-      }
-    }
-    for (int i = tid + 2 * kBlock; i < per; i += kBlock) {  // > 512 tiles per workgroup
-      const int t = (int)blockIdx.x + i * G;
-      if (a.flags[t] != a.epoch) {
-        for (int c = 0; c < F; ++c) a.feat[(int64_t)t * F + c] = 0.0f;
-        a.exist[t] = 0;
-      }
-    }
-  }
   C3H_PROF(7, true);
 }
 
@@ -548,6 +541,9 @@ size_t c3hlac_lds_bytes(int tw_max, int list_max) {
 
 // persistent grid: every workgroup resident at once (occupancy from LDS and VGPRs)
 int64_t c3hlac_grid(const C3Launch& l) {
+  // work workgroups: two per CU (a frame's few hundred non-empty tiles finish in a couple
+  // of rounds while the rest of the chip stays free for the other frames in flight),
+  // capped by what is resident at once; plus the zero-role workgroups
   const int tx_max = ((l.lmax[0] + 2) + 3 + 3) & ~3;
   const size_t lds = c3hlac_lds_bytes(tx_max * (l.lmax[1] + 2) * (l.lmax[2] + 1), l.lmax[0] * l.lmax[1] * l.lmax[2]);
   static thread_local size_t c_lds = 0;
@@ -566,9 +562,10 @@ int64_t c3hlac_grid(const C3Launch& l) {
     c_ncu = n_cu;
     c_dev = dev;
   }
-  int64_t grid = std::min<int64_t>(l.ntiles, (int64_t)c_ncu * c_per_cu);
-  if (const char* g = getenv("C3H_TILE_GRID")) grid = std::max<int64_t>(1, std::min<int64_t>(grid, atoi(g)));
-  return std::max<int64_t>(grid, 1);
+  int64_t work = std::min<int64_t>(l.ntiles, (int64_t)c_ncu * std::min(c_per_cu, 2));
+  if (const char* g = getenv("C3H_TILE_GRID")) work = std::max<int64_t>(1, std::min<int64_t>(l.ntiles, atoi(g)));
+  const int64_t zero = l.zero_empty ? std::min<int64_t>(64, l.ntiles) : 0;
+  return std::max<int64_t>(work, 1) + zero;
 }
 
 hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
@@ -576,7 +573,11 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
   const int64_t nvox = (int64_t)l.gx * l.gy * l.gz;
   const bool vec = (l.gx & 3) == 0;
   const int64_t items = vec ? nvox / 4 : nvox;
-  int g1 = (int)std::min<int64_t>((items + kBlock * kOccUnroll - 1) / (kBlock * kOccUnroll), 256 * 32);
+  // HBM-bound: ~3-4 resident workgroups per CU keep enough bytes in flight (128 B per
+  // lane); a smaller grid leaves CU slots to the latency-bound stages of other frames
+  int occ_cap = 1024;
+  if (const char* g = getenv("C3H_OCC_GRID")) occ_cap = std::max(1, atoi(g));  // diagnostics
+  int g1 = (int)std::min<int64_t>((items + kBlock * kOccUnroll - 1) / (kBlock * kOccUnroll), occ_cap);
   if (g1 < 1) g1 = 1;
   if (vec)
     c3_occupancy_kernel<true><<<g1, kBlock, 0, s>>>(l.grid, l.gx, l.gy, l.gz, l.axmap, l.nseg[0],
@@ -614,7 +615,7 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
   a.rows = l.rows;
   a.rowcnt = l.rowcnt;
   a.epoch = l.epoch;
-  a.zero_empty = l.zero_empty;
+  a.zblocks = l.zero_empty ? (int)std::min<int64_t>(64, l.ntiles) : 0;
   a.ntiles = (int)l.ntiles;
   a.debug = l.debug;
   a.prof = l.prof;

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include "c3h_internal.h"
 
@@ -72,6 +73,7 @@ struct Timed {
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
   Timed(c3h_ctx* c, int s) : ctx(c), T(c->parent ? &c->parent->timer : &c->timer), slot(s) {
     if (!(T->mask >> (s + 1) & 1)) return;
+    std::lock_guard<std::mutex> g(T->mu);
     if (T->pool.empty()) {
       hipEvent_t a, b;
       if (hipEventCreate(&a) != hipSuccess) return;
@@ -88,6 +90,7 @@ struct Timed {
   ~Timed() {
     if (!ev.first) return;
     (void)hipEventRecord(ev.second, ctx->stream);
+    std::lock_guard<std::mutex> g(T->mu);
     T->pending[slot].push_back(ev);
   }
 };
@@ -346,20 +349,6 @@ int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate
   const int64_t H = (int64_t)xn * yn * zn;
   if (ctx->lists.M != std::max(ctx->M, 1) || ctx->lists.rank != ctx->rank) init_lists(ctx);
   if (H < 1 || H != ctx->hist_num) return 0;  // setData returns early; search is skipped
-  if (!ctx->g_valid) {
-    ENSURE(ctx->G, (size_t)H * ctx->D);
-    Timed t(ctx, 2);
-    // sparse: only the non-empty rows of the extract's list (the rest stay stale and are
-    // gated on exist by every consumer)
-    const bool sparse = ctx->rows_valid && c3h::score_fast_ok(ctx->D, ctx->r);
-    HIPCHK(c3h::launch_compress(ctx->feat.p, H, ctx->F, ctx->axis_pt.p, ctx->D, ctx->Dpad,
-                                ctx->fmax.p, ctx->fmax_len, ctx->G.p,
-                                sparse ? ctx->rows.p : nullptr,
-                                sparse ? ctx->tileflags.p + (ctx->tile_epoch & 1) : nullptr,
-                                ctx->stream));
-    ctx->g_valid = true;
-    ctx->g_sparse = sparse;
-  }
   int modes[6];
   const int nm = mode_schedule(range[0], range[1], range[2], rotate, modes);
   c3h::ReplayModes rm{};
@@ -373,11 +362,26 @@ int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate
     total += rm.m[rm.n].P * ctx->M;
     rm.n++;
   }
-  ENSURE(ctx->scores, total);
+  ENSURE(ctx->scores, std::max<int64_t>(total, 1));
   ctx->scores_n = total;
-  // per-mode score launches; rank 1 uses the per-block partials (fast path only)
-  bool all_fast = c3h::score_fast_ok(ctx->D, ctx->r);
-  int64_t nparts = 0;
+  ENSURE(ctx->G, (size_t)H * ctx->D);
+  const bool fast = c3h::score_fast_ok(ctx->D, ctx->r);
+  // sparse compress: only the non-empty rows of the extract's list (the rest stay stale
+  // and every consumer gates them on exist)
+  const bool sparse_g = !ctx->g_valid && fast && ctx->rows_valid && c3h::compress_rows_ok(ctx->F, ctx->Dpad);
+  if (!ctx->g_valid && !sparse_g) {
+    Timed t(ctx, 2);
+    HIPCHK(c3h::launch_compress(ctx->feat.p, H, ctx->F, ctx->axis_pt.p, ctx->D, ctx->Dpad,
+                                ctx->fmax.p, ctx->fmax_len, ctx->G.p, nullptr, nullptr, ctx->stream));
+    ctx->g_valid = true;
+    ctx->g_sparse = false;
+  }
+  if (!ctx->lists_dev_valid) {
+    int rc = upload_lists(ctx);
+    if (rc != C3H_OK) return rc;
+  }
+  const int clean = ctx->pending_clean ? 1 : 0;
+  const bool use_argmax = fast && ctx->rank == 1;
   std::vector<c3h::ScoreLaunch> launches;
   for (int i = 0; i < rm.n; ++i) {
     int xr, yr, zr;
@@ -404,11 +408,8 @@ int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate
     a.scores = ctx->scores.p + rm.m[i].offset;
     a.order_base = (int64_t)i << 40;
     launches.push_back(a);
-    nparts += c3h::score_blocks(a);
   }
-  const bool use_argmax = all_fast && ctx->rank == 1;
-  const uint32_t* nlist = nullptr;
-  if (all_fast) {  // sparse: gate every position, project the passing ones
+  if (fast) {  // sparse: gate every position, project the passing ones
     c3h::SparseSearch q{};
     q.G = ctx->G.p;
     q.exist = ctx->exist.p;
@@ -427,26 +428,37 @@ int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate
     q.pstart[0] = 0;
     for (int i = 0; i < rm.n; ++i) {
       const auto& a = launches[i];
-      q.md[i] = c3h::ModeGeom{rm.m[i].offset, rm.m[i].P, a.xe, a.ye, a.xr, a.yr, a.zr};
+      q.md[i] = c3h::ModeGeom{rm.m[i].offset, rm.m[i].P, a.xe, a.ye, a.xr, a.yr, a.zr, rm.m[i].mode};
       q.pstart[i + 1] = q.pstart[i] + rm.m[i].P;
       q.order_base[i] = (int64_t)i << 40;
     }
     const int64_t ptot = q.pstart[rm.n];
     ENSURE(ctx->glist, (size_t)std::max<int64_t>(ptot, 1));
-    if (!ctx->gcnt.p) {
-      ENSURE(ctx->gcnt, 2);
-      HIPCHK(hipMemsetAsync(ctx->gcnt.p, 0, 8, ctx->stream));
+    if (!ctx->gcnt.p) {  // [2] list counters | [2] finished-workgroup counters
+      ENSURE(ctx->gcnt, 4);
+      HIPCHK(hipMemsetAsync(ctx->gcnt.p, 0, 16, ctx->stream));
       ctx->search_epoch = 0;
     }
     ++ctx->search_epoch;
     q.list = ctx->glist.p;
     q.cnt = ctx->gcnt.p;
+    q.done = ctx->gcnt.p + 2;
     q.epoch = ctx->search_epoch;
-    nparts = c3h::sparse_score_blocks(q);
-    if (use_argmax) {
+    const int64_t nparts = c3h::sparse_score_blocks(q);
+    if (use_argmax) {  // rank 1: the replay runs in the score launch's last workgroup
       ENSURE(ctx->partials, (size_t)std::max<int64_t>(nparts, 1) * ctx->M);
       q.partials = ctx->partials.p;
-      nlist = ctx->gcnt.p + (q.epoch & 1);
+      q.lists = ctx->d_lists.p;
+      q.out2 = d_out;
+      q.clean = clean;
+    }
+    c3h::SparseCompress sc{};
+    if (sparse_g) {
+      sc = c3h::SparseCompress{ctx->feat.p, ctx->axis_pt.p, ctx->fmax.p, ctx->G.p, ctx->rows.p,
+                               ctx->tileflags.p + (ctx->tile_epoch & 1), ctx->F, ctx->D, ctx->Dpad,
+                               ctx->fmax_len, H};
+      ctx->g_valid = true;
+      ctx->g_sparse = true;
     }
     {
       int rc = prof_prepare(ctx, nparts, &q.prof);
@@ -454,33 +466,29 @@ int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate
     }
     {
       Timed t(ctx, 3);
-      HIPCHK(c3h::launch_sparse_search(q, ctx->stream));
+      HIPCHK(c3h::launch_sparse_search(q, sparse_g ? &sc : nullptr, ctx->stream));
     }
     if (q.prof) {
       int rc = prof_dump(ctx, "score_list_kernel", nparts);
       if (rc != C3H_OK) return rc;
     }
+    if (!use_argmax) {
+      Timed t(ctx, 4);
+      HIPCHK(c3h::launch_replay(ctx->scores.p, rm, ctx->M, ctx->rank, range[0], range[1], range[2],
+                                clean, ctx->d_lists.p, d_out, ctx->stream));
+    }
   } else {
     if (ctx->g_sparse)
       return fail(ctx, C3H_ERR_STATE, "c3h_search: internal: sparse G on the dense score path");
-    Timed t(ctx, 3);
-    for (auto& a : launches) HIPCHK(c3h::launch_score(a, ctx->stream));
-  }
-  if (!ctx->lists_dev_valid) {
-    int rc = upload_lists(ctx);
-    if (rc != C3H_OK) return rc;
-  }
-  {
+    {
+      Timed t(ctx, 3);
+      for (auto& a : launches) HIPCHK(c3h::launch_score(a, ctx->stream));
+    }
     Timed t(ctx, 4);
-    const int clean = ctx->pending_clean ? 1 : 0;
-    if (use_argmax)
-      HIPCHK(c3h::launch_argmax_replay(ctx->partials.p, nparts, nlist, rm, ctx->M, clean, ctx->d_lists.p,
-                                       d_out, ctx->stream));
-    else
-      HIPCHK(c3h::launch_replay(ctx->scores.p, rm, ctx->M, ctx->rank, range[0], range[1],
-                                range[2], clean, ctx->d_lists.p, d_out, ctx->stream));
-    ctx->pending_clean = false;
+    HIPCHK(c3h::launch_replay(ctx->scores.p, rm, ctx->M, ctx->rank, range[0], range[1], range[2], clean,
+                              ctx->d_lists.p, d_out, ctx->stream));
   }
+  ctx->pending_clean = false;
   ctx->lists_host_valid = false;
   ctx->last_range[0] = range[0];
   ctx->last_range[1] = range[1];
@@ -510,6 +518,7 @@ int c3h_create(int hip_device, c3h_ctx** out) {
   if (hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess)
     return bail(C3H_ERR_HIP);
   ctx->stream = ctx->own_stream;
+
   if (hipHostMalloc(&ctx->h_small, 64 * sizeof(uint32_t)) != hipSuccess) return bail(C3H_ERR_HIP);
   if (ensure(ctx, ctx->scratch, 64) != C3H_OK) return bail(C3H_ERR_NOMEM);
   if (ensure(ctx, ctx->lut, 512) != C3H_OK) return bail(C3H_ERR_NOMEM);
@@ -1153,20 +1162,34 @@ int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes
   }
   HIPCHK(hipEventRecord(ctx->fork_ev, ctx->stream));  // inputs were produced on ctx's stream
   for (int l = 0; l < K - 1; ++l) HIPCHK(hipStreamWaitEvent(ctx->lanes[l]->stream, ctx->fork_ev, 0));
-  int nm = 0;
-  for (int32_t i = 0; i < nframes; ++i) {
-    const int lane = (int)((nframes - 1 - i) % K);
+  // each lane is enqueued by its own host thread (launch overhead is per thread)
+  std::vector<int> lane_rc(K, 0);
+  auto run_lane = [&](int lane) {
     c3h_ctx* c = lane == 0 ? ctx : ctx->lanes[lane - 1];
-    int rc = c3h_set_grid(c, d_grids[i], div_b, min_b, leaf, 1);
-    if (rc != C3H_OK) return rc;
-    rc = c3h_clean_max(c);
-    if (rc != C3H_OK) return rc;
-    rc = c3h_extract(c, p, nullptr, nullptr);
-    if (rc != C3H_OK) return lane ? fail(ctx, rc, c->err) : rc;
-    const int r = c3h_search_async(c, range, exist_threshold, rotate, d_out + (size_t)i * per_frame);
-    if (r < 0) return lane ? fail(ctx, r, c->err) : r;
-    if (lane == 0) nm = r;
-  }
+    if (lane) (void)hipSetDevice(c->device);
+    int nm_lane = 0;
+    for (int32_t i = 0; i < nframes; ++i) {
+      if ((int)((nframes - 1 - i) % K) != lane) continue;
+      int rc = c3h_set_grid(c, d_grids[i], div_b, min_b, leaf, 1);
+      if (rc == C3H_OK) rc = c3h_clean_max(c);
+      if (rc == C3H_OK) rc = c3h_extract(c, p, nullptr, nullptr);
+      if (rc == C3H_OK) rc = c3h_search_async(c, range, exist_threshold, rotate, d_out + (size_t)i * per_frame);
+      if (rc < 0) {
+        lane_rc[lane] = rc;
+        return;
+      }
+      nm_lane = rc;
+    }
+    lane_rc[lane] = nm_lane;
+  };
+  std::vector<std::thread> workers;
+  for (int l = 1; l < K; ++l) workers.emplace_back(run_lane, l);
+  run_lane(0);
+  for (auto& w : workers) w.join();
+  for (int l = 1; l < K; ++l)
+    if (lane_rc[l] < 0) return fail(ctx, lane_rc[l], std::string("c3h_run_frames lane: ") + ctx->lanes[l - 1]->err);
+  if (lane_rc[0] < 0) return lane_rc[0];
+  const int nm = lane_rc[0];
   for (int l = 0; l < K - 1; ++l) {  // join
     HIPCHK(hipEventRecord(ctx->lane_ev[l], ctx->lanes[l]->stream));
     HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[l], 0));
@@ -1295,6 +1318,7 @@ int c3h_kernel_times(c3h_ctx* ctx, float* ms_out, int32_t* counts_out, int32_t r
   if (!ctx) return C3H_ERR_ARG;
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  std::lock_guard<std::mutex> g(ctx->timer.mu);
   for (int s = 0; s < C3H_NTIMERS; ++s) {
     for (auto& e : ctx->timer.pending[s]) {
       float ms = 0;

@@ -100,16 +100,29 @@ __global__ __launch_bounds__(kCT) void compress_kernel(
 // in ascending j exactly like compress_kernel, so both paths give identical G rows.
 constexpr int kRR = 16, kRK = 32;
 
-__global__ __launch_bounds__(kBlock) void compress_rows_kernel(
-    const float* __restrict__ feat, int F, const float* __restrict__ PT, int D, int Dpad,
-    const float* __restrict__ fmax, int fmax_len, float* __restrict__ G,
-    const int32_t* __restrict__ rows, const uint32_t* __restrict__ nrows) {
+struct CompressRows {
+  const float* feat;
+  const float* PT;
+  const float* fmax;
+  float* G;
+  const int32_t* rows;
+  const uint32_t* nrows;
+  int F, D, Dpad, fmax_len;
+};
+
+__device__ __forceinline__ void compress_rows_body(const CompressRows& cr, int bid) {
+  const float* __restrict__ feat = cr.feat;
+  const float* __restrict__ PT = cr.PT;
+  const float* __restrict__ fmax = cr.fmax;
+  float* __restrict__ G = cr.G;
+  const int32_t* __restrict__ rows = cr.rows;
+  const int F = cr.F, D = cr.D, Dpad = cr.Dpad, fmax_len = cr.fmax_len;
   extern __shared__ __attribute__((aligned(16))) float csm[];
   float* pc = csm;                 // kRK x Dpad
   float* fs = csm + kRK * Dpad;    // kRR x F
   const int tid = threadIdx.x;
-  const int n = (int)*nrows;
-  const int r0 = blockIdx.x * kRR;
+  const int n = (int)*cr.nrows;
+  const int r0 = bid * kRR;
   if (r0 >= n) return;
   const int nq4 = kRK * Dpad / 4, tot4 = F * Dpad / 4;
   const float4* P4 = reinterpret_cast<const float4*>(PT);
@@ -175,6 +188,10 @@ __global__ __launch_bounds__(kBlock) void compress_rows_kernel(
     for (int q = 0; q < 8; ++q)
       if (8 * cg + q < D) G[h * D + 8 * cg + q] = acc[q];
   }
+}
+
+__global__ __launch_bounds__(kBlock) void compress_rows_kernel(CompressRows cr) {
+  compress_rows_body(cr, blockIdx.x);
 }
 
 // ---------------------------------------------------------------- score
@@ -276,10 +293,13 @@ __device__ __forceinline__ int find_mode(const SparseSearch& a, int64_t g) {
   return mi;
 }
 
-__global__ __launch_bounds__(kBlock) void gate_kernel(SparseSearch a) {
+__device__ __forceinline__ void gate_body(const SparseSearch& a, int bid) {
   const int tid = threadIdx.x, lane = tid & 63;
-  if (blockIdx.x == 0 && tid == 0) a.cnt[(a.epoch + 1) & 1] = 0;  // next search's counter
-  const int64_t g = blockIdx.x * (int64_t)kBlock + tid;
+  if (bid == 0 && tid == 0) {  // the next search's counters
+    a.cnt[(a.epoch + 1) & 1] = 0;
+    a.done[(a.epoch + 1) & 1] = 0;
+  }
+  const int64_t g = bid * (int64_t)kBlock + tid;
   bool pass = false;
   int64_t entry = 0;
   if (g < a.pstart[a.nmodes]) {
@@ -308,6 +328,63 @@ __global__ __launch_bounds__(kBlock) void gate_kernel(SparseSearch a) {
   }
 }
 
+__global__ __launch_bounds__(kBlock) void gate_kernel(SparseSearch a) { gate_body(a, blockIdx.x); }
+
+// one launch for two independent stages: gate workgroups first, then the sparse compress
+__global__ __launch_bounds__(kBlock) void compress_gate_kernel(CompressRows cr, SparseSearch a, int ngate) {
+  if ((int)blockIdx.x < ngate) gate_body(a, blockIdx.x);
+  else compress_rows_body(cr, blockIdx.x - ngate);
+}
+
+// Rank-1 replay fused into the score launch (search.cpp:464-474 with rank_num == 1:
+// checkOverlap returns slot 0, so the update is "first strictly greater maximum in scan
+// order").  One wave per model reduces the partials with (score desc, scan order asc);
+// partials of other workgroups are read with device-scope atomic loads.
+__device__ void argmax_finalize(const SparseSearch& a, int nparts) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int m = w; m < a.M; m += kBlock / 64) {
+    double best = -2.0;
+    long long bo = -1;
+    for (int i = lane; i < nparts; i += 64) {
+      const ScorePartial* q = a.partials + (int64_t)i * a.M + m;
+      const long long qo = __hip_atomic_load(&q->order, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const double qs = __hip_atomic_load(&q->score, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (qo >= 0 && (qs > best || (qs == best && qo < bo))) {
+        best = qs;
+        bo = qo;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double os = __shfl_xor(best, o, 64);
+      const long long oo = __shfl_xor(bo, o, 64);
+      if (oo >= 0 && (os > best || (os == best && (bo < 0 || oo < bo)))) {
+        best = os;
+        bo = oo;
+      }
+    }
+    if (lane == 0) {
+      c3h_det e = a.lists[m];
+      if (a.clean) {
+        e.score = 0.0;
+        e.x = e.y = e.z = 0;
+      }
+      if (bo >= 0 && best > e.score) {
+        const int mi = (int)(bo >> 40);
+        const int64_t p = bo & ((1ll << 40) - 1);
+        const ModeGeom& md = a.md[mi];
+        e.score = best;
+        e.x = (int)(p % md.xe);
+        e.y = (int)((p / md.xe) % md.ye);
+        e.z = (int)(p / ((int64_t)md.xe * md.ye));
+        e.mode = md.mode;
+      }
+      a.lists[m] = e;
+      if (a.out2) a.out2[m] = e;
+    }
+  }
+}
+
 // Fast-path projection over the gate list:
 // kFP entries per workgroup; box rows of empty subdivisions are skipped (their G rows
 // may be stale: the sparse compress only writes non-empty rows; an all-zero row adds
@@ -320,14 +397,17 @@ __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch a) {
   C3H_SPROF(0);
   const int n = (int)a.cnt[a.epoch & 1];
   const int64_t e0 = blockIdx.x * (int64_t)kFP;
-  if (e0 >= n) return;
+  if (e0 >= n) {
+    if (n == 0 && a.lists && blockIdx.x == 0 && blockIdx.y == 0) argmax_finalize(a, 0);  // clean / copy out
+    return;
+  }
   // model group of this workgroup: models [m0, m1), basis rows [m0*r, m1*r) padded to oc
   const int m0 = blockIdx.y * a.mpg, m1 = min(a.M, m0 + a.mpg);
   const int row0 = m0 * a.r, oc = ((m1 - m0) * a.r + 15) & ~15;  // <= kOC
   float* fT = ssm;                    // D x kFP (k-major box features)
-  float* qc = fT + D * kFP;           // 16 x kOC basis chunk
-  float* qv = ssm;                    // kFP x (kOC+1), aliases fT/qc after the GEMM
-  const int region = max(D * kFP + 16 * kOC, kFP * (kOC + 1));
+  float* qw = fT + D * kFP;           // D x oc: this group's whole basis window
+  float* qv = ssm;                    // kFP x (kOC+1), aliases fT/qw after the GEMM
+  const int region = max(D * (kFP + kOC), kFP * (kOC + 1));
   float* ffv = ssm + region;
   int* gate = reinterpret_cast<int*>(ffv + kFP);
   int* hrow = gate + kFP;
@@ -336,19 +416,6 @@ __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch a) {
   double* bsc = reinterpret_cast<double*>(ent + kFP);  // kFP * mpg
   const int tid = threadIdx.x;
   const int xyn = a.xn * a.yn;
-  // basis chunk c = qt rows [16c, 16c+16), columns [row0, row0+oc): one float4 per thread;
-  // chunk 0 is requested now so its latency overlaps the list / exist / G loads
-  const int D16 = (D + 15) >> 4;
-  float pre[4];  // 16 x oc floats per chunk, <= 4 per thread
-  auto load_chunk = [&](int c) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int e = tid + j * kBlock, dd = e / oc, o = e - dd * oc, d = 16 * c + dd;
-      pre[j] = (dd < 16 && d < D) ? a.qt[(int64_t)d * Qs + row0 + o] : 0.0f;
-    }
-  };
-  load_chunk(0);
-
   if (tid < kFP) {
     const int64_t e = e0 + tid;
     int ok = 0, h = 0, rr = 0;
@@ -368,6 +435,16 @@ __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch a) {
     hrow[tid] = h;
     rng[tid] = rr;
     ent[tid] = en;
+  }
+  // the group's basis window qt[0..D)[row0 .. row0+oc) is loaded into registers now
+  // (after the list entries: vmcnt retires in order) and parked in LDS after the box
+  // sums, so its latency overlaps the exist / G loads
+  constexpr int kQW = 160 * kOC / kBlock;  // window floats per lane at the largest D
+  float qwv[kQW];
+#pragma unroll
+  for (int j = 0; j < kQW; ++j) {
+    const int e = j * kBlock + tid, d = e / oc, o = e - d * oc;
+    qwv[j] = e < D * oc ? a.qt[(int64_t)d * Qs + row0 + o] : 0.0f;
   }
   lds_barrier();
   C3H_SPROF(1);
@@ -426,6 +503,9 @@ __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch a) {
       }
     }
   }
+#pragma unroll
+  for (int j = 0; j < kQW; ++j)
+    if (j * kBlock + tid < D * oc) qw[j * kBlock + tid] = qwv[j];
   lds_barrier();
   C3H_SPROF(2);
   if (tid < kFP) {
@@ -441,31 +521,22 @@ __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch a) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[i][q] = 0.0f;
-  for (int c = 0; c < D16; ++c) {
-    const int d0 = 16 * c, dn = min(16, D - d0);
-    lds_barrier();  // fT complete / the previous chunk's readers done
-#pragma unroll
-    for (int j = 0; j < 4; ++j)  // [dd][oc] row-major
-      if (tid + j * kBlock < 16 * oc) qc[tid + j * kBlock] = pre[j];
-    if (c + 1 < D16) load_chunk(c + 1);
-    lds_barrier();
-    if (active) {
+  if (active) {
 #pragma unroll 4
-      for (int dd = 0; dd < dn; ++dd) {
-        const float2 f = *reinterpret_cast<const float2*>(&fT[(d0 + dd) * kFP + 2 * tp]);
-        const float4 q = *reinterpret_cast<const float4*>(&qc[dd * oc + 4 * to]);
-        acc[0][0] = __builtin_fmaf(f.x, q.x, acc[0][0]);
-        acc[0][1] = __builtin_fmaf(f.x, q.y, acc[0][1]);
-        acc[0][2] = __builtin_fmaf(f.x, q.z, acc[0][2]);
-        acc[0][3] = __builtin_fmaf(f.x, q.w, acc[0][3]);
-        acc[1][0] = __builtin_fmaf(f.y, q.x, acc[1][0]);
-        acc[1][1] = __builtin_fmaf(f.y, q.y, acc[1][1]);
-        acc[1][2] = __builtin_fmaf(f.y, q.z, acc[1][2]);
-        acc[1][3] = __builtin_fmaf(f.y, q.w, acc[1][3]);
-      }
+    for (int d = 0; d < D; ++d) {
+      const float2 f = *reinterpret_cast<const float2*>(&fT[d * kFP + 2 * tp]);
+      const float4 q = *reinterpret_cast<const float4*>(&qw[d * oc + 4 * to]);
+      acc[0][0] = __builtin_fmaf(f.x, q.x, acc[0][0]);
+      acc[0][1] = __builtin_fmaf(f.x, q.y, acc[0][1]);
+      acc[0][2] = __builtin_fmaf(f.x, q.z, acc[0][2]);
+      acc[0][3] = __builtin_fmaf(f.x, q.w, acc[0][3]);
+      acc[1][0] = __builtin_fmaf(f.y, q.x, acc[1][0]);
+      acc[1][1] = __builtin_fmaf(f.y, q.y, acc[1][1]);
+      acc[1][2] = __builtin_fmaf(f.y, q.z, acc[1][2]);
+      acc[1][3] = __builtin_fmaf(f.y, q.w, acc[1][3]);
     }
   }
-  lds_barrier();  // qv aliases fT / qc
+  lds_barrier();  // qv aliases fT / qw
   C3H_SPROF(3);
   if (active) {
 #pragma unroll
@@ -505,7 +576,28 @@ __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch a) {
           bo = o;
         }
       }
-      a.partials[(int64_t)blockIdx.x * a.M + m0 + mm] = ScorePartial{best, bo};
+      ScorePartial* q = a.partials + (int64_t)blockIdx.x * a.M + m0 + mm;
+      if (a.lists) {  // handed to another workgroup inside this launch: sc1 stores
+        __hip_atomic_store(&q->score, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&q->order, bo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        *q = ScorePartial{best, bo};
+      }
+    }
+    if (a.lists) {
+      // rank 1, fused replay: the last workgroup to finish reduces.  Hand-off per
+      // MI355X_MICROARCH.md (inter-workgroup visibility, table row 1): sc1 stores, every
+      // storing wave waits vmcnt(0), a barrier, one agent atomic add per workgroup; the
+      // workgroup whose add returns total-1 reads the partials with sc1 loads.
+      __shared__ int s_last;
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();
+      if (tid == 0) {
+        const uint32_t total = (uint32_t)((n + kFP - 1) / kFP) * gridDim.y;
+        s_last = atomicAdd(&a.done[a.epoch & 1], 1u) == total - 1;
+      }
+      lds_barrier();
+      if (s_last) argmax_finalize(a, (n + kFP - 1) / kFP);
     }
   }
   C3H_SPROF(7);
@@ -614,75 +706,19 @@ __global__ __launch_bounds__(64) void replay_kernel(const double* __restrict__ s
   }
 }
 
-// rank 1: the update reduces to "first strictly greater maximum in scan order"
-// (checkOverlap returns slot 0 when rank_num == 1), so the per-block partials of the
-// score kernel are reduced with (score desc, scan order asc) and applied to slot 0.
-__global__ __launch_bounds__(kBlock) void argmax_replay_kernel(
-    const ScorePartial* __restrict__ partials, int64_t nparts, const uint32_t* __restrict__ nlist,
-    ReplayModes modes, int M, int clean, c3h_det* __restrict__ lists,
-    c3h_det* __restrict__ out2) {
-  if (nlist) nparts = ((int64_t)*nlist + kFP - 1) / kFP;  // sparse search: blocks that ran
-  __shared__ double s_sc[kBlock / 64];
-  __shared__ long long s_or[kBlock / 64];
-  const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  double best = -2.0;
-  long long bo = -1;
-  for (int64_t i = tid; i < nparts; i += kBlock) {
-    const ScorePartial q = partials[i * M + m];
-    if (q.order >= 0 && (q.score > best || (q.score == best && q.order < bo))) {
-      best = q.score;
-      bo = q.order;
-    }
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const double os = __shfl_xor(best, o, 64);
-    const long long oo = __shfl_xor(bo, o, 64);
-    if (oo >= 0 && (os > best || (os == best && (bo < 0 || oo < bo)))) {
-      best = os;
-      bo = oo;
-    }
-  }
-  if (lane == 0) {
-    s_sc[w] = best;
-    s_or[w] = bo;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    for (int i = 1; i < kBlock / 64; ++i)
-      if (s_or[i] >= 0 && (s_sc[i] > best || (s_sc[i] == best && (bo < 0 || s_or[i] < bo)))) {
-        best = s_sc[i];
-        bo = s_or[i];
-      }
-    c3h_det e = lists[m];
-    if (clean) {
-      e.score = 0.0;
-      e.x = e.y = e.z = 0;
-    }
-    if (bo >= 0 && best > e.score) {
-      const int mi = (int)(bo >> 40);
-      const int64_t p = bo & ((1ll << 40) - 1);
-      const ReplayMode md = modes.m[mi];
-      e.score = best;
-      e.x = (int)(p % md.xe);
-      e.y = (int)((p / md.xe) % md.ye);
-      e.z = (int)(p / ((int64_t)md.xe * md.ye));
-      e.mode = md.mode;
-    }
-    lists[m] = e;
-    if (out2) out2[m] = e;
-  }
-}
-
 }  // namespace
+
+bool compress_rows_ok(int F, int Dpad) {
+  return Dpad <= 128 && ((size_t)kRK * Dpad + (size_t)kRR * F) * 4 <= 65536;
+}
 
 hipError_t launch_compress(const float* feat, int64_t H, int F, const float* axis_pt, int D,
                            int Dpad, const float* fmax, int fmax_len, float* G,
                            const int32_t* rows, const uint32_t* nrows, hipStream_t s) {
-  if (rows && Dpad <= 128 && ((size_t)kRK * Dpad + (size_t)kRR * F) * 4 <= 65536) {  // sparse list
+  if (rows && compress_rows_ok(F, Dpad)) {  // sparse list
     const size_t lds = sizeof(float) * ((size_t)kRK * Dpad + (size_t)kRR * F);
-    compress_rows_kernel<<<(unsigned)((H + kRR - 1) / kRR), kBlock, lds, s>>>(
-        feat, F, axis_pt, D, Dpad, fmax, fmax_len, G, rows, nrows);
+    const CompressRows cr{feat, axis_pt, fmax, G, rows, nrows, F, D, Dpad, fmax_len};
+    compress_rows_kernel<<<(unsigned)((H + kRR - 1) / kRR), kBlock, lds, s>>>(cr);
     return hipGetLastError();
   }
   dim3 grid((unsigned)((H + kCM - 1) / kCM), (unsigned)((Dpad + kCN - 1) / kCN));
@@ -694,7 +730,7 @@ size_t score_lds_bytes(int D, int r, int SP) {
   return sizeof(float) * ((size_t)SP * (D + 1) + (size_t)r * SP + SP) + sizeof(int) * SP;
 }
 
-bool score_fast_ok(int D, int r) { return D <= 256 && (D & 3) == 0 && r <= kOC; }
+bool score_fast_ok(int D, int r) { return D <= 160 && (D & 3) == 0 && r <= kOC; }
 
 int64_t score_blocks(const ScoreLaunch& a) {
   const int64_t P = (int64_t)a.xe * a.ye * a.ze;
@@ -717,11 +753,18 @@ hipError_t launch_score(const ScoreLaunch& a, hipStream_t s) {
 
 int64_t sparse_score_blocks(const SparseSearch& a) { return (a.pstart[a.nmodes] + kFP - 1) / kFP; }
 
-hipError_t launch_sparse_search(const SparseSearch& a, hipStream_t s) {
+hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc, hipStream_t s) {
   const int64_t ptot = a.pstart[a.nmodes];
   if (ptot <= 0) return hipSuccess;
-  gate_kernel<<<(unsigned)((ptot + kBlock - 1) / kBlock), kBlock, 0, s>>>(a);
-  const size_t region = std::max((size_t)a.D * kFP + 16 * (size_t)kOC, (size_t)kFP * (kOC + 1));
+  const unsigned ngate = (unsigned)((ptot + kBlock - 1) / kBlock);
+  if (sc) {  // compress (non-empty rows) and gate in one launch
+    const CompressRows cr{sc->feat, sc->PT, sc->fmax, sc->G, sc->rows, sc->nrows, sc->F, sc->D, sc->Dpad, sc->fmax_len};
+    const size_t lds = sizeof(float) * ((size_t)kRK * sc->Dpad + (size_t)kRR * sc->F);
+    compress_gate_kernel<<<ngate + (unsigned)((sc->H + kRR - 1) / kRR), kBlock, lds, s>>>(cr, a, (int)ngate);
+  } else {
+    gate_kernel<<<ngate, kBlock, 0, s>>>(a);
+  }
+  const size_t region = std::max((size_t)a.D * (kFP + kOC), (size_t)kFP * (kOC + 1));
   const size_t lds = sizeof(float) * (region + kFP) + sizeof(int) * 4 * kFP + sizeof(long long) * kFP +
                      sizeof(double) * kFP * a.mpg + 16;
   const unsigned groups = (unsigned)((a.M + a.mpg - 1) / a.mpg);
@@ -737,11 +780,5 @@ hipError_t launch_replay(const double* scores, const ReplayModes& modes, int M, 
   return hipGetLastError();
 }
 
-hipError_t launch_argmax_replay(const ScorePartial* partials, int64_t nparts,
-                                const uint32_t* nlist, const ReplayModes& modes, int M, int clean,
-                                c3h_det* lists, c3h_det* out2, hipStream_t s) {
-  argmax_replay_kernel<<<M, kBlock, 0, s>>>(partials, nparts, nlist, modes, M, clean, lists, out2);
-  return hipGetLastError();
-}
 
 }  // namespace c3h

@@ -1,13 +1,15 @@
 #!/bin/bash
 # PMC passes (each its own rocprofv3 run; --pmc never combined with trace domains)
 set -o pipefail
-mkdir -p gpurun_out/pmc
+TAG=${1:-r1}
+mkdir -p gpurun_out/pmc_$TAG
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-rocprofv3 -L > $R/gpurun_out/pmc/counters_list.txt 2>&1 || true
 run() {  # name, counters...
   local name=$1; shift
-  timeout -k 10 240 rocprofv3 --pmc "$@" -d $R/gpurun_out/pmc/$name -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 2 --frames 2 --no-cpu-baseline > $R/gpurun_out/pmc/$name.log 2>&1
-  echo "$name rc=$?" >> $R/gpurun_out/pmc/summary.txt
+  timeout -k 10 240 rocprofv3 --pmc "$@" -d $R/gpurun_out/pmc_$TAG/$name -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu-baseline > $R/gpurun_out/pmc_$TAG/$name.log 2>&1
 }
-run fetch FETCH_SIZE && run write WRITE_SIZE && run sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY && run inst SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT && run grbm GRBM_GUI_ACTIVE GRBM_COUNT
+run fetch FETCH_SIZE && run write WRITE_SIZE && run sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY && run inst SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT
+rc=$?
+cd $R && python3 tools_pmc_summary.py gpurun_out/pmc_$TAG gpurun_out/pmc_$TAG/summary.json > /dev/null
+exit $rc

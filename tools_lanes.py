@@ -25,7 +25,15 @@ with c3hlac.Context(0) as ctx:
     N = 200
     gptr = np.array([grids[i % 6].data_ptr() for i in range(N)], np.uint64)
     dets = torch.zeros((N, 30), dtype=torch.int64, device=dev)
-    for lanes in (1, 2, 3, 4, 6, 8):
+    import os
+    cases = [(l, None, None) for l in (1, 2, 3, 4, 6)] + [(3, g, None) for g in ("256", "1280")] + \
+        [(3, None, o) for o in ("512", "2048", "4096")]
+    for lanes, tg, og in cases:
+        for k, v in (("C3H_TILE_GRID", tg), ("C3H_OCC_GRID", og)):
+            if v:
+                os.environ[k] = v
+            else:
+                os.environ.pop(k, None)
         ctx.set_lanes(lanes)
         for rep in range(2):
             torch.cuda.synchronize()
@@ -35,5 +43,5 @@ with c3hlac.Context(0) as ctx:
             t1 = time.perf_counter()
             torch.cuda.synchronize()
             t2 = time.perf_counter()
-        print("lanes=%d host_enqueue_us_per_frame=%.1f total_us_per_frame=%.1f" %
-              (lanes, (t1 - t0) / N * 1e6, (t2 - t0) / N * 1e6), flush=True)
+        print("lanes=%d tile_grid=%s occ_grid=%s host_enqueue_us_per_frame=%.1f total_us_per_frame=%.1f" %
+              (lanes, tg, og, (t1 - t0) / N * 1e6, (t2 - t0) / N * 1e6), flush=True)

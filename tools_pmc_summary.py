@@ -1,0 +1,47 @@
+"""Per-launch HBM traffic of the C3 stage from rocprofv3 --pmc passes (scripts_pmc.sh).
+
+FETCH_SIZE / WRITE_SIZE are in KB per dispatch.  gfx950 correction
+(MI355X_MICROARCH.md, HBM/rocprofv3): FETCH_SIZE reports exactly half of the bytes of a
+wide coalesced streaming read -> x2; WRITE_SIZE is exact for 16-B stores.
+Usage: python tools_pmc_summary.py <pmc_dir> <out.json>"""
+import collections
+import csv
+import json
+import sys
+from pathlib import Path
+
+KERNELS = ("c3_occupancy_kernel", "c3hlac_tile_kernel", "compress_gate_kernel", "gate_kernel",
+           "score_list_kernel")
+
+
+def per_kernel(path, counter):
+    acc = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        for k in KERNELS:
+            if k + "(" in r["Kernel_Name"] or k + "<" in r["Kernel_Name"]:
+                acc[k].append(float(r["Counter_Value"]))
+    return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
+
+
+def main():
+    d = Path(sys.argv[1])
+    fetch = per_kernel(next((d / "fetch").glob("*counter_collection.csv")), "FETCH_SIZE")
+    write = per_kernel(next((d / "write").glob("*counter_collection.csv")), "WRITE_SIZE")
+    out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; FETCH x2 (gfx950)",
+           "kernels": {}}
+    for k in KERNELS:
+        if k in fetch or k in write:
+            f = fetch.get(k, (0.0, 0))[0] * 1024 * 2
+            w = write.get(k, (0.0, 0))[0] * 1024
+            out["kernels"][k] = {"fetch_bytes": f, "write_bytes": w, "hbm_bytes": f + w,
+                                 "dispatches": max(fetch.get(k, (0, 0))[1], write.get(k, (0, 0))[1])}
+    c3 = [out["kernels"][k]["hbm_bytes"] for k in ("c3_occupancy_kernel", "c3hlac_tile_kernel") if k in out["kernels"]]
+    out["c3_stage_hbm_bytes_per_frame"] = sum(c3) if len(c3) == 2 else None
+    json.dump(out, open(sys.argv[2], "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
