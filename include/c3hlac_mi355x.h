@@ -137,9 +137,12 @@ int c3h_search(c3h_ctx* ctx, const int32_t range[3], int32_t exist_threshold,
  * lists into the device buffer d_out after the search (no removeOverlap). */
 int c3h_search_async(c3h_ctx* ctx, const int32_t range[3], int32_t exist_threshold,
                      int32_t rotate, c3h_det* d_out);
-/* Batch driver for device-resident frames (configs 3-5): for each frame i, bind
- * d_grids[i] (same dims/min_b/leaf), cleanMax, extract with *p, and search (async) into
- * d_out + i * M * rank.  One host call, no host synchronisation. */
+/* Batch driver for device-resident frames (configs 3-5): every frame i is bound from
+ * d_grids[i] (same dims/min_b/leaf), extracted with *p and searched (async) into
+ * d_out + i * M * rank, each frame starting from fresh lists (setRank state: scores 0,
+ * S_MODE_1).  Frames go c3h_set_batch at a time through one set of launches and are
+ * spread over c3h_set_lanes lanes; afterwards the context holds the last frame's state.
+ * One host call, no host synchronisation. */
 int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes,
                    const int32_t div_b[3], const int32_t min_b[3], float leaf,
                    const c3h_extract_params* p, const int32_t range[3], int32_t exist_threshold,
@@ -148,6 +151,8 @@ int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes
  * their own streams, so the latency-bound search of one frame overlaps the HBM stream of
  * the next.  Lane 0 (this context) takes the last frame.  1 = strictly sequential. */
 int c3h_set_lanes(c3h_ctx* ctx, int32_t lanes);
+/* Frames per launch in c3h_run_frames (1..8, default 4; the fast search path only). */
+int c3h_set_batch(c3h_ctx* ctx, int32_t frames);
 /* compressed features (setData before the summed-volume table): hist_num x D floats */
 int c3h_get_compressed(c3h_ctx* ctx, float* out, int on_device);
 /* per-position similarity of the last search, modes x M x P doubles (-1 = gated out).
@@ -164,7 +169,8 @@ int c3h_pca_read(const char* path, int32_t ascii, float* axis, float* var, float
 
 /* per-kernel device time (ms) accumulated since the last reset with HIP events on the
  * context stream; slots: 0 voxelize, 1 C3-HLAC, 2 compress, 3 score, 4 rank replay.
- * counts_out receives the number of launches per slot.  Enabling adds event records.
+ * counts_out receives the number of frames the timed launches processed per slot (a
+ * batched launch of B frames counts B).  Enabling adds event records.
  * enable: 0 = off, 1 = every slot, otherwise a mask of C3H_TIMING_* bits (the slots
  * bracketed by events; fewer events = less perturbation of back-to-back launches). */
 #define C3H_NTIMERS 5

@@ -192,6 +192,10 @@ class Context:
         """Frames in flight in run_frames (child contexts on their own streams)."""
         self._chk(self.lib.c3h_set_lanes(self.h, int(n)), "set_lanes")
 
+    def set_batch(self, n):
+        """Frames per launch in run_frames (1..8)."""
+        self._chk(self.lib.c3h_set_batch(self.h, int(n)), "set_batch")
+
     def compressed(self):
         out = np.zeros((self.hist_num, self.D), np.float32)
         self._chk(self.lib.c3h_get_compressed(self.h, ptr(out), 0), "get_compressed")

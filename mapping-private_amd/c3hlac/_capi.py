@@ -68,6 +68,7 @@ _SIGS = {
     "c3h_run_frames": (C.c_int, [_P, _P, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_float,
                                  C.POINTER(ExtractParams), C.POINTER(C.c_int32), C.c_int32, C.c_int32, _P]),
     "c3h_set_lanes": (C.c_int, [_P, C.c_int32]),
+    "c3h_set_batch": (C.c_int, [_P, C.c_int32]),
     "c3h_get_compressed": (C.c_int, [_P, _P, C.c_int]),
     "c3h_get_scores": (C.c_int, [_P, _P, C.POINTER(C.c_int64), C.c_int]),
     "c3h_remove_overlap": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(C.c_int32), _P]),

@@ -19,7 +19,7 @@ constexpr int kBlock = 256;
 // largest centre-voxel extent of one C3 tile per axis; subdivisions wider than this
 // are split into several tiles whose exact integer partial sums are added in 64 bit.
 constexpr int kTileMax = 16;
-constexpr int kChunk = 64;  // list entries per packed-operand chunk (16 groups of 4)
+constexpr int kChunk = 128;  // list entries per packed-operand chunk (32 groups of 4)
 
 // reference constants (c3_hlac/src/c3_hlac.cpp:38-45), as float
 constexpr float kNorm0 = 1 / 255.0;
@@ -45,9 +45,14 @@ struct ScorePartial {
   int64_t order;  // (mode index << 40) | position, -1 = none
 };
 
+struct TimedPair {
+  hipEvent_t a, b;
+  int weight;  // frames the bracketed launches processed
+};
+
 struct Timer {
   std::mutex mu;  // lanes enqueue from their own host threads
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[C3H_NTIMERS];
+  std::vector<TimedPair> pending[C3H_NTIMERS];
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
   float ms[C3H_NTIMERS] = {0, 0, 0, 0, 0};
   int count[C3H_NTIMERS] = {0, 0, 0, 0, 0};
@@ -69,6 +74,7 @@ struct c3h_ctx {
   std::vector<hipEvent_t> lane_ev;
   hipEvent_t fork_ev = nullptr;
   int nlanes = 3;
+  int nbatch = 4;                   // frames per launch in c3h_run_frames
   // host copy of the search setup, replayed into the lanes
   uint64_t setup_version = 0;
   std::vector<float> h_axis_p, h_var, h_axis_q, h_fmax;
@@ -103,12 +109,16 @@ struct c3h_ctx {
   c3h::DevBuf<uint32_t> tileflags;  // [2] row counters | [2] work counters | [ntiles] stamps
   c3h::DevBuf<int32_t> work;        // non-empty tiles of the last extract
   uint32_t tile_epoch = 0;
+  int64_t tf_stride = -1;           // tile-stamp layout the counters were zeroed for
+  int tf_frames = 0;
+  int nframes_feat = 1;             // frames of the last extract (frame 0 = the API view)
   c3h::DevBuf<int32_t> rows;        // non-empty subdivisions of the last extract (direct mode)
   bool rows_valid = false;          // rows/epoch describe the current features
   bool g_sparse = false;            // G holds only the listed rows (others stale)
   c3h::DevBuf<long long> glist;     // sparse search: gate list
   c3h::DevBuf<uint32_t> gcnt;       // [2] gate-list counters by search epoch parity
   uint32_t search_epoch = 0;
+  int gcnt_frames = 0;
   c3h::DevBuf<long long> prof;      // diagnostics (C3H_PROF)
 
   std::vector<int32_t> h_segs;      // host copy (kept alive for the async upload)
@@ -169,8 +179,14 @@ hipError_t launch_downsampled(const int32_t* leaf, const uint32_t* grid, int64_t
                               const float* sx, const float* sy, const float* sz,
                               uint64_t table_size, float* out, hipStream_t s);
 
+constexpr int kMaxBatch = 8;  // frames per launch (blockIdx.y) in c3h_run_frames
+
 struct C3Launch {
-  const uint32_t* grid;
+  const uint32_t* grid[kMaxBatch];  // one grid per frame of the batch
+  int nframes;
+  // per-frame buffers: frame f at base + f * stride
+  int64_t s_feat, s_h, s_acc, s_tf, s_work;
+  uint32_t* tf;           // [2] row counters | [2] work counters | [ntiles] epoch stamps
   int gx, gy, gz;
   const int32_t* segs;  // [3][nseg_max][3] = start, len, subdiv
   int nseg[3];
@@ -185,11 +201,8 @@ struct C3Launch {
   int32_t* exist;
   unsigned long long* acc64;
   const int16_t* axmap;   // per-axis centre coordinate -> segment index (-1 = none)
-  uint32_t* flags;        // ntiles epoch stamps
   int32_t* work;          // ntiles: non-empty tiles (pass 1 output)
-  uint32_t* workcnt;      // [2] work-list counters by epoch parity
   int32_t* rows;          // direct mode: non-empty subdivision list output (nullable)
-  uint32_t* rowcnt;       // [2] row-list counters by epoch parity
   uint32_t epoch;
   int zero_empty;
   int64_t ntiles;
@@ -200,7 +213,7 @@ struct C3Launch {
 int64_t c3hlac_grid(const C3Launch& a);  // persistent grid of the tile kernel
 hipError_t launch_c3hlac(const C3Launch& a, hipStream_t s);
 hipError_t launch_c3_finalize(const unsigned long long* acc64, int64_t hist_num, int variant,
-                              float* feat, int32_t* exist, hipStream_t s);
+                              float* feat, int32_t* exist, int nframes, hipStream_t s);
 
 // rows/nrows (device): compress only the listed rows (sparse mode), else all H rows
 hipError_t launch_compress(const float* feat, int64_t H, int F, const float* axis_pt, int D,
@@ -248,10 +261,12 @@ struct SparseSearch {
   long long* list;        // gate list entries (mode << 40 | position)
   uint32_t* cnt;          // [2] list counters by epoch parity
   uint32_t epoch;
+  int nframes;             // frames of the batch (launch z / y index)
+  int64_t s_G, s_exist, s_scores, s_list, s_cnt, s_partials, s_lists;  // per-frame strides
+  c3h_det* outs[kMaxBatch];  // per-frame copy of the lists after the update (nullable)
   ScorePartial* partials;  // per block per model (nullable)
   uint32_t* done;          // [2] finished-workgroup counters by epoch parity
   c3h_det* lists;          // rank 1 fused replay: M lists (nullable = no fused replay)
-  c3h_det* out2;           // copy of the lists after the update (nullable)
   int clean;               // apply a pending cleanMax first
   long long* prof;         // diagnostics (C3H_PROF): [blocks][8]
 };
@@ -265,6 +280,7 @@ struct SparseCompress {
   const uint32_t* nrows;
   int F, D, Dpad, fmax_len;
   int64_t H;
+  int64_t s_feat, s_G, s_rows, s_nrows;  // per-frame strides
 };
 bool compress_rows_ok(int F, int Dpad);
 hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc, hipStream_t s);

@@ -27,7 +27,7 @@
 // piece of one: partial sums then go through 64-bit atomics + a finalize kernel).
 //   1. stage the (lx+2) x (ly+2) x (lz+1) halo of packed grid words in LDS
 //   2. compact the occupied centre voxels into an LDS list (wave ballot)
-//   3. per chunk of 64 list entries: 240 threads build the packed operand dwords
+//   3. per chunk of 128 list entries: (group, k) jobs build the packed operand dwords
 //      (16 groups x 15 k x {colour, binary} x 6 channels) in LDS
 //   4. 180 threads accumulate 6 dot4 products per group into u32 registers
 //   5. scatter the 981 integer bins to LDS, fold/normalise, coalesced store
@@ -148,11 +148,28 @@ __device__ __forceinline__ void set_insert(int* s_set, int t, uint32_t epoch, ui
   stamp_tile(t, epoch, flags, cnt, work);  // set full
 }
 
+struct OccArgs {
+  const uint32_t* grid[kMaxBatch];  // frame f = blockIdx.y
+  int gx, gy, gz;
+  const int16_t* axmap;
+  int ns0, ns1;
+  uint32_t epoch;
+  uint32_t* tf;    // per frame: [2] row counters | [2] work counters | [ntiles] stamps
+  int32_t* work;   // per frame: [ntiles]
+  int64_t s_tf, s_work;
+};
+
 template <bool kVec>
-__global__ __launch_bounds__(kBlock) void c3_occupancy_kernel(
-    const uint32_t* __restrict__ grid, int gx, int gy, int gz, const int16_t* __restrict__ axmap,
-    int ns0, int ns1, uint32_t epoch, uint32_t* __restrict__ flags, uint32_t* __restrict__ cnt,
-    int32_t* __restrict__ work) {
+__global__ __launch_bounds__(kBlock) void c3_occupancy_kernel(OccArgs oa) {
+  const int f = blockIdx.y;
+  const uint32_t* __restrict__ grid = oa.grid[f];
+  const int gx = oa.gx, gy = oa.gy, gz = oa.gz;
+  const int16_t* __restrict__ axmap = oa.axmap;
+  const int ns0 = oa.ns0, ns1 = oa.ns1;
+  const uint32_t epoch = oa.epoch;
+  uint32_t* __restrict__ flags = oa.tf + f * oa.s_tf + 4;
+  uint32_t* __restrict__ cnt = oa.tf + f * oa.s_tf + 2;
+  int32_t* __restrict__ work = oa.work + f * oa.s_work;
   __shared__ int s_set[kOccSet];
   const int tid = threadIdx.x, lane = tid & 63;
   const int64_t nvox = (int64_t)gx * gy * gz;
@@ -233,6 +250,9 @@ __global__ __launch_bounds__(kBlock) void c3_occupancy_kernel(
 
 // ---------------------------------------------------------------- pass 2: features
 struct KArgs {
+  const uint32_t* grids[kMaxBatch];  // frame f = blockIdx.y; per-frame buffers at f * stride
+  int64_t s_feat, s_h, s_acc, s_tf, s_work;
+  uint32_t* tf;  // frame 0's [2] row counters | [2] work counters | [ntiles] stamps
   const uint32_t* grid;
   int gx, gy, gz;
   const int32_t* segs;
@@ -269,7 +289,22 @@ constexpr int kSegLds = 64;   // segment tables up to 64 segments per axis live 
 #define C3H_PROF(k, cond) \
   if (a.prof && tid == 0 && (cond)) a.prof[blockIdx.x * 8 + (k)] = (long long)wall_clock64()
 
-__global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
+__global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs ka) {
+  KArgs a = ka;  // this frame's view
+  {
+    const int64_t f = blockIdx.y;
+    a.grid = ka.grids[f];
+    a.feat = ka.feat + f * ka.s_feat;
+    a.exist = ka.exist + f * ka.s_h;
+    if (ka.acc64) a.acc64 = ka.acc64 + f * ka.s_acc;
+    uint32_t* tf = ka.tf + f * ka.s_tf;
+    a.rowcnt = tf;
+    a.workcnt = tf + 2;
+    a.flags = tf + 4;
+    a.work = ka.work + f * ka.s_work;
+    if (ka.rows) a.rows = ka.rows + f * ka.s_h;
+    if (f) a.prof = nullptr;
+  }
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint32_t* s_lut = smem;                       // 256
   uint32_t* s_tile = s_lut + 256;               // tw_max (16-B aligned)
@@ -314,7 +349,6 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
   const int32_t* segs = segs_lds ? s_segs : a.segs;
   if (segs_lds)
     for (int e = tid; e < 9 * a.seg_stride; e += kBlock) s_segs[e] = a.segs[e];
-  const int bg = tid / 15, bk = tid - bg * 15;  // build job (group, k), tid < 240
   const int at = tid / 90, arem = tid - at * 90, ak = arem / 6, an = arem - ak * 6;
   lds_barrier();
   C3H_PROF(1, true);
@@ -382,7 +416,7 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
       }
     }
     lds_barrier();
-    C3H_PROF(3, wi == (int)blockIdx.x);
+    C3H_PROF(3, wi == (int)blockIdx.x - a.zblocks);
     if (a.debug == 1) {
       if (tid == 0 && s_tile[0] == 0xdeadbeefu) a.exist[0] = 1;  // keep the loads live
       lds_barrier();
@@ -419,7 +453,7 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
       }
     }
     lds_barrier();
-    C3H_PROF(4, wi == (int)blockIdx.x);
+    C3H_PROF(4, wi == (int)blockIdx.x - a.zblocks);
     const int nlist = (int)s_misc[0];
     if (a.debug == 2) {
       if (tid == 0 && nlist == 0x7fffffff) a.exist[0] = 1;
@@ -427,45 +461,49 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
       continue;
     }
 
-    int delta = 0;
-    if (tid < 240 && bk < 13) delta = kRel[bk][0] + kRel[bk][1] * TX + kRel[bk][2] * TXY;
     uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
     for (int c0 = 0; c0 < nlist; c0 += kChunk) {
-      // 3. build packed operands for list entries [c0, c0+64)
-      if (tid < 240) {
+      // 3. build packed operands for list entries [c0, c0+kChunk): job = (group, k);
+      //    branch-free so each job's LDS reads (list, tile, LUT) issue back to back
+      for (int job = tid; job < kGroups * 15; job += kBlock) {
+        const int jg = job / 15, jk = job - jg * 15;
+        const int delta = jk < 13 ? kRel[jk][0] + kRel[jk][1] * TX + kRel[jk][2] * TXY : 0;
+        uint32_t w[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int e = c0 + jg * 4 + j;
+          w[j] = e < nlist ? s_tile[s_list[e] + delta] : 0u;
+        }
         uint32_t nb[6] = {0, 0, 0, 0, 0, 0}, bb[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int e = c0 + bg * 4 + j;
-          if (e >= nlist) break;
-          const uint32_t w = s_tile[s_list[e] + delta];
-          if (!w) continue;
           const int sh = 8 * j;
-          if (bk == 14) {
+          const uint32_t occ = w[j] ? 1u : 0u;
+          if (jk == 14) {  // the ones column: occupancy in every channel
 #pragma unroll
             for (int n = 0; n < 6; ++n) {
-              nb[n] |= 1u << sh;
-              bb[n] |= 1u << sh;
+              nb[n] |= occ << sh;
+              bb[n] |= occ << sh;
             }
-            continue;
+          } else {
+            const uint32_t r = (w[j] >> 16) & 0xffu, g = (w[j] >> 8) & 0xffu, b = w[j] & 0xffu;
+            const uint32_t lr = occ ? s_lut[r] : 0u, lg = occ ? s_lut[g] : 0u, lb = occ ? s_lut[b] : 0u;
+            nb[0] |= (lr & 0xffu) << sh;
+            nb[1] |= (lr >> 8) << sh;
+            nb[2] |= (lg & 0xffu) << sh;
+            nb[3] |= (lg >> 8) << sh;
+            nb[4] |= (lb & 0xffu) << sh;
+            nb[5] |= (lb >> 8) << sh;
+            const uint32_t br = (int)r > a.thr_r, bgn = (int)g > a.thr_g, bbl = (int)b > a.thr_b;
+            bb[0] |= (occ & br) << sh;
+            bb[1] |= (occ & (br ^ 1u)) << sh;
+            bb[2] |= (occ & bgn) << sh;
+            bb[3] |= (occ & (bgn ^ 1u)) << sh;
+            bb[4] |= (occ & bbl) << sh;
+            bb[5] |= (occ & (bbl ^ 1u)) << sh;
           }
-          const uint32_t r = (w >> 16) & 0xffu, g = (w >> 8) & 0xffu, b = w & 0xffu;
-          const uint32_t lr = s_lut[r], lg = s_lut[g], lb = s_lut[b];
-          nb[0] |= (lr & 0xffu) << sh;
-          nb[1] |= (lr >> 8) << sh;
-          nb[2] |= (lg & 0xffu) << sh;
-          nb[3] |= (lg >> 8) << sh;
-          nb[4] |= (lb & 0xffu) << sh;
-          nb[5] |= (lb >> 8) << sh;
-          const uint32_t br = (int)r > a.thr_r, bgn = (int)g > a.thr_g, bbl = (int)b > a.thr_b;
-          bb[0] |= br << sh;
-          bb[1] |= (br ^ 1u) << sh;
-          bb[2] |= bgn << sh;
-          bb[3] |= (bgn ^ 1u) << sh;
-          bb[4] |= bbl << sh;
-          bb[5] |= (bbl ^ 1u) << sh;
         }
-        uint32_t* dst = s_arr + bg * kArrStride + bk * 6;
+        uint32_t* dst = s_arr + jg * kArrStride + jk * 6;
 #pragma unroll
         for (int n = 0; n < 6; ++n) {
           dst[n] = nb[n];
@@ -487,7 +525,7 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
       }
       lds_barrier();
     }
-    C3H_PROF(5, wi == (int)blockIdx.x);
+    C3H_PROF(5, wi == (int)blockIdx.x - a.zblocks);
     // 5. epilogue: integer bins -> LDS, then fold / normalise / store
     if (tid < 180) {
 #pragma unroll
@@ -513,7 +551,7 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
     }
     if (a.rows && tid == 0) a.rows[atomicAdd(&a.rowcnt[a.epoch & 1], 1u)] = (int32_t)h;
     lds_barrier();  // LDS is reused by the next tile
-    C3H_PROF(6, wi == (int)blockIdx.x);
+    C3H_PROF(6, wi == (int)blockIdx.x - a.zblocks);
   }
   C3H_PROF(7, true);
 }
@@ -521,8 +559,11 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
 // multi-tile subdivisions: 64-bit exact partial sums -> features
 __global__ __launch_bounds__(kBlock) void c3_finalize_kernel(const unsigned long long* acc64,
                                                              int variant, float* feat,
-                                                             int32_t* exist) {
+                                                             int32_t* exist, int64_t hist_num) {
   const int64_t h = blockIdx.x;
+  acc64 += blockIdx.y * hist_num * 981;
+  feat += blockIdx.y * hist_num * variant;
+  exist += blockIdx.y * hist_num;
   const unsigned long long* hist = acc64 + h * 981;
   float* out = feat + h * variant;
   if (variant == 981) {
@@ -579,14 +620,33 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
   if (const char* g = getenv("C3H_OCC_GRID")) occ_cap = std::max(1, atoi(g));  // diagnostics
   int g1 = (int)std::min<int64_t>((items + kBlock * kOccUnroll - 1) / (kBlock * kOccUnroll), occ_cap);
   if (g1 < 1) g1 = 1;
+  if (l.nframes < 1 || l.nframes > kMaxBatch) return hipErrorInvalidValue;
+  OccArgs oa;
+  for (int f = 0; f < kMaxBatch; ++f) oa.grid[f] = f < l.nframes ? l.grid[f] : nullptr;
+  oa.gx = l.gx;
+  oa.gy = l.gy;
+  oa.gz = l.gz;
+  oa.axmap = l.axmap;
+  oa.ns0 = l.nseg[0];
+  oa.ns1 = l.nseg[1];
+  oa.epoch = l.epoch;
+  oa.tf = l.tf;
+  oa.work = l.work;
+  oa.s_tf = l.s_tf;
+  oa.s_work = l.s_work;
+  const dim3 g1d((unsigned)g1, (unsigned)l.nframes);
   if (vec)
-    c3_occupancy_kernel<true><<<g1, kBlock, 0, s>>>(l.grid, l.gx, l.gy, l.gz, l.axmap, l.nseg[0],
-                                                    l.nseg[1], l.epoch, l.flags, l.workcnt, l.work);
+    c3_occupancy_kernel<true><<<g1d, kBlock, 0, s>>>(oa);
   else
-    c3_occupancy_kernel<false><<<g1, kBlock, 0, s>>>(l.grid, l.gx, l.gy, l.gz, l.axmap, l.nseg[0],
-                                                     l.nseg[1], l.epoch, l.flags, l.workcnt, l.work);
+    c3_occupancy_kernel<false><<<g1d, kBlock, 0, s>>>(oa);
   KArgs a;
-  a.grid = l.grid;
+  for (int f = 0; f < kMaxBatch; ++f) a.grids[f] = f < l.nframes ? l.grid[f] : nullptr;
+  a.s_feat = l.s_feat;
+  a.s_h = l.s_h;
+  a.s_acc = l.s_acc;
+  a.s_tf = l.s_tf;
+  a.s_work = l.s_work;
+  a.grid = l.grid[0];
   a.gx = l.gx;
   a.gy = l.gy;
   a.gz = l.gz;
@@ -609,11 +669,12 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
   a.feat = l.feat;
   a.exist = l.exist;
   a.acc64 = l.acc64;
-  a.flags = l.flags;
+  a.tf = l.tf;
+  a.flags = l.tf + 4;
   a.work = l.work;
-  a.workcnt = l.workcnt;
+  a.workcnt = l.tf + 2;
   a.rows = l.rows;
-  a.rowcnt = l.rowcnt;
+  a.rowcnt = l.tf;
   a.epoch = l.epoch;
   a.zblocks = l.zero_empty ? (int)std::min<int64_t>(64, l.ntiles) : 0;
   a.ntiles = (int)l.ntiles;
@@ -621,13 +682,14 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
   a.prof = l.prof;
   const size_t lds = c3hlac_lds_bytes(a.tw_max, a.list_max);
   const int grid = (int)c3hlac_grid(l);
-  c3hlac_tile_kernel<<<grid, kBlock, lds, s>>>(a);
+  c3hlac_tile_kernel<<<dim3((unsigned)grid, (unsigned)l.nframes), kBlock, lds, s>>>(a);
   return hipGetLastError();
 }
 
 hipError_t launch_c3_finalize(const unsigned long long* acc64, int64_t hist_num, int variant,
-                              float* feat, int32_t* exist, hipStream_t s) {
-  c3_finalize_kernel<<<(unsigned)hist_num, kBlock, 0, s>>>(acc64, variant, feat, exist);
+                              float* feat, int32_t* exist, int nframes, hipStream_t s) {
+  c3_finalize_kernel<<<dim3((unsigned)hist_num, (unsigned)nframes), kBlock, 0, s>>>(acc64, variant, feat, exist,
+                                                                                    hist_num);
   return hipGetLastError();
 }
 

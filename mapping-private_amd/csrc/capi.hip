@@ -69,9 +69,10 @@ void release(DevBuf<T>& b) {
 struct Timed {
   c3h_ctx* ctx;
   c3h::Timer* T;
-  int slot;
+  int slot, weight;
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
-  Timed(c3h_ctx* c, int s) : ctx(c), T(c->parent ? &c->parent->timer : &c->timer), slot(s) {
+  Timed(c3h_ctx* c, int s, int w = 1)
+      : ctx(c), T(c->parent ? &c->parent->timer : &c->timer), slot(s), weight(w) {
     if (!(T->mask >> (s + 1) & 1)) return;
     std::lock_guard<std::mutex> g(T->mu);
     if (T->pool.empty()) {
@@ -91,7 +92,7 @@ struct Timed {
     if (!ev.first) return;
     (void)hipEventRecord(ev.second, ctx->stream);
     std::lock_guard<std::mutex> g(T->mu);
-    T->pending[slot].push_back(ev);
+    T->pending[slot].push_back(c3h::TimedPair{ev.first, ev.second, weight});
   }
 };
 
@@ -337,18 +338,24 @@ int sync_host_lists(c3h_ctx* ctx) {
 }
 
 // setData + searchPart for every scheduled mode; leaves the lists valid on the device
-int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate,
-               c3h_det* d_out) {
+// setData + search for the nf frames of the last extract_frames (frame f's results at
+// f * stride; d_out + f * M * rank).  clean: 0 = continue from the lists, 1 = cleanMax
+// first, 2 = reset the lists as setRank does (batched frames start fresh).
+int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int32_t rotate,
+                  c3h_det* const* d_outs, int clean) {
   if (!ctx->have_feat) return fail(ctx, C3H_ERR_STATE, "c3h_search: no features (call c3h_extract)");
   if (!ctx->have_setup) return fail(ctx, C3H_ERR_STATE, "c3h_search: no axes (call c3h_search_setup)");
   if (!range || range[0] < 1 || range[1] < 1 || range[2] < 1)
     return fail(ctx, C3H_ERR_ARG, "c3h_search: ranges must be >= 1");
   if (ctx->feat_dim != ctx->F)
     return fail(ctx, C3H_ERR_ARG, "c3h_search: feature dimension differs from the scene axis");
+  if (nf != ctx->nframes_feat) return fail(ctx, C3H_ERR_STATE, "search: frame count differs from the extract");
   const int xn = ctx->subdiv_b[0], yn = ctx->subdiv_b[1], zn = ctx->subdiv_b[2];
   const int64_t H = (int64_t)xn * yn * zn;
   if (ctx->lists.M != std::max(ctx->M, 1) || ctx->lists.rank != ctx->rank) init_lists(ctx);
   if (H < 1 || H != ctx->hist_num) return 0;  // setData returns early; search is skipped
+  const bool fast = c3h::score_fast_ok(ctx->D, ctx->r);
+  if (nf > 1 && !fast) return fail(ctx, C3H_ERR_STATE, "search: batched frames need the fast path");
   int modes[6];
   const int nm = mode_schedule(range[0], range[1], range[2], rotate, modes);
   c3h::ReplayModes rm{};
@@ -362,25 +369,33 @@ int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate
     total += rm.m[rm.n].P * ctx->M;
     rm.n++;
   }
-  ENSURE(ctx->scores, std::max<int64_t>(total, 1));
+  ENSURE(ctx->scores, (size_t)nf * std::max<int64_t>(total, 1));
   ctx->scores_n = total;
-  ENSURE(ctx->G, (size_t)H * ctx->D);
-  const bool fast = c3h::score_fast_ok(ctx->D, ctx->r);
+  ENSURE(ctx->G, (size_t)nf * H * ctx->D);
   // sparse compress: only the non-empty rows of the extract's list (the rest stay stale
   // and every consumer gates them on exist)
   const bool sparse_g = !ctx->g_valid && fast && ctx->rows_valid && c3h::compress_rows_ok(ctx->F, ctx->Dpad);
-  if (!ctx->g_valid && !sparse_g) {
+  if (!ctx->g_valid && !sparse_g) {  // nf == 1 here
     Timed t(ctx, 2);
     HIPCHK(c3h::launch_compress(ctx->feat.p, H, ctx->F, ctx->axis_pt.p, ctx->D, ctx->Dpad,
                                 ctx->fmax.p, ctx->fmax_len, ctx->G.p, nullptr, nullptr, ctx->stream));
     ctx->g_valid = true;
     ctx->g_sparse = false;
   }
-  if (!ctx->lists_dev_valid) {
+  const size_t per_lists = (size_t)std::max(ctx->M, 1) * ctx->rank;
+  if (ctx->d_lists.n < nf * per_lists) {  // grows: frame 0's copy is re-uploaded
+    if (!ctx->lists_host_valid) {
+      int rc = sync_host_lists(ctx);
+      if (rc != C3H_OK) return rc;
+    }
+    ENSURE(ctx->d_lists, nf * per_lists);
+    ctx->lists_dev_valid = false;
+  }
+  if (clean != 2 && !ctx->lists_dev_valid) {
     int rc = upload_lists(ctx);
     if (rc != C3H_OK) return rc;
   }
-  const int clean = ctx->pending_clean ? 1 : 0;
+  if (clean == 1 || (clean == 0 && ctx->pending_clean)) clean = 1;
   const bool use_argmax = fast && ctx->rank == 1;
   std::vector<c3h::ScoreLaunch> launches;
   for (int i = 0; i < rm.n; ++i) {
@@ -433,39 +448,48 @@ int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate
       q.order_base[i] = (int64_t)i << 40;
     }
     const int64_t ptot = q.pstart[rm.n];
-    ENSURE(ctx->glist, (size_t)std::max<int64_t>(ptot, 1));
-    if (!ctx->gcnt.p) {  // [2] list counters | [2] finished-workgroup counters
-      ENSURE(ctx->gcnt, 4);
-      HIPCHK(hipMemsetAsync(ctx->gcnt.p, 0, 16, ctx->stream));
-      ctx->search_epoch = 0;
+    ENSURE(ctx->glist, (size_t)nf * std::max<int64_t>(ptot, 1));
+    if (!ctx->gcnt.p || ctx->gcnt_frames != nf || ctx->gcnt.n < (size_t)nf * 4 || ++ctx->search_epoch == 0) {
+      // per frame: [2] list counters | [2] finished-workgroup counters
+      ENSURE(ctx->gcnt, (size_t)nf * 4);
+      HIPCHK(hipMemsetAsync(ctx->gcnt.p, 0, ctx->gcnt.n * 4, ctx->stream));
+      ctx->search_epoch = 1;
+      ctx->gcnt_frames = nf;
     }
-    ++ctx->search_epoch;
     q.list = ctx->glist.p;
     q.cnt = ctx->gcnt.p;
     q.done = ctx->gcnt.p + 2;
     q.epoch = ctx->search_epoch;
+    q.nframes = nf;
+    q.s_G = H * ctx->D;
+    q.s_exist = H;
+    q.s_scores = std::max<int64_t>(total, 1);
+    q.s_list = std::max<int64_t>(ptot, 1);
+    q.s_cnt = 4;
+    q.s_lists = (int64_t)per_lists;
+    for (int f = 0; f < c3h::kMaxBatch; ++f) q.outs[f] = (d_outs && f < nf) ? d_outs[f] : nullptr;
     const int64_t nparts = c3h::sparse_score_blocks(q);
+    q.s_partials = std::max<int64_t>(nparts, 1) * ctx->M;
     if (use_argmax) {  // rank 1: the replay runs in the score launch's last workgroup
-      ENSURE(ctx->partials, (size_t)std::max<int64_t>(nparts, 1) * ctx->M);
+      ENSURE(ctx->partials, (size_t)nf * q.s_partials);
       q.partials = ctx->partials.p;
       q.lists = ctx->d_lists.p;
-      q.out2 = d_out;
       q.clean = clean;
     }
     c3h::SparseCompress sc{};
     if (sparse_g) {
       sc = c3h::SparseCompress{ctx->feat.p, ctx->axis_pt.p, ctx->fmax.p, ctx->G.p, ctx->rows.p,
                                ctx->tileflags.p + (ctx->tile_epoch & 1), ctx->F, ctx->D, ctx->Dpad,
-                               ctx->fmax_len, H};
+                               ctx->fmax_len, H, H * ctx->F, H * ctx->D, H, ctx->tf_stride};
       ctx->g_valid = true;
       ctx->g_sparse = true;
     }
-    {
+    if (nf == 1) {
       int rc = prof_prepare(ctx, nparts, &q.prof);
       if (rc != C3H_OK) return rc;
     }
     {
-      Timed t(ctx, 3);
+      Timed t(ctx, 3, nf);
       HIPCHK(c3h::launch_sparse_search(q, sparse_g ? &sc : nullptr, ctx->stream));
     }
     if (q.prof) {
@@ -473,9 +497,14 @@ int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate
       if (rc != C3H_OK) return rc;
     }
     if (!use_argmax) {
-      Timed t(ctx, 4);
-      HIPCHK(c3h::launch_replay(ctx->scores.p, rm, ctx->M, ctx->rank, range[0], range[1], range[2],
-                                clean, ctx->d_lists.p, d_out, ctx->stream));
+      Timed t(ctx, 4, nf);
+      for (int f = 0; f < nf; ++f) {
+        c3h::ReplayModes rmf = rm;
+        for (int i = 0; i < rmf.n; ++i) rmf.m[i].offset += f * q.s_scores;
+        HIPCHK(c3h::launch_replay(ctx->scores.p, rmf, ctx->M, ctx->rank, range[0], range[1], range[2], clean,
+                                  ctx->d_lists.p + f * per_lists, d_outs ? d_outs[f] : nullptr,
+                                  ctx->stream));
+      }
     }
   } else {
     if (ctx->g_sparse)
@@ -486,14 +515,19 @@ int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate
     }
     Timed t(ctx, 4);
     HIPCHK(c3h::launch_replay(ctx->scores.p, rm, ctx->M, ctx->rank, range[0], range[1], range[2], clean,
-                              ctx->d_lists.p, d_out, ctx->stream));
+                              ctx->d_lists.p, d_outs ? d_outs[0] : nullptr, ctx->stream));
   }
   ctx->pending_clean = false;
   ctx->lists_host_valid = false;
+  ctx->lists_dev_valid = true;
   ctx->last_range[0] = range[0];
   ctx->last_range[1] = range[1];
   ctx->last_range[2] = range[2];
   return nm;
+}
+
+int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate, c3h_det* d_out) {
+  return search_frames(ctx, 1, range, thr, rotate, &d_out, 0);
 }
 
 }  // namespace
@@ -572,7 +606,7 @@ void c3h_destroy(c3h_ctx* ctx) {
   release(ctx->partials);
   release(ctx->d_lists);
   for (int s = 0; s < C3H_NTIMERS; ++s)
-    for (auto& e : ctx->timer.pending[s]) ctx->timer.pool.push_back(e);
+    for (auto& e : ctx->timer.pending[s]) ctx->timer.pool.push_back({e.a, e.b});
   for (auto& e : ctx->timer.pool) {
     (void)hipEventDestroy(e.first);
     (void)hipEventDestroy(e.second);
@@ -803,12 +837,16 @@ int c3h_set_grid(c3h_ctx* ctx, const uint32_t* words, const int32_t div_b[3],
   return C3H_OK;
 }
 
-int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3],
-                int64_t* hist_num_out) {
+// C3HLAC{981,117}Estimation::setVoxelFilter + compute for nf frames of one geometry
+// (grids[f], dims / min_b / leaf of ctx->info) in one set of launches; frame f's
+// per-frame buffers (features, exist, tile stamps, work / row lists) sit at f * stride.
+int extract_frames(c3h_ctx* ctx, const uint32_t* const* grids, int nf, const c3h_extract_params* p,
+                   int32_t subdiv_out[3], int64_t* hist_num_out) {
   if (!ctx || !p) return C3H_ERR_ARG;
   if (p->variant != 981 && p->variant != 117)
     return fail(ctx, C3H_ERR_ARG, "c3h_extract: variant must be 981 or 117");
   if (!ctx->have_grid) return fail(ctx, C3H_ERR_STATE, "c3h_extract: no grid");
+  if (nf < 1 || nf > c3h::kMaxBatch) return fail(ctx, C3H_ERR_ARG, "extract: bad frame count");
   HIPCHK(hipSetDevice(ctx->device));
   ctx->have_feat = false;
   ctx->g_valid = false;
@@ -857,11 +895,12 @@ int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3]
     }
   const bool atomic = split[0] || split[1] || split[2];
   const bool all_covered = covered[0] && covered[1] && covered[2] && ntiles > 0;
-  ENSURE(ctx->feat, (size_t)hist_num * F);
-  ENSURE(ctx->exist, (size_t)hist_num);
+  ENSURE(ctx->feat, (size_t)nf * hist_num * F);
+  ENSURE(ctx->exist, (size_t)nf * hist_num);
+  ctx->nframes_feat = nf;
   if (!all_covered || atomic) {
-    HIPCHK(hipMemsetAsync(ctx->feat.p, 0, (size_t)hist_num * F * 4, ctx->stream));
-    HIPCHK(hipMemsetAsync(ctx->exist.p, 0, (size_t)hist_num * 4, ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->feat.p, 0, (size_t)nf * hist_num * F * 4, ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->exist.p, 0, (size_t)nf * hist_num * 4, ctx->stream));
   }
   if (ntiles > 0) {
     int stride = 0, lmax[3] = {1, 1, 1};
@@ -894,21 +933,31 @@ int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3]
       HIPCHK(hipMemcpyAsync(ctx->axmap.p, ctx->h_axmap.data(), ctx->h_axmap.size() * 2,
                             hipMemcpyHostToDevice, ctx->stream));
     }
-    Timed t(ctx, 1);  // the whole C3 stage: flag reset, occupancy pass, tile kernel
-    // [2] row-list counters | [2] work-list counters | [ntiles] epoch stamps; zeroed only
-    // when (re)allocated or when the epoch wraps
-    const size_t tf_n = (size_t)ntiles + 4;
-    if (ctx->tileflags.n < tf_n || ++ctx->tile_epoch == 0) {
+    Timed t(ctx, 1, nf);  // the whole C3 stage: occupancy pass + tile kernel (+ finalize)
+    // per frame: [2] row-list counters | [2] work-list counters | [ntiles] epoch stamps.
+    // Zeroed only when (re)allocated, when the layout (stride, frame count) changes -- the
+    // counters rely on every frame slot seeing every epoch -- or when the epoch wraps
+    const int64_t s_tf = ntiles + 4;
+    const size_t tf_n = (size_t)nf * s_tf;
+    if (ctx->tileflags.n < tf_n || s_tf != ctx->tf_stride || nf != ctx->tf_frames || ++ctx->tile_epoch == 0) {
       ENSURE(ctx->tileflags, tf_n);
       HIPCHK(hipMemsetAsync(ctx->tileflags.p, 0, ctx->tileflags.n * 4, ctx->stream));
       ctx->tile_epoch = 1;
+      ctx->tf_stride = s_tf;
+      ctx->tf_frames = nf;
     }
     if (atomic) {
-      ENSURE(ctx->acc64, (size_t)hist_num * 981);
-      HIPCHK(hipMemsetAsync(ctx->acc64.p, 0, (size_t)hist_num * 981 * 8, ctx->stream));
+      ENSURE(ctx->acc64, (size_t)nf * hist_num * 981);
+      HIPCHK(hipMemsetAsync(ctx->acc64.p, 0, (size_t)nf * hist_num * 981 * 8, ctx->stream));
     }
     c3h::C3Launch l;
-    l.grid = ctx->grid_ptr;
+    for (int f = 0; f < c3h::kMaxBatch; ++f) l.grid[f] = f < nf ? grids[f] : nullptr;
+    l.nframes = nf;
+    l.s_feat = hist_num * F;
+    l.s_h = hist_num;
+    l.s_acc = hist_num * 981;
+    l.s_tf = s_tf;
+    l.s_work = ntiles;
     l.gx = div[0];
     l.gy = div[1];
     l.gz = div[2];
@@ -928,14 +977,12 @@ int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3]
     l.exist = ctx->exist.p;
     l.acc64 = ctx->acc64.p;
     l.axmap = ctx->axmap.p;
-    ENSURE(ctx->work, (size_t)ntiles);
-    l.rowcnt = ctx->tileflags.p;
-    l.workcnt = ctx->tileflags.p + 2;
-    l.flags = ctx->tileflags.p + 4;
+    ENSURE(ctx->work, (size_t)nf * ntiles);
+    l.tf = ctx->tileflags.p;
     l.work = ctx->work.p;
     l.rows = nullptr;
     if (!atomic) {  // the non-empty rows feed the sparse compress of the search
-      ENSURE(ctx->rows, (size_t)hist_num);
+      ENSURE(ctx->rows, (size_t)nf * hist_num);
       l.rows = ctx->rows.p;
     }
     ctx->rows_valid = !atomic;
@@ -946,7 +993,7 @@ int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3]
     l.prof = nullptr;
     if (const char* dbg = getenv("C3H_C3_DEBUG")) l.debug = atoi(dbg);  // diagnostics only
     const int64_t tgrid = c3h::c3hlac_grid(l);
-    {
+    if (nf == 1) {
       int rc = prof_prepare(ctx, tgrid, &l.prof);
       if (rc != C3H_OK) return rc;
     }
@@ -956,7 +1003,7 @@ int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3]
       if (rc != C3H_OK) return rc;
     }
     if (atomic)
-      HIPCHK(c3h::launch_c3_finalize(ctx->acc64.p, hist_num, F, ctx->feat.p, ctx->exist.p, ctx->stream));
+      HIPCHK(c3h::launch_c3_finalize(ctx->acc64.p, hist_num, F, ctx->feat.p, ctx->exist.p, nf, ctx->stream));
   }
   ctx->hist_num = hist_num;
   ctx->feat_dim = F;
@@ -968,6 +1015,13 @@ int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3]
   if (subdiv_out) memcpy(subdiv_out, sb, sizeof(sb));
   if (hist_num_out) *hist_num_out = hist_num;
   return C3H_OK;
+}
+
+int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3],
+                int64_t* hist_num_out) {
+  if (!ctx) return C3H_ERR_ARG;
+  const uint32_t* g = ctx->grid_ptr;
+  return extract_frames(ctx, &g, 1, p, subdiv_out, hist_num_out);
 }
 
 int c3h_get_features(c3h_ctx* ctx, float* out, int on_device) {
@@ -1122,6 +1176,12 @@ int c3h_set_lanes(c3h_ctx* ctx, int32_t lanes) {
   return C3H_OK;
 }
 
+int c3h_set_batch(c3h_ctx* ctx, int32_t frames) {
+  if (!ctx || frames < 1 || frames > c3h::kMaxBatch) return C3H_ERR_ARG;
+  ctx->nbatch = frames;
+  return C3H_OK;
+}
+
 int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes,
                    const int32_t div_b[3], const int32_t min_b[3], float leaf,
                    const c3h_extract_params* p, const int32_t range[3], int32_t exist_threshold,
@@ -1129,11 +1189,16 @@ int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes
   if (!ctx || !d_grids || nframes < 0 || !div_b || !min_b || !p || !range || !d_out)
     return C3H_ERR_ARG;
   if (!ctx->have_setup) return fail(ctx, C3H_ERR_STATE, "c3h_run_frames: no axes (call c3h_search_setup)");
+  if (nframes == 0) return 0;
   HIPCHK(hipSetDevice(ctx->device));
   const size_t per_frame = (size_t)std::max(ctx->M, 1) * ctx->rank;
-  // lanes: lane 0 is the context itself and takes the last frame, so afterwards the
-  // context holds that frame's features, scores and lists as a sequential run would
-  const int K = std::max(1, std::min<int>(ctx->nlanes, std::max<int32_t>(nframes, 1)));
+  // frames go in chunks of B (one set of launches per chunk, frame = launch y / z index);
+  // chunks are spread over K lanes (child contexts, own streams and host threads).  The
+  // chunk holding the last frame runs on lane 0 (this context) with that frame in slot 0,
+  // so afterwards the context holds the last frame's features, scores and lists.
+  const int B = c3h::score_fast_ok(ctx->D, ctx->r) ? std::max(1, std::min(ctx->nbatch, c3h::kMaxBatch)) : 1;
+  const int nchunks = (nframes + B - 1) / B;
+  const int K = std::max(1, std::min(ctx->nlanes, nchunks));
   while ((int)ctx->lanes.size() < K - 1) {
     c3h_ctx* c = nullptr;
     int rc = c3h_create(ctx->device, &c);
@@ -1162,23 +1227,30 @@ int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes
   }
   HIPCHK(hipEventRecord(ctx->fork_ev, ctx->stream));  // inputs were produced on ctx's stream
   for (int l = 0; l < K - 1; ++l) HIPCHK(hipStreamWaitEvent(ctx->lanes[l]->stream, ctx->fork_ev, 0));
-  // each lane is enqueued by its own host thread (launch overhead is per thread)
   std::vector<int> lane_rc(K, 0);
   auto run_lane = [&](int lane) {
     c3h_ctx* c = lane == 0 ? ctx : ctx->lanes[lane - 1];
     if (lane) (void)hipSetDevice(c->device);
     int nm_lane = 0;
-    for (int32_t i = 0; i < nframes; ++i) {
-      if ((int)((nframes - 1 - i) % K) != lane) continue;
-      int rc = c3h_set_grid(c, d_grids[i], div_b, min_b, leaf, 1);
-      if (rc == C3H_OK) rc = c3h_clean_max(c);
-      if (rc == C3H_OK) rc = c3h_extract(c, p, nullptr, nullptr);
-      if (rc == C3H_OK) rc = c3h_search_async(c, range, exist_threshold, rotate, d_out + (size_t)i * per_frame);
+    for (int ch = 0; ch < nchunks; ++ch) {
+      if ((nchunks - 1 - ch) % K != lane) continue;
+      const int f0 = ch * B, nb = std::min(B, nframes - f0);
+      const uint32_t* grids[c3h::kMaxBatch];
+      c3h_det* outs[c3h::kMaxBatch];
+      for (int j = 0; j < nb; ++j) {  // the last chunk puts its last frame in slot 0
+        const int fi = (ch == nchunks - 1) ? (j == 0 ? f0 + nb - 1 : f0 + j - 1) : f0 + j;
+        grids[j] = d_grids[fi];
+        outs[j] = d_out + (size_t)fi * per_frame;
+      }
+      int rc = c3h_set_grid(c, grids[0], div_b, min_b, leaf, 1);
+      if (rc == C3H_OK) rc = extract_frames(c, grids, nb, p, nullptr, nullptr);
+      if (rc == C3H_OK) rc = search_frames(c, nb, range, exist_threshold, rotate, outs, 2);
       if (rc < 0) {
         lane_rc[lane] = rc;
         return;
       }
       nm_lane = rc;
+      c->nframes_feat = 1;  // slot 0 is the context's view from here on
     }
     lane_rc[lane] = nm_lane;
   };
@@ -1189,12 +1261,11 @@ int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes
   for (int l = 1; l < K; ++l)
     if (lane_rc[l] < 0) return fail(ctx, lane_rc[l], std::string("c3h_run_frames lane: ") + ctx->lanes[l - 1]->err);
   if (lane_rc[0] < 0) return lane_rc[0];
-  const int nm = lane_rc[0];
   for (int l = 0; l < K - 1; ++l) {  // join
     HIPCHK(hipEventRecord(ctx->lane_ev[l], ctx->lanes[l]->stream));
     HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[l], 0));
   }
-  return nm;
+  return lane_rc[0];
 }
 
 int c3h_get_compressed(c3h_ctx* ctx, float* out, int on_device) {
@@ -1322,11 +1393,11 @@ int c3h_kernel_times(c3h_ctx* ctx, float* ms_out, int32_t* counts_out, int32_t r
   for (int s = 0; s < C3H_NTIMERS; ++s) {
     for (auto& e : ctx->timer.pending[s]) {
       float ms = 0;
-      if (hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) {
+      if (hipEventElapsedTime(&ms, e.a, e.b) == hipSuccess) {
         ctx->timer.ms[s] += ms;
-        ctx->timer.count[s] += 1;
+        ctx->timer.count[s] += e.weight;
       }
-      ctx->timer.pool.push_back(e);
+      ctx->timer.pool.push_back({e.a, e.b});
     }
     ctx->timer.pending[s].clear();
   }

@@ -108,20 +108,21 @@ struct CompressRows {
   const int32_t* rows;
   const uint32_t* nrows;
   int F, D, Dpad, fmax_len;
+  int64_t s_feat, s_G, s_rows, s_nrows;  // per-frame strides (frame = launch y / z index)
 };
 
-__device__ __forceinline__ void compress_rows_body(const CompressRows& cr, int bid) {
-  const float* __restrict__ feat = cr.feat;
+__device__ __forceinline__ void compress_rows_body(const CompressRows& cr, int bid, int64_t f) {
+  const float* __restrict__ feat = cr.feat + f * cr.s_feat;
   const float* __restrict__ PT = cr.PT;
   const float* __restrict__ fmax = cr.fmax;
-  float* __restrict__ G = cr.G;
-  const int32_t* __restrict__ rows = cr.rows;
+  float* __restrict__ G = cr.G + f * cr.s_G;
+  const int32_t* __restrict__ rows = cr.rows + f * cr.s_rows;
   const int F = cr.F, D = cr.D, Dpad = cr.Dpad, fmax_len = cr.fmax_len;
   extern __shared__ __attribute__((aligned(16))) float csm[];
   float* pc = csm;                 // kRK x Dpad
   float* fs = csm + kRK * Dpad;    // kRR x F
   const int tid = threadIdx.x;
-  const int n = (int)*cr.nrows;
+  const int n = (int)cr.nrows[f * cr.s_nrows];
   const int r0 = bid * kRR;
   if (r0 >= n) return;
   const int nq4 = kRK * Dpad / 4, tot4 = F * Dpad / 4;
@@ -191,7 +192,7 @@ __device__ __forceinline__ void compress_rows_body(const CompressRows& cr, int b
 }
 
 __global__ __launch_bounds__(kBlock) void compress_rows_kernel(CompressRows cr) {
-  compress_rows_body(cr, blockIdx.x);
+  compress_rows_body(cr, blockIdx.x, blockIdx.y);
 }
 
 // ---------------------------------------------------------------- score
@@ -287,6 +288,22 @@ constexpr int kOC = 64;  // basis rows per workgroup (whole models)
 // passing ones into a list; the projection then runs over the list only.  Entries are
 // (mode index << 40) | position; list order is irrelevant: scores are per position and
 // the per-block partials break ties on the scan order explicitly.
+// this frame's view of a batched search (per-frame buffers at base + f * stride)
+__device__ __forceinline__ SparseSearch frame_view(const SparseSearch& b, int64_t f) {
+  SparseSearch a = b;
+  a.G = b.G + f * b.s_G;
+  a.exist = b.exist + f * b.s_exist;
+  a.scores = b.scores + f * b.s_scores;
+  a.list = b.list + f * b.s_list;
+  a.cnt = b.cnt + f * b.s_cnt;
+  a.done = b.done + f * b.s_cnt;
+  if (b.partials) a.partials = b.partials + f * b.s_partials;
+  if (b.lists) a.lists = b.lists + f * b.s_lists;
+  a.outs[0] = b.outs[f];
+  if (f) a.prof = nullptr;
+  return a;
+}
+
 __device__ __forceinline__ int find_mode(const SparseSearch& a, int64_t g) {
   int mi = 0;
   while (mi + 1 < a.nmodes && g >= a.pstart[mi + 1]) ++mi;
@@ -328,25 +345,28 @@ __device__ __forceinline__ void gate_body(const SparseSearch& a, int bid) {
   }
 }
 
-__global__ __launch_bounds__(kBlock) void gate_kernel(SparseSearch a) { gate_body(a, blockIdx.x); }
+__global__ __launch_bounds__(kBlock) void gate_kernel(SparseSearch b) {
+  gate_body(frame_view(b, blockIdx.y), blockIdx.x);
+}
 
 // one launch for two independent stages: gate workgroups first, then the sparse compress
-__global__ __launch_bounds__(kBlock) void compress_gate_kernel(CompressRows cr, SparseSearch a, int ngate) {
-  if ((int)blockIdx.x < ngate) gate_body(a, blockIdx.x);
-  else compress_rows_body(cr, blockIdx.x - ngate);
+__global__ __launch_bounds__(kBlock) void compress_gate_kernel(CompressRows cr, SparseSearch b, int ngate) {
+  if ((int)blockIdx.x < ngate) gate_body(frame_view(b, blockIdx.y), blockIdx.x);
+  else compress_rows_body(cr, blockIdx.x - ngate, blockIdx.y);
 }
 
 // Rank-1 replay fused into the score launch (search.cpp:464-474 with rank_num == 1:
 // checkOverlap returns slot 0, so the update is "first strictly greater maximum in scan
 // order").  One wave per model reduces the partials with (score desc, scan order asc);
 // partials of other workgroups are read with device-scope atomic loads.
-__device__ void argmax_finalize(const SparseSearch& a, int nparts) {
+__device__ void argmax_finalize(const SparseSearch& a, const ScorePartial* partials, c3h_det* lists,
+                                c3h_det* out, int nparts) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int m = w; m < a.M; m += kBlock / 64) {
     double best = -2.0;
     long long bo = -1;
     for (int i = lane; i < nparts; i += 64) {
-      const ScorePartial* q = a.partials + (int64_t)i * a.M + m;
+      const ScorePartial* q = partials + (int64_t)i * a.M + m;
       const long long qo = __hip_atomic_load(&q->order, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const double qs = __hip_atomic_load(&q->score, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (qo >= 0 && (qs > best || (qs == best && qo < bo))) {
@@ -364,10 +384,11 @@ __device__ void argmax_finalize(const SparseSearch& a, int nparts) {
       }
     }
     if (lane == 0) {
-      c3h_det e = a.lists[m];
-      if (a.clean) {
+      c3h_det e = lists[m];
+      if (a.clean) {  // 1: cleanMax (modes kept, search.cpp:683-690); 2: setRank state
         e.score = 0.0;
         e.x = e.y = e.z = 0;
+        if (a.clean == 2) e.mode = 0;
       }
       if (bo >= 0 && best > e.score) {
         const int mi = (int)(bo >> 40);
@@ -379,8 +400,8 @@ __device__ void argmax_finalize(const SparseSearch& a, int nparts) {
         e.z = (int)(p / ((int64_t)md.xe * md.ye));
         e.mode = md.mode;
       }
-      a.lists[m] = e;
-      if (a.out2) a.out2[m] = e;
+      lists[m] = e;
+      if (out) out[m] = e;
     }
   }
 }
@@ -389,16 +410,28 @@ __device__ void argmax_finalize(const SparseSearch& a, int nparts) {
 // kFP entries per workgroup; box rows of empty subdivisions are skipped (their G rows
 // may be stale: the sparse compress only writes non-empty rows; an all-zero row adds
 // nothing to a sum that starts at +0).
-__global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch a) {
+__global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch b) {
+  const SparseSearch& a = b;  // frame-independent fields; per-frame pointers below
+  const int64_t fz = blockIdx.z;
+  const float* __restrict__ fG = b.G + fz * b.s_G;
+  const int32_t* __restrict__ fexist = b.exist + fz * b.s_exist;
+  double* __restrict__ fscores = b.scores + fz * b.s_scores;
+  const long long* __restrict__ flist = b.list + fz * b.s_list;
+  const uint32_t* fcnt = b.cnt + fz * b.s_cnt;
+  uint32_t* fdone = b.done + fz * b.s_cnt;
+  ScorePartial* fpart = b.partials ? b.partials + fz * b.s_partials : nullptr;
+  c3h_det* flists = b.lists ? b.lists + fz * b.s_lists : nullptr;
+  c3h_det* fout = b.outs[fz];
+  long long* fprof = fz ? nullptr : b.prof;
   extern __shared__ __attribute__((aligned(16))) float ssm[];
   const int D = a.D, D4 = a.D >> 2, Qs = a.Opad;  // qt row stride
 #define C3H_SPROF(k) \
-  if (a.prof && threadIdx.x == 0 && blockIdx.y == 0) a.prof[blockIdx.x * 8 + (k)] = (long long)wall_clock64()
+  if (fprof && threadIdx.x == 0 && blockIdx.y == 0) fprof[blockIdx.x * 8 + (k)] = (long long)wall_clock64()
   C3H_SPROF(0);
-  const int n = (int)a.cnt[a.epoch & 1];
+  const int n = (int)fcnt[a.epoch & 1];
   const int64_t e0 = blockIdx.x * (int64_t)kFP;
   if (e0 >= n) {
-    if (n == 0 && a.lists && blockIdx.x == 0 && blockIdx.y == 0) argmax_finalize(a, 0);  // clean / copy out
+    if (n == 0 && flists && blockIdx.x == 0 && blockIdx.y == 0) argmax_finalize(a, fpart, flists, fout, 0);  // clean / copy out
     return;
   }
   // model group of this workgroup: models [m0, m1), basis rows [m0*r, m1*r) padded to oc
@@ -421,7 +454,7 @@ __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch a) {
     int ok = 0, h = 0, rr = 0;
     long long en = -1;
     if (e < n) {
-      en = a.list[e];
+      en = flist[e];
       const int mi = (int)(en >> 40);
       const int64_t p = en & ((1ll << 40) - 1);
       const ModeGeom& md = a.md[mi];
@@ -458,7 +491,7 @@ __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch a) {
     const int h = hrow[pp], rr = rng[pp];
     const int xr = rr & 1023, yr = (rr >> 10) & 1023, zr = rr >> 20;
     const int ncell = ok ? xr * yr * zr : 0;
-    const float4* G4 = reinterpret_cast<const float4*>(a.G);
+    const float4* G4 = reinterpret_cast<const float4*>(fG);
     constexpr int kSlots = 4;  // d4 values per thread handled together (D4 <= 64)
     float4 s[kSlots];
 #pragma unroll
@@ -472,7 +505,7 @@ __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch a) {
           const int c = c0 + k;
           const int dx = c % xr, dy = (c / xr) % yr, dz = c / (xr * yr);
           const int hh = h + dz * xyn + dy * a.xn + dx;
-          lv[k] = c < ncell && a.exist[c < ncell ? hh : h] != 0;
+          lv[k] = c < ncell && fexist[c < ncell ? hh : h] != 0;
 #pragma unroll
           for (int q = 0; q < kSlots; ++q) {
             const int d4 = d4b + dg + q * kDG;
@@ -556,12 +589,12 @@ __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch a) {
       sc = sqrt((double)q2) / sqrt((double)ffv[pp]);
       const long long en = ent[pp];
       const ModeGeom& md = a.md[(int)(en >> 40)];
-      a.scores[md.offset + (int64_t)(m0 + mm) * md.P + (en & ((1ll << 40) - 1))] = sc;
+      fscores[md.offset + (int64_t)(m0 + mm) * md.P + (en & ((1ll << 40) - 1))] = sc;
     }
     bsc[e] = sc;
   }
   C3H_SPROF(4);
-  if (a.partials) {
+  if (fpart) {
     lds_barrier();
     for (int mm = tid; mm < nm; mm += kBlock) {  // (score desc, scan order asc)
       double best = -2.0;
@@ -576,15 +609,15 @@ __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch a) {
           bo = o;
         }
       }
-      ScorePartial* q = a.partials + (int64_t)blockIdx.x * a.M + m0 + mm;
-      if (a.lists) {  // handed to another workgroup inside this launch: sc1 stores
+      ScorePartial* q = fpart + (int64_t)blockIdx.x * a.M + m0 + mm;
+      if (flists) {  // handed to another workgroup inside this launch: sc1 stores
         __hip_atomic_store(&q->score, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&q->order, bo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         *q = ScorePartial{best, bo};
       }
     }
-    if (a.lists) {
+    if (flists) {
       // rank 1, fused replay: the last workgroup to finish reduces.  Hand-off per
       // MI355X_MICROARCH.md (inter-workgroup visibility, table row 1): sc1 stores, every
       // storing wave waits vmcnt(0), a barrier, one agent atomic add per workgroup; the
@@ -594,10 +627,10 @@ __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch a) {
       lds_barrier();
       if (tid == 0) {
         const uint32_t total = (uint32_t)((n + kFP - 1) / kFP) * gridDim.y;
-        s_last = atomicAdd(&a.done[a.epoch & 1], 1u) == total - 1;
+        s_last = atomicAdd(&fdone[a.epoch & 1], 1u) == total - 1;
       }
       lds_barrier();
-      if (s_last) argmax_finalize(a, (n + kFP - 1) / kFP);
+      if (s_last) argmax_finalize(a, fpart, flists, fout, (n + kFP - 1) / kFP);
     }
   }
   C3H_SPROF(7);
@@ -659,9 +692,10 @@ __global__ __launch_bounds__(64) void replay_kernel(const double* __restrict__ s
   c3h_det* gl = lists + (int64_t)m * rank;
   for (int i = lane; i < rank; i += 64) {
     c3h_det e = gl[i];
-    if (clean) {
+    if (clean) {  // 1: cleanMax (modes kept); 2: setRank state
       e.score = 0.0;
       e.x = e.y = e.z = 0;
+      if (clean == 2) e.mode = 0;
     }
     L[i] = e;
   }
@@ -717,7 +751,7 @@ hipError_t launch_compress(const float* feat, int64_t H, int F, const float* axi
                            const int32_t* rows, const uint32_t* nrows, hipStream_t s) {
   if (rows && compress_rows_ok(F, Dpad)) {  // sparse list
     const size_t lds = sizeof(float) * ((size_t)kRK * Dpad + (size_t)kRR * F);
-    const CompressRows cr{feat, axis_pt, fmax, G, rows, nrows, F, D, Dpad, fmax_len};
+    const CompressRows cr{feat, axis_pt, fmax, G, rows, nrows, F, D, Dpad, fmax_len, 0, 0, 0, 0};
     compress_rows_kernel<<<(unsigned)((H + kRR - 1) / kRR), kBlock, lds, s>>>(cr);
     return hipGetLastError();
   }
@@ -757,18 +791,20 @@ hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc,
   const int64_t ptot = a.pstart[a.nmodes];
   if (ptot <= 0) return hipSuccess;
   const unsigned ngate = (unsigned)((ptot + kBlock - 1) / kBlock);
+  const unsigned nf = (unsigned)a.nframes;
   if (sc) {  // compress (non-empty rows) and gate in one launch
-    const CompressRows cr{sc->feat, sc->PT, sc->fmax, sc->G, sc->rows, sc->nrows, sc->F, sc->D, sc->Dpad, sc->fmax_len};
+    const CompressRows cr{sc->feat, sc->PT, sc->fmax, sc->G, sc->rows, sc->nrows, sc->F, sc->D, sc->Dpad,
+                          sc->fmax_len, sc->s_feat, sc->s_G, sc->s_rows, sc->s_nrows};
     const size_t lds = sizeof(float) * ((size_t)kRK * sc->Dpad + (size_t)kRR * sc->F);
-    compress_gate_kernel<<<ngate + (unsigned)((sc->H + kRR - 1) / kRR), kBlock, lds, s>>>(cr, a, (int)ngate);
+    compress_gate_kernel<<<dim3(ngate + (unsigned)((sc->H + kRR - 1) / kRR), nf), kBlock, lds, s>>>(cr, a, (int)ngate);
   } else {
-    gate_kernel<<<ngate, kBlock, 0, s>>>(a);
+    gate_kernel<<<dim3(ngate, nf), kBlock, 0, s>>>(a);
   }
   const size_t region = std::max((size_t)a.D * (kFP + kOC), (size_t)kFP * (kOC + 1));
   const size_t lds = sizeof(float) * (region + kFP) + sizeof(int) * 4 * kFP + sizeof(long long) * kFP +
                      sizeof(double) * kFP * a.mpg + 16;
   const unsigned groups = (unsigned)((a.M + a.mpg - 1) / a.mpg);
-  score_list_kernel<<<dim3((unsigned)sparse_score_blocks(a), groups), kBlock, lds, s>>>(a);
+  score_list_kernel<<<dim3((unsigned)sparse_score_blocks(a), groups, nf), kBlock, lds, s>>>(a);
   return hipGetLastError();
 }
 

@@ -346,10 +346,12 @@ def test_dense_256_bin_block_linearity(ctx):
     assert whole[:6].sum() == 3 * 256 ** 3  # each voxel adds beta_c + (1-beta_c) per colour
 
 
-@pytest.mark.parametrize("lanes", [1, 3, 4])
-def test_run_frames_lanes_match_sequential(ctx, lanes):
-    """c3h_run_frames with frames in flight on lane contexts == frame-by-frame
-    cleanMax / extract / search on one context; the context ends with the last frame."""
+@pytest.mark.parametrize("lanes,batch,rank", [(1, 1, 1), (1, 4, 1), (3, 1, 1), (3, 4, 1), (2, 3, 2),
+                                              (4, 8, 1)])
+def test_run_frames_lanes_match_sequential(ctx, lanes, batch, rank):
+    """c3h_run_frames (frames batched per launch, batches in flight on lane contexts) ==
+    frame-by-frame setRank / extract / search on one context; the context ends with the
+    last frame's state."""
     import torch
     G, S, rng_box = 64, 8, (2, 2, 1)
     frames = [synth.kinect_scene(60_000, grid=G, leaf=0.01, seed=synth.BASE_SEED + 40 + i) for i in range(7)]
@@ -358,26 +360,30 @@ def test_run_frames_lanes_match_sequential(ctx, lanes):
         gi = ctx.voxelize(pts, 0.01)
         assert list(gi.div_b) == [G] * 3
         words.append(ctx.grid().reshape(-1).astype(np.uint32))
+    words.append(np.zeros_like(words[0]))  # an empty frame: no position passes the gate
     axis_t, var, axis_q = synth.random_bases(117, 24, 4, 6, seed=3)
     ctx.search_setup(axis_t, var, axis_q)
-    ctx.set_rank(2)
     ref = []
     for w in words:
         ctx.set_grid(w, (G, G, G))
-        ctx.clean_max()
+        ctx.set_rank(rank)  # run_frames: every frame starts from fresh lists
         ctx.extract(117, THR, S)
         det, _ = ctx.search(rng_box, 20)
         ref.append(det.copy())
     last_feat = ctx.features()
+    last_exist = ctx.exist()
     dev = torch.device("cuda", 0)
     d_grids = [torch.from_numpy(w.view(np.int32)).to(dev) for w in words]
-    d_out = torch.zeros((len(words), 4 * 2 * 3), dtype=torch.int64, device=dev)
+    d_out = torch.zeros((len(words), 4 * rank * 3), dtype=torch.int64, device=dev)
     ctx.set_lanes(lanes)
+    ctx.set_batch(batch)
     ctx.run_frames(np.array([g.data_ptr() for g in d_grids], np.uint64), (G, G, G), (0, 0, 0), 0.01, 117,
                    THR, S, rng_box, 20, True, d_out.data_ptr())
     torch.cuda.synchronize()
-    got = d_out.cpu().numpy().view(c3hlac.DET_DTYPE).reshape(len(words), 4, 2)
+    got = d_out.cpu().numpy().view(c3hlac.DET_DTYPE).reshape(len(words), 4, rank)
     for i in range(len(words)):
         np.testing.assert_array_equal(got[i], ref[i])
     np.testing.assert_array_equal(ctx.features(), last_feat)
-    ctx.set_lanes(4)
+    np.testing.assert_array_equal(ctx.exist(), last_exist)
+    ctx.set_lanes(3)
+    ctx.set_batch(4)

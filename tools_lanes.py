@@ -1,6 +1,10 @@
 """Diagnostics: host enqueue time vs device time of c3h_run_frames for 1..4 lanes."""
+import os
 import sys
 import time
+
+if len(sys.argv) > 1:  # e.g. GPU_MAX_HW_QUEUES=8 (must precede the HIP runtime's start)
+    os.environ["GPU_MAX_HW_QUEUES"] = sys.argv[1]
 
 sys.path[:0] = ["mapping-private_amd"]
 import numpy as np  # noqa: E402
@@ -26,15 +30,11 @@ with c3hlac.Context(0) as ctx:
     gptr = np.array([grids[i % 6].data_ptr() for i in range(N)], np.uint64)
     dets = torch.zeros((N, 30), dtype=torch.int64, device=dev)
     import os
-    cases = [(l, None, None) for l in (1, 2, 3, 4, 6)] + [(3, g, None) for g in ("256", "1280")] + \
-        [(3, None, o) for o in ("512", "2048", "4096")]
-    for lanes, tg, og in cases:
-        for k, v in (("C3H_TILE_GRID", tg), ("C3H_OCC_GRID", og)):
-            if v:
-                os.environ[k] = v
-            else:
-                os.environ.pop(k, None)
+    cases = [(2, 4), (3, 4), (4, 4), (6, 4), (2, 8), (3, 8), (4, 8), (6, 8)]
+    for lanes, batch in cases:
+        tg = og = None
         ctx.set_lanes(lanes)
+        ctx.set_batch(batch)
         for rep in range(2):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -43,5 +43,5 @@ with c3hlac.Context(0) as ctx:
             t1 = time.perf_counter()
             torch.cuda.synchronize()
             t2 = time.perf_counter()
-        print("lanes=%d tile_grid=%s occ_grid=%s host_enqueue_us_per_frame=%.1f total_us_per_frame=%.1f" %
-              (lanes, tg, og, (t1 - t0) / N * 1e6, (t2 - t0) / N * 1e6), flush=True)
+        print("lanes=%d batch=%d host_enqueue_us_per_frame=%.1f total_us_per_frame=%.1f" %
+              (lanes, batch, (t1 - t0) / N * 1e6, (t2 - t0) / N * 1e6), flush=True)
