@@ -19,7 +19,6 @@ constexpr int kBlock = 256;
 // largest centre-voxel extent of one C3 tile per axis; subdivisions wider than this
 // are split into several tiles whose exact integer partial sums are added in 64 bit.
 constexpr int kTileMax = 16;
-constexpr int kChunk = 128;  // list entries per packed-operand chunk (32 groups of 4)
 
 // reference constants (c3_hlac/src/c3_hlac.cpp:38-45), as float
 constexpr float kNorm0 = 1 / 255.0;
@@ -106,7 +105,7 @@ struct c3h_ctx {
   c3h::DevBuf<int32_t> segs;        // per-axis tile segment tables
   c3h::DevBuf<int16_t> axmap;       // per-axis coordinate -> segment (pass-1 tile lookup)
   std::vector<int16_t> h_axmap;
-  c3h::DevBuf<uint32_t> tileflags;  // [2] row counters | [2] work counters | [ntiles] stamps
+  c3h::DevBuf<uint32_t> tileflags;  // [2] reserved | [2] work counters | [ntiles] stamps
   c3h::DevBuf<int32_t> work;        // non-empty tiles of the last extract
   uint32_t tile_epoch = 0;
   int64_t tf_stride = -1;           // tile-stamp layout the counters were zeroed for
@@ -186,7 +185,7 @@ struct C3Launch {
   int nframes;
   // per-frame buffers: frame f at base + f * stride
   int64_t s_feat, s_h, s_acc, s_tf, s_work;
-  uint32_t* tf;           // [2] row counters | [2] work counters | [ntiles] epoch stamps
+  uint32_t* tf;           // [2] reserved | [2] work counters | [ntiles] epoch stamps
   int gx, gy, gz;
   const int32_t* segs;  // [3][nseg_max][3] = start, len, subdiv
   int nseg[3];

@@ -23,16 +23,20 @@
 // rounding (<= a few ulp); exist_voxel_num is reproduced bit-exactly from the integer
 // zero-order sums (search_c3_hlac.h:60-61).
 //
-// Mapping.  One 256-thread workgroup per tile; a tile is one subdivision (or a <=16^3
-// piece of one: partial sums then go through 64-bit atomics + a finalize kernel).
+// Mapping.  Two passes per frame (frame = launch y index, several frames per launch):
+//   pass 1 (c3_occupancy_kernel) streams the packed grid once and stamps the tiles (a
+//     subdivision, or a <=16^3 piece of one) holding occupied centre voxels, appending
+//     them to a dense work list;
+//   pass 2 (c3hlac_tile_kernel), persistent 256-thread workgroups over the work list:
 //   1. stage the (lx+2) x (ly+2) x (lz+1) halo of packed grid words in LDS
 //   2. compact the occupied centre voxels into an LDS list (wave ballot)
-//   3. per chunk of 128 list entries: (group, k) jobs build the packed operand dwords
-//      (16 groups x 15 k x {colour, binary} x 6 channels) in LDS
-//   4. 180 threads accumulate 6 dot4 products per group into u32 registers
+//   3. per chunk of 128 list entries, (group, k) jobs build the packed operand dwords
+//      (32 groups x 15 k x {colour, binary} x 6 channels: 4 voxels' bytes per dword)
+//   4. 180 threads, one (type, k, n) column each, accumulate 6 dot4 products per group
+//      into u32 registers
 //   5. scatter the 981 integer bins to LDS, fold/normalise, coalesced store
-// Tiles are enumerated x-fastest and dealt to XCDs in contiguous ranges so neighbouring
-// tiles (which share halo lines) run on the same L2.
+//   Leading zero-role workgroups write the all-zero rows of the unstamped subdivisions.
+//   Pieces of split subdivisions go through 64-bit atomics + c3_finalize_kernel.
 #include <algorithm>
 #include <cstdlib>
 
@@ -41,13 +45,10 @@
 namespace c3h {
 namespace {
 
-constexpr int kArrStride = 192;  // dwords per group: 2 types x 15 k x 6 n = 180, padded
+constexpr int kArrStride = 196;  // dwords per group: 2 types x 15 k x 6 n = 180, padded so
+                                 // groups start 4 banks apart (192 would alias all groups)
+constexpr int kChunk = 128;      // list entries per packed-operand chunk
 constexpr int kGroups = kChunk / 4;
-
-// relative_coordinates (c3_hlac.cpp:180-201)
-__constant__ int kRel[13][3] = {{-1, -1, -1}, {-1, 0, -1}, {-1, 1, -1}, {0, -1, -1}, {0, 0, -1},
-                                {0, 1, -1},   {1, -1, -1}, {1, 0, -1},  {1, 1, -1},  {-1, -1, 0},
-                                {0, -1, 0},   {1, -1, 0},  {-1, 0, 0}};
 
 __device__ __forceinline__ int bin981(int k, int c, int n) {
   return k <= 8 ? 6 + 78 * c + 9 * n + k : 60 + 78 * c + 4 * n + (k - 9);
@@ -118,7 +119,7 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t n) {
 // tile segment of centre coordinate c along that axis (-1 when c is no centre, e.g.
 // below the subdivision offset): the reference's float subdivision arithmetic is baked
 // into these host-built tables.
-constexpr int kOccUnroll = 8;  // 16-B loads per thread in flight per chunk
+constexpr int kOccUnroll = 16;  // 16-B loads per thread in flight per chunk (256 B / lane)
 constexpr int kOccSet = 1024;  // LDS set of tiles touched by one workgroup (4 KB)
 
 // Flags are epoch stamps: tile t is non-empty in this frame iff flags[t] == epoch, so
@@ -154,7 +155,7 @@ struct OccArgs {
   const int16_t* axmap;
   int ns0, ns1;
   uint32_t epoch;
-  uint32_t* tf;    // per frame: [2] row counters | [2] work counters | [ntiles] stamps
+  uint32_t* tf;    // per frame: [2] reserved | [2] work counters | [ntiles] stamps
   int32_t* work;   // per frame: [ntiles]
   int64_t s_tf, s_work;
 };
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(kBlock) void c3_occupancy_kernel(OccArgs oa) {
 struct KArgs {
   const uint32_t* grids[kMaxBatch];  // frame f = blockIdx.y; per-frame buffers at f * stride
   int64_t s_feat, s_h, s_acc, s_tf, s_work;
-  uint32_t* tf;  // frame 0's [2] row counters | [2] work counters | [ntiles] stamps
+  uint32_t* tf;  // frame 0's [2] reserved | [2] work counters | [ntiles] stamps
   const uint32_t* grid;
   int gx, gy, gz;
   const int32_t* segs;
@@ -269,7 +270,6 @@ struct KArgs {
   const int32_t* work;    // non-empty tiles of pass 1
   uint32_t* workcnt;      // [2] work-list counters by epoch parity
   int32_t* rows;          // direct mode: non-empty subdivisions of this frame (nullable)
-  uint32_t* rowcnt;       // [2] row-list counters by epoch parity
   uint32_t epoch;
   int ntiles;
   int zblocks;            // leading workgroups that zero the rows of unstamped tiles
@@ -287,24 +287,21 @@ constexpr int kSegLds = 64;   // segment tables up to 64 segments per axis live 
 // halo in LDS (all loads issued before the first LDS store), compact the occupied
 // centres, build the packed dot4 operands and accumulate exactly (see the header).
 #define C3H_PROF(k, cond) \
-  if (a.prof && tid == 0 && (cond)) a.prof[blockIdx.x * 8 + (k)] = (long long)wall_clock64()
+  if (fprof && tid == 0 && (cond)) fprof[blockIdx.x * 8 + (k)] = (long long)wall_clock64()
 
-__global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs ka) {
-  KArgs a = ka;  // this frame's view
-  {
-    const int64_t f = blockIdx.y;
-    a.grid = ka.grids[f];
-    a.feat = ka.feat + f * ka.s_feat;
-    a.exist = ka.exist + f * ka.s_h;
-    if (ka.acc64) a.acc64 = ka.acc64 + f * ka.s_acc;
-    uint32_t* tf = ka.tf + f * ka.s_tf;
-    a.rowcnt = tf;
-    a.workcnt = tf + 2;
-    a.flags = tf + 4;
-    a.work = ka.work + f * ka.s_work;
-    if (ka.rows) a.rows = ka.rows + f * ka.s_h;
-    if (f) a.prof = nullptr;
-  }
+__global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
+  // this frame's buffers (frame = blockIdx.y); the argument struct itself is not copied
+  const int64_t fy = blockIdx.y;
+  const uint32_t* __restrict__ fgrid = a.grids[fy];
+  float* __restrict__ ffeat = a.feat + fy * a.s_feat;
+  int32_t* __restrict__ fexist = a.exist + fy * a.s_h;
+  unsigned long long* facc = a.acc64 ? a.acc64 + fy * a.s_acc : nullptr;
+  uint32_t* ftf = a.tf + fy * a.s_tf;
+  const uint32_t* __restrict__ fflags = ftf + 4;
+  uint32_t* fworkcnt = ftf + 2;
+  const int32_t* __restrict__ fwork = a.work + fy * a.s_work;
+  int32_t* frows = a.rows ? a.rows + fy * a.s_h : nullptr;
+  long long* fprof = fy ? nullptr : a.prof;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint32_t* s_lut = smem;                       // 256
   uint32_t* s_tile = s_lut + 256;               // tw_max (16-B aligned)
@@ -318,22 +315,21 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs ka) {
   C3H_PROF(0, true);
   // issued together: the work count, this workgroup's first work item, its phase-Z flags
   if (blockIdx.x == 0 && tid == 0) {  // the next frame's counters
-    a.rowcnt[(a.epoch + 1) & 1] = 0;
-    a.workcnt[(a.epoch + 1) & 1] = 0;
+    fworkcnt[(a.epoch + 1) & 1] = 0;
   }
   if ((int)blockIdx.x < a.zblocks) {
     // zero role (direct mode, every subdivision one tile: h == tile): rows of the tiles
     // pass 1 left unstamped, one wave-wide store per 64 floats
     for (int t0 = (int)blockIdx.x * kBlock; t0 < a.ntiles; t0 += a.zblocks * kBlock) {
       const int t = t0 + tid;
-      unsigned long long m = __ballot(t < a.ntiles && a.flags[t] != a.epoch);
+      unsigned long long m = __ballot(t < a.ntiles && fflags[t] != a.epoch);
       while (m) {
         const int q = __ffsll((long long)m) - 1;
         m &= m - 1;
         const int tj = (t0 + (tid & ~63)) + q;
-        float* row = a.feat + (int64_t)tj * F;
+        float* row = ffeat + (int64_t)tj * F;
         for (int c = lane; c < F; c += 64) row[c] = 0.0f;
-        if (lane == 0) a.exist[tj] = 0;
+        if (lane == 0) fexist[tj] = 0;
       }
     }
     return;
@@ -341,8 +337,8 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs ka) {
   // work role: workgroup b takes items b, b + G, ... of the dense work list (balanced)
   const int G = (int)gridDim.x - a.zblocks;
   int wi = (int)blockIdx.x - a.zblocks;
-  int tile_next = wi < a.ntiles ? a.work[wi] : 0;  // speculative; used only if wi < nwork
-  const int nwork = (int)a.workcnt[a.epoch & 1];
+  int tile_next = wi < a.ntiles ? fwork[wi] : 0;  // speculative; used only if wi < nwork
+  const int nwork = (int)fworkcnt[a.epoch & 1];
   if (a.debug == 3) return;  // diagnostics: occupancy pass only
   s_lut[tid] = a.lut[tid];
   const bool segs_lds = a.seg_stride <= kSegLds;
@@ -355,7 +351,7 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs ka) {
 
   for (; wi < (a.debug == 4 ? 0 : nwork); wi += G) {
     const int tile = tile_next;
-    if (wi + G < nwork) tile_next = a.work[wi + G];
+    if (wi + G < nwork) tile_next = fwork[wi + G];
     const int ix = tile % a.ns0, iy = (tile / a.ns0) % a.ns1, iz = tile / (a.ns0 * a.ns1);
     const int32_t* sx = segs + 3 * ix;
     const int32_t* sy = segs + 3 * (a.seg_stride + iy);
@@ -385,7 +381,7 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs ka) {
           const int ty = q % TY, tz = q / TY;
           const int gy = y0 - 1 + ty, gz = z0 - 1 + tz;
           if ((unsigned)gy < (unsigned)a.gy && (unsigned)gz < (unsigned)a.gz)
-            w[j] = *reinterpret_cast<const uint4*>(a.grid + ((int64_t)gz * a.gy + gy) * a.gx + xs + 4 * r);
+            w[j] = *reinterpret_cast<const uint4*>(fgrid + ((int64_t)gz * a.gy + gy) * a.gx + xs + 4 * r);
         }
         q += sq;
         r += sr;
@@ -402,7 +398,7 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs ka) {
         const int gy = y0 - 1 + qq % TY, gz = z0 - 1 + qq / TY;
         uint4 v = make_uint4(0, 0, 0, 0);
         if ((unsigned)gy < (unsigned)a.gy && (unsigned)gz < (unsigned)a.gz)
-          v = *reinterpret_cast<const uint4*>(a.grid + ((int64_t)gz * a.gy + gy) * a.gx + xs + 4 * rr);
+          v = *reinterpret_cast<const uint4*>(fgrid + ((int64_t)gz * a.gy + gy) * a.gx + xs + 4 * rr);
         *reinterpret_cast<uint4*>(&s_tile[4 * e]) = v;
       }
     } else {
@@ -412,13 +408,13 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs ka) {
         const int gy = y0 - 1 + qq % TY, gz = z0 - 1 + qq / TY, gxx = xs + rr;
         s_tile[e] = ((unsigned)gy < (unsigned)a.gy && (unsigned)gz < (unsigned)a.gz &&
                      (unsigned)gxx < (unsigned)a.gx)
-                        ? a.grid[((int64_t)gz * a.gy + gy) * a.gx + gxx] : 0u;
+                        ? fgrid[((int64_t)gz * a.gy + gy) * a.gx + gxx] : 0u;
       }
     }
     lds_barrier();
     C3H_PROF(3, wi == (int)blockIdx.x - a.zblocks);
     if (a.debug == 1) {
-      if (tid == 0 && s_tile[0] == 0xdeadbeefu) a.exist[0] = 1;  // keep the loads live
+      if (tid == 0 && s_tile[0] == 0xdeadbeefu) fexist[0] = 1;  // keep the loads live
       lds_barrier();
       continue;
     }
@@ -456,7 +452,7 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs ka) {
     C3H_PROF(4, wi == (int)blockIdx.x - a.zblocks);
     const int nlist = (int)s_misc[0];
     if (a.debug == 2) {
-      if (tid == 0 && nlist == 0x7fffffff) a.exist[0] = 1;
+      if (tid == 0 && nlist == 0x7fffffff) fexist[0] = 1;
       lds_barrier();
       continue;
     }
@@ -467,18 +463,34 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs ka) {
       //    branch-free so each job's LDS reads (list, tile, LUT) issue back to back
       for (int job = tid; job < kGroups * 15; job += kBlock) {
         const int jg = job / 15, jk = job - jg * 15;
-        const int delta = jk < 13 ? kRel[jk][0] + kRel[jk][1] * TX + kRel[jk][2] * TXY : 0;
-        uint32_t w[4];
+        // relative_coordinates (c3_hlac.cpp:180-201), arithmetically: k <= 8 -> (k/3-1, k%3-1, -1),
+        // k = 9..11 -> (k-10, -1, 0), k = 12 -> (-1, 0, 0); 13, 14 = centre / ones columns
+        const int rdx = jk <= 8 ? jk / 3 - 1 : (jk <= 11 ? jk - 10 : -1);
+        const int rdy = jk <= 8 ? jk % 3 - 1 : (jk <= 11 ? -1 : 0);
+        const int rdz = jk <= 8 ? -1 : 0;
+        const int delta = jk < 13 ? rdx + rdy * TX + rdz * TXY : 0;
+        // every LDS read unconditional (indices clamped, results masked) so the 4 list,
+        // 4 tile and 12 LUT reads issue as three back-to-back batches
+        uint32_t li[4], w[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) li[j] = s_list[min(c0 + jg * 4 + j, nlist - 1)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = s_tile[li[j] + delta];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = (c0 + jg * 4 + j < nlist) ? w[j] : 0u;
+        uint32_t lr[4], lg[4], lb[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int e = c0 + jg * 4 + j;
-          w[j] = e < nlist ? s_tile[s_list[e] + delta] : 0u;
+          lr[j] = s_lut[(w[j] >> 16) & 0xffu];
+          lg[j] = s_lut[(w[j] >> 8) & 0xffu];
+          lb[j] = s_lut[w[j] & 0xffu];
         }
         uint32_t nb[6] = {0, 0, 0, 0, 0, 0}, bb[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int sh = 8 * j;
           const uint32_t occ = w[j] ? 1u : 0u;
+          const uint32_t m8 = occ ? 0xffu : 0u;
           if (jk == 14) {  // the ones column: occupancy in every channel
 #pragma unroll
             for (int n = 0; n < 6; ++n) {
@@ -487,13 +499,12 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs ka) {
             }
           } else {
             const uint32_t r = (w[j] >> 16) & 0xffu, g = (w[j] >> 8) & 0xffu, b = w[j] & 0xffu;
-            const uint32_t lr = occ ? s_lut[r] : 0u, lg = occ ? s_lut[g] : 0u, lb = occ ? s_lut[b] : 0u;
-            nb[0] |= (lr & 0xffu) << sh;
-            nb[1] |= (lr >> 8) << sh;
-            nb[2] |= (lg & 0xffu) << sh;
-            nb[3] |= (lg >> 8) << sh;
-            nb[4] |= (lb & 0xffu) << sh;
-            nb[5] |= (lb >> 8) << sh;
+            nb[0] |= (lr[j] & m8) << sh;
+            nb[1] |= ((lr[j] >> 8) & m8) << sh;
+            nb[2] |= (lg[j] & m8) << sh;
+            nb[3] |= ((lg[j] >> 8) & m8) << sh;
+            nb[4] |= (lb[j] & m8) << sh;
+            nb[5] |= ((lb[j] >> 8) & m8) << sh;
             const uint32_t br = (int)r > a.thr_r, bgn = (int)g > a.thr_g, bbl = (int)b > a.thr_b;
             bb[0] |= (occ & br) << sh;
             bb[1] |= (occ & (br ^ 1u)) << sh;
@@ -511,6 +522,7 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs ka) {
         }
       }
       lds_barrier();
+      C3H_PROF(2, c0 == 0 && wi == (int)blockIdx.x - a.zblocks);
       // 4. exact integer accumulation: acc[c] += sum_g dot4(A_c[g], N_{k,n}[g])
       if (tid < 180) {
         const int ng = (min(nlist - c0, kChunk) + 3) >> 2;
@@ -538,18 +550,20 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs ka) {
     if (a.atomic) {
       for (int i = tid; i < 981; i += kBlock) {
         const uint32_t v = s_hist[i];
-        if (v) atomicAdd(&a.acc64[h * 981 + i], (unsigned long long)v);
+        if (v) atomicAdd(&facc[h * 981 + i], (unsigned long long)v);
       }
     } else {
-      float* out = a.feat + h * F;
+      float* out = ffeat + h * F;
       if (F == 981) {
         for (int i = tid; i < 981; i += kBlock) out[i] = (float)s_hist[i] * norm981(i);
       } else {
         for (int i = tid; i < 117; i += kBlock) out[i] = (float)fold117(s_hist, i) * norm117(i);
       }
-      if (tid == 0) a.exist[h] = exist_from((float)s_hist[0], (float)s_hist[1]);
+      if (tid == 0) fexist[h] = exist_from((float)s_hist[0], (float)s_hist[1]);
     }
-    if (a.rows && tid == 0) a.rows[atomicAdd(&a.rowcnt[a.epoch & 1], 1u)] = (int32_t)h;
+    // direct mode: tile == subdivision and the work list is dense, so the row list of
+    // the sparse compress is the work list in subdivision terms (count = work count)
+    if (frows && tid == 0) frows[wi] = (int32_t)h;
     lds_barrier();  // LDS is reused by the next tile
     C3H_PROF(6, wi == (int)blockIdx.x - a.zblocks);
   }
@@ -614,9 +628,9 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
   const int64_t nvox = (int64_t)l.gx * l.gy * l.gz;
   const bool vec = (l.gx & 3) == 0;
   const int64_t items = vec ? nvox / 4 : nvox;
-  // HBM-bound: ~3-4 resident workgroups per CU keep enough bytes in flight (128 B per
-  // lane); a smaller grid leaves CU slots to the latency-bound stages of other frames
-  int occ_cap = 1024;
+  // HBM-bound: bytes in flight, not workgroups, set the rate; 256 B per lane lets few
+  // workgroups (CU slots) cover the latency, leaving the rest to the other stages
+  int occ_cap = 256;  // per frame: ~16 MB in flight at 64 KB per workgroup
   if (const char* g = getenv("C3H_OCC_GRID")) occ_cap = std::max(1, atoi(g));  // diagnostics
   int g1 = (int)std::min<int64_t>((items + kBlock * kOccUnroll - 1) / (kBlock * kOccUnroll), occ_cap);
   if (g1 < 1) g1 = 1;
@@ -674,7 +688,6 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
   a.work = l.work;
   a.workcnt = l.tf + 2;
   a.rows = l.rows;
-  a.rowcnt = l.tf;
   a.epoch = l.epoch;
   a.zblocks = l.zero_empty ? (int)std::min<int64_t>(64, l.ntiles) : 0;
   a.ntiles = (int)l.ntiles;

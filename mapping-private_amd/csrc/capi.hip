@@ -479,7 +479,7 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
     c3h::SparseCompress sc{};
     if (sparse_g) {
       sc = c3h::SparseCompress{ctx->feat.p, ctx->axis_pt.p, ctx->fmax.p, ctx->G.p, ctx->rows.p,
-                               ctx->tileflags.p + (ctx->tile_epoch & 1), ctx->F, ctx->D, ctx->Dpad,
+                               ctx->tileflags.p + 2 + (ctx->tile_epoch & 1), ctx->F, ctx->D, ctx->Dpad,
                                ctx->fmax_len, H, H * ctx->F, H * ctx->D, H, ctx->tf_stride};
       ctx->g_valid = true;
       ctx->g_sparse = true;
@@ -934,7 +934,7 @@ int extract_frames(c3h_ctx* ctx, const uint32_t* const* grids, int nf, const c3h
                             hipMemcpyHostToDevice, ctx->stream));
     }
     Timed t(ctx, 1, nf);  // the whole C3 stage: occupancy pass + tile kernel (+ finalize)
-    // per frame: [2] row-list counters | [2] work-list counters | [ntiles] epoch stamps.
+    // per frame: [2] reserved | [2] work-list counters | [ntiles] epoch stamps.
     // Zeroed only when (re)allocated, when the layout (stride, frame count) changes -- the
     // counters rely on every frame slot seeing every epoch -- or when the epoch wraps
     const int64_t s_tf = ntiles + 4;

@@ -30,9 +30,13 @@ with c3hlac.Context(0) as ctx:
     gptr = np.array([grids[i % 6].data_ptr() for i in range(N)], np.uint64)
     dets = torch.zeros((N, 30), dtype=torch.int64, device=dev)
     import os
-    cases = [(2, 4), (3, 4), (4, 4), (6, 4), (2, 8), (3, 8), (4, 8), (6, 8)]
-    for lanes, batch in cases:
-        tg = og = None
+    cases = [(1, 8, None, None), (1, 1, None, None), (3, 4, None, None), (3, 8, None, None)]
+    for lanes, batch, og, tg in cases:
+        for k, v in (("C3H_TILE_GRID", tg), ("C3H_OCC_GRID", og)):
+            if v:
+                os.environ[k] = v
+            else:
+                os.environ.pop(k, None)
         ctx.set_lanes(lanes)
         ctx.set_batch(batch)
         for rep in range(2):
@@ -43,5 +47,13 @@ with c3hlac.Context(0) as ctx:
             t1 = time.perf_counter()
             torch.cuda.synchronize()
             t2 = time.perf_counter()
-        print("lanes=%d batch=%d host_enqueue_us_per_frame=%.1f total_us_per_frame=%.1f" %
-              (lanes, batch, (t1 - t0) / N * 1e6, (t2 - t0) / N * 1e6), flush=True)
+        print("lanes=%d batch=%d occ=%s tile=%s host_enqueue_us_per_frame=%.1f total_us_per_frame=%.1f" %
+              (lanes, batch, og, tg, (t1 - t0) / N * 1e6, (t2 - t0) / N * 1e6), flush=True)
+        ctx.timing(True)
+        ctx.kernel_times(reset=True)
+        ctx.run_frames(gptr, (G,) * 3, (0, 0, 0), LEAF, 117, (147, 146, 148), 10, (2, 2, 2), 100, True,
+                       dets.data_ptr())
+        kt = ctx.kernel_times(reset=True)
+        ctx.timing(False)
+        print("   per-frame stage us (events; overlapping lanes inflate):",
+              {k: round(v[0] / v[1] * 1e3, 2) for k, v in kt.items() if v[1]}, flush=True)

@@ -3,7 +3,7 @@
 FETCH_SIZE / WRITE_SIZE are in KB per dispatch.  gfx950 correction
 (MI355X_MICROARCH.md, HBM/rocprofv3): FETCH_SIZE reports exactly half of the bytes of a
 wide coalesced streaming read -> x2; WRITE_SIZE is exact for 16-B stores.
-Usage: python tools_pmc_summary.py <pmc_dir> <out.json>"""
+Usage: python tools_pmc_summary.py <pmc_dir> <out.json> [frames_per_dispatch]"""
 import collections
 import csv
 import json
@@ -19,8 +19,9 @@ def per_kernel(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        for k in KERNELS:
-            if k + "(" in r["Kernel_Name"] or k + "<" in r["Kernel_Name"]:
+        name = r["Kernel_Name"]
+        for k in KERNELS:  # exact kernel identifier (gate_kernel is not compress_gate_kernel)
+            if ("::" + k + "(") in name or ("::" + k + "<") in name or name.startswith(k + "("):
                 acc[k].append(float(r["Counter_Value"]))
     return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
 
@@ -37,8 +38,11 @@ def main():
             w = write.get(k, (0.0, 0))[0] * 1024
             out["kernels"][k] = {"fetch_bytes": f, "write_bytes": w, "hbm_bytes": f + w,
                                  "dispatches": max(fetch.get(k, (0, 0))[1], write.get(k, (0, 0))[1])}
+    fpd = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+    out["frames_per_dispatch"] = fpd
     c3 = [out["kernels"][k]["hbm_bytes"] for k in ("c3_occupancy_kernel", "c3hlac_tile_kernel") if k in out["kernels"]]
-    out["c3_stage_hbm_bytes_per_frame"] = sum(c3) if len(c3) == 2 else None
+    out["c3_stage_hbm_bytes_per_dispatch"] = sum(c3) if len(c3) == 2 else None
+    out["c3_stage_hbm_bytes_per_frame"] = sum(c3) / fpd if len(c3) == 2 else None
     json.dump(out, open(sys.argv[2], "w"), indent=1)
     print(json.dumps(out, indent=1))
 
