@@ -114,6 +114,7 @@ struct c3h_ctx {
   c3h::DevBuf<int32_t> rows;        // non-empty subdivisions of the last extract (direct mode)
   bool rows_valid = false;          // rows/epoch describe the current features
   bool g_sparse = false;            // G holds only the listed rows (others stale)
+  bool feat_sparse = false;         // feature rows of empty subdivisions are stale (exist == 0)
   c3h::DevBuf<long long> glist;     // sparse search: gate list
   c3h::DevBuf<uint32_t> gcnt;       // [2] gate-list counters by search epoch parity
   uint32_t search_epoch = 0;
@@ -204,6 +205,7 @@ struct C3Launch {
   int32_t* rows;          // direct mode: non-empty subdivision list output (nullable)
   uint32_t epoch;
   int zero_empty;
+  int zero_feat;          // zero role also zero-fills feature rows (else exist only)
   int64_t ntiles;
   long long* prof;  // diagnostics (C3H_PROF)
   int debug;
@@ -217,7 +219,11 @@ hipError_t launch_c3_finalize(const unsigned long long* acc64, int64_t hist_num,
 // rows/nrows (device): compress only the listed rows (sparse mode), else all H rows
 hipError_t launch_compress(const float* feat, int64_t H, int F, const float* axis_pt, int D,
                            int Dpad, const float* fmax, int fmax_len, float* G,
-                           const int32_t* rows, const uint32_t* nrows, hipStream_t s);
+                           const int32_t* rows, const uint32_t* nrows, const int32_t* exist,
+                           hipStream_t s);
+// dst[h][:] = exist[h] ? src[h][:] : 0 (readback of buffers whose empty rows are stale)
+hipError_t launch_masked_rows(const float* src, const int32_t* exist, int64_t H, int W, float* dst,
+                              hipStream_t s);
 
 struct ScoreLaunch {
   const float* G;

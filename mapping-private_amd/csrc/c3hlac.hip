@@ -154,37 +154,209 @@ struct OccArgs {
   int gx, gy, gz;
   const int16_t* axmap;
   int ns0, ns1;
+  int ntiles;
   uint32_t epoch;
   uint32_t* tf;    // per frame: [2] reserved | [2] work counters | [ntiles] stamps
   int32_t* work;   // per frame: [ntiles]
   int64_t s_tf, s_work;
 };
 
-template <bool kVec>
+// Bitmap variant (every tile one bit of LDS, ntiles <= kOccBitsMax): an occupied centre
+// voxel costs VALU plus one fire-and-forget ds_or, so no LDS round trip sits behind the
+// stream data.  Per chunk the axis lookups are batched: x is fixed per lane whenever gx
+// divides the chunk stride (4 voxels, at most 4 x-segments, looked up once per chunk),
+// the 16 rows' (y, z) segments are looked up together.  The flush compacts the set bits
+// into an LDS list and stamps kBlock tiles at a time, every exchange in flight together.
+constexpr int kOccBitsMax = 1 << 17;  // 16 KB of LDS bits
+constexpr int kOccBitsUnroll = 8;     // 16-B non-temporal loads per lane in flight per chunk
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+constexpr int kAxLds = 3072;  // axis-map entries kept in LDS (gx + gy + gz <= 3072)
+
+// exclusive prefix sum over the workgroup (kBlock threads); total returned in *total
+__device__ __forceinline__ int block_excl_scan(int v, int* s_wsum, int* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_wsum[wid] = x;
+  __syncthreads();
+  int off = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < kBlock / 64; ++i) {
+    const int t = s_wsum[i];
+    off += i < wid ? t : 0;
+    tot += t;
+  }
+  __syncthreads();  // s_wsum is reused by the next scan
+  *total = tot;
+  return off + x - v;
+}
+
+__device__ __forceinline__ void occ_flush_bits(const uint32_t* s_bits, int nwords, int* s_list,
+                                               int* s_wsum, uint32_t epoch, uint32_t* flags,
+                                               uint32_t* cnt, int32_t* work) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (int w0 = 0; w0 < nwords; w0 += kBlock) {  // one bitmap word per thread per round
+    const int wi = w0 + tid;
+    const uint32_t m = wi < nwords ? s_bits[wi] : 0u;
+    int total;
+    const int base = block_excl_scan(__popc(m), s_wsum, &total);
+    for (int l0 = 0; l0 < total; l0 += kOccSet) {  // list slices of kOccSet tiles
+      uint32_t mm = m;
+      for (int idx = base; mm; ++idx) {
+        const int bit = __ffs(mm) - 1;
+        mm &= mm - 1;
+        if (idx >= l0 && idx < l0 + kOccSet) s_list[idx - l0] = wi * 32 + bit;
+      }
+      __syncthreads();
+      const int nl = min(total - l0, kOccSet);
+      int ts[kOccSet / kBlock];
+      bool fresh[kOccSet / kBlock];
+#pragma unroll
+      for (int j = 0; j < kOccSet / kBlock; ++j) {  // all exchanges in flight together
+        const int e = tid + j * kBlock;
+        ts[j] = e < nl ? s_list[e] : -1;
+        fresh[j] = ts[j] >= 0 && atomicExch(&flags[ts[j]], epoch) != epoch;
+      }
+#pragma unroll
+      for (int j = 0; j < kOccSet / kBlock; ++j) {
+        const unsigned long long b = __ballot(fresh[j]);
+        if (b) {
+          uint32_t b0 = 0;
+          if (lane == 0) b0 = atomicAdd(cnt, (uint32_t)__popcll(b));
+          b0 = __shfl(b0, 0, 64);
+          if (fresh[j]) work[b0 + __popcll(b & ((1ull << lane) - 1))] = ts[j];
+        }
+      }
+      __syncthreads();  // s_list is refilled by the next slice
+    }
+  }
+}
+
+template <bool kAx>
+__global__ __launch_bounds__(kBlock) void c3_occupancy_bits_kernel(OccArgs oa) {
+  const int f = blockIdx.y;
+  const uint32_t* __restrict__ grid = oa.grid[f];
+  const int gx = oa.gx, gy = oa.gy, gz = oa.gz;
+  const int ns0 = oa.ns0, ns1 = oa.ns1;
+  const uint32_t epoch = oa.epoch;
+  uint32_t* __restrict__ flags = oa.tf + f * oa.s_tf + 4;
+  uint32_t* __restrict__ cnt = oa.tf + f * oa.s_tf + 2 + (epoch & 1);
+  int32_t* __restrict__ work = oa.work + f * oa.s_work;
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_bits[];  // ceil(ntiles / 32)
+  __shared__ int s_list[kOccSet];
+  __shared__ int s_wsum[kBlock / 64];
+  __shared__ int16_t s_ax[kAx ? kAxLds : 1];
+  const int tid = threadIdx.x;
+  const int nwords = (oa.ntiles + 31) >> 5;
+  const int16_t* mx = kAx ? s_ax : oa.axmap;
+  const int16_t* my = mx + gx;
+  const int16_t* mz = my + gy;
+  for (int i = tid; i < nwords; i += kBlock) s_bits[i] = 0u;
+  if (kAx)
+    for (int i = tid; i < gx + gy + gz; i += kBlock) s_ax[i] = oa.axmap[i];
+  __syncthreads();
+  const int64_t n4 = ((int64_t)gx * gy * gz) >> 2;
+  const uint4* g4 = reinterpret_cast<const uint4*>(grid);
+  constexpr int kChunk4 = kBlock * kOccBitsUnroll;
+  // consecutive j of one thread are kBlock*4 voxels apart: step (x, y, z) incrementally
+  const int dxs = (kBlock * 4) % gx, drs = (kBlock * 4) / gx;
+  int last = -1;
+  for (int64_t c0 = blockIdx.x * (int64_t)kChunk4; c0 < n4; c0 += (int64_t)gridDim.x * kChunk4) {
+    uint4 w[kOccBitsUnroll];
+#pragma unroll
+    for (int j = 0; j < kOccBitsUnroll; ++j) {  // all loads first: bytes in flight, not latency
+      const int64_t i = c0 + j * kBlock + tid;
+      // non-temporal: the grid is read once here (the tile pass re-reads only the few
+      // occupied tiles' halos); measured 6.9-7.0 TB/s vs 6.0-6.3 for default-policy loads
+      const v4u t = i < n4 ? __builtin_nontemporal_load(reinterpret_cast<const v4u*>(g4) + i) : v4u{0, 0, 0, 0};
+      w[j] = make_uint4(t.x, t.y, t.z, t.w);
+    }
+    const uint32_t v0 = (uint32_t)((c0 + tid) << 2);  // nvox < 2^32 (host-checked)
+    const uint32_t row0 = v0 / (uint32_t)gx;
+    int x = (int)(v0 - row0 * (uint32_t)gx);
+    int y = (int)(row0 % (uint32_t)gy), z = (int)(row0 / (uint32_t)gy);
+    // the rows' (y, z) segments of all j, looked up together (clamped past the grid end)
+    int tyz[kOccBitsUnroll];
+    int txj[kOccBitsUnroll];  // x of row j (differs per j only when dxs != 0)
+#pragma unroll
+    for (int j = 0; j < kOccBitsUnroll; ++j) {
+      const int ty = my[y], tz = mz[min(z, gz - 1)];
+      tyz[j] = (ty >= 0 && tz >= 0 && z < gz) ? ns0 * (ty + ns1 * tz) : -1;
+      txj[j] = x;
+      x += dxs;
+      int dy = drs;
+      if (x >= gx) {
+        x -= gx;
+        ++dy;
+      }
+      y += dy;
+      while (y >= gy) {
+        y -= gy;
+        ++z;
+      }
+    }
+    int tx0[4];
+    if (dxs == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) tx0[k] = mx[txj[0] + k];
+    }
+#pragma unroll
+    for (int j = 0; j < kOccBitsUnroll; ++j) {
+      const uint32_t ws[4] = {w[j].x, w[j].y, w[j].z, w[j].w};
+      if ((ws[0] | ws[1] | ws[2] | ws[3]) == 0 || tyz[j] < 0) continue;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (!ws[k]) continue;
+        const int tx = dxs == 0 ? tx0[k] : mx[txj[j] + k];
+        if (tx < 0) continue;
+        const int t = tx + tyz[j];
+        if (t == last) continue;
+        last = t;
+        atomicOr(&s_bits[t >> 5], 1u << (t & 31));  // result unused: ds_or_b32, no wait
+      }
+    }
+  }
+  __syncthreads();
+  occ_flush_bits(s_bits, nwords, s_list, s_wsum, epoch, flags, cnt, work);
+}
+
+
+
+// kAx: the axis map lives in LDS, so the per-voxel tile lookup is LDS-only (no global
+// load in the chain behind the stream data)
+template <bool kVec, bool kAx>
 __global__ __launch_bounds__(kBlock) void c3_occupancy_kernel(OccArgs oa) {
   const int f = blockIdx.y;
   const uint32_t* __restrict__ grid = oa.grid[f];
   const int gx = oa.gx, gy = oa.gy, gz = oa.gz;
-  const int16_t* __restrict__ axmap = oa.axmap;
   const int ns0 = oa.ns0, ns1 = oa.ns1;
   const uint32_t epoch = oa.epoch;
   uint32_t* __restrict__ flags = oa.tf + f * oa.s_tf + 4;
   uint32_t* __restrict__ cnt = oa.tf + f * oa.s_tf + 2;
   int32_t* __restrict__ work = oa.work + f * oa.s_work;
   __shared__ int s_set[kOccSet];
+  __shared__ int16_t s_ax[kAx ? kAxLds : 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const int64_t nvox = (int64_t)gx * gy * gz;
-  const int16_t* mx = axmap;
-  const int16_t* my = axmap + gx;
-  const int16_t* mz = axmap + gx + gy;
+  const int16_t* mx = kAx ? s_ax : oa.axmap;
+  const int16_t* my = mx + gx;
+  const int16_t* mz = my + gy;
   cnt += epoch & 1;
   for (int i = tid; i < kOccSet; i += kBlock) s_set[i] = -1;
+  if (kAx)
+    for (int i = tid; i < gx + gy + gz; i += kBlock) s_ax[i] = oa.axmap[i];
   __syncthreads();
   int last = -1;
   if (kVec) {
     const int64_t n4 = nvox >> 2;
     const uint4* g4 = reinterpret_cast<const uint4*>(grid);
     constexpr int kChunk4 = kBlock * kOccUnroll;
+    // consecutive j of one thread are kBlock*4 voxels apart: step (x, y, z) incrementally
+    const int dxs = (kBlock * 4) % gx, drs = (kBlock * 4) / gx;
     for (int64_t c0 = blockIdx.x * (int64_t)kChunk4; c0 < n4; c0 += (int64_t)gridDim.x * kChunk4) {
       uint4 w[kOccUnroll];
 #pragma unroll
@@ -192,25 +364,39 @@ __global__ __launch_bounds__(kBlock) void c3_occupancy_kernel(OccArgs oa) {
         const int64_t i = c0 + j * kBlock + tid;
         w[j] = i < n4 ? g4[i] : make_uint4(0, 0, 0, 0);
       }
+      const uint32_t v0 = (uint32_t)((c0 + tid) << 2);  // nvox < 2^32 (host-checked)
+      const uint32_t row0 = v0 / (uint32_t)gx;
+      int x = (int)(v0 - row0 * (uint32_t)gx);
+      int y = (int)(row0 % (uint32_t)gy), z = (int)(row0 / (uint32_t)gy);
 #pragma unroll
       for (int j = 0; j < kOccUnroll; ++j) {
-        if ((w[j].x | w[j].y | w[j].z | w[j].w) == 0) continue;
-        const uint32_t v = (uint32_t)((c0 + j * kBlock + tid) << 2);  // nvox < 2^32 (host-checked)
-        const uint32_t row = v / (uint32_t)gx;
-        const int x = (int)(v - row * (uint32_t)gx);
-        const int y = (int)(row % (uint32_t)gy), z = (int)(row / (uint32_t)gy);
-        const int ty = my[y], tz = mz[z];
-        if (ty < 0 || tz < 0) continue;
-        const uint32_t ws[4] = {w[j].x, w[j].y, w[j].z, w[j].w};
+        if ((w[j].x | w[j].y | w[j].z | w[j].w) != 0) {
+          const int ty = my[y], tz = z < gz ? mz[z] : -1;
+          if (ty >= 0 && tz >= 0) {
+            const int tyz = ns0 * (ty + ns1 * tz);
+            const uint32_t ws[4] = {w[j].x, w[j].y, w[j].z, w[j].w};
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (!ws[k]) continue;
-          const int tx = mx[x + k];
-          if (tx < 0) continue;
-          const int t = tx + ns0 * (ty + ns1 * tz);
-          if (t == last) continue;
-          last = t;
-          set_insert(s_set, t, epoch, flags, cnt, work);
+            for (int k = 0; k < 4; ++k) {
+              if (!ws[k]) continue;
+              const int tx = mx[x + k];
+              if (tx < 0) continue;
+              const int t = tx + tyz;
+              if (t == last) continue;
+              last = t;
+              set_insert(s_set, t, epoch, flags, cnt, work);
+            }
+          }
+        }
+        x += dxs;
+        int dy = drs;
+        if (x >= gx) {
+          x -= gx;
+          ++dy;
+        }
+        y += dy;
+        while (y >= gy) {
+          y -= gy;
+          ++z;
         }
       }
     }
@@ -272,6 +458,7 @@ struct KArgs {
   int32_t* rows;          // direct mode: non-empty subdivisions of this frame (nullable)
   uint32_t epoch;
   int ntiles;
+  int zero_feat;          // zero role writes feature rows too (else exist only)
   int zblocks;            // leading workgroups that zero the rows of unstamped tiles
                           // (direct mode, every subdivision one tile: h == tile), else 0
   long long* prof;  // diagnostics only (C3H_PROF): per-block phase timestamps [grid][8]
@@ -318,8 +505,14 @@ __global__ __launch_bounds__(kBlock) void c3hlac_tile_kernel(KArgs a) {
     fworkcnt[(a.epoch + 1) & 1] = 0;
   }
   if ((int)blockIdx.x < a.zblocks) {
-    // zero role (direct mode, every subdivision one tile: h == tile): rows of the tiles
-    // pass 1 left unstamped, one wave-wide store per 64 floats
+    // zero role (direct mode, every subdivision one tile: h == tile): exist of the tiles
+    // pass 1 left unstamped (their feature rows stay stale unless zero_feat)
+    if (!a.zero_feat) {
+      for (int t = (int)blockIdx.x * kBlock + tid; t < a.ntiles; t += a.zblocks * kBlock)
+        if (fflags[t] != a.epoch) fexist[t] = 0;
+      return;
+    }
+    // rows too, one wave-wide store per 64 floats
     for (int t0 = (int)blockIdx.x * kBlock; t0 < a.ntiles; t0 += a.zblocks * kBlock) {
       const int t = t0 + tid;
       unsigned long long m = __ballot(t < a.ntiles && fflags[t] != a.epoch);
@@ -632,7 +825,9 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
   // workgroups (CU slots) cover the latency, leaving the rest to the other stages
   int occ_cap = 256;  // per frame: ~16 MB in flight at 64 KB per workgroup
   if (const char* g = getenv("C3H_OCC_GRID")) occ_cap = std::max(1, atoi(g));  // diagnostics
-  int g1 = (int)std::min<int64_t>((items + kBlock * kOccUnroll - 1) / (kBlock * kOccUnroll), occ_cap);
+  const bool bits = vec && l.ntiles <= kOccBitsMax;
+  const int unroll = bits ? kOccBitsUnroll : kOccUnroll;
+  int g1 = (int)std::min<int64_t>((items + kBlock * unroll - 1) / (kBlock * unroll), occ_cap);
   if (g1 < 1) g1 = 1;
   if (l.nframes < 1 || l.nframes > kMaxBatch) return hipErrorInvalidValue;
   OccArgs oa;
@@ -649,10 +844,22 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
   oa.s_tf = l.s_tf;
   oa.s_work = l.s_work;
   const dim3 g1d((unsigned)g1, (unsigned)l.nframes);
-  if (vec)
-    c3_occupancy_kernel<true><<<g1d, kBlock, 0, s>>>(oa);
+  const bool ax = l.gx + l.gy + l.gz <= kAxLds;
+  oa.ntiles = (int)l.ntiles;
+  if (bits) {
+    const size_t lds = sizeof(uint32_t) * (size_t)((l.ntiles + 31) / 32);
+    if (ax)
+      c3_occupancy_bits_kernel<true><<<g1d, kBlock, lds, s>>>(oa);
+    else
+      c3_occupancy_bits_kernel<false><<<g1d, kBlock, lds, s>>>(oa);
+  } else if (vec && ax)
+    c3_occupancy_kernel<true, true><<<g1d, kBlock, 0, s>>>(oa);
+  else if (vec)
+    c3_occupancy_kernel<true, false><<<g1d, kBlock, 0, s>>>(oa);
+  else if (ax)
+    c3_occupancy_kernel<false, true><<<g1d, kBlock, 0, s>>>(oa);
   else
-    c3_occupancy_kernel<false><<<g1d, kBlock, 0, s>>>(oa);
+    c3_occupancy_kernel<false, false><<<g1d, kBlock, 0, s>>>(oa);
   KArgs a;
   for (int f = 0; f < kMaxBatch; ++f) a.grids[f] = f < l.nframes ? l.grid[f] : nullptr;
   a.s_feat = l.s_feat;
@@ -674,6 +881,7 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
   const int tx_max = ((l.lmax[0] + 2) + 3 + 3) & ~3;
   a.tw_max = tx_max * (l.lmax[1] + 2) * (l.lmax[2] + 1);
   a.list_max = l.lmax[0] * l.lmax[1] * l.lmax[2];
+  a.zero_feat = l.zero_feat;
   a.thr_r = l.thr[0];
   a.thr_g = l.thr[1];
   a.thr_b = l.thr[2];

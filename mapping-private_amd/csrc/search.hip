@@ -30,7 +30,8 @@ constexpr int kCM = 64, kCN = 128, kCK = 128, kCT = 512, kCW = 16;
 __global__ __launch_bounds__(kCT) void compress_kernel(
     const float* __restrict__ feat, int64_t H, int F, const float* __restrict__ PT, int D,
     int Dpad, const float* __restrict__ fmax, int fmax_len, float* __restrict__ G,
-    const int32_t* __restrict__ rows, const uint32_t* __restrict__ nrows) {
+    const int32_t* __restrict__ rows, const uint32_t* __restrict__ nrows,
+    const int32_t* __restrict__ exist) {
   __shared__ float fs[kCK * (kCM + 1)];
   __shared__ int64_t s_row[kCM];
   const int tid = threadIdx.x;
@@ -56,7 +57,9 @@ __global__ __launch_bounds__(kCT) void compress_kernel(
       const int64_t hh = s_row[r];
       const int jj = j0 + c;
       float v = 0.0f;
-      if (hh >= 0) {
+      // exist gate (sparse features: rows of empty subdivisions are stale, their true
+      // value is 0, which is what an ungated zero row would give)
+      if (hh >= 0 && (!exist || exist[hh])) {
         v = feat[hh * F + jj];
         if (jj < fmax_len) {  // SearchObj::setData histogram normalisation (search.cpp:563-570)
           const float mx = fmax[jj];
@@ -99,6 +102,7 @@ __global__ __launch_bounds__(kCT) void compress_kernel(
 // load's latency is exposed; thread = (row, 8 columns); the fma chain per output runs
 // in ascending j exactly like compress_kernel, so both paths give identical G rows.
 constexpr int kRR = 16, kRK = 32;
+constexpr int kCompressGridCap = 128;  // row-block workgroups per frame of the fused launch
 
 struct CompressRows {
   const float* feat;
@@ -111,9 +115,8 @@ struct CompressRows {
   int64_t s_feat, s_G, s_rows, s_nrows;  // per-frame strides (frame = launch y / z index)
 };
 
-__device__ __forceinline__ void compress_rows_body(const CompressRows& cr, int bid, int64_t f) {
+__device__ __forceinline__ void compress_rows_body(const CompressRows& cr, int bid, int nblk, int64_t f) {
   const float* __restrict__ feat = cr.feat + f * cr.s_feat;
-  const float* __restrict__ PT = cr.PT;
   const float* __restrict__ fmax = cr.fmax;
   float* __restrict__ G = cr.G + f * cr.s_G;
   const int32_t* __restrict__ rows = cr.rows + f * cr.s_rows;
@@ -122,11 +125,8 @@ __device__ __forceinline__ void compress_rows_body(const CompressRows& cr, int b
   float* pc = csm;                 // kRK x Dpad
   float* fs = csm + kRK * Dpad;    // kRR x F
   const int tid = threadIdx.x;
-  const int n = (int)cr.nrows[f * cr.s_nrows];
-  const int r0 = bid * kRR;
-  if (r0 >= n) return;
   const int nq4 = kRK * Dpad / 4, tot4 = F * Dpad / 4;
-  const float4* P4 = reinterpret_cast<const float4*>(PT);
+  const float4* P4 = reinterpret_cast<const float4*>(cr.PT);
   float4 pre[4];
   auto load_chunk = [&](int c) {
 #pragma unroll
@@ -135,64 +135,71 @@ __device__ __forceinline__ void compress_rows_body(const CompressRows& cr, int b
       pre[j] = (e < nq4 && g < tot4) ? P4[g] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
+  // P's first chunk is independent of the row count: in flight before the count arrives
   load_chunk(0);
-  for (int e = tid; e < kRR * F; e += kBlock) {
-    const int r = e / F, j = e - r * F;
-    float v = 0.0f;
-    if (r0 + r < n) {
-      v = feat[(int64_t)rows[r0 + r] * F + j];
-      if (j < fmax_len) {  // setData max-normalisation (search.cpp:563-570)
-        const float mx = fmax[j];
-        if (mx == 0.0f) v = 0.0f;
-        else if (v == mx) v = 1.0f;
-        else v = __fdiv_rn(v, mx);
-      }
-    }
-    fs[e] = v;
-  }
+  const int n = (int)cr.nrows[f * cr.s_nrows];
   const int row = tid >> 4, cg = tid & 15;
   const bool active = 8 * cg < Dpad;
-  float acc[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) acc[q] = 0.0f;
   const int nch = (F + kRK - 1) / kRK;
-  for (int c = 0; c < nch; ++c) {
-    lds_barrier();
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int e = tid + j * kBlock;
-      if (e < nq4) reinterpret_cast<float4*>(pc)[e] = pre[j];
+  // row blocks bid, bid + nblk, ... (the launch holds few workgroups; dense scenes loop)
+  for (int r0 = bid * kRR; r0 < n; r0 += nblk * kRR) {
+    if (r0 != bid * kRR) load_chunk(0);
+    for (int e = tid; e < kRR * F; e += kBlock) {
+      const int r = e / F, j = e - r * F;
+      float v = 0.0f;
+      if (r0 + r < n) {
+        v = feat[(int64_t)rows[r0 + r] * F + j];
+        if (j < fmax_len) {  // setData max-normalisation (search.cpp:563-570)
+          const float mx = fmax[j];
+          if (mx == 0.0f) v = 0.0f;
+          else if (v == mx) v = 1.0f;
+          else v = __fdiv_rn(v, mx);
+        }
+      }
+      fs[e] = v;
     }
-    if (c + 1 < nch) load_chunk(c + 1);
-    lds_barrier();
-    if (active) {
-      const int kn = min(kRK, F - c * kRK);
-      const float* fr = fs + row * F + c * kRK;
-      for (int k = 0; k < kn; ++k) {
-        const float fv = fr[k];
-        const float4 p0 = *reinterpret_cast<const float4*>(&pc[k * Dpad + 8 * cg]);
-        const float4 p1 = *reinterpret_cast<const float4*>(&pc[k * Dpad + 8 * cg + 4]);
-        acc[0] = __builtin_fmaf(fv, p0.x, acc[0]);
-        acc[1] = __builtin_fmaf(fv, p0.y, acc[1]);
-        acc[2] = __builtin_fmaf(fv, p0.z, acc[2]);
-        acc[3] = __builtin_fmaf(fv, p0.w, acc[3]);
-        acc[4] = __builtin_fmaf(fv, p1.x, acc[4]);
-        acc[5] = __builtin_fmaf(fv, p1.y, acc[5]);
-        acc[6] = __builtin_fmaf(fv, p1.z, acc[6]);
-        acc[7] = __builtin_fmaf(fv, p1.w, acc[7]);
+    float acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = 0.0f;
+    for (int c = 0; c < nch; ++c) {
+      lds_barrier();
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int e = tid + j * kBlock;
+        if (e < nq4) reinterpret_cast<float4*>(pc)[e] = pre[j];
+      }
+      if (c + 1 < nch) load_chunk(c + 1);
+      lds_barrier();
+      if (active) {
+        const int kn = min(kRK, F - c * kRK);
+        const float* fr = fs + row * F + c * kRK;
+        for (int k = 0; k < kn; ++k) {
+          const float fv = fr[k];
+          const float4 p0 = *reinterpret_cast<const float4*>(&pc[k * Dpad + 8 * cg]);
+          const float4 p1 = *reinterpret_cast<const float4*>(&pc[k * Dpad + 8 * cg + 4]);
+          acc[0] = __builtin_fmaf(fv, p0.x, acc[0]);
+          acc[1] = __builtin_fmaf(fv, p0.y, acc[1]);
+          acc[2] = __builtin_fmaf(fv, p0.z, acc[2]);
+          acc[3] = __builtin_fmaf(fv, p0.w, acc[3]);
+          acc[4] = __builtin_fmaf(fv, p1.x, acc[4]);
+          acc[5] = __builtin_fmaf(fv, p1.y, acc[5]);
+          acc[6] = __builtin_fmaf(fv, p1.z, acc[6]);
+          acc[7] = __builtin_fmaf(fv, p1.w, acc[7]);
+        }
       }
     }
-  }
-  if (active && r0 + row < n) {
-    const int64_t h = rows[r0 + row];
+    if (active && r0 + row < n) {
+      const int64_t h = rows[r0 + row];
 #pragma unroll
-    for (int q = 0; q < 8; ++q)
-      if (8 * cg + q < D) G[h * D + 8 * cg + q] = acc[q];
+      for (int q = 0; q < 8; ++q)
+        if (8 * cg + q < D) G[h * D + 8 * cg + q] = acc[q];
+    }
+    lds_barrier();  // fs / pc are rewritten by the next row block
   }
 }
 
 __global__ __launch_bounds__(kBlock) void compress_rows_kernel(CompressRows cr) {
-  compress_rows_body(cr, blockIdx.x, blockIdx.y);
+  compress_rows_body(cr, blockIdx.x, gridDim.x, blockIdx.y);
 }
 
 // ---------------------------------------------------------------- score
@@ -281,6 +288,7 @@ __global__ __launch_bounds__(kBlock) void score_kernel(ScoreLaunch a, int64_t P)
 // per-model best (score, scan order) so rank-1 searches need no second pass.
 constexpr int kFP = 32;
 constexpr int kOC = 64;  // basis rows per workgroup (whole models)
+constexpr int kScoreGridCap = 128;  // workgroups per (model group, frame) of the score launch
 
 // ---------------------------------------------------------------- sparse search
 // The exist gate passes few positions on surface scenes (a depth camera sees a 2-D
@@ -352,7 +360,7 @@ __global__ __launch_bounds__(kBlock) void gate_kernel(SparseSearch b) {
 // one launch for two independent stages: gate workgroups first, then the sparse compress
 __global__ __launch_bounds__(kBlock) void compress_gate_kernel(CompressRows cr, SparseSearch b, int ngate) {
   if ((int)blockIdx.x < ngate) gate_body(frame_view(b, blockIdx.y), blockIdx.x);
-  else compress_rows_body(cr, blockIdx.x - ngate, blockIdx.y);
+  else compress_rows_body(cr, blockIdx.x - ngate, gridDim.x - ngate, blockIdx.y);
 }
 
 // Rank-1 replay fused into the score launch (search.cpp:464-474 with rank_num == 1:
@@ -428,50 +436,16 @@ __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch b) {
 #define C3H_SPROF(k) \
   if (fprof && threadIdx.x == 0 && blockIdx.y == 0) fprof[blockIdx.x * 8 + (k)] = (long long)wall_clock64()
   C3H_SPROF(0);
-  const int n = (int)fcnt[a.epoch & 1];
-  const int64_t e0 = blockIdx.x * (int64_t)kFP;
-  if (e0 >= n) {
-    if (n == 0 && flists && blockIdx.x == 0 && blockIdx.y == 0) argmax_finalize(a, fpart, flists, fout, 0);  // clean / copy out
-    return;
-  }
+  const int tid = threadIdx.x;
+  // issued together: the list count, this workgroup's first list chunk (speculative: the
+  // list buffer holds P_total entries, entries past the count are ignored) and the
+  // group's basis window, so the count costs no extra round trip
+  const int64_t ptot = a.pstart[a.nmodes];
+  long long en_first = -1;
+  if (tid < kFP) en_first = flist[min((int64_t)blockIdx.x * kFP + tid, ptot - 1)];
   // model group of this workgroup: models [m0, m1), basis rows [m0*r, m1*r) padded to oc
   const int m0 = blockIdx.y * a.mpg, m1 = min(a.M, m0 + a.mpg);
   const int row0 = m0 * a.r, oc = ((m1 - m0) * a.r + 15) & ~15;  // <= kOC
-  float* fT = ssm;                    // D x kFP (k-major box features)
-  float* qw = fT + D * kFP;           // D x oc: this group's whole basis window
-  float* qv = ssm;                    // kFP x (kOC+1), aliases fT/qw after the GEMM
-  const int region = max(D * (kFP + kOC), kFP * (kOC + 1));
-  float* ffv = ssm + region;
-  int* gate = reinterpret_cast<int*>(ffv + kFP);
-  int* hrow = gate + kFP;
-  int* rng = hrow + kFP;                       // packed xr | yr << 10 | zr << 20
-  long long* ent = reinterpret_cast<long long*>(rng + kFP + (kFP & 1));
-  double* bsc = reinterpret_cast<double*>(ent + kFP);  // kFP * mpg
-  const int tid = threadIdx.x;
-  const int xyn = a.xn * a.yn;
-  if (tid < kFP) {
-    const int64_t e = e0 + tid;
-    int ok = 0, h = 0, rr = 0;
-    long long en = -1;
-    if (e < n) {
-      en = flist[e];
-      const int mi = (int)(en >> 40);
-      const int64_t p = en & ((1ll << 40) - 1);
-      const ModeGeom& md = a.md[mi];
-      const int64_t xye = (int64_t)md.xe * md.ye;
-      const int x = (int)(p % md.xe), y = (int)((p / md.xe) % md.ye), z = (int)(p / xye);
-      h = z * xyn + y * a.xn + x;
-      rr = md.xr | (md.yr << 10) | (md.zr << 20);
-      ok = 1;
-    }
-    gate[tid] = ok;
-    hrow[tid] = h;
-    rng[tid] = rr;
-    ent[tid] = en;
-  }
-  // the group's basis window qt[0..D)[row0 .. row0+oc) is loaded into registers now
-  // (after the list entries: vmcnt retires in order) and parked in LDS after the box
-  // sums, so its latency overlaps the exist / G loads
   constexpr int kQW = 160 * kOC / kBlock;  // window floats per lane at the largest D
   float qwv[kQW];
 #pragma unroll
@@ -479,159 +453,200 @@ __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch b) {
     const int e = j * kBlock + tid, d = e / oc, o = e - d * oc;
     qwv[j] = e < D * oc ? a.qt[(int64_t)d * Qs + row0 + o] : 0.0f;
   }
-  lds_barrier();
-  C3H_SPROF(1);
-  {  // box sums in the fixed (dz, dy, dx) order over non-empty rows; lane = position.
-     // Cells go in batches of 4 x (this thread's d4 slots): every load of a batch is in
-     // flight together.  Rows of empty subdivisions read as 0 (their G rows may be stale;
-     // +0 added to a sum that starts at +0 changes nothing).
-    const int pp = tid & (kFP - 1), dg = tid / kFP;
-    constexpr int kDG = kBlock / kFP;  // d4 stride
-    const bool ok = gate[pp];
-    const int h = hrow[pp], rr = rng[pp];
-    const int xr = rr & 1023, yr = (rr >> 10) & 1023, zr = rr >> 20;
-    const int ncell = ok ? xr * yr * zr : 0;
-    const float4* G4 = reinterpret_cast<const float4*>(fG);
-    constexpr int kSlots = 4;  // d4 values per thread handled together (D4 <= 64)
-    float4 s[kSlots];
-#pragma unroll
-    for (int q = 0; q < kSlots; ++q) s[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int d4b = 0; d4b < D4; d4b += kSlots * kDG) {
-      for (int c0 = 0; c0 < ncell; c0 += 4) {
-        float4 g[4][kSlots];
-        bool lv[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int c = c0 + k;
-          const int dx = c % xr, dy = (c / xr) % yr, dz = c / (xr * yr);
-          const int hh = h + dz * xyn + dy * a.xn + dx;
-          lv[k] = c < ncell && fexist[c < ncell ? hh : h] != 0;
-#pragma unroll
-          for (int q = 0; q < kSlots; ++q) {
-            const int d4 = d4b + dg + q * kDG;
-            g[k][q] = (c < ncell && d4 < D4) ? G4[(int64_t)hh * D4 + d4] : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-          for (int q = 0; q < kSlots; ++q)
-            if (lv[k]) {
-              s[q].x += g[k][q].x;
-              s[q].y += g[k][q].y;
-              s[q].z += g[k][q].z;
-              s[q].w += g[k][q].w;
-            }
-      }
-#pragma unroll
-      for (int q = 0; q < kSlots; ++q) {
-        const int d4 = d4b + dg + q * kDG;
-        if (d4 < D4) {
-          fT[(4 * d4 + 0) * kFP + pp] = s[q].x;
-          fT[(4 * d4 + 1) * kFP + pp] = s[q].y;
-          fT[(4 * d4 + 2) * kFP + pp] = s[q].z;
-          fT[(4 * d4 + 3) * kFP + pp] = s[q].w;
-        }
-        s[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-    }
+  const int n = (int)fcnt[a.epoch & 1];
+  const int nch = (n + kFP - 1) / kFP;  // list chunks; chunk c -> workgroups c mod gridDim.x
+  if ((int)blockIdx.x >= nch) {
+    if (n == 0 && flists && blockIdx.x == 0 && blockIdx.y == 0) argmax_finalize(a, fpart, flists, fout, 0);  // clean / copy out
+    return;
   }
+  const int fts = max(D * kFP, kFP * (kOC + 1));
+  float* fT = ssm;                    // D x kFP (k-major box features)
+  float* qv = ssm;                    // kFP x (kOC+1), aliases fT after the GEMM
+  float* qw = ssm + fts;              // D x oc: this group's whole basis window
+  float* ffv = qw + D * kOC;
+  int* gate = reinterpret_cast<int*>(ffv + kFP);
+  int* hrow = gate + kFP;
+  int* rng = hrow + kFP;                       // packed xr | yr << 10 | zr << 20
+  long long* ent = reinterpret_cast<long long*>(rng + kFP + (kFP & 1));
+  double* bsc = reinterpret_cast<double*>(ent + kFP);  // kFP * mpg
+  const int xyn = a.xn * a.yn;
 #pragma unroll
-  for (int j = 0; j < kQW; ++j)
+  for (int j = 0; j < kQW; ++j)  // parked once; read by every chunk's GEMM
     if (j * kBlock + tid < D * oc) qw[j * kBlock + tid] = qwv[j];
-  lds_barrier();
-  C3H_SPROF(2);
-  if (tid < kFP) {
-    float s = 0.0f;
-    for (int d = 0; d < D; ++d) s = __builtin_fmaf(fT[d * kFP + tid], fT[d * kFP + tid], s);
-    ffv[tid] = s;
-  }
-  // GEMM: thread (tp, to): positions 2*tp, 2*tp+1; basis rows 4*to .. 4*to+3 of the group
-  const int tp = tid & 15, to = tid >> 4;
-  const bool active = 4 * to < oc;
-  float acc[2][4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[i][q] = 0.0f;
-  if (active) {
-#pragma unroll 4
-    for (int d = 0; d < D; ++d) {
-      const float2 f = *reinterpret_cast<const float2*>(&fT[d * kFP + 2 * tp]);
-      const float4 q = *reinterpret_cast<const float4*>(&qw[d * oc + 4 * to]);
-      acc[0][0] = __builtin_fmaf(f.x, q.x, acc[0][0]);
-      acc[0][1] = __builtin_fmaf(f.x, q.y, acc[0][1]);
-      acc[0][2] = __builtin_fmaf(f.x, q.z, acc[0][2]);
-      acc[0][3] = __builtin_fmaf(f.x, q.w, acc[0][3]);
-      acc[1][0] = __builtin_fmaf(f.y, q.x, acc[1][0]);
-      acc[1][1] = __builtin_fmaf(f.y, q.y, acc[1][1]);
-      acc[1][2] = __builtin_fmaf(f.y, q.z, acc[1][2]);
-      acc[1][3] = __builtin_fmaf(f.y, q.w, acc[1][3]);
+  for (int ch = blockIdx.x; ch < nch; ch += gridDim.x) {
+    const int64_t e0 = (int64_t)ch * kFP;
+    if (tid < kFP) {
+      const int64_t e = e0 + tid;
+      int ok = 0, h = 0, rr = 0;
+      long long en = -1;
+      if (e < n) {
+        en = ch == (int)blockIdx.x ? en_first : flist[e];
+        const int mi = (int)(en >> 40);
+        const int64_t p = en & ((1ll << 40) - 1);
+        const ModeGeom& md = a.md[mi];
+        const int64_t xye = (int64_t)md.xe * md.ye;
+        const int x = (int)(p % md.xe), y = (int)((p / md.xe) % md.ye), z = (int)(p / xye);
+        h = z * xyn + y * a.xn + x;
+        rr = md.xr | (md.yr << 10) | (md.zr << 20);
+        ok = 1;
+      }
+      gate[tid] = ok;
+      hrow[tid] = h;
+      rng[tid] = rr;
+      ent[tid] = en;
     }
-  }
-  lds_barrier();  // qv aliases fT / qw
-  C3H_SPROF(3);
-  if (active) {
+    lds_barrier();
+    C3H_SPROF(1);
+    {  // box sums in the fixed (dz, dy, dx) order over non-empty rows; lane = position.
+       // Cells go in batches of 4 x (this thread's d4 slots): every load of a batch is in
+       // flight together.  Rows of empty subdivisions read as 0 (their G rows may be stale;
+       // +0 added to a sum that starts at +0 changes nothing).
+      const int pp = tid & (kFP - 1), dg = tid / kFP;
+      constexpr int kDG = kBlock / kFP;  // d4 stride
+      const bool ok = gate[pp];
+      const int h = hrow[pp], rr = rng[pp];
+      const int xr = rr & 1023, yr = (rr >> 10) & 1023, zr = rr >> 20;
+      const int ncell = ok ? xr * yr * zr : 0;
+      const float4* G4 = reinterpret_cast<const float4*>(fG);
+      constexpr int kSlots = 4;  // d4 values per thread handled together (D4 <= 64)
+      float4 s[kSlots];
+#pragma unroll
+      for (int q = 0; q < kSlots; ++q) s[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int d4b = 0; d4b < D4; d4b += kSlots * kDG) {
+        for (int c0 = 0; c0 < ncell; c0 += 4) {
+          float4 g[4][kSlots];
+          bool lv[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int c = c0 + k;
+            const int dx = c % xr, dy = (c / xr) % yr, dz = c / (xr * yr);
+            const int hh = h + dz * xyn + dy * a.xn + dx;
+            lv[k] = c < ncell && fexist[c < ncell ? hh : h] != 0;
+#pragma unroll
+            for (int q = 0; q < kSlots; ++q) {
+              const int d4 = d4b + dg + q * kDG;
+              g[k][q] = (c < ncell && d4 < D4) ? G4[(int64_t)hh * D4 + d4] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int q = 0; q < kSlots; ++q)
+              if (lv[k]) {
+                s[q].x += g[k][q].x;
+                s[q].y += g[k][q].y;
+                s[q].z += g[k][q].z;
+                s[q].w += g[k][q].w;
+              }
+        }
+#pragma unroll
+        for (int q = 0; q < kSlots; ++q) {
+          const int d4 = d4b + dg + q * kDG;
+          if (d4 < D4) {
+            fT[(4 * d4 + 0) * kFP + pp] = s[q].x;
+            fT[(4 * d4 + 1) * kFP + pp] = s[q].y;
+            fT[(4 * d4 + 2) * kFP + pp] = s[q].z;
+            fT[(4 * d4 + 3) * kFP + pp] = s[q].w;
+          }
+          s[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+    }
+    lds_barrier();
+    C3H_SPROF(2);
+    if (tid < kFP) {
+      float s = 0.0f;
+      for (int d = 0; d < D; ++d) s = __builtin_fmaf(fT[d * kFP + tid], fT[d * kFP + tid], s);
+      ffv[tid] = s;
+    }
+    // GEMM: thread (tp, to): positions 2*tp, 2*tp+1; basis rows 4*to .. 4*to+3 of the group
+    const int tp = tid & 15, to = tid >> 4;
+    const bool active = 4 * to < oc;
+    float acc[2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) qv[(2 * tp + i) * (kOC + 1) + 4 * to + q] = acc[i][q];
-  }
-  lds_barrier();
-  const int nm = m1 - m0;
-  for (int e = tid; e < kFP * nm; e += kBlock) {
-    const int mm = e / kFP, pp = e - mm * kFP;
-    double sc = -2.0;
-    if (gate[pp]) {
-      float q2 = 0.0f;
-      const float* q = qv + pp * (kOC + 1) + mm * a.r;
-      for (int i = 0; i < a.r; ++i) q2 = __builtin_fmaf(q[i], q[i], q2);
-      sc = sqrt((double)q2) / sqrt((double)ffv[pp]);
-      const long long en = ent[pp];
-      const ModeGeom& md = a.md[(int)(en >> 40)];
-      fscores[md.offset + (int64_t)(m0 + mm) * md.P + (en & ((1ll << 40) - 1))] = sc;
+      for (int q = 0; q < 4; ++q) acc[i][q] = 0.0f;
+    if (active) {
+#pragma unroll 4
+      for (int d = 0; d < D; ++d) {
+        const float2 f = *reinterpret_cast<const float2*>(&fT[d * kFP + 2 * tp]);
+        const float4 q = *reinterpret_cast<const float4*>(&qw[d * oc + 4 * to]);
+        acc[0][0] = __builtin_fmaf(f.x, q.x, acc[0][0]);
+        acc[0][1] = __builtin_fmaf(f.x, q.y, acc[0][1]);
+        acc[0][2] = __builtin_fmaf(f.x, q.z, acc[0][2]);
+        acc[0][3] = __builtin_fmaf(f.x, q.w, acc[0][3]);
+        acc[1][0] = __builtin_fmaf(f.y, q.x, acc[1][0]);
+        acc[1][1] = __builtin_fmaf(f.y, q.y, acc[1][1]);
+        acc[1][2] = __builtin_fmaf(f.y, q.z, acc[1][2]);
+        acc[1][3] = __builtin_fmaf(f.y, q.w, acc[1][3]);
+      }
     }
-    bsc[e] = sc;
-  }
-  C3H_SPROF(4);
-  if (fpart) {
+    lds_barrier();  // qv aliases fT
+    C3H_SPROF(3);
+    if (active) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) qv[(2 * tp + i) * (kOC + 1) + 4 * to + q] = acc[i][q];
+    }
     lds_barrier();
-    for (int mm = tid; mm < nm; mm += kBlock) {  // (score desc, scan order asc)
-      double best = -2.0;
-      long long bo = -1;
-      for (int pp = 0; pp < kFP; ++pp) {
-        if (!gate[pp]) continue;
-        const double sc = bsc[mm * kFP + pp];
+    const int nm = m1 - m0;
+    for (int e = tid; e < kFP * nm; e += kBlock) {
+      const int mm = e / kFP, pp = e - mm * kFP;
+      double sc = -2.0;
+      if (gate[pp]) {
+        float q2 = 0.0f;
+        const float* q = qv + pp * (kOC + 1) + mm * a.r;
+        for (int i = 0; i < a.r; ++i) q2 = __builtin_fmaf(q[i], q[i], q2);
+        sc = sqrt((double)q2) / sqrt((double)ffv[pp]);
         const long long en = ent[pp];
-        const long long o = a.order_base[(int)(en >> 40)] + (en & ((1ll << 40) - 1));
-        if (sc > best || (sc == best && o < bo)) {
-          best = sc;
-          bo = o;
+        const ModeGeom& md = a.md[(int)(en >> 40)];
+        fscores[md.offset + (int64_t)(m0 + mm) * md.P + (en & ((1ll << 40) - 1))] = sc;
+      }
+      bsc[e] = sc;
+    }
+    C3H_SPROF(4);
+    if (fpart) {
+      lds_barrier();
+      for (int mm = tid; mm < nm; mm += kBlock) {  // (score desc, scan order asc)
+        double best = -2.0;
+        long long bo = -1;
+        for (int pp = 0; pp < kFP; ++pp) {
+          if (!gate[pp]) continue;
+          const double sc = bsc[mm * kFP + pp];
+          const long long en = ent[pp];
+          const long long o = a.order_base[(int)(en >> 40)] + (en & ((1ll << 40) - 1));
+          if (sc > best || (sc == best && o < bo)) {
+            best = sc;
+            bo = o;
+          }
+        }
+        ScorePartial* q = fpart + (int64_t)ch * a.M + m0 + mm;
+        if (flists) {  // handed to another workgroup inside this launch: sc1 stores
+          __hip_atomic_store(&q->score, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&q->order, bo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          *q = ScorePartial{best, bo};
         }
       }
-      ScorePartial* q = fpart + (int64_t)blockIdx.x * a.M + m0 + mm;
-      if (flists) {  // handed to another workgroup inside this launch: sc1 stores
-        __hip_atomic_store(&q->score, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&q->order, bo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        *q = ScorePartial{best, bo};
-      }
     }
-    if (flists) {
-      // rank 1, fused replay: the last workgroup to finish reduces.  Hand-off per
-      // MI355X_MICROARCH.md (inter-workgroup visibility, table row 1): sc1 stores, every
-      // storing wave waits vmcnt(0), a barrier, one agent atomic add per workgroup; the
-      // workgroup whose add returns total-1 reads the partials with sc1 loads.
-      __shared__ int s_last;
-      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lds_barrier();
-      if (tid == 0) {
-        const uint32_t total = (uint32_t)((n + kFP - 1) / kFP) * gridDim.y;
-        s_last = atomicAdd(&fdone[a.epoch & 1], 1u) == total - 1;
-      }
-      lds_barrier();
-      if (s_last) argmax_finalize(a, fpart, flists, fout, (n + kFP - 1) / kFP);
+    lds_barrier();  // LDS is reused by the next chunk
+  }
+  if (fpart && flists) {
+    // rank 1, fused replay: the last workgroup to finish reduces.  Hand-off per
+    // MI355X_MICROARCH.md (inter-workgroup visibility, table row 1): sc1 stores, every
+    // storing wave waits vmcnt(0), a barrier, one agent atomic add per workgroup; the
+    // workgroup whose add returns total-1 reads the partials with sc1 loads.
+    __shared__ int s_last;
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    if (tid == 0) {
+      const uint32_t total = (uint32_t)min(nch, (int)gridDim.x) * gridDim.y;
+      s_last = atomicAdd(&fdone[a.epoch & 1], 1u) == total - 1;
     }
+    lds_barrier();
+    if (s_last) argmax_finalize(a, fpart, flists, fout, nch);
   }
   C3H_SPROF(7);
 }
@@ -748,7 +763,8 @@ bool compress_rows_ok(int F, int Dpad) {
 
 hipError_t launch_compress(const float* feat, int64_t H, int F, const float* axis_pt, int D,
                            int Dpad, const float* fmax, int fmax_len, float* G,
-                           const int32_t* rows, const uint32_t* nrows, hipStream_t s) {
+                           const int32_t* rows, const uint32_t* nrows, const int32_t* exist,
+                           hipStream_t s) {
   if (rows && compress_rows_ok(F, Dpad)) {  // sparse list
     const size_t lds = sizeof(float) * ((size_t)kRK * Dpad + (size_t)kRR * F);
     const CompressRows cr{feat, axis_pt, fmax, G, rows, nrows, F, D, Dpad, fmax_len, 0, 0, 0, 0};
@@ -756,7 +772,27 @@ hipError_t launch_compress(const float* feat, int64_t H, int F, const float* axi
     return hipGetLastError();
   }
   dim3 grid((unsigned)((H + kCM - 1) / kCM), (unsigned)((Dpad + kCN - 1) / kCN));
-  compress_kernel<<<grid, kCT, 0, s>>>(feat, H, F, axis_pt, D, Dpad, fmax, fmax_len, G, rows, nrows);
+  compress_kernel<<<grid, kCT, 0, s>>>(feat, H, F, axis_pt, D, Dpad, fmax, fmax_len, G, rows, nrows, exist);
+  return hipGetLastError();
+}
+
+// dst[h][:] = exist[h] ? src[h][:] : 0 (readback of sparse feature / G buffers)
+__global__ __launch_bounds__(kBlock) void masked_rows_kernel(const float* __restrict__ src,
+                                                             const int32_t* __restrict__ exist,
+                                                             int64_t H, int W, float* __restrict__ dst) {
+  const int64_t n = H * W;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const int64_t h = i / W;
+    dst[i] = exist[h] ? src[i] : 0.0f;
+  }
+}
+
+hipError_t launch_masked_rows(const float* src, const int32_t* exist, int64_t H, int W, float* dst,
+                              hipStream_t s) {
+  const int64_t n = H * W;
+  if (n <= 0) return hipSuccess;
+  const unsigned g = (unsigned)std::min<int64_t>((n + kBlock - 1) / kBlock, 4096);
+  masked_rows_kernel<<<g, kBlock, 0, s>>>(src, exist, H, W, dst);
   return hipGetLastError();
 }
 
@@ -796,15 +832,20 @@ hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc,
     const CompressRows cr{sc->feat, sc->PT, sc->fmax, sc->G, sc->rows, sc->nrows, sc->F, sc->D, sc->Dpad,
                           sc->fmax_len, sc->s_feat, sc->s_G, sc->s_rows, sc->s_nrows};
     const size_t lds = sizeof(float) * ((size_t)kRK * sc->Dpad + (size_t)kRR * sc->F);
-    compress_gate_kernel<<<dim3(ngate + (unsigned)((sc->H + kRR - 1) / kRR), nf), kBlock, lds, s>>>(cr, a, (int)ngate);
+    // compress workgroups: surface frames have ~700 non-empty rows (~44 row blocks)
+    const unsigned ncomp = (unsigned)std::min<int64_t>((sc->H + kRR - 1) / kRR, kCompressGridCap);
+    compress_gate_kernel<<<dim3(ngate + ncomp, nf), kBlock, lds, s>>>(cr, a, (int)ngate);
   } else {
     gate_kernel<<<dim3(ngate, nf), kBlock, 0, s>>>(a);
   }
-  const size_t region = std::max((size_t)a.D * (kFP + kOC), (size_t)kFP * (kOC + 1));
+  const size_t region = std::max((size_t)a.D * kFP, (size_t)kFP * (kOC + 1)) + (size_t)a.D * kOC;
   const size_t lds = sizeof(float) * (region + kFP) + sizeof(int) * 4 * kFP + sizeof(long long) * kFP +
                      sizeof(double) * kFP * a.mpg + 16;
   const unsigned groups = (unsigned)((a.M + a.mpg - 1) / a.mpg);
-  score_list_kernel<<<dim3((unsigned)sparse_score_blocks(a), groups, nf), kBlock, lds, s>>>(a);
+  // workgroups per (group, frame): list chunks beyond the cap loop (dense scenes only);
+  // surface frames pass ~1k positions (~30 chunks), so few workgroups exit unused
+  const unsigned gx = (unsigned)std::min<int64_t>(sparse_score_blocks(a), kScoreGridCap);
+  score_list_kernel<<<dim3(gx, groups, nf), kBlock, lds, s>>>(a);
   return hipGetLastError();
 }
 

@@ -6,7 +6,7 @@ import time
 if len(sys.argv) > 1:  # e.g. GPU_MAX_HW_QUEUES=8 (must precede the HIP runtime's start)
     os.environ["GPU_MAX_HW_QUEUES"] = sys.argv[1]
 
-sys.path[:0] = ["mapping-private_amd"]
+sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), "mapping-private_amd")]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import c3hlac  # noqa: E402
@@ -23,6 +23,8 @@ with c3hlac.Context(0) as ctx:
         w = torch.empty(G ** 3, dtype=torch.int32, device=dev)
         ctx.lib.c3h_get_grid(ctx.h, c3hlac.ptr(w), 1)
         grids += [w, torch.roll(w.view(G, G, G), 37, 2).reshape(-1).contiguous()]
+    if os.environ.get("LANES_ZERO"):  # diagnostics: empty frames (pure streaming)
+        grids = [torch.zeros_like(g) for g in grids]
     axis_t, var, axis_q = synth.random_bases(117, 100, 10, 20, seed=synth.BASE_SEED)
     ctx.search_setup(axis_t, var, axis_q)
     ctx.set_rank(1)
@@ -31,6 +33,9 @@ with c3hlac.Context(0) as ctx:
     dets = torch.zeros((N, 30), dtype=torch.int64, device=dev)
     import os
     cases = [(1, 8, None, None), (1, 1, None, None), (3, 4, None, None), (3, 8, None, None)]
+    if os.environ.get("LANES_CASES"):  # "lanes,batch,occ_grid,tile_grid;..." (empty grid = default)
+        cases = [tuple(int(v) if i < 2 else (v or None) for i, v in enumerate(c.split(",")))
+                 for c in os.environ["LANES_CASES"].split(";")]
     for lanes, batch, og, tg in cases:
         for k, v in (("C3H_TILE_GRID", tg), ("C3H_OCC_GRID", og)):
             if v:
