@@ -153,6 +153,11 @@ int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes
 int c3h_set_lanes(c3h_ctx* ctx, int32_t lanes);
 /* Frames per launch in c3h_run_frames (1..8, default 4; the fast search path only). */
 int c3h_set_batch(c3h_ctx* ctx, int32_t frames);
+/* c3h_run_frames scheduling (default 1): 1 = software pipeline on the context stream, one
+ * fused launch per tick running occupancy (batch t) | tile (t-1) | compress+gate (t-2) |
+ * score + rank-1 argmax (t-3); applies to rank 1 on the fast search path without split
+ * subdivisions, other configurations use the lanes.  0 = lanes only. */
+int c3h_set_pipeline(c3h_ctx* ctx, int32_t enable);
 /* compressed features (setData before the summed-volume table): hist_num x D floats */
 int c3h_get_compressed(c3h_ctx* ctx, float* out, int on_device);
 /* per-position similarity of the last search, modes x M x P doubles (-1 = gated out).
@@ -168,18 +173,20 @@ int c3h_pca_read(const char* path, int32_t ascii, float* axis, float* var, float
                  int32_t* has_mean, int32_t max_dim);
 
 /* per-kernel device time (ms) accumulated since the last reset with HIP events on the
- * context stream; slots: 0 voxelize, 1 C3-HLAC, 2 compress, 3 score, 4 rank replay.
+ * context stream; slots: 0 voxelize, 1 C3-HLAC, 2 compress, 3 score, 4 rank replay,
+ * 5 pipeline tick (c3h_run_frames' fused launches: every stage of four batches).
  * counts_out receives the number of frames the timed launches processed per slot (a
  * batched launch of B frames counts B).  Enabling adds event records.
  * enable: 0 = off, 1 = every slot, otherwise a mask of C3H_TIMING_* bits (the slots
  * bracketed by events; fewer events = less perturbation of back-to-back launches). */
-#define C3H_NTIMERS 5
+#define C3H_NTIMERS 6
 #define C3H_TIMING_VOXELIZE 0x2
 #define C3H_TIMING_C3HLAC 0x4
 #define C3H_TIMING_COMPRESS 0x8
 #define C3H_TIMING_SCORE 0x10
 #define C3H_TIMING_REPLAY 0x20
-#define C3H_TIMING_ALL 0x3e
+#define C3H_TIMING_PIPELINE 0x40
+#define C3H_TIMING_ALL 0x7e
 int c3h_timing(c3h_ctx* ctx, int32_t enable);
 int c3h_kernel_times(c3h_ctx* ctx, float* ms_out, int32_t* counts_out, int32_t reset);
 

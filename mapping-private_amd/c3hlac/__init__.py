@@ -196,6 +196,10 @@ class Context:
         """Frames per launch in run_frames (1..8)."""
         self._chk(self.lib.c3h_set_batch(self.h, int(n)), "set_batch")
 
+    def set_pipeline(self, on):
+        """run_frames scheduling: True = pipelined tick launches, False = lanes."""
+        self._chk(self.lib.c3h_set_pipeline(self.h, int(bool(on))), "set_pipeline")
+
     def compressed(self):
         out = np.zeros((self.hist_num, self.D), np.float32)
         self._chk(self.lib.c3h_get_compressed(self.h, ptr(out), 0), "get_compressed")

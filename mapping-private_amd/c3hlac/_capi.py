@@ -19,8 +19,8 @@ ERRORS = {
     -1: "C3H_ERR_ARG", -2: "C3H_ERR_HIP", -3: "C3H_ERR_STATE", -4: "C3H_ERR_NOMEM",
     -5: "C3H_ERR_RANGE", -6: "C3H_ERR_NOTFOUND", -7: "C3H_ERR_FORMAT",
 }
-NTIMERS = 5
-TIMER_NAMES = ("voxelize", "c3hlac", "compress", "score", "replay")
+NTIMERS = 6
+TIMER_NAMES = ("voxelize", "c3hlac", "compress", "score", "replay", "pipeline")
 
 
 class GridInfo(C.Structure):
@@ -69,6 +69,7 @@ _SIGS = {
                                  C.POINTER(ExtractParams), C.POINTER(C.c_int32), C.c_int32, C.c_int32, _P]),
     "c3h_set_lanes": (C.c_int, [_P, C.c_int32]),
     "c3h_set_batch": (C.c_int, [_P, C.c_int32]),
+    "c3h_set_pipeline": (C.c_int, [_P, C.c_int32]),
     "c3h_get_compressed": (C.c_int, [_P, _P, C.c_int]),
     "c3h_get_scores": (C.c_int, [_P, _P, C.POINTER(C.c_int64), C.c_int]),
     "c3h_remove_overlap": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(C.c_int32), _P]),

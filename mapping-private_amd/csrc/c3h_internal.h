@@ -53,104 +53,12 @@ struct Timer {
   std::mutex mu;  // lanes enqueue from their own host threads
   std::vector<TimedPair> pending[C3H_NTIMERS];
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
-  float ms[C3H_NTIMERS] = {0, 0, 0, 0, 0};
-  int count[C3H_NTIMERS] = {0, 0, 0, 0, 0};
+  float ms[C3H_NTIMERS] = {};
+  int count[C3H_NTIMERS] = {};
   uint32_t mask = 0;  // slots being timed
 };
 
 }  // namespace c3h
-
-struct c3h_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  hipStream_t own_stream = nullptr;
-  std::string err;
-
-  // frame lanes of c3h_run_frames: child contexts on their own streams (frames are
-  // independent, so K frames are in flight at once); children time into the parent
-  c3h_ctx* parent = nullptr;
-  std::vector<c3h_ctx*> lanes;
-  std::vector<hipEvent_t> lane_ev;
-  hipEvent_t fork_ev = nullptr;
-  int nlanes = 3;
-  int nbatch = 4;                   // frames per launch in c3h_run_frames
-  // host copy of the search setup, replayed into the lanes
-  uint64_t setup_version = 0;
-  std::vector<float> h_axis_p, h_var, h_axis_q, h_fmax;
-
-  // voxel grid
-  bool have_grid = false;
-  c3h_grid_info info{};
-  c3h::DevBuf<uint32_t> grid;       // owned packed grid
-  const uint32_t* grid_ptr = nullptr;  // the grid in use (owned or bound)
-  c3h::DevBuf<float> pts;           // staging copy of host points
-  c3h::DevBuf<uint32_t> keys, cnt, sr, sg, sb;  // voxel hash table
-  c3h::DevBuf<float> sx, sy, sz;
-  uint64_t table_size = 0;          // power of two
-  c3h::DevBuf<uint32_t> scratch;    // minmax / counters
-  c3h::DevBuf<uint32_t> tmp_u32;    // leaf-layout block sums
-  c3h::DevBuf<int32_t> tmp_i32;     // leaf layout for host copies
-  uint32_t* h_small = nullptr;      // pinned host scratch (64 words)
-  bool table_valid = false;         // hash table matches the grid (voxelize path)
-
-  // features
-  bool have_feat = false;
-  c3h_extract_params last{};
-  int64_t hist_num = 0;
-  int32_t subdiv_b[3] = {0, 0, 0};
-  int feat_dim = 0;
-  c3h::DevBuf<float> feat;
-  c3h::DevBuf<int32_t> exist;
-  c3h::DevBuf<unsigned long long> acc64;
-  c3h::DevBuf<int32_t> segs;        // per-axis tile segment tables
-  c3h::DevBuf<int16_t> axmap;       // per-axis coordinate -> segment (pass-1 tile lookup)
-  std::vector<int16_t> h_axmap;
-  c3h::DevBuf<uint32_t> tileflags;  // [2] reserved | [2] work counters | [ntiles] stamps
-  c3h::DevBuf<int32_t> work;        // non-empty tiles of the last extract
-  uint32_t tile_epoch = 0;
-  int64_t tf_stride = -1;           // tile-stamp layout the counters were zeroed for
-  int tf_frames = 0;
-  int nframes_feat = 1;             // frames of the last extract (frame 0 = the API view)
-  c3h::DevBuf<int32_t> rows;        // non-empty subdivisions of the last extract (direct mode)
-  bool rows_valid = false;          // rows/epoch describe the current features
-  bool g_sparse = false;            // G holds only the listed rows (others stale)
-  bool feat_sparse = false;         // feature rows of empty subdivisions are stale (exist == 0)
-  c3h::DevBuf<long long> glist;     // sparse search: gate list
-  c3h::DevBuf<uint32_t> gcnt;       // [2] gate-list counters by search epoch parity
-  uint32_t search_epoch = 0;
-  int gcnt_frames = 0;
-  c3h::DevBuf<long long> prof;      // diagnostics (C3H_PROF)
-
-  std::vector<int32_t> h_segs;      // host copy (kept alive for the async upload)
-  c3h::DevBuf<uint32_t> lut;        // 256 packed (sin | cos<<8), two variants
-  bool lut_ready = false;
-
-  // search
-  bool have_setup = false;
-  int D = 0, F = 0, M = 0, r = 0, Dpad = 0;
-  bool compress = true;
-  c3h::DevBuf<float> axis_pt;       // F x Dpad (transposed, whitened)
-  c3h::DevBuf<float> axis_q;        // M x r x D
-  c3h::DevBuf<float> fmax;
-  int fmax_len = 0;
-  c3h::DevBuf<float> G;             // hist_num x D compressed features
-  bool g_valid = false;
-  c3h::DevBuf<double> scores;
-  int64_t scores_n = 0;
-  c3h::DevBuf<float> qt;            // D x Opad transposed model basis (fast score path)
-  int Opad = 0;
-  c3h::DevBuf<c3h::ScorePartial> partials;
-  bool pending_clean = false;       // cleanMax requested while the device lists are current
-  int rank = 1;
-  c3h::SearchLists lists;
-  std::vector<c3h_det> h_lists;     // host staging of the lists
-  c3h::DevBuf<c3h_det> d_lists;
-  bool lists_host_valid = true;     // host lists are current
-  bool lists_dev_valid = false;     // device lists are current
-  int32_t last_range[3] = {0, 0, 0};
-
-  c3h::Timer timer;
-};
 
 namespace c3h {
 
@@ -306,7 +214,119 @@ hipError_t launch_replay(const double* scores, const ReplayModes& modes, int M, 
                          hipStream_t s);
 
 hipError_t launch_clean_lists(c3h_det* lists, int n, hipStream_t s);
+
+// one pipeline tick of c3h_run_frames (pipeline.hip): every role nullable
+struct TickParts {
+  const C3Launch* occ = nullptr;        // batch t: occupancy stream
+  const C3Launch* tile = nullptr;       // batch t-1: C3 tile pass
+  const SparseSearch* gate = nullptr;   // batch t-2: exist gate ...
+  const SparseCompress* comp = nullptr; //   ... + sparse compress
+  const SparseSearch* score = nullptr;  // batch t-3: list scoring + rank-1 argmax
+};
+bool tick_ok(const C3Launch& l);  // the C3 launch fits the tick's roles
+hipError_t launch_tick(const TickParts& p, hipStream_t s);
 size_t c3hlac_lds_bytes(int tw_max, int list_max);
 int64_t leaf_layout_blocks(int64_t nvox);
 
 }  // namespace c3h
+
+struct c3h_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t own_stream = nullptr;
+  std::string err;
+
+  // frame lanes of c3h_run_frames: child contexts on their own streams (frames are
+  // independent, so K frames are in flight at once); children time into the parent
+  c3h_ctx* parent = nullptr;
+  std::vector<c3h_ctx*> lanes;
+  std::vector<hipEvent_t> lane_ev;
+  hipEvent_t fork_ev = nullptr;
+  int nlanes = 3;
+  int nbatch = 4;                   // frames per launch in c3h_run_frames
+  bool pipeline = true;             // c3h_run_frames: pipelined tick launches (else lanes)
+  // host copy of the search setup, replayed into the lanes
+  uint64_t setup_version = 0;
+  std::vector<float> h_axis_p, h_var, h_axis_q, h_fmax;
+
+  // voxel grid
+  bool have_grid = false;
+  c3h_grid_info info{};
+  c3h::DevBuf<uint32_t> grid;       // owned packed grid
+  const uint32_t* grid_ptr = nullptr;  // the grid in use (owned or bound)
+  c3h::DevBuf<float> pts;           // staging copy of host points
+  c3h::DevBuf<uint32_t> keys, cnt, sr, sg, sb;  // voxel hash table
+  c3h::DevBuf<float> sx, sy, sz;
+  uint64_t table_size = 0;          // power of two
+  c3h::DevBuf<uint32_t> scratch;    // minmax / counters
+  c3h::DevBuf<uint32_t> tmp_u32;    // leaf-layout block sums
+  c3h::DevBuf<int32_t> tmp_i32;     // leaf layout for host copies
+  uint32_t* h_small = nullptr;      // pinned host scratch (64 words)
+  bool table_valid = false;         // hash table matches the grid (voxelize path)
+
+  // features
+  bool have_feat = false;
+  c3h_extract_params last{};
+  int64_t hist_num = 0;
+  int32_t subdiv_b[3] = {0, 0, 0};
+  int feat_dim = 0;
+  c3h::DevBuf<float> feat;
+  c3h::DevBuf<int32_t> exist;
+  c3h::DevBuf<unsigned long long> acc64;
+  c3h::DevBuf<int32_t> segs;        // per-axis tile segment tables
+  c3h::DevBuf<int16_t> axmap;       // per-axis coordinate -> segment (pass-1 tile lookup)
+  std::vector<int16_t> h_axmap;
+  c3h::DevBuf<uint32_t> tileflags;  // [2] reserved | [2] work counters | [ntiles] stamps
+  c3h::DevBuf<int32_t> work;        // non-empty tiles of the last extract
+  uint32_t tile_epoch = 0;
+  int64_t tf_stride = -1;           // tile-stamp layout the counters were zeroed for
+  int tf_frames = 0;
+  int nframes_feat = 1;             // frames of the last extract (frame 0 = the API view)
+  c3h::DevBuf<int32_t> rows;        // non-empty subdivisions of the last extract (direct mode)
+  bool rows_valid = false;          // rows/epoch describe the current features
+  bool g_sparse = false;            // G holds only the listed rows (others stale)
+  bool feat_sparse = false;         // feature rows of empty subdivisions are stale (exist == 0)
+  c3h::DevBuf<long long> glist;     // sparse search: gate list
+  c3h::DevBuf<uint32_t> gcnt;       // [2] gate-list counters by search epoch parity
+  uint32_t search_epoch = 0;
+  int gcnt_frames = 0;
+  c3h::DevBuf<long long> prof;      // diagnostics (C3H_PROF)
+
+  std::vector<int32_t> h_segs;      // host copy (kept alive for the async upload)
+  c3h::DevBuf<uint32_t> lut;        // 256 packed (sin | cos<<8), two variants
+  bool lut_ready = false;
+
+  // search
+  bool have_setup = false;
+  int D = 0, F = 0, M = 0, r = 0, Dpad = 0;
+  bool compress = true;
+  c3h::DevBuf<float> axis_pt;       // F x Dpad (transposed, whitened)
+  c3h::DevBuf<float> axis_q;        // M x r x D
+  c3h::DevBuf<float> fmax;
+  int fmax_len = 0;
+  c3h::DevBuf<float> G;             // hist_num x D compressed features
+  bool g_valid = false;
+  c3h::DevBuf<double> scores;
+  int64_t scores_n = 0;
+  c3h::DevBuf<float> qt;            // D x Opad transposed model basis (fast score path)
+  int Opad = 0;
+  c3h::DevBuf<c3h::ScorePartial> partials;
+  bool pending_clean = false;       // cleanMax requested while the device lists are current
+  int rank = 1;
+  c3h::SearchLists lists;
+  std::vector<c3h_det> h_lists;     // host staging of the lists
+  c3h::DevBuf<c3h_det> d_lists;
+  bool lists_host_valid = true;     // host lists are current
+  bool lists_dev_valid = false;     // device lists are current
+  int32_t last_range[3] = {0, 0, 0};
+
+  c3h::Timer timer;
+
+  // capture mode (c3h_run_frames pipeline): extract/search record their launches here
+  // instead of enqueueing them
+  bool capture = false;
+  bool cap_c3_valid = false, cap_search_valid = false, cap_sparse_g = false, cap_argmax = false;
+  c3h::C3Launch cap_c3{};
+  c3h::SparseSearch cap_q{};
+  c3h::SparseCompress cap_sc{};
+};

@@ -73,7 +73,7 @@ struct Timed {
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
   Timed(c3h_ctx* c, int s, int w = 1)
       : ctx(c), T(c->parent ? &c->parent->timer : &c->timer), slot(s), weight(w) {
-    if (!(T->mask >> (s + 1) & 1)) return;
+    if (!(T->mask >> (s + 1) & 1) || c->capture) return;
     std::lock_guard<std::mutex> g(T->mu);
     if (T->pool.empty()) {
       hipEvent_t a, b;
@@ -375,6 +375,7 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
   // sparse compress: only the non-empty rows of the extract's list (the rest stay stale
   // and every consumer gates them on exist)
   const bool sparse_g = !ctx->g_valid && fast && ctx->rows_valid && c3h::compress_rows_ok(ctx->F, ctx->Dpad);
+  if (ctx->capture && !sparse_g) return 0;  // not pipelinable: the caller falls back
   if (!ctx->g_valid && !sparse_g) {  // nf == 1 here
     Timed t(ctx, 2);
     HIPCHK(c3h::launch_compress(ctx->feat.p, H, ctx->F, ctx->axis_pt.p, ctx->D, ctx->Dpad,
@@ -484,6 +485,18 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
                                ctx->fmax_len, H, H * ctx->F, H * ctx->D, H, ctx->tf_stride};
       ctx->g_valid = true;
       ctx->g_sparse = true;
+    }
+    if (ctx->capture) {  // pipelined c3h_run_frames: the tick kernel runs these stages
+      ctx->cap_q = q;
+      ctx->cap_sc = sc;
+      ctx->cap_sparse_g = sparse_g;
+      ctx->cap_argmax = use_argmax;
+      ctx->cap_search_valid = true;
+      ctx->pending_clean = false;
+      ctx->lists_host_valid = false;
+      ctx->lists_dev_valid = true;
+      memcpy(ctx->last_range, range, sizeof(ctx->last_range));
+      return nm;
     }
     if (nf == 1) {
       int rc = prof_prepare(ctx, nparts, &q.prof);
@@ -1003,13 +1016,18 @@ int extract_frames(c3h_ctx* ctx, const uint32_t* const* grids, int nf, const c3h
       int rc = prof_prepare(ctx, tgrid, &l.prof);
       if (rc != C3H_OK) return rc;
     }
-    HIPCHK(c3h::launch_c3hlac(l, ctx->stream));
-    if (l.prof) {
-      int rc = prof_dump(ctx, "c3hlac_tile_kernel", tgrid);
-      if (rc != C3H_OK) return rc;
+    if (ctx->capture) {  // pipelined c3h_run_frames: the tick kernel runs this launch
+      ctx->cap_c3 = l;
+      ctx->cap_c3_valid = true;
+    } else {
+      HIPCHK(c3h::launch_c3hlac(l, ctx->stream));
+      if (l.prof) {
+        int rc = prof_dump(ctx, "c3hlac_tile_kernel", tgrid);
+        if (rc != C3H_OK) return rc;
+      }
+      if (atomic)
+        HIPCHK(c3h::launch_c3_finalize(ctx->acc64.p, hist_num, F, ctx->feat.p, ctx->exist.p, nf, ctx->stream));
     }
-    if (atomic)
-      HIPCHK(c3h::launch_c3_finalize(ctx->acc64.p, hist_num, F, ctx->feat.p, ctx->exist.p, nf, ctx->stream));
   }
   ctx->hist_num = hist_num;
   ctx->feat_dim = F;
@@ -1207,24 +1225,13 @@ int c3h_set_batch(c3h_ctx* ctx, int32_t frames) {
   return C3H_OK;
 }
 
-int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes,
-                   const int32_t div_b[3], const int32_t min_b[3], float leaf,
-                   const c3h_extract_params* p, const int32_t range[3], int32_t exist_threshold,
-                   int32_t rotate, c3h_det* d_out) {
-  if (!ctx || !d_grids || nframes < 0 || !div_b || !min_b || !p || !range || !d_out)
-    return C3H_ERR_ARG;
-  if (!ctx->have_setup) return fail(ctx, C3H_ERR_STATE, "c3h_run_frames: no axes (call c3h_search_setup)");
-  if (nframes == 0) return 0;
-  HIPCHK(hipSetDevice(ctx->device));
-  const size_t per_frame = (size_t)std::max(ctx->M, 1) * ctx->rank;
-  // frames go in chunks of B (one set of launches per chunk, frame = launch y / z index);
-  // chunks are spread over K lanes (child contexts, own streams and host threads).  The
-  // chunk holding the last frame runs on lane 0 (this context) with that frame in slot 0,
-  // so afterwards the context holds the last frame's features, scores and lists.
-  const int B = c3h::score_fast_ok(ctx->D, ctx->r) ? std::max(1, std::min(ctx->nbatch, c3h::kMaxBatch)) : 1;
-  const int nchunks = (nframes + B - 1) / B;
-  const int K = std::max(1, std::min(ctx->nlanes, nchunks));
-  while ((int)ctx->lanes.size() < K - 1) {
+}  // extern "C"
+
+namespace {
+
+// child contexts lanes[0 .. n-1] exist and carry the context's search setup and rank
+int ensure_lanes(c3h_ctx* ctx, int n) {
+  while ((int)ctx->lanes.size() < n) {
     c3h_ctx* c = nullptr;
     int rc = c3h_create(ctx->device, &c);
     if (rc != C3H_OK) return fail(ctx, rc, "c3h_run_frames: lane context");
@@ -1234,8 +1241,7 @@ int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes
     HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     ctx->lane_ev.push_back(e);
   }
-  if (!ctx->fork_ev) HIPCHK(hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming));
-  for (int l = 0; l < K - 1; ++l) {  // lanes take the context's setup and rank
+  for (int l = 0; l < n; ++l) {
     c3h_ctx* c = ctx->lanes[l];
     if (c->setup_version != ctx->setup_version || !c->have_setup) {
       int rc = c3h_search_setup(c, ctx->h_axis_p.empty() ? nullptr : ctx->h_axis_p.data(),
@@ -1250,6 +1256,130 @@ int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes
       if (rc != C3H_OK) return rc;
     }
   }
+  return C3H_OK;
+}
+
+// frames of chunk ch (B per chunk); the last chunk puts its last frame in slot 0, so the
+// context that runs it ends up holding the last frame's state
+int chunk_frames(const uint32_t* const* d_grids, c3h_det* d_out, size_t per_frame, int nframes, int B,
+                 int nchunks, int ch, const uint32_t** grids, c3h_det** outs) {
+  const int f0 = ch * B, nb = std::min(B, nframes - f0);
+  for (int j = 0; j < nb; ++j) {
+    const int fi = (ch == nchunks - 1) ? (j == 0 ? f0 + nb - 1 : f0 + j - 1) : f0 + j;
+    grids[j] = d_grids[fi];
+    outs[j] = d_out + (size_t)fi * per_frame;
+  }
+  return nb;
+}
+
+// Software-pipelined batches (pipeline.hip): batch b is prepared on buffer set
+// (nchunks-1-b) % 4 (set 0 = this context, so it ends with the last batch) and runs as
+// the occupancy role of tick b, the tile role of tick b+1, compress+gate of b+2 and
+// scoring + rank-1 argmax of b+3.  All buffer sets work on this context's stream.
+// Returns > 0 (modes searched) when it ran, 0 when the configuration does not fit the
+// tick (the caller then runs the lanes), < 0 on error.
+constexpr int kPipeDepth = 4;
+
+int run_frames_pipelined(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes,
+                         const int32_t div_b[3], const int32_t min_b[3], float leaf,
+                         const c3h_extract_params* p, const int32_t range[3], int32_t exist_threshold,
+                         int32_t rotate, c3h_det* d_out, int B) {
+  const size_t per_frame = (size_t)std::max(ctx->M, 1) * ctx->rank;
+  const int nchunks = (nframes + B - 1) / B;
+  int rc = ensure_lanes(ctx, kPipeDepth - 1);
+  if (rc != C3H_OK) return rc;
+  auto set_ctx = [&](int b) {
+    const int set = (nchunks - 1 - b) % kPipeDepth;
+    return set == 0 ? ctx : ctx->lanes[set - 1];
+  };
+  hipStream_t saved[kPipeDepth - 1];
+  for (int l = 0; l < kPipeDepth - 1; ++l) {
+    saved[l] = ctx->lanes[l]->stream;
+    ctx->lanes[l]->stream = ctx->stream;
+  }
+  struct Batch {
+    c3h::C3Launch l;
+    c3h::SparseSearch q;
+    c3h::SparseCompress sc;
+    int nf;
+  };
+  std::vector<Batch> bt(nchunks);
+  int nm = 0;
+  for (int t = 0; t < nchunks + kPipeDepth - 1 && rc >= 0; ++t) {
+    if (t < nchunks) {  // prepare batch t (host state, first-use buffer clears on the stream)
+      c3h_ctx* c = set_ctx(t);
+      const uint32_t* grids[c3h::kMaxBatch];
+      c3h_det* outs[c3h::kMaxBatch];
+      const int nb = chunk_frames(d_grids, d_out, per_frame, nframes, B, nchunks, t, grids, outs);
+      c->capture = true;
+      c->cap_c3_valid = c->cap_search_valid = false;
+      rc = c3h_set_grid(c, grids[0], div_b, min_b, leaf, 1);
+      if (rc == C3H_OK) rc = extract_frames(c, grids, nb, p, nullptr, nullptr);
+      if (rc == C3H_OK) rc = search_frames(c, nb, range, exist_threshold, rotate, outs, 2);
+      c->capture = false;
+      if (rc < 0) {
+        if (c != ctx) ctx->err = c->err;
+        break;
+      }
+      const bool fits = c->cap_c3_valid && c->cap_search_valid && c->cap_sparse_g && c->cap_argmax &&
+                        c3h::tick_ok(c->cap_c3);
+      if (!fits) {  // same geometry for every batch: decided on the first
+        if (t != 0) rc = fail(ctx, C3H_ERR_STATE, "c3h_run_frames: internal: pipeline geometry changed");
+        else rc = 0;
+        break;
+      }
+      nm = rc;
+      bt[t] = Batch{c->cap_c3, c->cap_q, c->cap_sc, nb};
+      c->nframes_feat = 1;  // slot 0 is the context's view from here on
+    }
+    c3h::TickParts tp;
+    if (t < nchunks) tp.occ = &bt[t].l;
+    if (t >= 1 && t - 1 < nchunks) tp.tile = &bt[t - 1].l;
+    if (t >= 2 && t - 2 < nchunks) {
+      tp.gate = &bt[t - 2].q;
+      tp.comp = &bt[t - 2].sc;
+    }
+    if (t >= 3 && t - 3 < nchunks) tp.score = &bt[t - 3].q;
+    Timed tm(ctx, 5, t < nchunks ? bt[t].nf : 0);
+    hipError_t e = c3h::launch_tick(tp, ctx->stream);
+    if (e != hipSuccess) rc = hip_fail(ctx, "launch_tick", e);
+  }
+  for (int l = 0; l < kPipeDepth - 1; ++l) ctx->lanes[l]->stream = saved[l];
+  if (rc < 0) return rc;
+  if (rc == 0) return 0;
+  // the lane contexts' stream work was enqueued on ctx->stream: nothing to join
+  return nm;
+}
+
+}  // namespace
+
+extern "C" {
+
+int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes,
+                   const int32_t div_b[3], const int32_t min_b[3], float leaf,
+                   const c3h_extract_params* p, const int32_t range[3], int32_t exist_threshold,
+                   int32_t rotate, c3h_det* d_out) {
+  if (!ctx || !d_grids || nframes < 0 || !div_b || !min_b || !p || !range || !d_out)
+    return C3H_ERR_ARG;
+  if (!ctx->have_setup) return fail(ctx, C3H_ERR_STATE, "c3h_run_frames: no axes (call c3h_search_setup)");
+  if (nframes == 0) return 0;
+  HIPCHK(hipSetDevice(ctx->device));
+  const size_t per_frame = (size_t)std::max(ctx->M, 1) * ctx->rank;
+  // frames go in chunks of B (one set of launches per chunk, frame = launch y / z index)
+  const int B = c3h::score_fast_ok(ctx->D, ctx->r) ? std::max(1, std::min(ctx->nbatch, c3h::kMaxBatch)) : 1;
+  const int nchunks = (nframes + B - 1) / B;
+  if (ctx->pipeline && ctx->rank == 1 && c3h::score_fast_ok(ctx->D, ctx->r)) {
+    const int rc = run_frames_pipelined(ctx, d_grids, nframes, div_b, min_b, leaf, p, range, exist_threshold,
+                                        rotate, d_out, B);
+    if (rc != 0) return rc;
+  }
+  // lanes: chunks are spread over K child contexts on their own streams and host threads
+  const int K = std::max(1, std::min(ctx->nlanes, nchunks));
+  {
+    int rc = ensure_lanes(ctx, K - 1);
+    if (rc != C3H_OK) return rc;
+  }
+  if (!ctx->fork_ev) HIPCHK(hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming));
   HIPCHK(hipEventRecord(ctx->fork_ev, ctx->stream));  // inputs were produced on ctx's stream
   for (int l = 0; l < K - 1; ++l) HIPCHK(hipStreamWaitEvent(ctx->lanes[l]->stream, ctx->fork_ev, 0));
   std::vector<int> lane_rc(K, 0);
@@ -1259,14 +1389,9 @@ int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes
     int nm_lane = 0;
     for (int ch = 0; ch < nchunks; ++ch) {
       if ((nchunks - 1 - ch) % K != lane) continue;
-      const int f0 = ch * B, nb = std::min(B, nframes - f0);
       const uint32_t* grids[c3h::kMaxBatch];
       c3h_det* outs[c3h::kMaxBatch];
-      for (int j = 0; j < nb; ++j) {  // the last chunk puts its last frame in slot 0
-        const int fi = (ch == nchunks - 1) ? (j == 0 ? f0 + nb - 1 : f0 + j - 1) : f0 + j;
-        grids[j] = d_grids[fi];
-        outs[j] = d_out + (size_t)fi * per_frame;
-      }
+      const int nb = chunk_frames(d_grids, d_out, per_frame, nframes, B, nchunks, ch, grids, outs);
       int rc = c3h_set_grid(c, grids[0], div_b, min_b, leaf, 1);
       if (rc == C3H_OK) rc = extract_frames(c, grids, nb, p, nullptr, nullptr);
       if (rc == C3H_OK) rc = search_frames(c, nb, range, exist_threshold, rotate, outs, 2);
@@ -1291,6 +1416,12 @@ int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes
     HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[l], 0));
   }
   return lane_rc[0];
+}
+
+int c3h_set_pipeline(c3h_ctx* ctx, int32_t enable) {
+  if (!ctx) return C3H_ERR_ARG;
+  ctx->pipeline = enable != 0;
+  return C3H_OK;
 }
 
 int c3h_get_compressed(c3h_ctx* ctx, float* out, int on_device) {

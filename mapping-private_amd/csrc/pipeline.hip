@@ -1,0 +1,188 @@
+// pipeline.hip -- the software-pipelined "tick" kernel of c3h_run_frames.
+//
+// A frame batch goes through four dependent stages: occupancy stream (HBM-bound),
+// C3 tile pass, sparse compress + exist gate, list scoring with the fused rank-1 argmax
+// (all latency-bound).  Launched back to back per batch, or on parallel streams that
+// drift into lock-step, the HBM stream idles while the latency-bound stages run.  Here
+// every launch is one pipeline tick that hosts all four stages of four different batches
+// as block roles:
+//
+//   tick t:  score(batch t-3) | compress+gate(t-2) | tile(t-1) | occupancy(t)
+//
+// Dependencies run only from one tick to the next (stream order), so no workgroup ever
+// waits on another role; the batches use four rotating buffer sets (c3h_ctx lanes).
+// Roles are laid out in dispatch order latency-bound first, so their workgroups are
+// resident early and the occupancy stream fills the rest of the chip.
+#include <algorithm>
+#include <climits>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "c3hlac_dev.h"
+#include "search_dev.h"
+
+namespace c3h {
+namespace {
+
+struct TickArgs {
+  int n_score, n_cg, n_tile, n_occ;  // workgroups per role (all frames of its batch)
+  SparseSearch sq;                   // score role
+  int s_gx, s_groups;
+  SparseSearch gq;                   // compress + gate role
+  CompressRows cr;
+  int g_ngate, g_ncomp;
+  KArgs ka;                          // tile role
+  int t_grid;
+  OccArgs oa;                        // occupancy role
+  int o_grid;
+  long long* prof;                   // diagnostics (C3H_TICK_PROF): [block][2] start, end
+};
+
+// dispatch order: occupancy first (it streams for the whole tick from the first
+// cycle), then tile, compress+gate and scoring in the remaining workgroup slots
+__device__ __forceinline__ void tick_roles(const TickArgs& t, uint32_t* tick_smem) {
+  int b = blockIdx.x;
+  if (b < t.n_occ) {
+    const int f = b / t.o_grid;
+    occupancy_bits_body<true>(t.oa, b - f * t.o_grid, f, t.o_grid, tick_smem);
+    return;
+  }
+  b -= t.n_occ;
+  if (b < t.n_tile) {
+    const int f = b / t.t_grid;
+    if (t.ka.wave117) c3hlac_wave117_body(t.ka, b - f * t.t_grid, f, t.t_grid, tick_smem);
+    else c3hlac_tile_body(t.ka, b - f * t.t_grid, f, t.t_grid, tick_smem);
+    return;
+  }
+  b -= t.n_tile;
+  if (b < t.n_cg) {
+    const int per = t.g_ngate + t.g_ncomp, f = b / per, r = b - f * per;
+    if (r < t.g_ngate) gate_body(t.gq, r, f);
+    else compress_rows_body(t.cr, r - t.g_ngate, t.g_ncomp, f, reinterpret_cast<float*>(tick_smem));
+    return;
+  }
+  b -= t.n_cg;
+  const int per = t.s_gx * t.s_groups, f = b / per, r = b - f * per;
+  score_list_body(t.sq, r % t.s_gx, r / t.s_gx, f, t.s_gx, t.s_groups, reinterpret_cast<float*>(tick_smem));
+}
+
+__global__ __launch_bounds__(kBlock) void c3h_tick_kernel(TickArgs t) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t tick_smem[];
+  if (t.prof && threadIdx.x == 0) t.prof[2 * blockIdx.x] = (long long)wall_clock64();
+  tick_roles(t, tick_smem);
+  if (t.prof) {
+    __syncthreads();
+    if (threadIdx.x == 0) t.prof[2 * blockIdx.x + 1] = (long long)wall_clock64();
+  }
+}
+
+// diagnostics (env C3H_TICK_PROF=<file>): per tick and role, block start/end spread in
+// microseconds (wall_clock64: 100 MHz) from the tick's first block start.  Synchronises.
+void tick_prof_dump(const TickArgs& t, long long* d_prof, int total, hipStream_t s) {
+  std::vector<long long> v((size_t)2 * total);
+  if (hipMemcpyAsync(v.data(), d_prof, v.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess) return;
+  if (hipStreamSynchronize(s) != hipSuccess) return;
+  FILE* fp = fopen(getenv("C3H_TICK_PROF"), "a");
+  if (!fp) return;
+  long long t0 = LLONG_MAX;
+  for (int b = 0; b < total; ++b) t0 = std::min(t0, v[2 * b]);
+  const int n[4] = {t.n_occ, t.n_tile, t.n_cg, t.n_score};
+  const char* names[4] = {"occ", "tile", "cg", "score"};
+  int b0 = 0;
+  fprintf(fp, "tick");
+  for (int r = 0; r < 4; ++r) {
+    if (n[r]) {
+      long long smin = LLONG_MAX, smax = 0, emax = 0;
+      double dsum = 0;
+      for (int b = b0; b < b0 + n[r]; ++b) {
+        smin = std::min(smin, v[2 * b]);
+        smax = std::max(smax, v[2 * b]);
+        emax = std::max(emax, v[2 * b + 1]);
+        dsum += v[2 * b + 1] - v[2 * b];
+      }
+      fprintf(fp, " %s[n=%d start=%.1f..%.1f end=%.1f mean=%.1f]", names[r], n[r], (smin - t0) * 0.01,
+              (smax - t0) * 0.01, (emax - t0) * 0.01, dsum / n[r] * 0.01);
+    }
+    b0 += n[r];
+  }
+  fprintf(fp, "\n");
+  fclose(fp);
+}
+
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+
+}  // namespace
+
+bool tick_ok(const C3Launch& l) {
+  const C3Args c = build_c3_args(l);
+  return c.bits && c.ax && !l.atomic && l.prof == nullptr && l.debug == 0;
+}
+
+hipError_t launch_tick(const TickParts& p, hipStream_t s) {
+  TickArgs t{};
+  size_t lds = 16;
+  if (p.score) {
+    const SparseSearch& a = *p.score;
+    t.sq = a;
+    t.s_gx = (int)std::max<int64_t>(1, std::min<int64_t>(sparse_score_blocks(a), env_int("C3H_TICK_SCORE", 32)));
+    t.s_groups = (a.M + a.mpg - 1) / a.mpg;
+    t.n_score = t.s_gx * t.s_groups * a.nframes;
+    lds = std::max(lds, score_list_lds_bytes(a.D, a.mpg));
+  }
+  if (p.gate) {
+    const SparseSearch& a = *p.gate;
+    const SparseCompress& sc = *p.comp;
+    t.gq = a;
+    t.cr = CompressRows{sc.feat, sc.PT, sc.fmax, sc.G, sc.rows, sc.nrows, sc.F, sc.D, sc.Dpad,
+                        sc.fmax_len, sc.s_feat, sc.s_G, sc.s_rows, sc.s_nrows};
+    t.g_ngate = (int)((a.pstart[a.nmodes] + kBlock - 1) / kBlock);
+    t.g_ncomp = (int)std::max<int64_t>(1, std::min<int64_t>((sc.H + kRR - 1) / kRR, env_int("C3H_TICK_COMP", 32)));
+    t.n_cg = (t.g_ngate + t.g_ncomp) * a.nframes;
+    lds = std::max(lds, sizeof(float) * ((size_t)kRK * sc.Dpad + (size_t)kRR * sc.F));
+  }
+  if (p.tile) {
+    const C3Args c = build_c3_args(*p.tile);
+    t.ka = c.ka;
+    // persistent tile workgroups per frame: the zero role + the work role
+    const int work = std::max(1, std::min(c.tgrid - c.ka.zblocks, env_int("C3H_TICK_TILE", 48)));
+    t.ka.zblocks = std::min(c.ka.zblocks, env_int("C3H_TICK_ZERO", 8));
+    t.t_grid = t.ka.zblocks + work;
+    t.n_tile = t.t_grid * c.nframes;
+    lds = std::max(lds, c.tile_lds);
+  }
+  if (p.occ) {
+    const C3Args c = build_c3_args(*p.occ);
+    t.oa = c.oa;
+    t.o_grid = std::max(1, std::min(c.g1, env_int("C3H_TICK_OCC", 128)));
+    t.n_occ = t.o_grid * c.nframes;
+    lds = std::max(lds, c.occ_lds);
+  }
+  if (const char* m = getenv("C3H_TICK_ROLES")) {  // diagnostics only: bit mask of roles run
+    const int mask = atoi(m);                       // 1 score, 2 compress+gate, 4 tile, 8 occupancy
+    if (!(mask & 1)) t.n_score = 0;
+    if (!(mask & 2)) t.n_cg = 0;
+    if (!(mask & 4)) t.n_tile = 0;
+    if (!(mask & 8)) t.n_occ = 0;
+  }
+  const int total = t.n_score + t.n_cg + t.n_tile + t.n_occ;
+  if (total == 0) return hipSuccess;
+  static long long* d_prof = nullptr;  // diagnostics only
+  static int d_prof_n = 0;
+  if (getenv("C3H_TICK_PROF")) {
+    if (d_prof_n < total) {
+      if (d_prof) (void)hipFree(d_prof);
+      if (hipMalloc(&d_prof, (size_t)2 * total * 8) != hipSuccess) return hipErrorOutOfMemory;
+      d_prof_n = total;
+    }
+    t.prof = d_prof;
+  }
+  c3h_tick_kernel<<<(unsigned)total, kBlock, lds, s>>>(t);
+  if (t.prof) tick_prof_dump(t, d_prof, total, s);
+  return hipGetLastError();
+}
+
+}  // namespace c3h

@@ -1,0 +1,476 @@
+// search_dev.h -- device bodies of the sparse search stages (sparse compress, exist
+// gate, list scoring with the fused rank-1 argmax), shared by the stand-alone kernels
+// (search.hip) and the pipelined tick kernel (pipeline.hip).  Bodies take their block
+// coordinates and LDS base explicitly.  See search.hip for the method.
+#pragma once
+#include "c3h_internal.h"
+
+namespace c3h {
+
+// Sparse compress (row list from the extract): 16 listed rows per workgroup x all
+// columns (Dpad <= 128).  The 16 feature rows (max-normalised) and 32-row chunks of P
+// are staged in LDS, P prefetched one chunk ahead into registers so only the first
+// load's latency is exposed; thread = (row, 8 columns); the fma chain per output runs
+// in ascending j exactly like compress_kernel, so both paths give identical G rows.
+constexpr int kRR = 16, kRK = 32;
+constexpr int kCompressGridCap = 128;  // row-block workgroups per frame of the fused launch
+
+struct CompressRows {
+  const float* feat;
+  const float* PT;
+  const float* fmax;
+  float* G;
+  const int32_t* rows;
+  const uint32_t* nrows;
+  int F, D, Dpad, fmax_len;
+  int64_t s_feat, s_G, s_rows, s_nrows;  // per-frame strides (frame = launch y / z index)
+};
+
+__device__ __forceinline__ void compress_rows_body(const CompressRows& cr, int bid, int nblk, int64_t f,
+                                                   float* csm) {
+  const float* __restrict__ feat = cr.feat + f * cr.s_feat;
+  const float* __restrict__ fmax = cr.fmax;
+  float* __restrict__ G = cr.G + f * cr.s_G;
+  const int32_t* __restrict__ rows = cr.rows + f * cr.s_rows;
+  const int F = cr.F, D = cr.D, Dpad = cr.Dpad, fmax_len = cr.fmax_len;
+  float* pc = csm;                 // kRK x Dpad
+  float* fs = csm + kRK * Dpad;    // kRR x F
+  const int tid = threadIdx.x;
+  const int nq4 = kRK * Dpad / 4, tot4 = F * Dpad / 4;
+  const float4* P4 = reinterpret_cast<const float4*>(cr.PT);
+  float4 pre[4];
+  auto load_chunk = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = tid + j * kBlock, g = c * nq4 + e;
+      pre[j] = (e < nq4 && g < tot4) ? P4[g] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  // P's first chunk is independent of the row count: in flight before the count arrives
+  load_chunk(0);
+  const int n = (int)cr.nrows[f * cr.s_nrows];
+  const int row = tid >> 4, cg = tid & 15;
+  const bool active = 8 * cg < Dpad;
+  const int nch = (F + kRK - 1) / kRK;
+  // row blocks bid, bid + nblk, ... (the launch holds few workgroups; dense scenes loop)
+  for (int r0 = bid * kRR; r0 < n; r0 += nblk * kRR) {
+    if (r0 != bid * kRR) load_chunk(0);
+    for (int e = tid; e < kRR * F; e += kBlock) {
+      const int r = e / F, j = e - r * F;
+      float v = 0.0f;
+      if (r0 + r < n) {
+        v = feat[(int64_t)rows[r0 + r] * F + j];
+        if (j < fmax_len) {  // setData max-normalisation (search.cpp:563-570)
+          const float mx = fmax[j];
+          if (mx == 0.0f) v = 0.0f;
+          else if (v == mx) v = 1.0f;
+          else v = __fdiv_rn(v, mx);
+        }
+      }
+      fs[e] = v;
+    }
+    float acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = 0.0f;
+    for (int c = 0; c < nch; ++c) {
+      lds_barrier();
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int e = tid + j * kBlock;
+        if (e < nq4) reinterpret_cast<float4*>(pc)[e] = pre[j];
+      }
+      if (c + 1 < nch) load_chunk(c + 1);
+      lds_barrier();
+      if (active) {
+        const int kn = min(kRK, F - c * kRK);
+        const float* fr = fs + row * F + c * kRK;
+        for (int k = 0; k < kn; ++k) {
+          const float fv = fr[k];
+          const float4 p0 = *reinterpret_cast<const float4*>(&pc[k * Dpad + 8 * cg]);
+          const float4 p1 = *reinterpret_cast<const float4*>(&pc[k * Dpad + 8 * cg + 4]);
+          acc[0] = __builtin_fmaf(fv, p0.x, acc[0]);
+          acc[1] = __builtin_fmaf(fv, p0.y, acc[1]);
+          acc[2] = __builtin_fmaf(fv, p0.z, acc[2]);
+          acc[3] = __builtin_fmaf(fv, p0.w, acc[3]);
+          acc[4] = __builtin_fmaf(fv, p1.x, acc[4]);
+          acc[5] = __builtin_fmaf(fv, p1.y, acc[5]);
+          acc[6] = __builtin_fmaf(fv, p1.z, acc[6]);
+          acc[7] = __builtin_fmaf(fv, p1.w, acc[7]);
+        }
+      }
+    }
+    if (active && r0 + row < n) {
+      const int64_t h = rows[r0 + row];
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (8 * cg + q < D) G[h * D + 8 * cg + q] = acc[q];
+    }
+    lds_barrier();  // fs / pc are rewritten by the next row block
+  }
+}
+
+// Fast path (D <= 256, D % 4 == 0, M*r <= 256) = the sparse search below: 32 list
+// entries per workgroup.  Box features are summed with float4 loads and staged k-major in
+// LDS (lanes = positions: conflict-free); the projection onto all M*r basis rows is a
+// 32 x Opad x D fp32 GEMM with a 2-position x 16-row register tile per thread (one
+// ds_read_b64 of box features + four ds_read_b128 of basis rows feed 32 FMAs), the basis
+// streamed through LDS in 16-row chunks prefetched one chunk ahead into registers;
+// |Q_m f|^2 is summed per (position, model) in a fixed order.  The block also emits its
+// per-model best (score, scan order) so rank-1 searches need no second pass.
+constexpr int kFP = 32;
+constexpr int kOC = 64;  // basis rows per workgroup (whole models)
+constexpr int kScoreGridCap = 128;  // workgroups per (model group, frame) of the score launch
+
+// ---------------------------------------------------------------- sparse search
+// The exist gate passes few positions on surface scenes (a depth camera sees a 2-D
+// manifold), so the gate runs first over every position of every mode and compacts the
+// passing ones into a list; the projection then runs over the list only.  Entries are
+// (mode index << 40) | position; list order is irrelevant: scores are per position and
+// the per-block partials break ties on the scan order explicitly.
+__device__ __forceinline__ int find_mode(const SparseSearch& a, int64_t g) {
+  int mi = 0;
+  while (mi + 1 < a.nmodes && g >= a.pstart[mi + 1]) ++mi;
+  return mi;
+}
+
+// frame f of a batched search: per-frame pointers at base + f * stride (no struct copy:
+// a by-value SparseSearch with its dynamically indexed mode table would live in scratch)
+__device__ __forceinline__ void gate_body(const SparseSearch& a, int bid, int64_t f) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  uint32_t* __restrict__ fcnt = a.cnt + f * a.s_cnt;
+  uint32_t* __restrict__ fdone = a.done + f * a.s_cnt;
+  const int32_t* __restrict__ fexist = a.exist + f * a.s_exist;
+  double* __restrict__ fscores = a.scores + f * a.s_scores;
+  long long* __restrict__ flist = a.list + f * a.s_list;
+  if (bid == 0 && tid == 0) {  // the next search's counters
+    fcnt[(a.epoch + 1) & 1] = 0;
+    fdone[(a.epoch + 1) & 1] = 0;
+  }
+  const int64_t g = bid * (int64_t)kBlock + tid;
+  bool pass = false;
+  int64_t entry = 0;
+  if (g < a.pstart[a.nmodes]) {
+    const int mi = find_mode(a, g);
+    const ModeGeom& md = a.md[mi];
+    const int64_t p = g - a.pstart[mi];
+    const int64_t xye = (int64_t)md.xe * md.ye;
+    const int x = (int)(p % md.xe), y = (int)((p / md.xe) % md.ye), z = (int)(p / xye);
+    const int xyn = a.xn * a.yn;
+    const int h = z * xyn + y * a.xn + x;
+    int e = 0;  // SearchObj::clipValue<int> on exist_voxel_num (search.cpp:484-535), exact
+    for (int dz = 0; dz < md.zr; ++dz)
+      for (int dy = 0; dy < md.yr; ++dy)
+        for (int dx = 0; dx < md.xr; ++dx) e += fexist[h + dz * xyn + dy * a.xn + dx];
+    pass = e > a.thr;
+    entry = ((int64_t)mi << 40) | p;
+    if (!pass)
+      for (int m = 0; m < a.M; ++m) fscores[md.offset + (int64_t)m * md.P + p] = -1.0;
+  }
+  const unsigned long long m = __ballot(pass);
+  if (m) {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&fcnt[a.epoch & 1], (uint32_t)__popcll(m));
+    base = __shfl(base, 0, 64);
+    if (pass) flist[base + __popcll(m & ((1ull << lane) - 1))] = entry;
+  }
+}
+
+// Rank-1 replay fused into the score launch (search.cpp:464-474 with rank_num == 1:
+// checkOverlap returns slot 0, so the update is "first strictly greater maximum in scan
+// order").  One wave per model reduces the partials with (score desc, scan order asc);
+// partials of other workgroups are read with device-scope atomic loads.
+__device__ void argmax_finalize(const SparseSearch& a, const ScorePartial* partials, c3h_det* lists,
+                                c3h_det* out, int nparts) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int m = w; m < a.M; m += kBlock / 64) {
+    double best = -2.0;
+    long long bo = -1;
+    for (int i = lane; i < nparts; i += 64) {
+      const ScorePartial* q = partials + (int64_t)i * a.M + m;
+      const long long qo = __hip_atomic_load(&q->order, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const double qs = __hip_atomic_load(&q->score, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (qo >= 0 && (qs > best || (qs == best && qo < bo))) {
+        best = qs;
+        bo = qo;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double os = __shfl_xor(best, o, 64);
+      const long long oo = __shfl_xor(bo, o, 64);
+      if (oo >= 0 && (os > best || (os == best && (bo < 0 || oo < bo)))) {
+        best = os;
+        bo = oo;
+      }
+    }
+    if (lane == 0) {
+      c3h_det e = lists[m];
+      if (a.clean) {  // 1: cleanMax (modes kept, search.cpp:683-690); 2: setRank state
+        e.score = 0.0;
+        e.x = e.y = e.z = 0;
+        if (a.clean == 2) e.mode = 0;
+      }
+      if (bo >= 0 && best > e.score) {
+        const int mi = (int)(bo >> 40);
+        const int64_t p = bo & ((1ll << 40) - 1);
+        const ModeGeom& md = a.md[mi];
+        e.score = best;
+        e.x = (int)(p % md.xe);
+        e.y = (int)((p / md.xe) % md.ye);
+        e.z = (int)(p / ((int64_t)md.xe * md.ye));
+        e.mode = md.mode;
+      }
+      lists[m] = e;
+      if (out) out[m] = e;
+    }
+  }
+}
+
+// Fast-path projection over the gate list:
+// kFP entries per workgroup; box rows of empty subdivisions are skipped (their G rows
+// may be stale: the sparse compress only writes non-empty rows; an all-zero row adds
+// nothing to a sum that starts at +0).
+// LDS bytes of the score body: feature/projection region, basis window, per-position
+// scratch, per-block best scores, the last-workgroup flag
+__host__ __device__ inline size_t score_list_lds_bytes(int D, int mpg) {
+  const size_t region = ((size_t)D * kFP > (size_t)kFP * (kOC + 1) ? (size_t)D * kFP : (size_t)kFP * (kOC + 1)) +
+                        (size_t)D * kOC;
+  return sizeof(float) * (region + kFP) + sizeof(int) * 4 * kFP + sizeof(long long) * kFP +
+         sizeof(double) * kFP * mpg + 16 + 16;
+}
+
+// block (bx, by, fz) of a (gdx, gdy, frames) launch; smem: score_list_lds_bytes(D, mpg)
+__device__ __forceinline__ void score_list_body(const SparseSearch& b, int bx, int by, int fz_, int gdx, int gdy,
+                                                float* ssm) {
+  const SparseSearch& a = b;  // frame-independent fields; per-frame pointers below
+  const int64_t fz = fz_;
+  const float* __restrict__ fG = b.G + fz * b.s_G;
+  const int32_t* __restrict__ fexist = b.exist + fz * b.s_exist;
+  double* __restrict__ fscores = b.scores + fz * b.s_scores;
+  const long long* __restrict__ flist = b.list + fz * b.s_list;
+  const uint32_t* fcnt = b.cnt + fz * b.s_cnt;
+  uint32_t* fdone = b.done + fz * b.s_cnt;
+  ScorePartial* fpart = b.partials ? b.partials + fz * b.s_partials : nullptr;
+  c3h_det* flists = b.lists ? b.lists + fz * b.s_lists : nullptr;
+  c3h_det* fout = b.outs[fz];
+  long long* fprof = fz ? nullptr : b.prof;
+  const int D = a.D, D4 = a.D >> 2, Qs = a.Opad;  // qt row stride
+#define C3H_SPROF(k) \
+  if (fprof && threadIdx.x == 0 && by == 0) fprof[bx * 8 + (k)] = (long long)wall_clock64()
+  C3H_SPROF(0);
+  const int tid = threadIdx.x;
+  // issued together: the list count, this workgroup's first list chunk (speculative: the
+  // list buffer holds P_total entries, entries past the count are ignored) and the
+  // group's basis window, so the count costs no extra round trip
+  const int64_t ptot = a.pstart[a.nmodes];
+  long long en_first = -1;
+  if (tid < kFP) en_first = flist[min((int64_t)bx * kFP + tid, ptot - 1)];
+  // model group of this workgroup: models [m0, m1), basis rows [m0*r, m1*r) padded to oc
+  const int m0 = by * a.mpg, m1 = min(a.M, m0 + a.mpg);
+  const int row0 = m0 * a.r, oc = ((m1 - m0) * a.r + 15) & ~15;  // <= kOC
+  constexpr int kQW = 160 * kOC / kBlock;  // window floats per lane at the largest D
+  float qwv[kQW];
+#pragma unroll
+  for (int j = 0; j < kQW; ++j) {
+    const int e = j * kBlock + tid, d = e / oc, o = e - d * oc;
+    qwv[j] = e < D * oc ? a.qt[(int64_t)d * Qs + row0 + o] : 0.0f;
+  }
+  const int n = (int)fcnt[a.epoch & 1];
+  const int nch = (n + kFP - 1) / kFP;  // list chunks; chunk c -> workgroups c mod gdx
+  if (bx >= nch) {
+    if (n == 0 && flists && bx == 0 && by == 0) argmax_finalize(a, fpart, flists, fout, 0);  // clean / copy out
+    return;
+  }
+  const int fts = max(D * kFP, kFP * (kOC + 1));
+  float* fT = ssm;                    // D x kFP (k-major box features)
+  float* qv = ssm;                    // kFP x (kOC+1), aliases fT after the GEMM
+  float* qw = ssm + fts;              // D x oc: this group's whole basis window
+  float* ffv = qw + D * kOC;
+  int* gate = reinterpret_cast<int*>(ffv + kFP);
+  int* hrow = gate + kFP;
+  int* rng = hrow + kFP;                       // packed xr | yr << 10 | zr << 20
+  long long* ent = reinterpret_cast<long long*>(rng + kFP + (kFP & 1));
+  double* bsc = reinterpret_cast<double*>(ent + kFP);  // kFP * mpg
+  const int xyn = a.xn * a.yn;
+#pragma unroll
+  for (int j = 0; j < kQW; ++j)  // parked once; read by every chunk's GEMM
+    if (j * kBlock + tid < D * oc) qw[j * kBlock + tid] = qwv[j];
+  for (int ch = bx; ch < nch; ch += gdx) {
+    const int64_t e0 = (int64_t)ch * kFP;
+    if (tid < kFP) {
+      const int64_t e = e0 + tid;
+      int ok = 0, h = 0, rr = 0;
+      long long en = -1;
+      if (e < n) {
+        en = ch == bx ? en_first : flist[e];
+        const int mi = (int)(en >> 40);
+        const int64_t p = en & ((1ll << 40) - 1);
+        const ModeGeom& md = a.md[mi];
+        const int64_t xye = (int64_t)md.xe * md.ye;
+        const int x = (int)(p % md.xe), y = (int)((p / md.xe) % md.ye), z = (int)(p / xye);
+        h = z * xyn + y * a.xn + x;
+        rr = md.xr | (md.yr << 10) | (md.zr << 20);
+        ok = 1;
+      }
+      gate[tid] = ok;
+      hrow[tid] = h;
+      rng[tid] = rr;
+      ent[tid] = en;
+    }
+    lds_barrier();
+    C3H_SPROF(1);
+    {  // box sums in the fixed (dz, dy, dx) order over non-empty rows; lane = position.
+       // Cells go in batches of 4 x (this thread's d4 slots): every load of a batch is in
+       // flight together.  Rows of empty subdivisions read as 0 (their G rows may be stale;
+       // +0 added to a sum that starts at +0 changes nothing).
+      const int pp = tid & (kFP - 1), dg = tid / kFP;
+      constexpr int kDG = kBlock / kFP;  // d4 stride
+      const bool ok = gate[pp];
+      const int h = hrow[pp], rr = rng[pp];
+      const int xr = rr & 1023, yr = (rr >> 10) & 1023, zr = rr >> 20;
+      const int ncell = ok ? xr * yr * zr : 0;
+      const float4* G4 = reinterpret_cast<const float4*>(fG);
+      constexpr int kSlots = 4;  // d4 values per thread handled together (D4 <= 64)
+      float4 s[kSlots];
+#pragma unroll
+      for (int q = 0; q < kSlots; ++q) s[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int d4b = 0; d4b < D4; d4b += kSlots * kDG) {
+        for (int c0 = 0; c0 < ncell; c0 += 4) {
+          float4 g[4][kSlots];
+          bool lv[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int c = c0 + k;
+            const int dx = c % xr, dy = (c / xr) % yr, dz = c / (xr * yr);
+            const int hh = h + dz * xyn + dy * a.xn + dx;
+            lv[k] = c < ncell && fexist[c < ncell ? hh : h] != 0;
+#pragma unroll
+            for (int q = 0; q < kSlots; ++q) {
+              const int d4 = d4b + dg + q * kDG;
+              g[k][q] = (c < ncell && d4 < D4) ? G4[(int64_t)hh * D4 + d4] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int q = 0; q < kSlots; ++q)
+              if (lv[k]) {
+                s[q].x += g[k][q].x;
+                s[q].y += g[k][q].y;
+                s[q].z += g[k][q].z;
+                s[q].w += g[k][q].w;
+              }
+        }
+#pragma unroll
+        for (int q = 0; q < kSlots; ++q) {
+          const int d4 = d4b + dg + q * kDG;
+          if (d4 < D4) {
+            fT[(4 * d4 + 0) * kFP + pp] = s[q].x;
+            fT[(4 * d4 + 1) * kFP + pp] = s[q].y;
+            fT[(4 * d4 + 2) * kFP + pp] = s[q].z;
+            fT[(4 * d4 + 3) * kFP + pp] = s[q].w;
+          }
+          s[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+    }
+    lds_barrier();
+    C3H_SPROF(2);
+    if (tid < kFP) {
+      float s = 0.0f;
+      for (int d = 0; d < D; ++d) s = __builtin_fmaf(fT[d * kFP + tid], fT[d * kFP + tid], s);
+      ffv[tid] = s;
+    }
+    // GEMM: thread (tp, to): positions 2*tp, 2*tp+1; basis rows 4*to .. 4*to+3 of the group
+    const int tp = tid & 15, to = tid >> 4;
+    const bool active = 4 * to < oc;
+    float acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[i][q] = 0.0f;
+    if (active) {
+#pragma unroll 4
+      for (int d = 0; d < D; ++d) {
+        const float2 f = *reinterpret_cast<const float2*>(&fT[d * kFP + 2 * tp]);
+        const float4 q = *reinterpret_cast<const float4*>(&qw[d * oc + 4 * to]);
+        acc[0][0] = __builtin_fmaf(f.x, q.x, acc[0][0]);
+        acc[0][1] = __builtin_fmaf(f.x, q.y, acc[0][1]);
+        acc[0][2] = __builtin_fmaf(f.x, q.z, acc[0][2]);
+        acc[0][3] = __builtin_fmaf(f.x, q.w, acc[0][3]);
+        acc[1][0] = __builtin_fmaf(f.y, q.x, acc[1][0]);
+        acc[1][1] = __builtin_fmaf(f.y, q.y, acc[1][1]);
+        acc[1][2] = __builtin_fmaf(f.y, q.z, acc[1][2]);
+        acc[1][3] = __builtin_fmaf(f.y, q.w, acc[1][3]);
+      }
+    }
+    lds_barrier();  // qv aliases fT
+    C3H_SPROF(3);
+    if (active) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) qv[(2 * tp + i) * (kOC + 1) + 4 * to + q] = acc[i][q];
+    }
+    lds_barrier();
+    const int nm = m1 - m0;
+    for (int e = tid; e < kFP * nm; e += kBlock) {
+      const int mm = e / kFP, pp = e - mm * kFP;
+      double sc = -2.0;
+      if (gate[pp]) {
+        float q2 = 0.0f;
+        const float* q = qv + pp * (kOC + 1) + mm * a.r;
+        for (int i = 0; i < a.r; ++i) q2 = __builtin_fmaf(q[i], q[i], q2);
+        sc = sqrt((double)q2) / sqrt((double)ffv[pp]);
+        const long long en = ent[pp];
+        const ModeGeom& md = a.md[(int)(en >> 40)];
+        fscores[md.offset + (int64_t)(m0 + mm) * md.P + (en & ((1ll << 40) - 1))] = sc;
+      }
+      bsc[e] = sc;
+    }
+    C3H_SPROF(4);
+    if (fpart) {
+      lds_barrier();
+      for (int mm = tid; mm < nm; mm += kBlock) {  // (score desc, scan order asc)
+        double best = -2.0;
+        long long bo = -1;
+        for (int pp = 0; pp < kFP; ++pp) {
+          if (!gate[pp]) continue;
+          const double sc = bsc[mm * kFP + pp];
+          const long long en = ent[pp];
+          const long long o = a.order_base[(int)(en >> 40)] + (en & ((1ll << 40) - 1));
+          if (sc > best || (sc == best && o < bo)) {
+            best = sc;
+            bo = o;
+          }
+        }
+        ScorePartial* q = fpart + (int64_t)ch * a.M + m0 + mm;
+        if (flists) {  // handed to another workgroup inside this launch: sc1 stores
+          __hip_atomic_store(&q->score, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&q->order, bo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          *q = ScorePartial{best, bo};
+        }
+      }
+    }
+    lds_barrier();  // LDS is reused by the next chunk
+  }
+  if (fpart && flists) {
+    // rank 1, fused replay: the last workgroup to finish reduces.  Hand-off per
+    // MI355X_MICROARCH.md (inter-workgroup visibility, table row 1): sc1 stores, every
+    // storing wave waits vmcnt(0), a barrier, one agent atomic add per workgroup; the
+    // workgroup whose add returns total-1 reads the partials with sc1 loads.
+    int& s_last = *reinterpret_cast<int*>(reinterpret_cast<char*>(ssm) + score_list_lds_bytes(D, a.mpg) - 16);
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    if (tid == 0) {
+      const uint32_t total = (uint32_t)min(nch, gdx) * gdy;
+      s_last = atomicAdd(&fdone[a.epoch & 1], 1u) == total - 1;
+    }
+    lds_barrier();
+    if (s_last) argmax_finalize(a, fpart, flists, fout, nch);
+  }
+  C3H_SPROF(7);
+}
+
+}  // namespace c3h

@@ -346,12 +346,14 @@ def test_dense_256_bin_block_linearity(ctx):
     assert whole[:6].sum() == 3 * 256 ** 3  # each voxel adds beta_c + (1-beta_c) per colour
 
 
-@pytest.mark.parametrize("lanes,batch,rank", [(1, 1, 1), (1, 4, 1), (3, 1, 1), (3, 4, 1), (2, 3, 2),
-                                              (4, 8, 1)])
-def test_run_frames_lanes_match_sequential(ctx, lanes, batch, rank):
-    """c3h_run_frames (frames batched per launch, batches in flight on lane contexts) ==
-    frame-by-frame setRank / extract / search on one context; the context ends with the
-    last frame's state."""
+@pytest.mark.parametrize("lanes,batch,rank,pipe", [(1, 1, 1, 0), (1, 4, 1, 0), (3, 1, 1, 0), (3, 4, 1, 0),
+                                                   (2, 3, 2, 0), (4, 8, 1, 0), (1, 1, 1, 1), (1, 2, 1, 1),
+                                                   (1, 3, 1, 1), (1, 8, 1, 1), (2, 3, 2, 1)])
+def test_run_frames_lanes_match_sequential(ctx, lanes, batch, rank, pipe):
+    """c3h_run_frames (frames batched per launch; batches in flight on lane contexts, or
+    software-pipelined through the tick kernel: 8 frames at batch 1/2 rotate through all
+    four buffer sets) == frame-by-frame setRank / extract / search on one context; the
+    context ends with the last frame's state."""
     import torch
     G, S, rng_box = 64, 8, (2, 2, 1)
     frames = [synth.kinect_scene(60_000, grid=G, leaf=0.01, seed=synth.BASE_SEED + 40 + i) for i in range(7)]
@@ -377,6 +379,7 @@ def test_run_frames_lanes_match_sequential(ctx, lanes, batch, rank):
     d_out = torch.zeros((len(words), 4 * rank * 3), dtype=torch.int64, device=dev)
     ctx.set_lanes(lanes)
     ctx.set_batch(batch)
+    ctx.set_pipeline(pipe)
     ctx.run_frames(np.array([g.data_ptr() for g in d_grids], np.uint64), (G, G, G), (0, 0, 0), 0.01, 117,
                    THR, S, rng_box, 20, True, d_out.data_ptr())
     torch.cuda.synchronize()
@@ -387,3 +390,4 @@ def test_run_frames_lanes_match_sequential(ctx, lanes, batch, rank):
     np.testing.assert_array_equal(ctx.exist(), last_exist)
     ctx.set_lanes(3)
     ctx.set_batch(4)
+    ctx.set_pipeline(1)

@@ -1,0 +1,77 @@
+"""Diagnostics: pipelined c3h_run_frames throughput vs tick role sizes and batch.
+PIPE_CASES="batch,occ,tile,score,comp;..." (empty = default)."""
+import os
+import sys
+import time
+
+sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), "mapping-private_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import c3hlac  # noqa: E402
+from c3hlac import synth  # noqa: E402
+
+G, LEAF = 256, 0.01
+dev = torch.device("cuda", 0)
+with c3hlac.Context(0) as ctx:
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    grids = []
+    for s in range(3):
+        pts = synth.kinect_scene(1_000_000, grid=G, leaf=LEAF, seed=synth.BASE_SEED + s)
+        ctx.voxelize(pts, LEAF)
+        w = torch.empty(G ** 3, dtype=torch.int32, device=dev)
+        ctx.lib.c3h_get_grid(ctx.h, c3hlac.ptr(w), 1)
+        grids += [w, torch.roll(w.view(G, G, G), 37, 2).reshape(-1).contiguous()]
+    axis_t, var, axis_q = synth.random_bases(117, 100, 10, 20, seed=synth.BASE_SEED)
+    ctx.search_setup(axis_t, var, axis_q)
+    ctx.set_rank(1)
+    N = 240
+    gptr = np.array([grids[i % 6].data_ptr() for i in range(N)], np.uint64)
+    dets = torch.zeros((N, 30), dtype=torch.int64, device=dev)
+    ref = None
+    cases = os.environ.get("PIPE_CASES", "4,,,,;8,,,,;2,,,,;lanes")
+    for case in cases.split(";"):
+        if case == "lanes":
+            ctx.set_pipeline(False)
+            ctx.set_batch(4)
+            label = "lanes=3 batch=4"
+        else:
+            b, occ, tile, score, comp = case.split(",")[:5]
+            roles = case.split(",")[5] if len(case.split(",")) > 5 else ""
+            if roles:
+                os.environ["C3H_TICK_ROLES"] = roles
+            else:
+                os.environ.pop("C3H_TICK_ROLES", None)
+            ctx.set_pipeline(True)
+            ctx.set_batch(int(b))
+            for k, v in (("C3H_TICK_OCC", occ), ("C3H_TICK_TILE", tile), ("C3H_TICK_SCORE", score),
+                         ("C3H_TICK_COMP", comp)):
+                if v:
+                    os.environ[k] = v
+                else:
+                    os.environ.pop(k, None)
+            label = "pipe batch=%s occ=%s tile=%s score=%s comp=%s roles=%s" % (b, occ, tile, score, comp, roles)
+        best = 1e9
+        for rep in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ctx.run_frames(gptr, (G,) * 3, (0, 0, 0), LEAF, 117, (147, 146, 148), 10, (2, 2, 2), 100, True,
+                           dets.data_ptr())
+            t1 = time.perf_counter()
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            best = min(best, t2 - t0)
+        d = dets.cpu().numpy()
+        if ref is None:
+            ref = d.copy()
+        same = np.array_equal(d, ref)
+        if case != "lanes" and roles:
+            same = "n/a"
+        ctx.timing(c3hlac.timing_mask("pipeline"))
+        ctx.kernel_times(reset=True)
+        ctx.run_frames(gptr, (G,) * 3, (0, 0, 0), LEAF, 117, (147, 146, 148), 10, (2, 2, 2), 100, True,
+                       dets.data_ptr())
+        kt = ctx.kernel_times(reset=True)
+        ctx.timing(False)
+        ms, nf = kt["pipeline"]
+        print("%-50s us/frame=%.2f host_enqueue_us/frame=%.2f tick_ms_total=%.3f same_as_first=%s" %
+              (label, best / N * 1e6, (t1 - t0) / N * 1e6, ms, same), flush=True)
