@@ -166,6 +166,8 @@ struct SparseSearch {
   const float* qt;        // D x Opad (row stride), zero-padded past M*r
   int M, r, Opad;
   int mpg;                // models per workgroup (whole models, mpg*r <= 64)
+  int v2;                 // lane-per-position scoring (score2_body, search2_dev.h)
+  const float* qw;        // its per-wave basis windows (score2_pack)
   double* scores;
   ModeGeom md[6];
   int nmodes;
@@ -194,8 +196,16 @@ struct SparseCompress {
   int F, D, Dpad, fmax_len;
   int64_t H;
   int64_t s_feat, s_G, s_rows, s_nrows;  // per-frame strides
+  const float* PW;  // per-wave column slices of P for the lane-per-row compress
 };
 bool compress_rows_ok(int F, int Dpad);
+bool compress2_fits(int F, int D);        // lane-per-row sparse compress applies
+bool score2_fits(int D, int M, int r);    // lane-per-position scoring applies
+// host: per-wave weight layouts of the lane-per-item bodies (search2_dev.h)
+size_t compress2_pw_floats(int F);
+void compress2_pack_host(const float* PT, int F, int D, int Dpad, float* PW);
+size_t score2_qw_floats(int D);
+void score2_pack_host(const float* axis_q, int M, int r, int D, float* QW);
 hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc, hipStream_t s);
 int64_t sparse_score_blocks(const SparseSearch& a);
 
@@ -309,6 +319,8 @@ struct c3h_ctx {
   c3h::DevBuf<double> scores;
   int64_t scores_n = 0;
   c3h::DevBuf<float> qt;            // D x Opad transposed model basis (fast score path)
+  c3h::DevBuf<float> qw2;           // per-wave basis windows (lane-per-position scoring)
+  c3h::DevBuf<float> pw2;           // per-wave slices of P (lane-per-row compress)
   int Opad = 0;
   c3h::DevBuf<c3h::ScorePartial> partials;
   bool pending_clean = false;       // cleanMax requested while the device lists are current

@@ -186,7 +186,7 @@ bool wave117_ok(const C3Launch& l) {
   if (const char* e = getenv("C3H_WAVE117"))  // diagnostics: 0 forces the block body
     if (!atoi(e)) return false;
   const int tw = w117_halo_words(l.lmax[0], l.lmax[1], l.lmax[2]);
-  return l.variant == 117 && !l.atomic && l.debug == 0 && l.prof == nullptr && tw <= 64 * kW117HaloRegs &&
+  return l.variant == 117 && !l.atomic && l.debug == 0 && tw <= 64 * kW117HaloRegs &&
          w117_lds_bytes(tw, l.lmax[0] * l.lmax[1] * l.lmax[2]) <= 65536;
 }
 
@@ -217,7 +217,7 @@ int64_t c3hlac_grid(const C3Launch& l) {
     c_ncu = n_cu;
     c_dev = dev;
   }
-  const int64_t items = w117 ? (l.ntiles + 3) / 4 : l.ntiles;
+  const int64_t items = w117 ? (l.ntiles + kW117Waves - 1) / kW117Waves : l.ntiles;
   int64_t work = std::min<int64_t>(items, (int64_t)c_ncu * std::min(c_per_cu, 2));
   if (const char* g = getenv("C3H_TILE_GRID")) work = std::max<int64_t>(1, std::min<int64_t>(items, atoi(g)));
   const int64_t zero = l.zero_empty ? std::min<int64_t>(64, l.ntiles) : 0;

@@ -232,16 +232,26 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
   // consecutive j of one thread are kBlock*4 voxels apart: step (x, y, z) incrementally
   const int dxs = (kBlock * 4) % gx, drs = (kBlock * 4) / gx;
   int last = -1;
-  for (int64_t c0 = bx * (int64_t)kChunk4; c0 < n4; c0 += (int64_t)gdx * kChunk4) {
-    uint4 w[kOccBitsUnroll];
+  // software-pipelined: chunk c+1's loads are issued before chunk c is processed, so
+  // every wave keeps 2 x kOccBitsUnroll x 16 B per lane in flight.  Non-temporal: the grid
+  // is read once here (the tile pass re-reads only the occupied tiles' halos); measured
+  // 6.9-7.0 TB/s vs 6.0-6.3 for default-policy loads.  Past the grid end the address is
+  // clamped and the value zeroed (no per-element branch around the load).
+  const int64_t cstride = (int64_t)gdx * kChunk4;
+  auto load_chunk = [&](uint4 (&dst)[kOccBitsUnroll], int64_t c) {
 #pragma unroll
-    for (int j = 0; j < kOccBitsUnroll; ++j) {  // all loads first: bytes in flight, not latency
-      const int64_t i = c0 + j * kBlock + tid;
-      // non-temporal: the grid is read once here (the tile pass re-reads only the few
-      // occupied tiles' halos); measured 6.9-7.0 TB/s vs 6.0-6.3 for default-policy loads
-      const v4u t = i < n4 ? __builtin_nontemporal_load(reinterpret_cast<const v4u*>(g4) + i) : v4u{0, 0, 0, 0};
-      w[j] = make_uint4(t.x, t.y, t.z, t.w);
+    for (int j = 0; j < kOccBitsUnroll; ++j) {
+      const int64_t i = c + j * kBlock + tid;
+      const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(g4) + (i < n4 ? i : n4 - 1));
+      dst[j] = i < n4 ? make_uint4(t.x, t.y, t.z, t.w) : make_uint4(0, 0, 0, 0);
     }
+  };
+  uint4 w[kOccBitsUnroll];
+  int64_t c0 = bx * (int64_t)kChunk4;
+  if (c0 < n4) load_chunk(w, c0);
+  for (; c0 < n4; c0 += cstride) {
+    uint4 nx[kOccBitsUnroll];
+    if (c0 + cstride < n4) load_chunk(nx, c0 + cstride);
     const uint32_t v0 = (uint32_t)((c0 + tid) << 2);  // nvox < 2^32 (host-checked)
     const uint32_t row0 = v0 / (uint32_t)gx;
     int x = (int)(v0 - row0 * (uint32_t)gx);
@@ -286,6 +296,8 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
         atomicOr(&s_bits[t >> 5], 1u << (t & 31));  // result unused: ds_or_b32, no wait
       }
     }
+#pragma unroll
+    for (int j = 0; j < kOccBitsUnroll; ++j) w[j] = nx[j];
   }
   __syncthreads();
   occ_flush_bits(s_bits, nwords, s_list, s_wsum, epoch, flags, cnt, work);
@@ -647,6 +659,7 @@ __device__ __forceinline__ void c3hlac_tile_body(const KArgs& a, int bx, int fy_
 constexpr int kW117Ch = 25;
 constexpr int kW117ChStride = 36;  // dwords per channel row (64 u16 + pad: 16-B aligned rows 4 banks apart)
 constexpr int kW117HaloRegs = 26;  // halo dwords per lane kept in flight (<= 1664-word halos)
+constexpr int kW117Waves = 3;      // tile waves per workgroup (the 4th exits: LDS <= 40 KB at S=10)
 
 __host__ __device__ inline int w117_halo_words(int lx, int ly, int lz) { return (lx + 2) * (ly + 2) * (lz + 1); }
 // per-wave LDS words (halo + list + channel table), 4-dword aligned
@@ -654,7 +667,7 @@ __host__ __device__ inline int w117_wave_words(int tw, int list_max) {
   return ((tw + 3) & ~3) + (((list_max + 1) / 2 + 3) & ~3) + kW117Ch * kW117ChStride;
 }
 __host__ __device__ inline size_t w117_lds_bytes(int tw, int list_max) {
-  return 4 * ((size_t)256 + 9 * kSegLds + 4 * (size_t)w117_wave_words(tw, list_max));
+  return 4 * ((size_t)256 + 9 * kSegLds + kW117Waves * (size_t)w117_wave_words(tw, list_max));
 }
 
 // channels (X, Y) of 117-bin b (Appendix A of SURVEY.md; the same layout fold117 builds)
@@ -727,7 +740,9 @@ __device__ __forceinline__ void w117_load_halo(const KArgs& a, const uint32_t* _
     const int yy = g.y0 - 1 + q % TY, zz = g.z0 - 1 + q / TY, xx = g.x0 - 1 + r;
     const bool in = e < n && (unsigned)xx < (unsigned)a.gx && (unsigned)yy < (unsigned)a.gy &&
                     (unsigned)zz < (unsigned)a.gz;
-    hv[j] = in ? fgrid[((int64_t)zz * a.gy + yy) * a.gx + xx] : 0u;
+    // clamped address + select: a "load or zero" per element would be a branch per load
+    const uint32_t v = fgrid[in ? ((int64_t)zz * a.gy + yy) * a.gx + xx : 0];
+    hv[j] = in ? v : 0u;
     q += sq;
     r += sr;
     if (r >= TX) {
@@ -741,6 +756,11 @@ __device__ __forceinline__ void w117_load_halo(const KArgs& a, const uint32_t* _
 __device__ __forceinline__ void wave_lds_fence() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 typedef unsigned short w117_u16x2 __attribute__((ext_vector_type(2)));
+
+// LUT entry (sin | cos << 8) -> the channel pair sin | cos << 16
+__device__ __forceinline__ uint32_t w117_pk(uint32_t l) { return (l & 0xffu) | ((l & 0xff00u) << 8); }
+// binarised colour -> the channel pair beta | (1 - beta) << 16
+__device__ __forceinline__ uint32_t w117_beta(bool bt) { return bt ? 1u : 0x10000u; }
 
 __device__ __forceinline__ uint32_t udot2(uint32_t x, uint32_t y, uint32_t acc) {
   return __builtin_amdgcn_udot2(__builtin_bit_cast(w117_u16x2, x), __builtin_bit_cast(w117_u16x2, y), acc, false);
@@ -758,6 +778,8 @@ __device__ __forceinline__ void c3hlac_wave117_body(const KArgs& a, int bx, int 
   const int32_t* __restrict__ fwork = a.work + fy * a.s_work;
   int32_t* frows = a.rows ? a.rows + fy * a.s_h : nullptr;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  long long* fprof = fy ? nullptr : a.prof;  // diagnostics: wave 0 of each block, first tile
+  C3H_PROF(0, true);
   if (bx == 0 && tid == 0) fworkcnt[(a.epoch + 1) & 1] = 0;  // the next frame's counter
   if (bx < a.zblocks) {
     c3_zero_role(a, bx, fflags, ffeat, fexist);
@@ -771,8 +793,8 @@ __device__ __forceinline__ void c3hlac_wave117_body(const KArgs& a, int bx, int 
   uint32_t* s_ch = s_halo + ((a.tw_max + 3) & ~3) + (((a.list_max + 1) / 2 + 3) & ~3);
   uint16_t* s_ch16 = reinterpret_cast<uint16_t*>(s_ch);
   // work items of this frame: wave gw takes gw, gw + NW, ...; the next two are in flight
-  const int NW = (gdx - a.zblocks) * (kBlock / 64);
-  int wi = (bx - a.zblocks) * (kBlock / 64) + wave;
+  const int NW = (gdx - a.zblocks) * kW117Waves;
+  int wi = (bx - a.zblocks) * kW117Waves + wave;
   int t_cur = wi < a.ntiles ? fwork[wi] : 0;             // speculative: used only below nwork
   int t_nxt = wi + NW < a.ntiles ? fwork[wi + NW] : 0;
   const int nwork = (int)fworkcnt[a.epoch & 1];
@@ -782,7 +804,9 @@ __device__ __forceinline__ void c3hlac_wave117_body(const KArgs& a, int bx, int 
   if (segs_lds)
     for (int e = tid; e < 9 * a.seg_stride; e += kBlock) s_segs[e] = a.segs[e];
   lds_barrier();  // the only workgroup barrier: LUT and segment tables staged
-  if (wi >= nwork) return;
+  C3H_PROF(1, true);
+  if (wave >= kW117Waves || wi >= nwork) return;
+  bool first = true;
   // this lane's two bins (lane, lane + 64) and their channel rows
   int X0, Y0, X1 = 0, Y1 = 0;
   w117_bin_channels(lane, X0, Y0);
@@ -809,6 +833,7 @@ __device__ __forceinline__ void c3hlac_wave117_body(const KArgs& a, int bx, int 
     }
     t_nxt = t_after;
     wave_lds_fence();
+    C3H_PROF(2, first);
     // 3. compact the occupied centres (halo index) into the list
     int nlist = 0;
     {
@@ -836,23 +861,15 @@ __device__ __forceinline__ void c3hlac_wave117_body(const KArgs& a, int bx, int 
       }
     }
     wave_lds_fence();
+    C3H_PROF(3, first);
     // 4. per 64-voxel chunk: lane = voxel builds its 25 channels; lane = bin accumulates
     uint32_t acc0 = 0, acc1 = 0;
     for (int c0 = 0; c0 < nlist; c0 += 64) {
-      uint32_t ch[kW117Ch];
-#pragma unroll
-      for (int x = 0; x < kW117Ch; ++x) ch[x] = 0;
+      // channel pairs packed lo | hi << 16 (every channel < 2^16, sums never carry):
+      // cA = A pairs (r, r_), (g, g_), (b, b_); cB = beta pairs; cN / cQ = neighbour sums
+      uint32_t one = 0, cA[3] = {0, 0, 0}, cB[3] = {0, 0, 0}, cN[3] = {0, 0, 0}, cQ[3] = {0, 0, 0};
       if (c0 + lane < nlist) {
         const int ti = s_list[c0 + lane];
-        const uint32_t w = s_halo[ti];
-        const uint32_t r = (w >> 16) & 0xffu, gg = (w >> 8) & 0xffu, b = w & 0xffu;
-        const uint32_t lr = s_lut[r], lg = s_lut[gg], lb = s_lut[b];
-        ch[0] = 1;
-        ch[1] = lr & 0xffu; ch[2] = (lr >> 8) & 0xffu;
-        ch[3] = lg & 0xffu; ch[4] = (lg >> 8) & 0xffu;
-        ch[5] = lb & 0xffu; ch[6] = (lb >> 8) & 0xffu;
-        const uint32_t br = (int)r > thr_r, bgn = (int)gg > thr_g, bbl = (int)b > thr_b;
-        ch[7] = br; ch[8] = br ^ 1u; ch[9] = bgn; ch[10] = bgn ^ 1u; ch[11] = bbl; ch[12] = bbl ^ 1u;
         uint32_t wn[13];
 #pragma unroll
         for (int k = 0; k < 13; ++k) {  // relative_coordinates (c3_hlac.cpp:180-201), arithmetically
@@ -861,23 +878,44 @@ __device__ __forceinline__ void c3hlac_wave117_body(const KArgs& a, int bx, int 
           const int rdz = k <= 8 ? -1 : 0;
           wn[k] = s_halo[ti + rdx + rdy * TX + rdz * TXY];
         }
+        const uint32_t w = s_halo[ti];
+        const uint32_t r = (w >> 16) & 0xffu, gg = (w >> 8) & 0xffu, b = w & 0xffu;
+        one = 1;
+        cA[0] = w117_pk(s_lut[r]);
+        cA[1] = w117_pk(s_lut[gg]);
+        cA[2] = w117_pk(s_lut[b]);
+        cB[0] = w117_beta((int)r > thr_r);
+        cB[1] = w117_beta((int)gg > thr_g);
+        cB[2] = w117_beta((int)b > thr_b);
 #pragma unroll
         for (int k = 0; k < 13; ++k) {
           const uint32_t v = wn[k];
           if (v) {
             const uint32_t nr = (v >> 16) & 0xffu, ng = (v >> 8) & 0xffu, nb = v & 0xffu;
-            const uint32_t mr = s_lut[nr], mg = s_lut[ng], mb = s_lut[nb];
-            ch[13] += mr & 0xffu; ch[14] += (mr >> 8) & 0xffu;
-            ch[15] += mg & 0xffu; ch[16] += (mg >> 8) & 0xffu;
-            ch[17] += mb & 0xffu; ch[18] += (mb >> 8) & 0xffu;
-            const uint32_t qr = (int)nr > thr_r, qg = (int)ng > thr_g, qb = (int)nb > thr_b;
-            ch[19] += qr; ch[20] += qr ^ 1u; ch[21] += qg; ch[22] += qg ^ 1u; ch[23] += qb; ch[24] += qb ^ 1u;
+            cN[0] += w117_pk(s_lut[nr]);
+            cN[1] += w117_pk(s_lut[ng]);
+            cN[2] += w117_pk(s_lut[nb]);
+            cQ[0] += w117_beta((int)nr > thr_r);
+            cQ[1] += w117_beta((int)ng > thr_g);
+            cQ[2] += w117_beta((int)nb > thr_b);
           }
         }
       }
+      constexpr int RS = 2 * kW117ChStride;  // u16 per channel row
+      s_ch16[lane] = (uint16_t)one;
 #pragma unroll
-      for (int x = 0; x < kW117Ch; ++x) s_ch16[x * (2 * kW117ChStride) + lane] = (uint16_t)ch[x];
+      for (int i = 0; i < 3; ++i) {
+        s_ch16[(1 + 2 * i) * RS + lane] = (uint16_t)cA[i];
+        s_ch16[(2 + 2 * i) * RS + lane] = (uint16_t)(cA[i] >> 16);
+        s_ch16[(7 + 2 * i) * RS + lane] = (uint16_t)cB[i];
+        s_ch16[(8 + 2 * i) * RS + lane] = (uint16_t)(cB[i] >> 16);
+        s_ch16[(13 + 2 * i) * RS + lane] = (uint16_t)cN[i];
+        s_ch16[(14 + 2 * i) * RS + lane] = (uint16_t)(cN[i] >> 16);
+        s_ch16[(19 + 2 * i) * RS + lane] = (uint16_t)cQ[i];
+        s_ch16[(20 + 2 * i) * RS + lane] = (uint16_t)(cQ[i] >> 16);
+      }
       wave_lds_fence();
+      C3H_PROF(4, first && c0 == 0);
       const int np = (min(nlist - c0, 64) + 1) >> 1;  // voxel pairs in this chunk
       const uint32_t* x0r = s_ch + X0 * kW117ChStride;
       const uint32_t* y0r = s_ch + Y0 * kW117ChStride;
@@ -899,6 +937,7 @@ __device__ __forceinline__ void c3hlac_wave117_body(const KArgs& a, int bx, int 
       }
       wave_lds_fence();  // the channel table is rewritten by the next chunk
     }
+    C3H_PROF(5, first);
     // 5. epilogue: normalise (c3_hlac.cpp:233-250), exist gate, row list
     float* out = ffeat + gc.h * 117;
     out[lane] = (float)acc0 * norm117(lane);
@@ -908,8 +947,11 @@ __device__ __forceinline__ void c3hlac_wave117_body(const KArgs& a, int bx, int 
       fexist[gc.h] = exist_from((float)s0, (float)s1);
       if (frows) frows[wi] = (int32_t)gc.h;
     }
+    C3H_PROF(6, first);
+    first = false;
     if (!more) break;
   }
+  C3H_PROF(7, true);
 }
 
 // everything a C3 launch needs (built on the host by build_c3_args, c3hlac.hip)

@@ -374,7 +374,8 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
   ENSURE(ctx->G, (size_t)nf * H * ctx->D);
   // sparse compress: only the non-empty rows of the extract's list (the rest stay stale
   // and every consumer gates them on exist)
-  const bool sparse_g = !ctx->g_valid && fast && ctx->rows_valid && c3h::compress_rows_ok(ctx->F, ctx->Dpad);
+  const bool sparse_g = !ctx->g_valid && fast && ctx->rows_valid &&
+                        (c3h::compress_rows_ok(ctx->F, ctx->Dpad) || c3h::compress2_fits(ctx->F, ctx->D));
   if (ctx->capture && !sparse_g) return 0;  // not pipelinable: the caller falls back
   if (!ctx->g_valid && !sparse_g) {  // nf == 1 here
     Timed t(ctx, 2);
@@ -440,6 +441,8 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
     q.r = ctx->r;
     q.Opad = ctx->Opad;
     q.mpg = std::max(1, 64 / ctx->r);
+    q.v2 = ctx->qw2.p && c3h::score2_fits(ctx->D, ctx->M, ctx->r) ? 1 : 0;
+    q.qw = ctx->qw2.p;
     q.scores = ctx->scores.p;
     q.nmodes = rm.n;
     q.pstart[0] = 0;
@@ -482,7 +485,7 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
     if (sparse_g) {
       sc = c3h::SparseCompress{ctx->feat.p, ctx->axis_pt.p, ctx->fmax.p, ctx->G.p, ctx->rows.p,
                                ctx->tileflags.p + 2 + (ctx->tile_epoch & 1), ctx->F, ctx->D, ctx->Dpad,
-                               ctx->fmax_len, H, H * ctx->F, H * ctx->D, H, ctx->tf_stride};
+                               ctx->fmax_len, H, H * ctx->F, H * ctx->D, H, ctx->tf_stride, ctx->pw2.p};
       ctx->g_valid = true;
       ctx->g_sparse = true;
     }
@@ -1111,6 +1114,12 @@ int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_
   }
   ENSURE(ctx->axis_pt, pt.size());
   HIPCHK(hipMemcpy(ctx->axis_pt.p, pt.data(), pt.size() * 4, hipMemcpyHostToDevice));
+  if (c3h::compress2_fits(F, D)) {  // per-wave column slices for the lane-per-row compress
+    std::vector<float> pw(c3h::compress2_pw_floats(F));
+    c3h::compress2_pack_host(pt.data(), F, D, Dpad, pw.data());
+    ENSURE(ctx->pw2, pw.size());
+    HIPCHK(hipMemcpy(ctx->pw2.p, pw.data(), pw.size() * 4, hipMemcpyHostToDevice));
+  }
   ENSURE(ctx->axis_q, (size_t)M * r * D);
   HIPCHK(hipMemcpy(ctx->axis_q.p, axis_q, (size_t)M * r * D * 4, hipMemcpyHostToDevice));
   // transposed basis for the fast score path: qt[d][m*r + i] = axis_q[m][i][d]
@@ -1122,6 +1131,12 @@ int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_
       for (int d = 0; d < D; ++d) qt[(size_t)d * Opad + m * r + i] = axis_q[((size_t)m * r + i) * D + d];
   ENSURE(ctx->qt, qt.size());
   HIPCHK(hipMemcpy(ctx->qt.p, qt.data(), qt.size() * 4, hipMemcpyHostToDevice));
+  if (c3h::score2_fits(D, M, r)) {  // per-wave basis windows for the lane-per-position scoring
+    std::vector<float> qw(c3h::score2_qw_floats(D));
+    c3h::score2_pack_host(axis_q, M, r, D, qw.data());
+    ENSURE(ctx->qw2, qw.size());
+    HIPCHK(hipMemcpy(ctx->qw2.p, qw.data(), qw.size() * 4, hipMemcpyHostToDevice));
+  }
   ctx->Opad = Opad;
   ctx->fmax_len = feature_max_len;
   if (feature_max_len > 0) {

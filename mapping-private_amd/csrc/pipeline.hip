@@ -20,7 +20,7 @@
 #include <vector>
 
 #include "c3hlac_dev.h"
-#include "search_dev.h"
+#include "search2_dev.h"
 
 namespace c3h {
 namespace {
@@ -31,7 +31,7 @@ struct TickArgs {
   int s_gx, s_groups;
   SparseSearch gq;                   // compress + gate role
   CompressRows cr;
-  int g_ngate, g_ncomp;
+  int g_ngate, g_ncomp, g_comp2;
   KArgs ka;                          // tile role
   int t_grid;
   OccArgs oa;                        // occupancy role
@@ -59,15 +59,17 @@ __device__ __forceinline__ void tick_roles(const TickArgs& t, uint32_t* tick_sme
   if (b < t.n_cg) {
     const int per = t.g_ngate + t.g_ncomp, f = b / per, r = b - f * per;
     if (r < t.g_ngate) gate_body(t.gq, r, f);
+    else if (t.g_comp2) compress2_body(t.cr, r - t.g_ngate, t.g_ncomp, f, reinterpret_cast<float*>(tick_smem));
     else compress_rows_body(t.cr, r - t.g_ngate, t.g_ncomp, f, reinterpret_cast<float*>(tick_smem));
     return;
   }
   b -= t.n_cg;
   const int per = t.s_gx * t.s_groups, f = b / per, r = b - f * per;
-  score_list_body(t.sq, r % t.s_gx, r / t.s_gx, f, t.s_gx, t.s_groups, reinterpret_cast<float*>(tick_smem));
+  if (t.sq.v2) score2_body(t.sq, r, f, t.s_gx, reinterpret_cast<float*>(tick_smem));
+  else score_list_body(t.sq, r % t.s_gx, r / t.s_gx, f, t.s_gx, t.s_groups, reinterpret_cast<float*>(tick_smem));
 }
 
-__global__ __launch_bounds__(kBlock) void c3h_tick_kernel(TickArgs t) {
+__global__ __launch_bounds__(kBlock, 4) void c3h_tick_kernel(TickArgs t) {
   extern __shared__ __attribute__((aligned(16))) uint32_t tick_smem[];
   if (t.prof && threadIdx.x == 0) t.prof[2 * blockIdx.x] = (long long)wall_clock64();
   tick_roles(t, tick_smem);
@@ -128,21 +130,34 @@ hipError_t launch_tick(const TickParts& p, hipStream_t s) {
   if (p.score) {
     const SparseSearch& a = *p.score;
     t.sq = a;
-    t.s_gx = (int)std::max<int64_t>(1, std::min<int64_t>(sparse_score_blocks(a), env_int("C3H_TICK_SCORE", 32)));
-    t.s_groups = (a.M + a.mpg - 1) / a.mpg;
+    if (a.v2) {  // lane = position: one workgroup per 64 listed positions, all models
+      t.s_gx = (int)std::max<int64_t>(1, std::min<int64_t>(score2_chunks(a.pstart[a.nmodes]),
+                                                           env_int("C3H_TICK_SCORE", 24)));
+      t.s_groups = 1;
+      lds = std::max(lds, score2_lds_bytes(a.D));
+    } else {
+      t.s_gx = (int)std::max<int64_t>(1, std::min<int64_t>(sparse_score_blocks(a), env_int("C3H_TICK_SCORE", 32)));
+      t.s_groups = (a.M + a.mpg - 1) / a.mpg;
+      lds = std::max(lds, score_list_lds_bytes(a.D, a.mpg));
+    }
     t.n_score = t.s_gx * t.s_groups * a.nframes;
-    lds = std::max(lds, score_list_lds_bytes(a.D, a.mpg));
   }
   if (p.gate) {
     const SparseSearch& a = *p.gate;
     const SparseCompress& sc = *p.comp;
     t.gq = a;
     t.cr = CompressRows{sc.feat, sc.PT, sc.fmax, sc.G, sc.rows, sc.nrows, sc.F, sc.D, sc.Dpad,
-                        sc.fmax_len, sc.s_feat, sc.s_G, sc.s_rows, sc.s_nrows};
+                        sc.fmax_len, sc.s_feat, sc.s_G, sc.s_rows, sc.s_nrows, sc.PW};
     t.g_ngate = (int)((a.pstart[a.nmodes] + kBlock - 1) / kBlock);
-    t.g_ncomp = (int)std::max<int64_t>(1, std::min<int64_t>((sc.H + kRR - 1) / kRR, env_int("C3H_TICK_COMP", 32)));
+    t.g_comp2 = sc.PW && compress2_ok(sc.F, sc.D) ? 1 : 0;
+    if (t.g_comp2) {
+      t.g_ncomp = (int)std::max<int64_t>(1, std::min<int64_t>((sc.H + kC2Rows - 1) / kC2Rows, env_int("C3H_TICK_COMP", 16)));
+      lds = std::max(lds, compress2_lds_bytes(sc.F));
+    } else {
+      t.g_ncomp = (int)std::max<int64_t>(1, std::min<int64_t>((sc.H + kRR - 1) / kRR, env_int("C3H_TICK_COMP", 32)));
+      lds = std::max(lds, sizeof(float) * ((size_t)kRK * sc.Dpad + (size_t)kRR * sc.F));
+    }
     t.n_cg = (t.g_ngate + t.g_ncomp) * a.nframes;
-    lds = std::max(lds, sizeof(float) * ((size_t)kRK * sc.Dpad + (size_t)kRR * sc.F));
   }
   if (p.tile) {
     const C3Args c = build_c3_args(*p.tile);
