@@ -253,7 +253,7 @@ struct c3h_ctx {
   std::vector<hipEvent_t> lane_ev;
   hipEvent_t fork_ev = nullptr;
   int nlanes = 3;
-  int nbatch = 4;                   // frames per launch in c3h_run_frames
+  int nbatch = 8;                   // frames per launch in c3h_run_frames
   bool pipeline = true;             // c3h_run_frames: pipelined tick launches (else lanes)
   // host copy of the search setup, replayed into the lanes
   uint64_t setup_version = 0;

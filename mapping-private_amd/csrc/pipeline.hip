@@ -17,6 +17,7 @@
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "c3hlac_dev.h"
@@ -36,13 +37,30 @@ struct TickArgs {
   int t_grid;
   OccArgs oa;                        // occupancy role
   int o_grid;
+  int order;                         // role ids in dispatch order, 4 bits each (first in the low bits)
   long long* prof;                   // diagnostics (C3H_TICK_PROF): [block][2] start, end
 };
 
-// dispatch order: occupancy first (it streams for the whole tick from the first
-// cycle), then tile, compress+gate and scoring in the remaining workgroup slots
-__device__ __forceinline__ void tick_roles(const TickArgs& t, uint32_t* tick_smem) {
+// Workgroups of a role occupy one consecutive block range; t.order lists the role ids
+// (0 occupancy, 1 tile, 2 compress+gate, 3 score) first-dispatched first.  The block index
+// is mapped to the canonical layout (occupancy, tile, compress+gate, score) first, so the
+// role bodies below see one fixed layout.
+__device__ __forceinline__ int tick_canonical_block(const TickArgs& t) {
+  const int n[4] = {t.n_occ, t.n_tile, t.n_cg, t.n_score};
   int b = blockIdx.x;
+  for (int i = 0; i < 4; ++i) {
+    const int r = (t.order >> (4 * i)) & 15;
+    if (b < n[r]) {
+      for (int k = 0; k < r; ++k) b += n[k];
+      return b;
+    }
+    b -= n[r];
+  }
+  return b;
+}
+
+__device__ __forceinline__ void tick_roles(const TickArgs& t, uint32_t* tick_smem) {
+  int b = t.order == 0x3210 ? (int)blockIdx.x : tick_canonical_block(t);
   if (b < t.n_occ) {
     const int f = b / t.o_grid;
     occupancy_bits_body<true>(t.oa, b - f * t.o_grid, f, t.o_grid, tick_smem);
@@ -93,7 +111,8 @@ void tick_prof_dump(const TickArgs& t, long long* d_prof, int total, hipStream_t
   const char* names[4] = {"occ", "tile", "cg", "score"};
   int b0 = 0;
   fprintf(fp, "tick");
-  for (int r = 0; r < 4; ++r) {
+  for (int i = 0; i < 4; ++i) {
+    const int r = (t.order >> (4 * i)) & 15;
     if (n[r]) {
       long long smin = LLONG_MAX, smax = 0, emax = 0;
       double dsum = 0;
@@ -127,6 +146,15 @@ bool tick_ok(const C3Launch& l) {
 hipError_t launch_tick(const TickParts& p, hipStream_t s) {
   TickArgs t{};
   size_t lds = 16;
+  // dispatch order: occupancy first (it streams for the whole tick from the first cycle),
+  // then tile, compress+gate and scoring in the remaining workgroup slots.
+  // C3H_TICK_ORDER="3210" etc. (diagnostics) lists role ids first-dispatched first.
+  t.order = 0x3210;
+  if (const char* o = getenv("C3H_TICK_ORDER"))
+    if (strlen(o) == 4) {
+      t.order = 0;
+      for (int i = 0; i < 4; ++i) t.order |= (o[i] - '0') << (4 * i);
+    }
   if (p.score) {
     const SparseSearch& a = *p.score;
     t.sq = a;
@@ -172,7 +200,9 @@ hipError_t launch_tick(const TickParts& p, hipStream_t s) {
   if (p.occ) {
     const C3Args c = build_c3_args(*p.occ);
     t.oa = c.oa;
-    t.o_grid = std::max(1, std::min(c.g1, env_int("C3H_TICK_OCC", 128)));
+    // ~512 streaming workgroups per tick whatever the batch (2 per CU: the rest of the
+    // slots go to the latency-bound roles); measured best at batch 4 and 8
+    t.o_grid = std::max(1, std::min(c.g1, env_int("C3H_TICK_OCC", std::max(16, 512 / std::max(1, c.nframes)))));
     t.n_occ = t.o_grid * c.nframes;
     lds = std::max(lds, c.occ_lds);
   }

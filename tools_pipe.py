@@ -1,5 +1,5 @@
 """Diagnostics: pipelined c3h_run_frames throughput vs tick role sizes and batch.
-PIPE_CASES="batch,occ,tile,score,comp;..." (empty = default)."""
+PIPE_CASES="batch,occ,tile,score,comp[,roles[,order]];..." (empty = default)."""
 import os
 import sys
 import time
@@ -37,6 +37,11 @@ with c3hlac.Context(0) as ctx:
         else:
             b, occ, tile, score, comp = case.split(",")[:5]
             roles = case.split(",")[5] if len(case.split(",")) > 5 else ""
+            order = case.split(",")[6] if len(case.split(",")) > 6 else ""
+            if order:
+                os.environ["C3H_TICK_ORDER"] = order
+            else:
+                os.environ.pop("C3H_TICK_ORDER", None)
             if roles:
                 os.environ["C3H_TICK_ROLES"] = roles
             else:
@@ -49,7 +54,8 @@ with c3hlac.Context(0) as ctx:
                     os.environ[k] = v
                 else:
                     os.environ.pop(k, None)
-            label = "pipe batch=%s occ=%s tile=%s score=%s comp=%s roles=%s" % (b, occ, tile, score, comp, roles)
+            label = "pipe batch=%s occ=%s tile=%s score=%s comp=%s roles=%s order=%s" % (b, occ, tile, score, comp, roles,
+                                                                                 order)
         best = 1e9
         for rep in range(3):
             torch.cuda.synchronize()
@@ -73,5 +79,5 @@ with c3hlac.Context(0) as ctx:
         kt = ctx.kernel_times(reset=True)
         ctx.timing(False)
         ms, nf = kt["pipeline"]
-        print("%-50s us/frame=%.2f host_enqueue_us/frame=%.2f tick_ms_total=%.3f same_as_first=%s" %
+        print("%-60s us/frame=%.2f host_enqueue_us/frame=%.2f tick_ms_total=%.3f same_as_first=%s" %
               (label, best / N * 1e6, (t1 - t0) / N * 1e6, ms, same), flush=True)
