@@ -130,7 +130,14 @@ struct OccArgs {
 // the 16 rows' (y, z) segments are looked up together.  The flush compacts the set bits
 // into an LDS list and stamps kBlock tiles at a time, every exchange in flight together.
 constexpr int kOccBitsMax = 1 << 17;  // 16 KB of LDS bits
-constexpr int kOccBitsUnroll = 8;     // 16-B non-temporal loads per lane in flight per chunk
+#ifndef C3H_OCC_UNROLL
+#define C3H_OCC_UNROLL 8
+#endif
+#ifndef C3H_OCC_PIPE
+#define C3H_OCC_PIPE 1
+#endif
+constexpr int kOccBitsUnroll = C3H_OCC_UNROLL;  // 16-B non-temporal loads per lane per chunk
+constexpr bool kOccPipe = C3H_OCC_PIPE;         // next chunk's loads issued before this one is used
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 constexpr int kAxLds = 3072;  // axis-map entries kept in LDS (gx + gy + gz <= 3072)
 
@@ -251,7 +258,7 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
   if (c0 < n4) load_chunk(w, c0);
   for (; c0 < n4; c0 += cstride) {
     uint4 nx[kOccBitsUnroll];
-    if (c0 + cstride < n4) load_chunk(nx, c0 + cstride);
+    if (kOccPipe && c0 + cstride < n4) load_chunk(nx, c0 + cstride);
     const uint32_t v0 = (uint32_t)((c0 + tid) << 2);  // nvox < 2^32 (host-checked)
     const uint32_t row0 = v0 / (uint32_t)gx;
     int x = (int)(v0 - row0 * (uint32_t)gx);
@@ -296,8 +303,12 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
         atomicOr(&s_bits[t >> 5], 1u << (t & 31));  // result unused: ds_or_b32, no wait
       }
     }
+    if (kOccPipe) {
 #pragma unroll
-    for (int j = 0; j < kOccBitsUnroll; ++j) w[j] = nx[j];
+      for (int j = 0; j < kOccBitsUnroll; ++j) w[j] = nx[j];
+    } else if (c0 + cstride < n4) {
+      load_chunk(w, c0 + cstride);
+    }
   }
   __syncthreads();
   occ_flush_bits(s_bits, nwords, s_list, s_wsum, epoch, flags, cnt, work);
@@ -817,13 +828,38 @@ __device__ __forceinline__ void c3hlac_wave117_body(const KArgs& a, int bx, int 
   w117_load_halo(a, fgrid, g, true, lane, hv);
   const int thr_r = a.thr_r, thr_g = a.thr_g, thr_b = a.thr_b;
   for (; wi < nwork; wi += NW) {
-    // 1. stage the halo held in registers
-    const int TX = g.lx + 2, TXY = TX * (g.ly + 2);
+    // 1. stage the halo held in registers and, from the same registers, compact the
+    //    occupied centres (halo index, ascending) into the list: no LDS read-back
+    const int TX = g.lx + 2, TY = g.ly + 2, TXY = TX * TY;
     const int nh = TXY * (g.lz + 1);
+    int nlist = 0;
+    {
+      int q = lane / TX, r = lane - q * TX;  // e = lane + 64 j -> (row q = y + TY z, col r)
+      int qy = q % TY, qz = q / TY;
+      const int sq = 64 / TX, sr = 64 - sq * TX;
 #pragma unroll
-    for (int j = 0; j < kW117HaloRegs; ++j)
-      if (lane + 64 * j < nh) s_halo[lane + 64 * j] = hv[j];
-    // 2. prefetch: the tile after next's index, the next tile's halo (in flight during 3-5)
+      for (int j = 0; j < kW117HaloRegs; ++j) {
+        const int e = lane + 64 * j;
+        if (e < nh) s_halo[e] = hv[j];
+        // centre: 1 <= x <= lx, 1 <= y <= ly, z >= 1 (plane 0 is the -z halo)
+        const bool occ = e < nh && hv[j] != 0u && (unsigned)(r - 1) < (unsigned)g.lx &&
+                         (unsigned)(qy - 1) < (unsigned)g.ly && qz >= 1;
+        const unsigned long long m = __ballot(occ);
+        if (occ) s_list[nlist + __popcll(m & ((1ull << lane) - 1))] = (uint16_t)e;
+        nlist += __popcll(m);
+        r += sr;
+        qy += sq;
+        if (r >= TX) {
+          r -= TX;
+          ++qy;
+        }
+        while (qy >= TY) {
+          qy -= TY;
+          ++qz;
+        }
+      }
+    }
+    // 2. prefetch: the tile after next's index, the next tile's halo (in flight during 4-5)
     const W117Geom gc = g;
     const bool more = wi + NW < nwork;
     const int t_after = wi + 2 * NW < a.ntiles ? fwork[wi + 2 * NW] : 0;
@@ -834,33 +870,6 @@ __device__ __forceinline__ void c3hlac_wave117_body(const KArgs& a, int bx, int 
     t_nxt = t_after;
     wave_lds_fence();
     C3H_PROF(2, first);
-    // 3. compact the occupied centres (halo index) into the list
-    int nlist = 0;
-    {
-      const int V = gc.lx * gc.ly * gc.lz;
-      int cx = lane % gc.lx, rq = lane / gc.lx;  // v = lane + 64 i -> (cx, rq = cy + ly * cz)
-      const int sq = 64 / gc.lx, sr = 64 - sq * gc.lx;
-      for (int v0 = 0; v0 < V; v0 += 64) {
-        const int v = v0 + lane;
-        int ti = 0;
-        bool occ = false;
-        if (v < V) {
-          const int cy = rq % gc.ly, cz = rq / gc.ly;
-          ti = (cx + 1) + (cy + 1) * TX + (cz + 1) * TXY;
-          occ = s_halo[ti] != 0;
-        }
-        const unsigned long long m = __ballot(occ);
-        if (occ) s_list[nlist + __popcll(m & ((1ull << lane) - 1))] = (uint16_t)ti;
-        nlist += __popcll(m);
-        cx += sr;
-        rq += sq;
-        if (cx >= gc.lx) {
-          cx -= gc.lx;
-          ++rq;
-        }
-      }
-    }
-    wave_lds_fence();
     C3H_PROF(3, first);
     // 4. per 64-voxel chunk: lane = voxel builds its 25 channels; lane = bin accumulates
     uint32_t acc0 = 0, acc1 = 0;

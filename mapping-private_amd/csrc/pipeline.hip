@@ -11,8 +11,9 @@
 //
 // Dependencies run only from one tick to the next (stream order), so no workgroup ever
 // waits on another role; the batches use four rotating buffer sets (c3h_ctx lanes).
-// Roles are laid out in dispatch order latency-bound first, so their workgroups are
-// resident early and the occupancy stream fills the rest of the chip.
+// Roles are dispatched occupancy first (one streaming workgroup per CU from the first
+// cycle), then tile, compress+gate and scoring in the remaining workgroup slots; other
+// orders measured slower (profiles/r1/o2_tick_order.log).
 #include <algorithm>
 #include <climits>
 #include <cstdio>
@@ -164,7 +165,7 @@ hipError_t launch_tick(const TickParts& p, hipStream_t s) {
       t.s_groups = 1;
       lds = std::max(lds, score2_lds_bytes(a.D));
     } else {
-      t.s_gx = (int)std::max<int64_t>(1, std::min<int64_t>(sparse_score_blocks(a), env_int("C3H_TICK_SCORE", 32)));
+      t.s_gx = (int)std::max<int64_t>(1, std::min<int64_t>(sparse_score_blocks(a), env_int("C3H_TICK_SCORE", 16)));
       t.s_groups = (a.M + a.mpg - 1) / a.mpg;
       lds = std::max(lds, score_list_lds_bytes(a.D, a.mpg));
     }
@@ -200,9 +201,10 @@ hipError_t launch_tick(const TickParts& p, hipStream_t s) {
   if (p.occ) {
     const C3Args c = build_c3_args(*p.occ);
     t.oa = c.oa;
-    // ~512 streaming workgroups per tick whatever the batch (2 per CU: the rest of the
-    // slots go to the latency-bound roles); measured best at batch 4 and 8
-    t.o_grid = std::max(1, std::min(c.g1, env_int("C3H_TICK_OCC", std::max(16, 512 / std::max(1, c.nframes)))));
+    // ~256 streaming workgroups per tick whatever the batch (one per CU): alone they stream
+    // at ~4 TB/s, but the latency-bound roles then see a short HBM queue and the whole tick
+    // is shortest (profiles/r1/v1_occ_variants.log: 19.4 us/frame vs 20.8 at 512)
+    t.o_grid = std::max(1, std::min(c.g1, env_int("C3H_TICK_OCC", std::max(16, 256 / std::max(1, c.nframes)))));
     t.n_occ = t.o_grid * c.nframes;
     lds = std::max(lds, c.occ_lds);
   }

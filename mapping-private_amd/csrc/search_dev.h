@@ -119,6 +119,9 @@ __device__ __forceinline__ void compress_rows_body(const CompressRows& cr, int b
 // |Q_m f|^2 is summed per (position, model) in a fixed order.  The block also emits its
 // per-model best (score, scan order) so rank-1 searches need no second pass.
 constexpr int kFP = 32;
+#ifndef C3H_SCORE_CB
+#define C3H_SCORE_CB 2
+#endif
 constexpr int kOC = 64;  // basis rows per workgroup (whole models)
 constexpr int kScoreGridCap = 128;  // workgroups per (model group, frame) of the score launch
 
@@ -269,20 +272,29 @@ __device__ __forceinline__ void score_list_body(const SparseSearch& b, int bx, i
   // model group of this workgroup: models [m0, m1), basis rows [m0*r, m1*r) padded to oc
   const int m0 = by * a.mpg, m1 = min(a.M, m0 + a.mpg);
   const int row0 = m0 * a.r, oc = ((m1 - m0) * a.r + 15) & ~15;  // <= kOC
-  constexpr int kQW = 160 * kOC / kBlock;  // window floats per lane at the largest D
-  float qwv[kQW];
-#pragma unroll
-  for (int j = 0; j < kQW; ++j) {
-    const int e = j * kBlock + tid, d = e / oc, o = e - d * oc;
-    qwv[j] = e < D * oc ? a.qt[(int64_t)d * Qs + row0 + o] : 0.0f;
+  const int fts = max(D * kFP, kFP * (kOC + 1));
+  // the group's basis window goes straight to LDS (global_load_lds: no VGPR staging, the
+  // score role would otherwise spill in the tick kernel); element e = j*kBlock + tid lands
+  // at qw[e] (wave-uniform base + lane*4); retired by the vmcnt(0) before the GEMM barrier
+  {
+    constexpr int kQW = 160 * kOC / kBlock;  // window floats per lane at the largest D
+    float* qwl = ssm + fts;
+    const int wave = tid >> 6;
+#pragma unroll 4
+    for (int j = 0; j < kQW; ++j) {
+      const int e = j * kBlock + tid, d = e / oc, o = e - d * oc;
+      if (j * kBlock >= D * oc) break;  // uniform
+      if (e < D * oc)
+        __builtin_amdgcn_global_load_lds(a.qt + (int64_t)d * Qs + row0 + o, qwl + j * kBlock + wave * 64, 4, 0, 0);
+    }
   }
   const int n = (int)fcnt[a.epoch & 1];
   const int nch = (n + kFP - 1) / kFP;  // list chunks; chunk c -> workgroups c mod gdx
   if (bx >= nch) {
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
     if (n == 0 && flists && bx == 0 && by == 0) argmax_finalize(a, fpart, flists, fout, 0);  // clean / copy out
     return;
   }
-  const int fts = max(D * kFP, kFP * (kOC + 1));
   float* fT = ssm;                    // D x kFP (k-major box features)
   float* qv = ssm;                    // kFP x (kOC+1), aliases fT after the GEMM
   float* qw = ssm + fts;              // D x oc: this group's whole basis window
@@ -293,9 +305,6 @@ __device__ __forceinline__ void score_list_body(const SparseSearch& b, int bx, i
   long long* ent = reinterpret_cast<long long*>(rng + kFP + (kFP & 1));
   double* bsc = reinterpret_cast<double*>(ent + kFP);  // kFP * mpg
   const int xyn = a.xn * a.yn;
-#pragma unroll
-  for (int j = 0; j < kQW; ++j)  // parked once; read by every chunk's GEMM
-    if (j * kBlock + tid < D * oc) qw[j * kBlock + tid] = qwv[j];
   for (int ch = bx; ch < nch; ch += gdx) {
     const int64_t e0 = (int64_t)ch * kFP;
     if (tid < kFP) {
@@ -332,15 +341,16 @@ __device__ __forceinline__ void score_list_body(const SparseSearch& b, int bx, i
       const int ncell = ok ? xr * yr * zr : 0;
       const float4* G4 = reinterpret_cast<const float4*>(fG);
       constexpr int kSlots = 4;  // d4 values per thread handled together (D4 <= 64)
+      constexpr int kCB = C3H_SCORE_CB;  // box cells whose loads are in flight together
       float4 s[kSlots];
 #pragma unroll
       for (int q = 0; q < kSlots; ++q) s[q] = make_float4(0.f, 0.f, 0.f, 0.f);
       for (int d4b = 0; d4b < D4; d4b += kSlots * kDG) {
-        for (int c0 = 0; c0 < ncell; c0 += 4) {
-          float4 g[4][kSlots];
-          bool lv[4];
+        for (int c0 = 0; c0 < ncell; c0 += kCB) {
+          float4 g[kCB][kSlots];
+          bool lv[kCB];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
+          for (int k = 0; k < kCB; ++k) {
             const int c = c0 + k;
             const int dx = c % xr, dy = (c / xr) % yr, dz = c / (xr * yr);
             const int hh = h + dz * xyn + dy * a.xn + dx;
@@ -352,7 +362,7 @@ __device__ __forceinline__ void score_list_body(const SparseSearch& b, int bx, i
             }
           }
 #pragma unroll
-          for (int k = 0; k < 4; ++k)
+          for (int k = 0; k < kCB; ++k)
 #pragma unroll
             for (int q = 0; q < kSlots; ++q)
               if (lv[k]) {
@@ -375,6 +385,7 @@ __device__ __forceinline__ void score_list_body(const SparseSearch& b, int bx, i
         }
       }
     }
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the basis window's LDS-DMA (first chunk)
     lds_barrier();
     C3H_SPROF(2);
     if (tid < kFP) {
