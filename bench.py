@@ -213,7 +213,7 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": pmc_traffic(),
+            "traffic": pmc_traffic(tick_frames / n_ticks),
             "algorithmic_bytes_per_launch": alg_bytes,
             "algorithmic_bytes_per_frame": algorithmic_bytes_c3(GRID, H, VARIANT),
             "frames_per_launch": BATCH,
@@ -230,16 +230,17 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic():
-    """HBM bytes per C3-stage launch (occupancy + tile kernel) from the committed
-    rocprofv3 --pmc summary of this build (scripts_pmc.sh -> tools_pmc_summary.py):
-    FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE.  PMC needs its own profiler pass, so
+def pmc_traffic(frames_per_tick):
+    """HBM bytes per tick launch (the bench's average frames per tick, fill/drain
+    included, like `achieved`) from the committed rocprofv3 --pmc summary of this build
+    (scripts_pmc.sh -> tools_pmc_summary.py): FETCH_SIZE x2 (gfx950 correction) +
+    WRITE_SIZE of c3h_tick_kernel, per frame through the pipeline.  PMC needs its own profiler pass, so
     it cannot be collected inside the timed run; None when no summary is committed."""
     f = ROOT / "profiles" / "pmc_c3_traffic.json"
     if not f.exists():
         return None
-    per_frame = json.load(open(f)).get("c3_stage_hbm_bytes_per_frame")
-    return per_frame * BATCH if per_frame is not None else None
+    per_frame = json.load(open(f)).get("tick_hbm_bytes_per_frame")
+    return per_frame * frames_per_tick if per_frame is not None else None
 
 
 def cpu_baseline(pts, seconds):
