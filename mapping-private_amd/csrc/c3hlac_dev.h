@@ -83,6 +83,7 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t n) {
 // into these host-built tables.
 constexpr int kOccUnroll = 16;  // 16-B loads per thread in flight per chunk (256 B / lane)
 constexpr int kOccSet = 1024;  // LDS set of tiles touched by one workgroup (4 KB)
+constexpr int kOccProbes = 32;  // linear-probe bound of the set
 
 // Flags are epoch stamps: tile t is non-empty in this frame iff flags[t] == epoch, so
 // nothing is reset between frames.  Each workgroup streams contiguous 16-KB chunks
@@ -100,7 +101,9 @@ __device__ __forceinline__ void set_insert(int* s_set, int t, uint32_t epoch, ui
                                            uint32_t* cnt, int32_t* work) {
   int h = (int)(((uint32_t)t * 0x9E3779B1u) >> 22);  // 10-bit hash
   static_assert(kOccSet == 1024 && kOccSet % kBlock == 0, "set slots per thread");
-  for (int probe = 0; probe < kOccSet; ++probe, h = (h + 1) & (kOccSet - 1)) {
+  // bounded probing: once the set is (nearly) full -- dense grids, tiny subdivisions --
+  // a miss costs a few probes and a direct stamp, not a walk over the whole table
+  for (int probe = 0; probe < kOccProbes; ++probe, h = (h + 1) & (kOccSet - 1)) {
     const int cur = s_set[h];
     if (cur == t) return;
     if (cur == -1) {
@@ -129,7 +132,7 @@ struct OccArgs {
 // divides the chunk stride (4 voxels, at most 4 x-segments, looked up once per chunk),
 // the 16 rows' (y, z) segments are looked up together.  The flush compacts the set bits
 // into an LDS list and stamps kBlock tiles at a time, every exchange in flight together.
-constexpr int kOccBitsMax = 1 << 17;  // 16 KB of LDS bits
+constexpr int kOccBitsMax = 1 << 18;  // 32 KB of LDS bits (512^3 at S >= 8)
 #ifndef C3H_OCC_UNROLL
 #define C3H_OCC_UNROLL 8
 #endif

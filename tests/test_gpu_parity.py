@@ -391,3 +391,50 @@ def test_run_frames_lanes_match_sequential(ctx, lanes, batch, rank, pipe):
     ctx.set_lanes(3)
     ctx.set_batch(4)
     ctx.set_pipeline(1)
+
+
+def test_config5_dense_512_periodic(ctx):
+    """Config 5 at full size (512^3, 100 % occupancy, C3-HLAC-981, compress 981->100,
+    10 models x r=20): size-independent property checks.  The grid is periodic with the
+    subdivision side (10), so every subdivision whose half-neighbourhood lies inside the
+    grid (indices 1..50 per axis) must hold exactly the features of the centre
+    subdivision of a 30^3 periodic grid from the numpy oracle; every box position over
+    those subdivisions must score bit-identically (fixed-order box sums) and match the
+    float64 score of that feature row within SCORE_RTOL_F64."""
+    G, S, n = 512, 10, 52
+    base = synth.dense_words(S, seed=51)
+    small = np.tile(base, (3, 3, 3))
+    fr, exr, _ = npr.c3hlac(small, 981, THR, S)
+    ref, ref_ex = fr[13], exr[13]  # subdivision (1, 1, 1) of 3^3
+    words = np.tile(base, (n, n, n))[:G, :G, :G]
+    ctx.set_grid(np.ascontiguousarray(words).reshape(-1), (G, G, G))
+    del words
+    sb, hn = ctx.extract(981, THR, S)
+    assert sb == (n, n, n) and hn == n ** 3
+    f = ctx.features().reshape(n, n, n, 981)
+    for z in range(1, n - 1):  # per slab: bounded host temporaries
+        assert (f[z, 1:n - 1, 1:n - 1] == ref).all(), "interior subdivision differs (z=%d)" % z
+    ex = ctx.exist().reshape(n, n, n)
+    assert (ex[1:n - 1, 1:n - 1, 1:n - 1] == ref_ex).all()
+    del f
+    M, D, R = 10, 100, 20
+    axis_t, var, axis_q = synth.random_bases(981, D, M, R, seed=52)
+    ctx.search_setup(axis_t, var, axis_q)
+    ctx.set_rank(1)
+    lists, nm = ctx.search((2, 2, 2), 100)
+    P = (n - 1) ** 3
+    sc = ctx.scores().reshape(M, n - 1, n - 1, n - 1)
+    assert sc.size == M * P and (sc > 0).all()  # dense: every position passes the gate
+    inner = sc[:, 1:n - 2, 1:n - 2, 1:n - 2].reshape(M, -1)
+    assert (inner == inner[:, :1]).all(), "interior positions must score bit-identically"
+    g = synth.whiten(axis_t, var).astype(np.float64) @ ref.astype(np.float64)
+    q = axis_q.astype(np.float64) @ g
+    s64 = np.sqrt((q * q).sum(1)) / np.sqrt(g @ g)
+    np.testing.assert_allclose(inner[:, 0], s64, rtol=SCORE_RTOL_F64)
+    # rank 1 = first maximum in scan order over all positions (boundary ones included)
+    flat = sc.reshape(M, -1)
+    for m in range(M):
+        p = int(np.argmax(flat[m]))
+        assert float(lists[m, 0]["score"]) == flat[m, p]
+        assert (int(lists[m, 0]["z"]), int(lists[m, 0]["y"]), int(lists[m, 0]["x"])) == \
+            np.unravel_index(p, (n - 1,) * 3)
