@@ -98,6 +98,19 @@ int c3h_get_grid_info(c3h_ctx* ctx, c3h_grid_info* info);
  * context on the same device); valid until the next voxelize / set_grid. */
 int c3h_grid_device_ptr(c3h_ctx* ctx, const uint32_t** out);
 
+/* ---- automatic colour threshold (color_voxel_recognition/test/calc_scene_auto_threshold.cpp)
+ * c3h_color_histogram replaces the per-voxel loop of calc_scene_auto_threshold.cpp:92-108
+ * over the downsampled cloud (one voxel = one count; colours = the grid's centroid colours):
+ * hist[c * 256 + v] (c = 0 r, 1 g, 2 b) counts the occupied voxels of the context's current
+ * grid with channel c == v.  accumulate != 0 adds to hist (several frames, as the tool's
+ * file loop does); 0 overwrites it.  hist is host memory, 768 int64.
+ * c3h_auto_threshold is the tool's arithmetic (:111-146): total/cumulative averages and the
+ * first j in 1..255 maximising the between-class variance, per channel; thr_out[3];
+ * total_ave_out[3] (may be NULL) = the printed "totalAverage".  An empty histogram gives
+ * C3H_ERR_ARG (the tool divides by zero). */
+int c3h_color_histogram(c3h_ctx* ctx, int64_t* hist, int32_t accumulate);
+int c3h_auto_threshold(const int64_t* hist, int32_t thr_out[3], double* total_ave_out);
+
 /* C3HLAC{981,117}Estimation::setVoxelFilter + compute (c3_hlac/src/c3_hlac.cpp:204-416),
  * as called by extractC3HLACSignature981/117 (c3_hlac_tools.hpp:134-202).  Writes the
  * subdivision counts (getSubdivNum) and the number of feature vectors (hist_num; 0 for

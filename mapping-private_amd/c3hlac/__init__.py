@@ -137,6 +137,14 @@ class Context:
             self._chk(self.lib.c3h_get_exist(self.h, ptr(out), 0), "get_exist")
         return out
 
+    def color_histogram(self, hist=None):
+        """Per-channel 256-bin histograms (3, 256) int64 of the current grid's occupied voxel
+        colours (calc_scene_auto_threshold.cpp:92-108); adds into `hist` when given."""
+        out = np.zeros((3, 256), np.int64) if hist is None else hist
+        assert out.dtype == np.int64 and out.shape == (3, 256) and out.flags.c_contiguous
+        self._chk(self.lib.c3h_color_histogram(self.h, ptr(out), 0 if hist is None else 1), "color_histogram")
+        return out
+
     # --- search -----------------------------------------------------------------------
     def search_setup(self, axis_p, var, axis_q, feature_max=None):
         """axis_p: (D,F) or None; var: (D,) or None (whitening); axis_q: (M,r,D)."""
@@ -224,6 +232,15 @@ class Context:
         cnt = np.zeros(_capi.NTIMERS, np.int32)
         self._chk(self.lib.c3h_kernel_times(self.h, ptr(ms), ptr(cnt), int(bool(reset))), "kernel_times")
         return {n: (float(ms[i]), int(cnt[i])) for i, n in enumerate(TIMER_NAMES)}
+
+
+def auto_threshold(hist):
+    """calc_scene_auto_threshold.cpp:111-146 on (3, 256) histograms -> (thr (3,), total_ave (3,))."""
+    h = np.ascontiguousarray(hist, dtype=np.int64)
+    thr = np.zeros(3, np.int32)
+    ave = np.zeros(3, np.float64)
+    check(_capi.load().c3h_auto_threshold(ptr(h), ptr(thr), ptr(ave)), None, "auto_threshold")
+    return thr, ave
 
 
 def remove_overlap(lists, ranges):

@@ -121,6 +121,8 @@ struct C3Launch {
 
 int64_t c3hlac_grid(const C3Launch& a);  // persistent grid of the tile kernel
 hipError_t launch_c3hlac(const C3Launch& a, hipStream_t s);
+// colour.hip: per-channel 256-bin histograms of the occupied voxels (adds into out[768])
+hipError_t launch_colour_hist(const uint32_t* grid, int64_t nvox, unsigned long long* out, hipStream_t s);
 hipError_t launch_c3_finalize(const unsigned long long* acc64, int64_t hist_num, int variant,
                               float* feat, int32_t* exist, int nframes, hipStream_t s);
 
@@ -301,6 +303,7 @@ struct c3h_ctx {
   uint32_t search_epoch = 0;
   int gcnt_frames = 0;
   c3h::DevBuf<long long> prof;      // diagnostics (C3H_PROF)
+  c3h::DevBuf<unsigned long long> chist;  // colour histograms (c3h_color_histogram): 3 x 256
 
   std::vector<int32_t> h_segs;      // host copy (kept alive for the async upload)
   c3h::DevBuf<uint32_t> lut;        // 256 packed (sin | cos<<8), two variants

@@ -766,6 +766,58 @@ int c3h_get_grid(c3h_ctx* ctx, uint32_t* out, int on_device) {
   return C3H_OK;
 }
 
+// calc_scene_auto_threshold.cpp:92-108: one count per occupied voxel and channel
+int c3h_color_histogram(c3h_ctx* ctx, int64_t* hist, int32_t accumulate) {
+  if (!ctx || !hist) return C3H_ERR_ARG;
+  if (!ctx->have_grid) return fail(ctx, C3H_ERR_STATE, "color_histogram: no grid");
+  HIPCHK(hipSetDevice(ctx->device));
+  ENSURE(ctx->chist, 768);
+  HIPCHK(hipMemsetAsync(ctx->chist.p, 0, 768 * sizeof(unsigned long long), ctx->stream));
+  HIPCHK(c3h::launch_colour_hist(ctx->grid_ptr, grid_voxels(ctx), ctx->chist.p, ctx->stream));
+  unsigned long long h[768];
+  HIPCHK(hipMemcpyAsync(h, ctx->chist.p, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  for (int i = 0; i < 768; ++i) hist[i] = (accumulate ? hist[i] : 0) + (int64_t)h[i];
+  return C3H_OK;
+}
+
+// calc_scene_auto_threshold.cpp:111-146 (int64 where the tool's int sums would overflow,
+// i.e. identical results whenever the tool's own arithmetic is defined)
+int c3h_auto_threshold(const int64_t* hist, int32_t thr_out[3], double* total_ave_out) {
+  if (!hist || !thr_out) return C3H_ERR_ARG;
+  int64_t total = 0;
+  for (int j = 0; j < 256; ++j) total += hist[j];
+  if (total <= 0) return C3H_ERR_ARG;
+  for (int c = 0; c < 3; ++c) {
+    const int64_t* h = hist + 256 * c;
+    for (int j = 0; j < 256; ++j)
+      if (h[j] < 0) return C3H_ERR_ARG;
+    double tot_ave = 0;  // :113-118
+    for (int j = 0; j < 256; ++j) tot_ave += (double)(j * h[j]);
+    tot_ave *= 1 / (double)total;
+    int64_t each_num = h[0], acc = 0;  // :120-133 (eachAve[0] = 0)
+    double max_var = 0;
+    int thr = 0;
+    for (int j = 1; j < 256; ++j) {  // :135-146, fused with the cumulative pass
+      each_num += h[j];
+      acc += j * h[j];
+      const double each_ave = each_num == 0 ? 0.0 : (double)acc / (double)each_num;
+      if (each_num != 0) {
+        if (each_num == total) break;
+        const double ave_sub = each_ave - tot_ave;
+        const double var = ave_sub * ave_sub * (each_num / (double)(total - each_num));
+        if (var > max_var) {
+          max_var = var;
+          thr = j;
+        }
+      }
+    }
+    thr_out[c] = thr;
+    if (total_ave_out) total_ave_out[c] = tot_ave;
+  }
+  return C3H_OK;
+}
+
 static int compute_leaf_layout(c3h_ctx* ctx, int32_t* d_out) {
   const int64_t nvox = grid_voxels(ctx);
   const int64_t nb = c3h::leaf_layout_blocks(nvox);

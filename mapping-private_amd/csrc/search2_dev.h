@@ -51,7 +51,7 @@ __device__ __forceinline__ void compress2_body(const CompressRows& cr, int bid, 
   const float* __restrict__ fmax = cr.fmax;
   float* __restrict__ G = cr.G + f * cr.s_G;
   const int32_t* __restrict__ rows = cr.rows + f * cr.s_rows;
-  const int F = cr.F, D = cr.D, Dpad = cr.Dpad, fmax_len = cr.fmax_len;
+  const int F = cr.F, D = cr.D, fmax_len = cr.fmax_len;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int cpw = (D + 3) >> 2, c0 = wave * cpw;

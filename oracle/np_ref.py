@@ -269,3 +269,48 @@ def replay(mode_scores, r, rank, lists=None):
                             Lm[i] = [float(dot), x, y, z, mode]
                         break
     return lists
+
+
+# ---------------------------------------------------------------- auto colour threshold
+def color_histogram(words):
+    """calc_scene_auto_threshold.cpp:92-108: per occupied voxel of the downsampled cloud
+    (= the packed grid's non-empty words) one count in each channel's 256-bin histogram."""
+    w = np.asarray(words, dtype=np.uint32).reshape(-1)
+    w = w[w != 0]
+    r, g, b = (w >> 16) & 255, (w >> 8) & 255, w & 255
+    return np.stack([np.bincount(c.astype(np.int64), minlength=256) for c in (r, g, b)]).astype(np.int64)
+
+
+def auto_threshold(hist):
+    """calc_scene_auto_threshold.cpp:111-146, loop for loop (Python ints: exact where the
+    tool's int sums are defined) -> (threshold[3], totalAve[3])."""
+    hist = np.asarray(hist, dtype=np.int64)
+    total = int(hist[0].sum())
+    if total <= 0:
+        raise ValueError("empty histogram (the tool divides by zero)")
+    thr, ave = [], []
+    for i in range(3):
+        h = [int(v) for v in hist[i]]
+        total_ave = 0.0
+        for j in range(256):  # :113-118
+            total_ave += j * h[j]
+        total_ave *= 1 / float(total)
+        each_ave, each_num = [0.0] * 256, [0] * 256  # :120-133
+        each_num[0] = h[0]
+        tmp = 0
+        for j in range(1, 256):
+            each_num[j] = each_num[j - 1] + h[j]
+            tmp += j * h[j]
+            each_ave[j] = 0.0 if each_num[j] == 0 else tmp / each_num[j]
+        max_var, t = 0.0, 0  # :135-146
+        for j in range(1, 256):
+            if each_num[j] != 0:
+                if each_num[j] == total:
+                    break
+                ave_sub = each_ave[j] - total_ave
+                var = ave_sub * ave_sub * (each_num[j] / float(total - each_num[j]))
+                if var > max_var:
+                    max_var, t = var, j
+        thr.append(t)
+        ave.append(total_ave)
+    return np.array(thr, np.int32), np.array(ave)
