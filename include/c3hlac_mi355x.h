@@ -111,6 +111,26 @@ int c3h_grid_device_ptr(c3h_ctx* ctx, const uint32_t** out);
 int c3h_color_histogram(c3h_ctx* ctx, int64_t* hist, int32_t accumulate);
 int c3h_auto_threshold(const int64_t* hist, int32_t thr_out[3], double* total_ave_out);
 
+/* ---- wire formats (host only, no device) ----
+ * c3h_pcd_read_xyzrgb: a PCD point cloud as the reference's tools load it
+ * (pcl::io::loadPCDFile, e.g. color_voxel_recognition/test/calc_scene_auto_threshold.cpp:89):
+ * v0.7 header with FIELDS x y z rgb (any order, other fields skipped; 4-byte scalars),
+ * DATA ascii or binary.  Binary data sits right after the header, or at the next 4096-byte
+ * page for ROS-era PCL writers (the reference's demo clouds); the file size decides.
+ * out: n x 4 floats (x, y, z, rgb bits) -- the c3h_voxelize input layout; out == NULL
+ * returns the point count in *n, else *n is the capacity in points on entry.
+ * c3h_feature_pcd_read: readFeature (c3_hlac/include/c3_hlac/c3_hlac_tools.hpp:46-71):
+ * COUNT = dim, POINTS = rows, "%f " scans; out == NULL returns the sizes, else *rows and
+ * *dim are the capacity on entry.
+ * c3h_feature_pcd_write: writeFeature (c3_hlac_tools.hpp:83-113): "%f " per value, one row
+ * per line, all-zero rows dropped when remove_zero; fields = the FIELDS name (NULL =
+ * "descriptor" as there; grsd_colorCHLAC_tools.hpp:32-58 writes "vfh").
+ * Errors: C3H_ERR_NOTFOUND (open), C3H_ERR_FORMAT (malformed), C3H_ERR_ARG. */
+int c3h_pcd_read_xyzrgb(const char* path, float* out, int64_t* n);
+int c3h_feature_pcd_read(const char* path, float* out, int64_t* rows, int32_t* dim);
+int c3h_feature_pcd_write(const char* path, const float* feat, int64_t rows, int32_t dim,
+                          int32_t remove_zero, const char* fields);
+
 /* C3HLAC{981,117}Estimation::setVoxelFilter + compute (c3_hlac/src/c3_hlac.cpp:204-416),
  * as called by extractC3HLACSignature981/117 (c3_hlac_tools.hpp:134-202).  Writes the
  * subdivision counts (getSubdivNum) and the number of feature vectors (hist_num; 0 for

@@ -243,6 +243,39 @@ def auto_threshold(hist):
     return thr, ave
 
 
+def read_pcd(path):
+    """c3h_pcd_read_xyzrgb -> (n, 4) float32 x, y, z, rgb-bits (the c3h_voxelize input)."""
+    lib = _capi.load()
+    n = C.c_int64(0)
+    check(lib.c3h_pcd_read_xyzrgb(str(path).encode(), None, C.byref(n)), None, "pcd_read")
+    out = np.zeros((n.value, 4), np.float32)
+    if n.value:
+        check(lib.c3h_pcd_read_xyzrgb(str(path).encode(), ptr(out), C.byref(n)), None, "pcd_read")
+    return out
+
+
+def read_feature(path):
+    """readFeature (c3_hlac_tools.hpp:46-71) -> (rows, dim) float32."""
+    lib = _capi.load()
+    rows, dim = C.c_int64(0), C.c_int32(0)
+    check(lib.c3h_feature_pcd_read(str(path).encode(), None, C.byref(rows), C.byref(dim)), None, "feature_read")
+    out = np.zeros((rows.value, dim.value), np.float32)
+    if out.size:
+        check(lib.c3h_feature_pcd_read(str(path).encode(), ptr(out), C.byref(rows), C.byref(dim)), None,
+              "feature_read")
+    return out
+
+
+def write_feature(path, feat, remove_zero=True, fields=None):
+    """writeFeature (c3_hlac_tools.hpp:83-113)."""
+    f = np.ascontiguousarray(feat, dtype=np.float32)
+    if f.ndim == 1:
+        f = f[None, :]
+    check(_capi.load().c3h_feature_pcd_write(str(path).encode(), ptr(f), f.shape[0], f.shape[1],
+                                             int(bool(remove_zero)), None if fields is None else fields.encode()),
+          None, "feature_write")
+
+
 def remove_overlap(lists, ranges):
     """SearchObjMulti::removeOverlap on (M, rank) DET_DTYPE lists (host function)."""
     lists = np.ascontiguousarray(lists, dtype=DET_DTYPE)

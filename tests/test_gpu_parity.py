@@ -438,3 +438,30 @@ def test_config5_dense_512_periodic(ctx):
         assert float(lists[m, 0]["score"]) == flat[m, p]
         assert (int(lists[m, 0]["z"]), int(lists[m, 0]["y"]), int(lists[m, 0]["x"])) == \
             np.unravel_index(p, (n - 1,) * 3)
+
+
+# bowl1_0000.pcd is a real Kinect capture, its coordinates quantised to 1 mm: at leaf 4 mm
+# 10 of its 945 voxel centroids round across a cell boundary (floor(c * inv_leaf) is not the
+# voxel's own index).  The reference takes the subdivision (c3_hlac.cpp:177-178) and the
+# neighbour base (PCL getNeighborCentroidIndices) of such a voxel from its float centroid;
+# the GPU path takes both from the voxel index.  Known parity gap, see DESIGN.md §5.
+_CENTROID_GAP = pytest.mark.xfail(strict=True, reason="centroid-boundary voxels (DESIGN.md §5)")
+
+
+@pytest.mark.parametrize("name,leaf", [("noisy_torus_blue.pcd", 0.005),
+                                       pytest.param("bowl1_0000.pcd", 0.004, marks=_CENTROID_GAP),
+                                       ("tmp_normal.pcd", 0.005), ("obj_torus_black.pcd", 0.004)])
+def test_reference_clouds_end_to_end(ctx, name, leaf):
+    """The reference's own demo clouds (tests/golden/ref_fixtures/pcd): c3h_pcd_read_xyzrgb ->
+    voxelise -> C3-HLAC-981/117 on the GPU, against the oracle on the same points (voxel
+    indices, leaf layout, packed colours bit-exact; exact-integer features bit-exact)."""
+    from pathlib import Path
+    pts = c3hlac.read_pcd(Path(__file__).resolve().parent / "golden" / "ref_fixtures" / "pcd" / name)
+    gi = ctx.voxelize(pts, leaf)
+    g, layout, cloud = po.voxelize(pts, leaf)
+    assert list(gi.div_b) == list(g.div_b) and gi.n_occ == g.n_occ
+    assert np.array_equal(ctx.leaf_layout(), layout)
+    for variant in (981, 117):
+        sb, hn = ctx.extract(variant, THR, 5)
+        fe, _, _ = po.c3hlac(g, layout, cloud, variant, THR, leaf, 5, exact=True)
+        assert np.array_equal(ctx.features(), fe)
