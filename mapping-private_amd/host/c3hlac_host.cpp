@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <iostream>
 #include <sstream>
 
 namespace c3hlac {
@@ -151,6 +152,67 @@ void getVoxelGrid(VoxelGrid& grid, const std::vector<PointXYZRGB>& input,
   if (info.n_occ > 0)
     grid.ctx_.check(c3h_get_downsampled(grid.ctx_.get(), reinterpret_cast<float*>(output.data()), 0),
                     "c3h_get_downsampled");
+}
+
+int loadPCDFile(const std::string& file_name, std::vector<PointXYZRGB>& cloud) {
+  int64_t n = 0;
+  if (c3h_pcd_read_xyzrgb(file_name.c_str(), nullptr, &n) != C3H_OK) return -1;
+  cloud.resize((size_t)n);
+  if (n > 0 && c3h_pcd_read_xyzrgb(file_name.c_str(), reinterpret_cast<float*>(cloud.data()), &n) != C3H_OK)
+    return -1;
+  return 0;
+}
+
+void readFeature(const char* name, std::vector<std::vector<float> >& feature) {
+  feature.resize(0);
+  int64_t rows = 0;
+  int32_t dim = 0;
+  int rc = c3h_feature_pcd_read(name, nullptr, &rows, &dim);
+  if (rc != C3H_OK) throw Error(rc, std::string("readFeature: ") + name);
+  std::vector<float> buf((size_t)rows * dim);
+  if (!buf.empty()) {
+    rc = c3h_feature_pcd_read(name, buf.data(), &rows, &dim);
+    if (rc != C3H_OK) throw Error(rc, std::string("readFeature: ") + name);
+  }
+  for (int64_t r = 0; r < rows; ++r) feature.emplace_back(buf.begin() + r * dim, buf.begin() + (r + 1) * dim);
+}
+
+void readFeature(const char* name, std::vector<float>& feature) {
+  std::vector<std::vector<float> > features;
+  readFeature(name, features);
+  if (features.size() != 1)
+    std::cerr << "Warning in readFeature(): the number of features in " << name << " is not 1. ("
+              << features.size() << ")" << std::endl;
+  feature = features.empty() ? std::vector<float>() : features[0];
+}
+
+void writeFeature(const char* name, const std::vector<std::vector<float> > feature, bool remove_0_flg) {
+  if (feature.empty()) throw Error(C3H_ERR_ARG, "writeFeature: no rows");
+  const size_t dim = feature[0].size();
+  std::vector<float> buf;
+  buf.reserve(feature.size() * dim);
+  for (const auto& row : feature) {
+    if (row.size() != dim) throw Error(C3H_ERR_ARG, "writeFeature: ragged rows");
+    buf.insert(buf.end(), row.begin(), row.end());
+  }
+  const int rc = c3h_feature_pcd_write(name, buf.data(), (int64_t)feature.size(), (int32_t)dim, remove_0_flg ? 1 : 0,
+                                       nullptr);
+  if (rc != C3H_OK) throw Error(rc, std::string("writeFeature: ") + name);
+}
+
+void writeFeature(const char* name, const std::vector<float> feature, bool remove_0_flg) {
+  writeFeature(name, std::vector<std::vector<float> >(1, feature), remove_0_flg);
+}
+
+void ColorThreshold::addScene(const VoxelGrid& grid) {
+  grid.context().check(c3h_color_histogram(grid.context().get(), hist_, 1), "c3h_color_histogram");
+}
+
+void ColorThreshold::compute(int threshold[3], double total_average[3]) const {
+  int32_t t[3];
+  const int rc = c3h_auto_threshold(hist_, t, total_average);
+  if (rc != C3H_OK) throw Error(rc, "ColorThreshold::compute: no occupied voxels");
+  for (int i = 0; i < 3; ++i) threshold[i] = t[i];
 }
 
 Vector3i extractC3HLACSignature981(VoxelGrid& grid, std::vector<std::vector<float> >& feature, int r,

@@ -120,6 +120,28 @@ void extractC3HLACSignature117(VoxelGrid& grid, std::vector<float>& feature, int
                                int color_threshold_g, int color_threshold_b, float voxel_size,
                                bool lut_double = true);
 
+// pcl::io::loadPCDFile for x y z rgb clouds (c3h_pcd_read_xyzrgb): 0 on success, -1 when
+// the file cannot be opened or parsed, as PCL returns.
+int loadPCDFile(const std::string& file_name, std::vector<PointXYZRGB>& cloud);
+
+// readFeature / writeFeature (c3_hlac_tools.hpp:46-113): ASCII feature PCD files.
+void readFeature(const char* name, std::vector<std::vector<float> >& feature);
+void readFeature(const char* name, std::vector<float>& feature);
+void writeFeature(const char* name, const std::vector<std::vector<float> > feature, bool remove_0_flg = true);
+void writeFeature(const char* name, const std::vector<float> feature, bool remove_0_flg = true);
+
+// calc_scene_auto_threshold.cpp:84-146 as a class: addScene() per voxelised scene frame
+// (histograms of its voxel colours, on the GPU), compute() the RGB binarisation thresholds.
+class ColorThreshold {
+ public:
+  void addScene(const VoxelGrid& grid);
+  void compute(int threshold[3], double total_average[3] = nullptr) const;
+  const int64_t* histogram() const { return hist_; }  // [c * 256 + v], c = r, g, b
+
+ private:
+  int64_t hist_[768] = {};
+};
+
 // PCA file reader (pca.cpp:119-185).  getAxis() is dim x dim with eigenvector i in
 // column i, as Eigen holds it.
 class PCA {

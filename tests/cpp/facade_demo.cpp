@@ -4,7 +4,10 @@
 // search -> maxX/maxY/maxZ/maxDot.  Prints one JSON object on stdout.
 //   facade_demo params <param_dir> <models_dir>       (host only: Param + PCA readers)
 //   facade_demo run <xyzrgb.bin> <out_features.bin>   (GPU: the detection pipeline)
+//   facade_demo io <cloud.pcd> <feature.pcd> <out.pcd>  (host only: loadPCDFile, read/writeFeature)
+//   facade_demo thr <cloud.pcd> <leaf>                  (GPU: calc_scene_auto_threshold flow)
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <string>
@@ -108,10 +111,46 @@ static int run(const std::string& cloud_path, const std::string& feat_path) {
   return 0;
 }
 
+static int io(const char* cloud_pcd, const char* feat_pcd, const char* out_pcd) {
+  std::vector<PointXYZRGB> cloud;
+  if (loadPCDFile(cloud_pcd, cloud) != 0) return 3;
+  std::vector<std::vector<float> > f;
+  readFeature(feat_pcd, f);
+  writeFeature(out_pcd, f, false);
+  uint32_t c0;
+  memcpy(&c0, &cloud[0].rgb, 4);
+  printf("{\"n_points\": %zu, \"p0\": [%.9g, %.9g, %.9g, %u], \"rows\": %zu, \"dim\": %zu, "
+         "\"missing\": %d}\n", cloud.size(), cloud[0].x, cloud[0].y, cloud[0].z, c0, f.size(), f[0].size(),
+         loadPCDFile("no/such/file.pcd", cloud));
+  return 0;
+}
+
+static int thr(const char* cloud_pcd, float leaf) {
+  std::vector<PointXYZRGB> cloud, down;
+  if (loadPCDFile(cloud_pcd, cloud) != 0) return 3;
+  VoxelGrid grid(0);
+  getVoxelGrid(grid, cloud, down, leaf);
+  ColorThreshold ct;
+  ct.addScene(grid);
+  ct.addScene(grid);  // the tool's file loop: two frames of the same scene
+  int t[3];
+  double ave[3];
+  ct.compute(t, ave);
+  printf("{\"n_occ\": %zu, \"thr\": [%d, %d, %d], \"ave\": [%.17g, %.17g, %.17g], \"h_sum\": %lld}\n",
+         down.size(), t[0], t[1], t[2], ave[0], ave[1], ave[2], (long long)[&] {
+           int64_t s = 0;
+           for (int i = 0; i < 256; ++i) s += ct.histogram()[i];
+           return s;
+         }());
+  return 0;
+}
+
 int main(int argc, char** argv) {
   try {
     if (argc == 4 && !strcmp(argv[1], "params")) return params(argv[2], argv[3]);
     if (argc == 4 && !strcmp(argv[1], "run")) return run(argv[2], argv[3]);
+    if (argc == 5 && !strcmp(argv[1], "io")) return io(argv[2], argv[3], argv[4]);
+    if (argc == 4 && !strcmp(argv[1], "thr")) return thr(argv[2], (float)atof(argv[3]));
   } catch (const Error& e) {
     fprintf(stderr, "c3hlac::Error %d: %s\n", e.code, e.what());
     return 2;

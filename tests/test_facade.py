@@ -106,3 +106,34 @@ def test_facade_pipeline_matches_binding(demo, tmp_path, ctx):
         s, x, y, z, mode, xr = j["dets"][m]
         assert (s, x, y, z, mode) == (det["score"][m], det["x"][m], det["y"][m], det["z"][m], det["mode"][m])
         assert xr == (2 if mode in (0, 1) else (2 if mode in (2, 3) else 1))
+
+
+PCD = FIX / "pcd"
+
+
+def test_facade_pcd_and_feature_io(demo, tmp_path):
+    """loadPCDFile / readFeature / writeFeature through the facade (host only)."""
+    out = tmp_path / "f.pcd"
+    j = json.loads(subprocess.run([str(demo), "io", str(PCD / "bowl1_0000.pcd"),
+                                   str(PCD / "noisy_cube_black_GRSD_CCHLAC.pcd"), str(out)],
+                                  check=True, capture_output=True, text=True).stdout)
+    ref = c3hlac.read_pcd(PCD / "bowl1_0000.pcd")
+    assert j["n_points"] == ref.shape[0] and j["missing"] == -1
+    assert np.float32(j["p0"][0]) == ref[0, 0] and j["p0"][3] == int(ref[0:1, 3].view(np.uint32)[0])
+    assert (j["rows"], j["dim"]) == (1, 137)
+    # the c3_hlac writer names the field "descriptor"; everything else is the reference's file
+    a = out.read_text().splitlines()
+    b = (PCD / "noisy_cube_black_GRSD_CCHLAC.pcd").read_text().splitlines()
+    assert a[1] == "FIELDS descriptor" and b[1] == "FIELDS vfh" and a[:1] + a[2:] == b[:1] + b[2:]
+
+
+@pytest.mark.gpu
+def test_facade_auto_threshold(demo, ctx):
+    import np_ref as npr
+    j = json.loads(subprocess.run([str(demo), "thr", str(PCD / "noisy_torus_blue.pcd"), "0.005"],
+                                  check=True, capture_output=True, text=True).stdout)
+    ctx.voxelize(c3hlac.read_pcd(PCD / "noisy_torus_blue.pcd"), 0.005)
+    h = 2 * npr.color_histogram(ctx.grid())
+    t, ave = npr.auto_threshold(h)
+    assert j["n_occ"] == h[0].sum() // 2 and j["h_sum"] == h[0].sum()
+    assert j["thr"] == list(t) and j["ave"] == list(ave)
