@@ -256,6 +256,76 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
       dst[j] = i < n4 ? make_uint4(t.x, t.y, t.z, t.w) : make_uint4(0, 0, 0, 0);
     }
   };
+  // Row-wave fast path (gx = 256, 512 or 1024, axis maps in LDS): a wave's 64 lanes x 4
+  // voxels of step j are 256 consecutive voxels of ONE grid row (chunk, wave and j offsets
+  // are multiples of 256 and j steps whole rows), so the row's (y, z) segment is
+  // wave-uniform: its two lookups per j are uniform-address LDS reads, all 2 x unroll issued
+  // together and moved to SGPRs, and a lane's 4 x-segments are loop invariant.  The general
+  // path below steps and looks up (x, y, z) per lane and per j.
+  if (kAx && (gx & 255) == 0 && 1024 % gx == 0) {
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int rpj = (kBlock * 4) / gx;                 // rows per j step
+    const int xl = (wv * 256) % gx + 4 * (tid & 63);   // this lane's x (every chunk, every j)
+    int tx0[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tx0[k] = mx[xl + k];
+    uint4 w[kOccBitsUnroll];
+    int64_t c0 = bx * (int64_t)kChunk4;
+    uint32_t crow = (uint32_t)(((c0 + (int64_t)wv * 64) << 2) / gx);
+    const uint32_t crow_step = (uint32_t)((cstride << 2) / gx);
+    if (c0 < n4) load_chunk(w, c0);
+    for (; c0 < n4; c0 += cstride) {
+      uint4 nx[kOccBitsUnroll];
+      if (kOccPipe && c0 + cstride < n4) load_chunk(nx, c0 + cstride);
+      // uniform 32-bit row arithmetic (rows < 2^24: nvox < 2^32 is host-checked): the
+      // chunk's first row is stepped per chunk, (y, z) by whole rows per j
+      const uint32_t row0 = crow;
+      crow += crow_step;
+      int tyz[kOccBitsUnroll];
+      {
+        int ty[kOccBitsUnroll], tz[kOccBitsUnroll], zj[kOccBitsUnroll];
+        int y = (int)(row0 % (uint32_t)gy), z = (int)(row0 / (uint32_t)gy);
+#pragma unroll
+        for (int j = 0; j < kOccBitsUnroll; ++j) {
+          zj[j] = z;
+          ty[j] = my[y];
+          tz[j] = mz[min(z, gz - 1)];
+          y += rpj;
+          while (y >= gy) {
+            y -= gy;
+            ++z;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < kOccBitsUnroll; ++j) {
+          const int a = __builtin_amdgcn_readfirstlane(ty[j]), b = __builtin_amdgcn_readfirstlane(tz[j]);
+          tyz[j] = (a >= 0 && b >= 0 && zj[j] < gz) ? ns0 * (a + ns1 * b) : -1;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kOccBitsUnroll; ++j) {
+        if (tyz[j] < 0) continue;  // uniform: not a centre row (or past the grid end)
+        const uint32_t ws[4] = {w[j].x, w[j].y, w[j].z, w[j].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!ws[k] || tx0[k] < 0) continue;
+          const int t = tx0[k] + tyz[j];
+          if (t == last) continue;
+          last = t;
+          atomicOr(&s_bits[t >> 5], 1u << (t & 31));  // result unused: ds_or_b32, no wait
+        }
+      }
+      if (kOccPipe) {
+#pragma unroll
+        for (int j = 0; j < kOccBitsUnroll; ++j) w[j] = nx[j];
+      } else if (c0 + cstride < n4) {
+        load_chunk(w, c0 + cstride);
+      }
+    }
+    __syncthreads();
+    occ_flush_bits(s_bits, nwords, s_list, s_wsum, epoch, flags, cnt, work);
+    return;
+  }
   uint4 w[kOccBitsUnroll];
   int64_t c0 = bx * (int64_t)kChunk4;
   if (c0 < n4) load_chunk(w, c0);
