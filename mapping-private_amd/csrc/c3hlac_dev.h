@@ -133,11 +133,13 @@ struct OccArgs {
 // the 16 rows' (y, z) segments are looked up together.  The flush compacts the set bits
 // into an LDS list and stamps kBlock tiles at a time, every exchange in flight together.
 constexpr int kOccBitsMax = 1 << 18;  // 32 KB of LDS bits (512^3 at S >= 8)
+// 16 loads per lane issued together, not software-pipelined: the same 64 VGPRs of data in
+// flight as 2 x 8 pipelined, 4 % shorter tick (profiles/r1/v2_occ_variants.log, v3)
 #ifndef C3H_OCC_UNROLL
-#define C3H_OCC_UNROLL 8
+#define C3H_OCC_UNROLL 16
 #endif
 #ifndef C3H_OCC_PIPE
-#define C3H_OCC_PIPE 1
+#define C3H_OCC_PIPE 0
 #endif
 constexpr int kOccBitsUnroll = C3H_OCC_UNROLL;  // 16-B non-temporal loads per lane per chunk
 constexpr bool kOccPipe = C3H_OCC_PIPE;         // next chunk's loads issued before this one is used
@@ -242,8 +244,8 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
   // consecutive j of one thread are kBlock*4 voxels apart: step (x, y, z) incrementally
   const int dxs = (kBlock * 4) % gx, drs = (kBlock * 4) / gx;
   int last = -1;
-  // software-pipelined: chunk c+1's loads are issued before chunk c is processed, so
-  // every wave keeps 2 x kOccBitsUnroll x 16 B per lane in flight.  Non-temporal: the grid
+  // kOccBitsUnroll 16-B loads per lane issued together (with kOccPipe, chunk c+1's loads
+  // are issued before chunk c is processed: 2 x kOccBitsUnroll in flight).  Non-temporal: the grid
   // is read once here (the tile pass re-reads only the occupied tiles' halos); measured
   // 6.9-7.0 TB/s vs 6.0-6.3 for default-policy loads.  Past the grid end the address is
   // clamped and the value zeroed (no per-element branch around the load).
