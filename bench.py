@@ -31,7 +31,9 @@ GRID, LEAF, VARIANT, SUBDIV = 256, 0.01, 117, 10
 D, M, R = 100, 10, 20
 BOX, RANK, EXIST_THR = (2, 2, 2), 1, 100
 LANES = 3  # batches in flight per GPU on the lanes path (breakdown pass only)
-BATCH = int(os.environ.get("C3H_BENCH_BATCH", "8"))  # frames per launch (c3h_set_batch)
+BATCH_MAX = 32  # frames per tick (c3h_set_batch); the tick's latency-bound roles need many
+                # frames in flight: 12.8 us/frame at 32 vs 14.1 at 16, 17.9 at 8 (profiles/r1/v8)
+BATCH = BATCH_MAX  # set per run in main(): at least ~8 batches, so pipeline fill/drain stays small
 PIPE_DEPTH = 4  # pipeline ticks a batch spends in flight (occupancy | tile | compress+gate | score)
 THR = (147, 146, 148)
 N_RAYS = 1_000_000
@@ -41,9 +43,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--frames", type=int, default=6)
+    ap.add_argument("--steps", type=int, default=960)
+    ap.add_argument("--warmup", type=int, default=64)
+    ap.add_argument("--frames", type=int, default=0,
+                    help="resident grids (0: BATCH + 8, at least 40; > the 256 MB Infinity Cache, and every "
+                         "frame of a tick reads its own grid)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -76,13 +80,16 @@ def main():
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
     ctx.set_lanes(LANES)
+    global BATCH
+    BATCH = int(os.environ.get("C3H_BENCH_BATCH", "0")) or min(BATCH_MAX, max(8, args.steps // 8 // 8 * 8))
     ctx.set_batch(BATCH)
     ctx.set_pipeline(True)
 
     # ---- inputs: frames voxelised on the GPU, grids kept resident in HBM ------------
-    nf = max(1, args.frames)
+    nf = args.frames if args.frames > 0 else max(40, BATCH + 8)
     grids, frame_pts = [], []
-    n_scene = max(1, (nf + 1) // 2)
+    per_scene = 4  # frames per scene: the scene and three x-shifts of it (distinct buffers)
+    n_scene = max(1, -(-nf // per_scene))
     t_vox_ms, n_points = [], 0
     for s in range(n_scene):
         seed = synth.BASE_SEED + 1000 * rank + s
@@ -99,9 +106,10 @@ def main():
         words = torch.empty(GRID ** 3, dtype=torch.int32, device=dev)
         ctx.lib.c3h_get_grid(ctx.h, c3hlac.ptr(words), 1)
         grids.append(words)
-        # a second frame from the same scene: shifted along x by a non-subdivision step
-        if len(grids) < nf:
-            grids.append(torch.roll(words.view(GRID, GRID, GRID), shifts=37, dims=2).reshape(-1).contiguous())
+        # more frames from the same scene: shifted along x by non-subdivision steps
+        for k in range(1, per_scene):
+            if len(grids) < nf:
+                grids.append(torch.roll(words.view(GRID, GRID, GRID), shifts=37 * k, dims=2).reshape(-1).contiguous())
     grids = grids[:nf]
     torch.cuda.synchronize(dev)
 

@@ -87,7 +87,10 @@ hipError_t launch_downsampled(const int32_t* leaf, const uint32_t* grid, int64_t
                               const float* sx, const float* sy, const float* sz,
                               uint64_t table_size, float* out, hipStream_t s);
 
-constexpr int kMaxBatch = 8;  // frames per launch (blockIdx.y) in c3h_run_frames
+#ifndef C3H_MAX_BATCH
+#define C3H_MAX_BATCH 64
+#endif
+constexpr int kMaxBatch = C3H_MAX_BATCH;  // frames per launch (blockIdx.y) in c3h_run_frames
 
 struct C3Launch {
   const uint32_t* grid[kMaxBatch];  // one grid per frame of the batch
@@ -255,7 +258,7 @@ struct c3h_ctx {
   std::vector<hipEvent_t> lane_ev;
   hipEvent_t fork_ev = nullptr;
   int nlanes = 3;
-  int nbatch = 8;                   // frames per launch in c3h_run_frames
+  int nbatch = 32;                  // frames per launch in c3h_run_frames
   bool pipeline = true;             // c3h_run_frames: pipelined tick launches (else lanes)
   // host copy of the search setup, replayed into the lanes
   uint64_t setup_version = 0;

@@ -283,38 +283,41 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
       // chunk's first row is stepped per chunk, (y, z) by whole rows per j
       const uint32_t row0 = crow;
       crow += crow_step;
-      int tyz[kOccBitsUnroll];
+#ifdef C3H_OCC_NOPROC  // diagnostics: stream only (the words are OR-reduced into one bit)
       {
-        int ty[kOccBitsUnroll], tz[kOccBitsUnroll], zj[kOccBitsUnroll];
+        uint32_t o = 0;
+#pragma unroll
+        for (int j = 0; j < kOccBitsUnroll; ++j) o |= w[j].x | w[j].y | w[j].z | w[j].w;
+        if (o == 0x12345678u) atomicOr(&s_bits[0], 1u);
+        if (c0 + cstride < n4) load_chunk(w, c0 + cstride);
+        continue;
+      }
+#endif
+      // rows are mostly empty: skip a row unless some lane of the wave holds a voxel of it
+      // (one ballot), look its (y, z) segment up only then
+      {
         int y = (int)(row0 % (uint32_t)gy), z = (int)(row0 / (uint32_t)gy);
 #pragma unroll
         for (int j = 0; j < kOccBitsUnroll; ++j) {
-          zj[j] = z;
-          ty[j] = my[y];
-          tz[j] = mz[min(z, gz - 1)];
+          const int yj = y, zjj = z;
           y += rpj;
           while (y >= gy) {
             y -= gy;
             ++z;
           }
-        }
+          const uint32_t ws[4] = {w[j].x, w[j].y, w[j].z, w[j].w};
+          if (__ballot((ws[0] | ws[1] | ws[2] | ws[3]) != 0u) == 0ull || zjj >= gz) continue;
+          const int a = __builtin_amdgcn_readfirstlane(my[yj]), b = __builtin_amdgcn_readfirstlane(mz[zjj]);
+          if (a < 0 || b < 0) continue;  // uniform: not a centre row
+          const int tyz = ns0 * (a + ns1 * b);
 #pragma unroll
-        for (int j = 0; j < kOccBitsUnroll; ++j) {
-          const int a = __builtin_amdgcn_readfirstlane(ty[j]), b = __builtin_amdgcn_readfirstlane(tz[j]);
-          tyz[j] = (a >= 0 && b >= 0 && zj[j] < gz) ? ns0 * (a + ns1 * b) : -1;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < kOccBitsUnroll; ++j) {
-        if (tyz[j] < 0) continue;  // uniform: not a centre row (or past the grid end)
-        const uint32_t ws[4] = {w[j].x, w[j].y, w[j].z, w[j].w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (!ws[k] || tx0[k] < 0) continue;
-          const int t = tx0[k] + tyz[j];
-          if (t == last) continue;
-          last = t;
-          atomicOr(&s_bits[t >> 5], 1u << (t & 31));  // result unused: ds_or_b32, no wait
+          for (int k = 0; k < 4; ++k) {
+            const int t = tx0[k] + tyz;
+            if (ws[k] && tx0[k] >= 0 && t != last) {
+              last = t;
+              atomicOr(&s_bits[t >> 5], 1u << (t & 31));  // result unused: ds_or_b32, no wait
+            }
+          }
         }
       }
       if (kOccPipe) {

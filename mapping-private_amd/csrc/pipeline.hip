@@ -201,10 +201,11 @@ hipError_t launch_tick(const TickParts& p, hipStream_t s) {
   if (p.occ) {
     const C3Args c = build_c3_args(*p.occ);
     t.oa = c.oa;
-    // ~256 streaming workgroups per tick whatever the batch (one per CU): alone they stream
-    // at ~4 TB/s, but the latency-bound roles then see a short HBM queue and the whole tick
-    // is shortest (profiles/r1/v1_occ_variants.log: 19.4 us/frame vs 20.8 at 512)
-    t.o_grid = std::max(1, std::min(c.g1, env_int("C3H_TICK_OCC", std::max(16, 256 / std::max(1, c.nframes)))));
+    // ~256 streaming workgroups per tick whatever the batch (one per CU): the latency-bound
+    // roles then see a short HBM queue and the whole tick is shortest
+    // (profiles/r1/v1_occ_variants.log, v8/v9: at 32 frames per tick 12.8 us/frame with 256,
+    // 14.3 with 384, 15.5 with 192)
+    t.o_grid = std::max(1, std::min(c.g1, env_int("C3H_TICK_OCC", std::max(1, 256 / std::max(1, c.nframes)))));
     t.n_occ = t.o_grid * c.nframes;
     lds = std::max(lds, c.occ_lds);
   }

@@ -9,9 +9,9 @@ rc=$?; echo "pytest rc=$rc" >> gpurun_out/gpu_tests_$TAG.log
 [ $rc -ge 124 ] && exit $rc
 timeout -k 10 200 python tools_phase_probe.py gpurun_out/probe_$TAG.txt > gpurun_out/probe_$TAG.log 2>&1 || exit 4
 timeout -k 10 300 python tools_lanes.py > gpurun_out/lanes_$TAG.log 2>&1 || exit 6
-timeout -k 10 300 python bench.py --steps 200 --warmup 20 --cpu-seconds 5 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit 3
+timeout -k 10 300 python bench.py --cpu-seconds 5 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit 3
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_$TAG -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 200 --warmup 20 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof_$TAG.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_$TAG -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 960 --warmup 64 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof_$TAG.log 2>&1
 echo "rocprof rc=$?" >> $GRAFT_REPO_ROOT/gpurun_out/prof_$TAG.log
 cd $GRAFT_REPO_ROOT
-python tools_tick_trace.py gpurun_out/prof_$TAG/run_kernel_trace.csv 20 200 ${C3H_BENCH_BATCH:-8} gpurun_out/bench_$TAG.json > gpurun_out/tick_trace_$TAG.json
+python tools_tick_trace.py gpurun_out/prof_$TAG/run_kernel_trace.csv 64 960 32 gpurun_out/bench_$TAG.json > gpurun_out/tick_trace_$TAG.json

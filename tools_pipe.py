@@ -24,7 +24,7 @@ with c3hlac.Context(0) as ctx:
     axis_t, var, axis_q = synth.random_bases(117, 100, 10, 20, seed=synth.BASE_SEED)
     ctx.search_setup(axis_t, var, axis_q)
     ctx.set_rank(1)
-    N = 240
+    N = int(os.environ.get("PIPE_FRAMES", "240"))
     gptr = np.array([grids[i % 6].data_ptr() for i in range(N)], np.uint64)
     dets = torch.zeros((N, 30), dtype=torch.int64, device=dev)
     ref = None

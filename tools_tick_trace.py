@@ -7,6 +7,8 @@ import sys
 
 PIPE_DEPTH = 4
 trace, warmup, steps, batch = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
+if len(sys.argv) > 5:  # the bench line knows its frames per launch
+    batch = json.load(open(sys.argv[5]))["config"].get("frames_per_launch", batch)
 rows = [r for r in csv.DictReader(open(trace)) if "c3h_tick_kernel" in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 ticks = lambda n: -(-n // batch) + PIPE_DEPTH - 1 if n else 0  # noqa: E731
