@@ -348,7 +348,8 @@ def test_dense_256_bin_block_linearity(ctx):
 
 @pytest.mark.parametrize("lanes,batch,rank,pipe", [(1, 1, 1, 0), (1, 4, 1, 0), (3, 1, 1, 0), (3, 4, 1, 0),
                                                    (2, 3, 2, 0), (4, 8, 1, 0), (1, 1, 1, 1), (1, 2, 1, 1),
-                                                   (1, 3, 1, 1), (1, 8, 1, 1), (2, 3, 2, 1)])
+                                                   (1, 3, 1, 1), (1, 8, 1, 1), (2, 3, 2, 1), (1, 32, 1, 1),
+                                                   (1, 64, 1, 1), (2, 32, 1, 0)])
 def test_run_frames_lanes_match_sequential(ctx, lanes, batch, rank, pipe):
     """c3h_run_frames (frames batched per launch; batches in flight on lane contexts, or
     software-pipelined through the tick kernel: 8 frames at batch 1/2 rotate through all
@@ -465,3 +466,38 @@ def test_reference_clouds_end_to_end(ctx, name, leaf):
         sb, hn = ctx.extract(variant, THR, 5)
         fe, _, _ = po.c3hlac(g, layout, cloud, variant, THR, leaf, 5, exact=True)
         assert np.array_equal(ctx.features(), fe)
+
+
+@pytest.mark.parametrize("batch", [32, 64])
+def test_run_frames_pipelined_many_batches(ctx, batch):
+    """The production configuration: the pipelined tick at 32 / 64 frames per tick over 150
+    distinct resident grids (several full batches, a ragged last one, the fill/drain ticks,
+    all four buffer sets) == frame-by-frame extract + search."""
+    import torch
+    G, S, rng_box = 64, 8, (2, 2, 2)
+    base = []
+    for i in range(5):
+        ctx.voxelize(synth.kinect_scene(60_000, grid=G, leaf=0.01, seed=synth.BASE_SEED + 70 + i), 0.01)
+        base.append(ctx.grid().reshape(G, G, G).astype(np.uint32))
+    words = [np.roll(base[i % 5], 3 * (i // 5), axis=2).reshape(-1) for i in range(150)]
+    axis_t, var, axis_q = synth.random_bases(117, 24, 4, 6, seed=5)
+    ctx.search_setup(axis_t, var, axis_q)
+    ref = []
+    for w in words:
+        ctx.set_grid(w, (G, G, G))
+        ctx.set_rank(1)
+        ctx.extract(117, THR, S)
+        det, _ = ctx.search(rng_box, 20)
+        ref.append(det.copy())
+    dev = torch.device("cuda", 0)
+    d_grids = [torch.from_numpy(w.view(np.int32)).to(dev) for w in words]
+    d_out = torch.zeros((len(words), 4 * 3), dtype=torch.int64, device=dev)
+    ctx.set_batch(batch)
+    ctx.set_pipeline(1)
+    ctx.run_frames(np.array([g.data_ptr() for g in d_grids], np.uint64), (G, G, G), (0, 0, 0), 0.01, 117,
+                   THR, S, rng_box, 20, True, d_out.data_ptr())
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy().view(c3hlac.DET_DTYPE).reshape(len(words), 4, 1)
+    for i in range(len(words)):
+        np.testing.assert_array_equal(got[i], ref[i], err_msg="frame %d" % i)
+    ctx.set_batch(4)
