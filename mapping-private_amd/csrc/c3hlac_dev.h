@@ -264,32 +264,34 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
   // wave-uniform: its two lookups per j are uniform-address LDS reads, all 2 x unroll issued
   // together and moved to SGPRs, and a lane's 4 x-segments are loop invariant.  The general
   // path below steps and looks up (x, y, z) per lane and per j.
-  if (kAx && (gx & 255) == 0 && 1024 % gx == 0) {
+  if (kAx && !kOccPipe && (gx & 255) == 0 && 1024 % gx == 0) {
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int rpj = (kBlock * 4) / gx;                 // rows per j step
     const int xl = (wv * 256) % gx + 4 * (tid & 63);   // this lane's x (every chunk, every j)
     int tx0[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) tx0[k] = mx[xl + k];
+    // Chunk i of this workgroup is chunk i * gdx + (bx + i) % gdx of the frame: rotated, so
+    // every workgroup visits every y band of the grid (a fixed stride would give workgroup
+    // bx the same rows of every plane, and frames' occupancy varies with y: the workgroups of
+    // one frame ended up to 70 us apart, profiles/r1/tq3_occ_spread.txt).
+    const int lg = gx == 256 ? 8 : gx == 512 ? 9 : 10;
+    const int64_t nch = (n4 + kChunk4 - 1) / kChunk4;
     uint4 w[kOccBitsUnroll];
-    int64_t c0 = bx * (int64_t)kChunk4;
-    uint32_t crow = (uint32_t)(((c0 + (int64_t)wv * 64) << 2) / gx);
-    const uint32_t crow_step = (uint32_t)((cstride << 2) / gx);
-    if (c0 < n4) load_chunk(w, c0);
-    for (; c0 < n4; c0 += cstride) {
-      uint4 nx[kOccBitsUnroll];
-      if (kOccPipe && c0 + cstride < n4) load_chunk(nx, c0 + cstride);
+    for (int64_t i = 0; i * gdx < nch; ++i) {
+      const int64_t cidx = i * gdx + (bx + i) % gdx;
+      if (cidx >= nch) continue;  // uniform: the last, partial round of chunks
+      const int64_t c0 = cidx * kChunk4;
+      load_chunk(w, c0);
       // uniform 32-bit row arithmetic (rows < 2^24: nvox < 2^32 is host-checked): the
-      // chunk's first row is stepped per chunk, (y, z) by whole rows per j
-      const uint32_t row0 = crow;
-      crow += crow_step;
+      // chunk's first row, then (y, z) stepped by whole rows per j
+      const uint32_t row0 = (uint32_t)(((uint64_t)c0 * 4 + (uint64_t)wv * 256) >> lg);
 #ifdef C3H_OCC_NOPROC  // diagnostics: stream only (the words are OR-reduced into one bit)
       {
         uint32_t o = 0;
 #pragma unroll
         for (int j = 0; j < kOccBitsUnroll; ++j) o |= w[j].x | w[j].y | w[j].z | w[j].w;
         if (o == 0x12345678u) atomicOr(&s_bits[0], 1u);
-        if (c0 + cstride < n4) load_chunk(w, c0 + cstride);
         continue;
       }
 #endif
@@ -319,12 +321,6 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
             }
           }
         }
-      }
-      if (kOccPipe) {
-#pragma unroll
-        for (int j = 0; j < kOccBitsUnroll; ++j) w[j] = nx[j];
-      } else if (c0 + cstride < n4) {
-        load_chunk(w, c0 + cstride);
       }
     }
     __syncthreads();

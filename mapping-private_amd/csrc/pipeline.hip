@@ -125,6 +125,20 @@ void tick_prof_dump(const TickArgs& t, long long* d_prof, int total, hipStream_t
       }
       fprintf(fp, " %s[n=%d start=%.1f..%.1f end=%.1f mean=%.1f]", names[r], n[r], (smin - t0) * 0.01,
               (smax - t0) * 0.01, (emax - t0) * 0.01, dsum / n[r] * 0.01);
+      if (r == 0 && t.o_grid > 0) {  // occupancy: end-time spread across frames and within them
+        double fmin = 1e30, fmax = 0, wmax = 0;
+        for (int f0 = b0; f0 < b0 + n[r]; f0 += t.o_grid) {
+          long long lo = LLONG_MAX, hi = 0;
+          for (int b = f0; b < f0 + t.o_grid; ++b) {
+            lo = std::min(lo, v[2 * b + 1]);
+            hi = std::max(hi, v[2 * b + 1]);
+          }
+          fmin = std::min(fmin, (hi - t0) * 0.01);
+          fmax = std::max(fmax, (hi - t0) * 0.01);
+          wmax = std::max(wmax, (hi - lo) * 0.01);
+        }
+        fprintf(fp, " occ_frame_end[%.1f..%.1f within<=%.1f]", fmin, fmax, wmax);
+      }
     }
     b0 += n[r];
   }
