@@ -43,7 +43,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=960)
+    ap.add_argument("--steps", type=int, default=3840)
     ap.add_argument("--warmup", type=int, default=64)
     ap.add_argument("--frames", type=int, default=0,
                     help="resident grids (0: BATCH + 8, at least 40; > the 256 MB Infinity Cache, and every "
