@@ -88,7 +88,12 @@ __device__ __forceinline__ void tick_roles(const TickArgs& t, uint32_t* tick_sme
   else score_list_body(t.sq, r % t.s_gx, r / t.s_gx, f, t.s_gx, t.s_groups, reinterpret_cast<float*>(tick_smem));
 }
 
-__global__ __launch_bounds__(kBlock, 4) void c3h_tick_kernel(TickArgs t) {
+// waves per SIMD the register allocation must allow (4: the 128-VGPR cap); diagnostics builds
+// try more resident workgroups per CU (tools/build_variant.sh NAME -DC3H_TICK_MINW=5)
+#ifndef C3H_TICK_MINW
+#define C3H_TICK_MINW 4
+#endif
+__global__ __launch_bounds__(kBlock, C3H_TICK_MINW) void c3h_tick_kernel(TickArgs t) {
   extern __shared__ __attribute__((aligned(16))) uint32_t tick_smem[];
   if (t.prof && threadIdx.x == 0) t.prof[2 * blockIdx.x] = (long long)wall_clock64();
   tick_roles(t, tick_smem);
