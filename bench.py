@@ -31,8 +31,9 @@ GRID, LEAF, VARIANT, SUBDIV = 256, 0.01, 117, 10
 D, M, R = 100, 10, 20
 BOX, RANK, EXIST_THR = (2, 2, 2), 1, 100
 LANES = 3  # batches in flight per GPU on the lanes path (breakdown pass only)
-BATCH_MAX = 32  # frames per tick (c3h_set_batch); the tick's latency-bound roles need many
-                # frames in flight: 12.8 us/frame at 32 vs 14.1 at 16, 17.9 at 8 (profiles/r1/v8)
+BATCH_MAX = 64  # frames per tick (c3h_set_batch); the tick's latency-bound roles need many
+                # frames in flight: 12.8 us/frame at 32 vs 14.1 at 16, 17.9 at 8 (profiles/r1/v8);
+                # 64 beats 32 by 2.4 % on the bench (profiles/r1/abbatch_32_vs_64.log)
 BATCH = BATCH_MAX  # set per run in main(): at least ~8 batches, so pipeline fill/drain stays small
 PIPE_DEPTH = 4  # pipeline ticks a batch spends in flight (occupancy | tile | compress+gate | score)
 THR = (147, 146, 148)

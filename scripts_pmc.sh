@@ -12,5 +12,5 @@ run() {  # name, counters...
 run fetch FETCH_SIZE && run write WRITE_SIZE && run sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY && run inst SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT
 rc=$?
 # frames through the pipeline: bench's allocation prime (4 x BATCH) + warmup + steps
-cd $R && python3 tools_pmc_summary.py gpurun_out/pmc_$TAG gpurun_out/pmc_$TAG/summary.json 32 $((4 * 32 + 64 + 960)) > /dev/null
+cd $R && python3 tools_pmc_summary.py gpurun_out/pmc_$TAG gpurun_out/pmc_$TAG/summary.json 64 $((4 * 64 + 64 + 960)) > /dev/null
 exit $rc
