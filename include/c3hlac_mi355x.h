@@ -184,7 +184,24 @@ int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes
  * their own streams, so the latency-bound search of one frame overlaps the HBM stream of
  * the next.  Lane 0 (this context) takes the last frame.  1 = strictly sequential. */
 int c3h_set_lanes(c3h_ctx* ctx, int32_t lanes);
-/* Frames per launch in c3h_run_frames (1..8, default 4; the fast search path only). */
+/* Streaming form of c3h_run_frames for a continuous frame source (the ROS callback loop
+ * of color_voxel_recognition/test/detect_object.cpp:139-215, one frame after another):
+ * same arguments and per-frame results, but the software pipeline stays filled between
+ * calls.  Each call enqueues its frames as ceil(nframes / batch) batches, one pipeline
+ * tick each, and returns without draining: a batch's detections are complete in d_out
+ * once three more batches have been pushed, or after c3h_stream_flush.  The grids and
+ * d_out must stay valid until then.  A call with a different geometry / parameter set,
+ * and every other entry point that touches this context's buffers, drains the open
+ * stream first.  Configurations the pipeline does not cover (rank > 1, ...) complete
+ * synchronously as in c3h_run_frames.  Returns the number of searched modes. */
+int c3h_stream_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes,
+                      const int32_t div_b[3], const int32_t min_b[3], float leaf,
+                      const c3h_extract_params* p, const int32_t range[3], int32_t exist_threshold,
+                      int32_t rotate, c3h_det* d_out);
+/* Runs the remaining ticks of an open stream (no host synchronisation). */
+int c3h_stream_flush(c3h_ctx* ctx);
+/* Frames per pipeline batch / launch in c3h_run_frames and c3h_stream_frames
+ * (1..64, default 32; the fast search path only). */
 int c3h_set_batch(c3h_ctx* ctx, int32_t frames);
 /* c3h_run_frames scheduling (default 1): 1 = software pipeline on the context stream, one
  * fused launch per tick running occupancy (batch t) | tile (t-1) | compress+gate (t-2) |

@@ -57,7 +57,13 @@ class Context:
         return check(rc, self.h, what)
 
     def set_stream(self, stream_handle):
-        self._chk(self.lib.c3h_set_stream(self.h, C.c_void_p(stream_handle) if stream_handle else None), "set_stream")
+        """Bind the context to a HIP stream handle (torch.cuda.Stream.cuda_stream).  The
+        legacy default stream (handle 0) cannot be named through the C-ABI, where NULL
+        means the context's own non-blocking stream: run under a non-default torch
+        stream instead, or synchronize() before torch reads the results."""
+        if not stream_handle:
+            raise ValueError("set_stream: handle 0 is the legacy default stream; use a torch.cuda.Stream()")
+        self._chk(self.lib.c3h_set_stream(self.h, C.c_void_p(stream_handle)), "set_stream")
 
     def synchronize(self):
         self._chk(self.lib.c3h_synchronize(self.h), "synchronize")
@@ -181,27 +187,34 @@ class Context:
                                                    int(bool(rotate)), ptr(d_out)), "search_async")
 
     def run_frames(self, grid_ptrs, div_b, min_b, leaf, variant, thr, subdiv, ranges, exist_threshold,
-                   rotate=True, d_out=None, offset=(0, 0, 0), lut_double=True):
-        """c3h_run_frames: grid_ptrs = uint64 numpy array of device pointers."""
+                   rotate=True, d_out=None, offset=(0, 0, 0), lut_double=True, stream=False):
+        """c3h_run_frames (stream=True: c3h_stream_frames, the pipeline stays filled;
+        call stream_flush() before reading the last batches): grid_ptrs = uint64 numpy
+        array of device pointers."""
         gp = np.ascontiguousarray(grid_ptrs, dtype=np.uint64)
+        fn = self.lib.c3h_stream_frames if stream else self.lib.c3h_run_frames
         p = _capi.ExtractParams()
         p.variant = int(variant)
         p.thr = (C.c_int32 * 3)(*[int(t) for t in thr])
         p.subdiv = int(subdiv)
         p.offset = (C.c_int32 * 3)(*[int(o) for o in offset])
         p.lut_double = int(bool(lut_double))
-        nm = self._chk(self.lib.c3h_run_frames(self.h, ptr(gp), gp.size, i32x3(div_b), i32x3(min_b), float(leaf),
-                                               C.byref(p), i32x3(ranges), int(exist_threshold),
-                                               int(bool(rotate)), ptr(d_out)), "run_frames")
+        nm = self._chk(fn(self.h, ptr(gp), gp.size, i32x3(div_b), i32x3(min_b), float(leaf),
+                          C.byref(p), i32x3(ranges), int(exist_threshold),
+                          int(bool(rotate)), ptr(d_out)), "run_frames")
         self.variant = int(variant)
         return nm
+
+    def stream_flush(self):
+        """c3h_stream_flush: the remaining ticks of an open frame stream (no host sync)."""
+        self._chk(self.lib.c3h_stream_flush(self.h), "stream_flush")
 
     def set_lanes(self, n):
         """Frames in flight in run_frames (child contexts on their own streams)."""
         self._chk(self.lib.c3h_set_lanes(self.h, int(n)), "set_lanes")
 
     def set_batch(self, n):
-        """Frames per launch in run_frames (1..8)."""
+        """Frames per pipeline batch / launch in run_frames (1..64)."""
         self._chk(self.lib.c3h_set_batch(self.h, int(n)), "set_batch")
 
     def set_pipeline(self, on):

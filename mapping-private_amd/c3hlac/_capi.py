@@ -72,6 +72,9 @@ _SIGS = {
     "c3h_search_async": (C.c_int, [_P, C.POINTER(C.c_int32), C.c_int32, C.c_int32, _P]),
     "c3h_run_frames": (C.c_int, [_P, _P, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_float,
                                  C.POINTER(ExtractParams), C.POINTER(C.c_int32), C.c_int32, C.c_int32, _P]),
+    "c3h_stream_frames": (C.c_int, [_P, _P, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_float,
+                                    C.POINTER(ExtractParams), C.POINTER(C.c_int32), C.c_int32, C.c_int32, _P]),
+    "c3h_stream_flush": (C.c_int, [_P]),
     "c3h_set_lanes": (C.c_int, [_P, C.c_int32]),
     "c3h_set_batch": (C.c_int, [_P, C.c_int32]),
     "c3h_set_pipeline": (C.c_int, [_P, C.c_int32]),

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 #include <mutex>
 #include <vector>
@@ -67,6 +68,19 @@ namespace c3h {
 // barrier stay in flight (__syncthreads() also drains vmcnt on gfx9).
 __device__ __forceinline__ void lds_barrier() {
   __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Diagnostics knobs read from the environment (dispatch order, role sizes, per-block
+// timestamps) exist only in diagnostics builds (make DIAG=1 -> -DC3H_DIAG); the product
+// library ignores the environment.
+inline const char* diag_env(const char* name) {
+#ifdef C3H_DIAG
+  const char* v = getenv(name);
+  return v && *v ? v : nullptr;
+#else
+  (void)name;
+  return nullptr;
+#endif
 }
 
 // ---- launchers (defined in the .hip files) ----------------------------------------
@@ -171,8 +185,6 @@ struct SparseSearch {
   const float* qt;        // D x Opad (row stride), zero-padded past M*r
   int M, r, Opad;
   int mpg;                // models per workgroup (whole models, mpg*r <= 64)
-  int v2;                 // lane-per-position scoring (score2_body, search2_dev.h)
-  const float* qw;        // its per-wave basis windows (score2_pack)
   double* scores;
   ModeGeom md[6];
   int nmodes;
@@ -201,16 +213,8 @@ struct SparseCompress {
   int F, D, Dpad, fmax_len;
   int64_t H;
   int64_t s_feat, s_G, s_rows, s_nrows;  // per-frame strides
-  const float* PW;  // per-wave column slices of P for the lane-per-row compress
 };
 bool compress_rows_ok(int F, int Dpad);
-bool compress2_fits(int F, int D);        // lane-per-row sparse compress applies
-bool score2_fits(int D, int M, int r);    // lane-per-position scoring applies
-// host: per-wave weight layouts of the lane-per-item bodies (search2_dev.h)
-size_t compress2_pw_floats(int F);
-void compress2_pack_host(const float* PT, int F, int D, int Dpad, float* PW);
-size_t score2_qw_floats(int D);
-void score2_pack_host(const float* axis_q, int M, int r, int D, float* QW);
 hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc, hipStream_t s);
 int64_t sparse_score_blocks(const SparseSearch& a);
 
@@ -237,6 +241,7 @@ struct TickParts {
   const SparseSearch* gate = nullptr;   // batch t-2: exist gate ...
   const SparseCompress* comp = nullptr; //   ... + sparse compress
   const SparseSearch* score = nullptr;  // batch t-3: list scoring + rank-1 argmax
+  DevBuf<long long>* prof = nullptr;    // diagnostics builds: the context's timestamp buffer
 };
 bool tick_ok(const C3Launch& l);  // the C3 launch fits the tick's roles
 hipError_t launch_tick(const TickParts& p, hipStream_t s);
@@ -325,8 +330,6 @@ struct c3h_ctx {
   c3h::DevBuf<double> scores;
   int64_t scores_n = 0;
   c3h::DevBuf<float> qt;            // D x Opad transposed model basis (fast score path)
-  c3h::DevBuf<float> qw2;           // per-wave basis windows (lane-per-position scoring)
-  c3h::DevBuf<float> pw2;           // per-wave slices of P (lane-per-row compress)
   int Opad = 0;
   c3h::DevBuf<c3h::ScorePartial> partials;
   bool pending_clean = false;       // cleanMax requested while the device lists are current
@@ -347,4 +350,28 @@ struct c3h_ctx {
   c3h::C3Launch cap_c3{};
   c3h::SparseSearch cap_q{};
   c3h::SparseCompress cap_sc{};
+
+  // the software pipeline of c3h_run_frames / c3h_stream_frames: batches whose later
+  // stages are still to run, each tagged with the tick role it runs next (1 tile,
+  // 2 compress+gate, 3 score); the buffer set of batch number s is s % 4 (0 = this
+  // context, k = lanes[k-1]); `key` identifies the stream's geometry and parameters
+  struct PipeBatch {
+    c3h::C3Launch l;
+    c3h::SparseSearch q;
+    c3h::SparseCompress sc;
+    int nf;
+    int age;
+  };
+  struct PipeKey {
+    int32_t div_b[3], min_b[3];
+    float leaf;
+    c3h_extract_params p;
+    int32_t range[3], thr, rotate, batch, rank;
+    uint64_t setup_version;
+  };
+  std::vector<PipeBatch> pipe;   // in flight, oldest first
+  uint64_t pipe_seq = 0;
+  PipeKey pipe_key{};
+  int pipe_nm = 0;
+  bool pipe_busy = false;        // inside a pipeline call (set contexts are being prepared)
 };

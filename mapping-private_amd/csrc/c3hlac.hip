@@ -183,7 +183,7 @@ size_t c3hlac_lds_bytes(int tw_max, int list_max) {
 // C3-HLAC-117 per-wave tiles apply (exact u32 sums need <= ~5000 centres per tile; the
 // halo must fit the prefetch registers)
 bool wave117_ok(const C3Launch& l) {
-  if (const char* e = getenv("C3H_WAVE117"))  // diagnostics: 0 forces the block body
+  if (const char* e = diag_env("C3H_WAVE117"))  // diagnostics: 0 forces the block body
     if (!atoi(e)) return false;
   const int tw = w117_halo_words(l.lmax[0], l.lmax[1], l.lmax[2]);
   return l.variant == 117 && !l.atomic && l.debug == 0 && tw <= 64 * kW117HaloRegs &&
@@ -222,7 +222,7 @@ int64_t c3hlac_grid(const C3Launch& l) {
   // dense C3-981 runs 28 % faster at full occupancy than at 2 workgroups per CU
   const int cap = items > (int64_t)c_ncu * 8 ? c_per_cu : std::min(c_per_cu, 2);
   int64_t work = std::min<int64_t>(items, (int64_t)c_ncu * cap);
-  if (const char* g = getenv("C3H_TILE_GRID")) work = std::max<int64_t>(1, std::min<int64_t>(items, atoi(g)));
+  if (const char* g = diag_env("C3H_TILE_GRID")) work = std::max<int64_t>(1, std::min<int64_t>(items, atoi(g)));
   const int64_t zero = l.zero_empty ? std::min<int64_t>(64, l.ntiles) : 0;
   return std::max<int64_t>(work, 1) + zero;
 }
@@ -237,7 +237,7 @@ C3Args build_c3_args(const C3Launch& l) {
   // HBM-bound: bytes in flight, not workgroups, set the rate; 256 B per lane lets few
   // workgroups (CU slots) cover the latency, leaving the rest to the other stages
   int occ_cap = 256;  // per frame: ~16 MB in flight at 64 KB per workgroup
-  if (const char* g = getenv("C3H_OCC_GRID")) occ_cap = std::max(1, atoi(g));  // diagnostics
+  if (const char* g = diag_env("C3H_OCC_GRID")) occ_cap = std::max(1, atoi(g));  // diagnostics
   c.bits = vec && l.ntiles <= kOccBitsMax;
   c.ax = l.gx + l.gy + l.gz <= kAxLds;
   c.vec = vec;

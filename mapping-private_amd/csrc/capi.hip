@@ -59,6 +59,16 @@ void release(DevBuf<T>& b) {
   b.n = 0;
 }
 
+int pipe_quiesce(c3h_ctx* ctx);  // defined with the pipeline below
+int pipe_flush(c3h_ctx* ctx);
+
+// entry points that touch a context's buffers first drain its open frame stream
+#define QUIESCE(ctx)                            \
+  do {                                          \
+    int rq_ = pipe_quiesce(ctx);                \
+    if (rq_ != C3H_OK) return rq_;              \
+  } while (0)
+
 #define ENSURE(buf, n)                          \
   do {                                          \
     int rc_ = ensure(ctx, buf, (size_t)(n));    \
@@ -222,7 +232,7 @@ Segs axis_segments(int div, int off, float inv_s, bool mode1, int sb, bool* cove
 // for each probe k, median over blocks of (t_k - t_0) and max over blocks of
 // (t_k - min_b t_0), in microseconds (wall_clock64: 100 MHz).  Synchronises: never on.
 const char* prof_path() {
-  static const char* p = getenv("C3H_PROF");
+  static const char* p = c3h::diag_env("C3H_PROF");
   return p && *p ? p : nullptr;
 }
 
@@ -375,7 +385,7 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
   // sparse compress: only the non-empty rows of the extract's list (the rest stay stale
   // and every consumer gates them on exist)
   const bool sparse_g = !ctx->g_valid && fast && ctx->rows_valid &&
-                        (c3h::compress_rows_ok(ctx->F, ctx->Dpad) || c3h::compress2_fits(ctx->F, ctx->D));
+                        c3h::compress_rows_ok(ctx->F, ctx->Dpad);
   if (ctx->capture && !sparse_g) return 0;  // not pipelinable: the caller falls back
   if (!ctx->g_valid && !sparse_g) {  // nf == 1 here
     Timed t(ctx, 2);
@@ -441,8 +451,6 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
     q.r = ctx->r;
     q.Opad = ctx->Opad;
     q.mpg = std::max(1, 64 / ctx->r);
-    q.v2 = ctx->qw2.p && c3h::score2_fits(ctx->D, ctx->M, ctx->r) ? 1 : 0;
-    q.qw = ctx->qw2.p;
     q.scores = ctx->scores.p;
     q.nmodes = rm.n;
     q.pstart[0] = 0;
@@ -485,7 +493,7 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
     if (sparse_g) {
       sc = c3h::SparseCompress{ctx->feat.p, ctx->axis_pt.p, ctx->fmax.p, ctx->G.p, ctx->rows.p,
                                ctx->tileflags.p + 2 + (ctx->tile_epoch & 1), ctx->F, ctx->D, ctx->Dpad,
-                               ctx->fmax_len, H, H * ctx->F, H * ctx->D, H, ctx->tf_stride, ctx->pw2.p};
+                               ctx->fmax_len, H, H * ctx->F, H * ctx->D, H, ctx->tf_stride};
       ctx->g_valid = true;
       ctx->g_sparse = true;
     }
@@ -586,6 +594,8 @@ int c3h_create(int hip_device, c3h_ctx** out) {
 void c3h_destroy(c3h_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+  (void)pipe_flush(ctx);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   for (c3h_ctx* l : ctx->lanes) c3h_destroy(l);
   for (hipEvent_t e : ctx->lane_ev) (void)hipEventDestroy(e);
   if (ctx->fork_ev) (void)hipEventDestroy(ctx->fork_ev);
@@ -622,6 +632,8 @@ void c3h_destroy(c3h_ctx* ctx) {
   release(ctx->qt);
   release(ctx->partials);
   release(ctx->d_lists);
+  release(ctx->prof);
+  release(ctx->chist);
   for (int s = 0; s < C3H_NTIMERS; ++s)
     for (auto& e : ctx->timer.pending[s]) ctx->timer.pool.push_back({e.a, e.b});
   for (auto& e : ctx->timer.pool) {
@@ -651,6 +663,7 @@ const char* c3h_last_error(const c3h_ctx* ctx) { return ctx ? ctx->err.c_str() :
 int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, float leaf,
                  float z_limit, c3h_grid_info* info) {
   if (!ctx) return C3H_ERR_ARG;
+  QUIESCE(ctx);
   if (n < 0 || (n > 0 && !xyzrgb) || !(leaf > 0))
     return fail(ctx, C3H_ERR_ARG, "c3h_voxelize: bad arguments");
   HIPCHK(hipSetDevice(ctx->device));
@@ -756,6 +769,7 @@ static int64_t grid_voxels(const c3h_ctx* ctx) {
 
 int c3h_get_grid(c3h_ctx* ctx, uint32_t* out, int on_device) {
   if (!ctx || !out) return C3H_ERR_ARG;
+  QUIESCE(ctx);
   if (!ctx->have_grid) return fail(ctx, C3H_ERR_STATE, "no grid");
   HIPCHK(hipSetDevice(ctx->device));
   const int64_t nvox = grid_voxels(ctx);
@@ -769,6 +783,7 @@ int c3h_get_grid(c3h_ctx* ctx, uint32_t* out, int on_device) {
 // calc_scene_auto_threshold.cpp:92-108: one count per occupied voxel and channel
 int c3h_color_histogram(c3h_ctx* ctx, int64_t* hist, int32_t accumulate) {
   if (!ctx || !hist) return C3H_ERR_ARG;
+  QUIESCE(ctx);
   if (!ctx->have_grid) return fail(ctx, C3H_ERR_STATE, "color_histogram: no grid");
   HIPCHK(hipSetDevice(ctx->device));
   ENSURE(ctx->chist, 768);
@@ -828,6 +843,7 @@ static int compute_leaf_layout(c3h_ctx* ctx, int32_t* d_out) {
 
 int c3h_get_leaf_layout(c3h_ctx* ctx, int32_t* out, int on_device) {
   if (!ctx || !out) return C3H_ERR_ARG;
+  QUIESCE(ctx);
   if (!ctx->have_grid) return fail(ctx, C3H_ERR_STATE, "no grid");
   HIPCHK(hipSetDevice(ctx->device));
   const int64_t nvox = grid_voxels(ctx);
@@ -847,6 +863,7 @@ int c3h_get_leaf_layout(c3h_ctx* ctx, int32_t* out, int on_device) {
 
 int c3h_get_downsampled(c3h_ctx* ctx, float* out, int on_device) {
   if (!ctx || !out) return C3H_ERR_ARG;
+  QUIESCE(ctx);
   if (!ctx->have_grid) return fail(ctx, C3H_ERR_STATE, "no grid");
   if (!ctx->table_valid)
     return fail(ctx, C3H_ERR_STATE, "c3h_get_downsampled: grid was not produced by c3h_voxelize");
@@ -873,6 +890,7 @@ int c3h_get_downsampled(c3h_ctx* ctx, float* out, int on_device) {
 int c3h_set_grid(c3h_ctx* ctx, const uint32_t* words, const int32_t div_b[3],
                  const int32_t min_b[3], float leaf, int on_device) {
   if (!ctx || !div_b || !min_b || !(leaf > 0)) return C3H_ERR_ARG;
+  QUIESCE(ctx);
   int64_t nvox = 1;
   for (int a = 0; a < 3; ++a) {
     if (div_b[a] < 0) return fail(ctx, C3H_ERR_ARG, "c3h_set_grid: negative dims");
@@ -1065,7 +1083,7 @@ int extract_frames(c3h_ctx* ctx, const uint32_t* const* grids, int nf, const c3h
     l.ntiles = ntiles;
     l.debug = 0;
     l.prof = nullptr;
-    if (const char* dbg = getenv("C3H_C3_DEBUG")) l.debug = atoi(dbg);  // diagnostics only
+    if (const char* dbg = c3h::diag_env("C3H_C3_DEBUG")) l.debug = atoi(dbg);  // diagnostics only
     const int64_t tgrid = c3h::c3hlac_grid(l);
     if (nf == 1) {
       int rc = prof_prepare(ctx, tgrid, &l.prof);
@@ -1099,6 +1117,7 @@ int extract_frames(c3h_ctx* ctx, const uint32_t* const* grids, int nf, const c3h
 int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3],
                 int64_t* hist_num_out) {
   if (!ctx) return C3H_ERR_ARG;
+  QUIESCE(ctx);
   const uint32_t* g = ctx->grid_ptr;
   return extract_frames(ctx, &g, 1, p, subdiv_out, hist_num_out);
 }
@@ -1123,6 +1142,7 @@ static int masked_readback(c3h_ctx* ctx, const float* src, int W, float* out, in
 
 int c3h_get_features(c3h_ctx* ctx, float* out, int on_device) {
   if (!ctx || !out) return C3H_ERR_ARG;
+  QUIESCE(ctx);
   if (!ctx->have_feat) return fail(ctx, C3H_ERR_STATE, "no features");
   HIPCHK(hipSetDevice(ctx->device));
   const size_t n = (size_t)ctx->hist_num * ctx->feat_dim;
@@ -1134,6 +1154,7 @@ int c3h_get_features(c3h_ctx* ctx, float* out, int on_device) {
 
 int c3h_get_exist(c3h_ctx* ctx, int32_t* out, int on_device) {
   if (!ctx || !out) return C3H_ERR_ARG;
+  QUIESCE(ctx);
   if (!ctx->have_feat) return fail(ctx, C3H_ERR_STATE, "no features");
   HIPCHK(hipSetDevice(ctx->device));
   const size_t n = (size_t)ctx->hist_num;
@@ -1146,12 +1167,16 @@ int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_
                      const float* axis_q, int32_t M, int32_t r, const float* feature_max,
                      int32_t feature_max_len) {
   if (!ctx) return C3H_ERR_ARG;
+  QUIESCE(ctx);
   if (D < 1 || F < 1 || M < 1 || r < 1 || !axis_q || feature_max_len < 0 ||
       (feature_max_len > 0 && !feature_max))
     return fail(ctx, C3H_ERR_ARG, "c3h_search_setup: bad arguments");
   if (!axis_p && D != F)
     return fail(ctx, C3H_ERR_ARG, "c3h_search_setup: without compression D must equal F");
   HIPCHK(hipSetDevice(ctx->device));
+  // the bases are replaced with synchronous copies: queued kernels of this context may
+  // still read them
+  HIPCHK(hipStreamSynchronize(ctx->stream));
   const int Dpad = (D + 7) / 8 * 8;
   std::vector<float> pt((size_t)F * Dpad, 0.0f);
   for (int d = 0; d < D; ++d) {
@@ -1166,12 +1191,6 @@ int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_
   }
   ENSURE(ctx->axis_pt, pt.size());
   HIPCHK(hipMemcpy(ctx->axis_pt.p, pt.data(), pt.size() * 4, hipMemcpyHostToDevice));
-  if (c3h::compress2_fits(F, D)) {  // per-wave column slices for the lane-per-row compress
-    std::vector<float> pw(c3h::compress2_pw_floats(F));
-    c3h::compress2_pack_host(pt.data(), F, D, Dpad, pw.data());
-    ENSURE(ctx->pw2, pw.size());
-    HIPCHK(hipMemcpy(ctx->pw2.p, pw.data(), pw.size() * 4, hipMemcpyHostToDevice));
-  }
   ENSURE(ctx->axis_q, (size_t)M * r * D);
   HIPCHK(hipMemcpy(ctx->axis_q.p, axis_q, (size_t)M * r * D * 4, hipMemcpyHostToDevice));
   // transposed basis for the fast score path: qt[d][m*r + i] = axis_q[m][i][d]
@@ -1183,12 +1202,6 @@ int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_
       for (int d = 0; d < D; ++d) qt[(size_t)d * Opad + m * r + i] = axis_q[((size_t)m * r + i) * D + d];
   ENSURE(ctx->qt, qt.size());
   HIPCHK(hipMemcpy(ctx->qt.p, qt.data(), qt.size() * 4, hipMemcpyHostToDevice));
-  if (c3h::score2_fits(D, M, r)) {  // per-wave basis windows for the lane-per-position scoring
-    std::vector<float> qw(c3h::score2_qw_floats(D));
-    c3h::score2_pack_host(axis_q, M, r, D, qw.data());
-    ENSURE(ctx->qw2, qw.size());
-    HIPCHK(hipMemcpy(ctx->qw2.p, qw.data(), qw.size() * 4, hipMemcpyHostToDevice));
-  }
   ctx->Opad = Opad;
   ctx->fmax_len = feature_max_len;
   if (feature_max_len > 0) {
@@ -1215,6 +1228,7 @@ int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_
 
 int c3h_set_rank(c3h_ctx* ctx, int32_t rank) {
   if (!ctx || rank < 1 || rank > 4096) return C3H_ERR_ARG;
+  QUIESCE(ctx);
   ctx->rank = rank;
   init_lists(ctx);
   return C3H_OK;
@@ -1222,6 +1236,7 @@ int c3h_set_rank(c3h_ctx* ctx, int32_t rank) {
 
 int c3h_clean_max(c3h_ctx* ctx) {
   if (!ctx) return C3H_ERR_ARG;
+  QUIESCE(ctx);
   if (ctx->lists.M != std::max(ctx->M, 1) || ctx->lists.rank != ctx->rank) init_lists(ctx);
   if (!ctx->lists_host_valid && ctx->lists_dev_valid) {  // device copy is authoritative:
     ctx->pending_clean = true;  // applied by the next replay kernel (or the next download)
@@ -1239,6 +1254,7 @@ int c3h_clean_max(c3h_ctx* ctx) {
 int c3h_search(c3h_ctx* ctx, const int32_t range[3], int32_t exist_threshold, int32_t rotate,
                int32_t remove_overlap, c3h_det* out) {
   if (!ctx) return C3H_ERR_ARG;
+  QUIESCE(ctx);
   HIPCHK(hipSetDevice(ctx->device));
   const int nm = run_search(ctx, range, exist_threshold, rotate, nullptr);
   if (nm < 0) return nm;
@@ -1266,6 +1282,7 @@ int c3h_search(c3h_ctx* ctx, const int32_t range[3], int32_t exist_threshold, in
 int c3h_search_async(c3h_ctx* ctx, const int32_t range[3], int32_t exist_threshold,
                      int32_t rotate, c3h_det* d_out) {
   if (!ctx) return C3H_ERR_ARG;
+  QUIESCE(ctx);
   HIPCHK(hipSetDevice(ctx->device));
   const int nm = run_search(ctx, range, exist_threshold, rotate, d_out);
   if (nm < 0) return nm;
@@ -1288,6 +1305,7 @@ int c3h_set_lanes(c3h_ctx* ctx, int32_t lanes) {
 
 int c3h_set_batch(c3h_ctx* ctx, int32_t frames) {
   if (!ctx || frames < 1 || frames > c3h::kMaxBatch) return C3H_ERR_ARG;
+  QUIESCE(ctx);
   ctx->nbatch = frames;
   return C3H_OK;
 }
@@ -1308,9 +1326,14 @@ int ensure_lanes(c3h_ctx* ctx, int n) {
     HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     ctx->lane_ev.push_back(e);
   }
+  bool synced = false;
   for (int l = 0; l < n; ++l) {
     c3h_ctx* c = ctx->lanes[l];
     if (c->setup_version != ctx->setup_version || !c->have_setup) {
+      if (!synced) {  // pipelined batches of this lane may still be queued on the parent's stream
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        synced = true;
+      }
       int rc = c3h_search_setup(c, ctx->h_axis_p.empty() ? nullptr : ctx->h_axis_p.data(),
                                 ctx->h_var.empty() ? nullptr : ctx->h_var.data(), ctx->D, ctx->F,
                                 ctx->h_axis_q.data(), ctx->M, ctx->r,
@@ -1331,7 +1354,7 @@ int ensure_lanes(c3h_ctx* ctx, int n) {
 int chunk_frames(const uint32_t* const* d_grids, c3h_det* d_out, size_t per_frame, int nframes, int B,
                  int nchunks, int ch, const uint32_t** grids, c3h_det** outs) {
   const int f0 = ch * B, nb = std::min(B, nframes - f0);
-  for (int j = 0; j < nb; ++j) {
+  for (int j = 0; j < nb; ++j) {  // nchunks < 0: natural order throughout
     const int fi = (ch == nchunks - 1) ? (j == 0 ? f0 + nb - 1 : f0 + j - 1) : f0 + j;
     grids[j] = d_grids[fi];
     outs[j] = d_out + (size_t)fi * per_frame;
@@ -1339,82 +1362,184 @@ int chunk_frames(const uint32_t* const* d_grids, c3h_det* d_out, size_t per_fram
   return nb;
 }
 
-// Software-pipelined batches (pipeline.hip): batch b is prepared on buffer set
-// (nchunks-1-b) % 4 (set 0 = this context, so it ends with the last batch) and runs as
-// the occupancy role of tick b, the tile role of tick b+1, compress+gate of b+2 and
-// scoring + rank-1 argmax of b+3.  All buffer sets work on this context's stream.
-// Returns > 0 (modes searched) when it ran, 0 when the configuration does not fit the
-// tick (the caller then runs the lanes), < 0 on error.
+// Software-pipelined batches (pipeline.hip).  Batch number s is prepared on buffer set
+// s % 4 (set 0 = this context) and runs as the occupancy role of one tick, the tile role
+// of the next, compress+gate of the one after and scoring + rank-1 argmax of the fourth.
+// All buffer sets work on this context's stream, so ticks order themselves; the host
+// only enqueues.  The pipeline persists across c3h_stream_frames calls (a continuous
+// frame source keeps it full); c3h_run_frames and c3h_stream_flush drain it.
 constexpr int kPipeDepth = 4;
 
+c3h_ctx* pipe_set(c3h_ctx* ctx, uint64_t seq) {
+  const int set = (int)(seq % kPipeDepth);
+  return set == 0 ? ctx : ctx->lanes[set - 1];
+}
+
+// lane contexts enqueue on the parent's stream while a pipeline call runs
+struct PipeScope {
+  c3h_ctx* ctx;
+  hipStream_t saved[kPipeDepth - 1];
+  explicit PipeScope(c3h_ctx* c) : ctx(c) {
+    ctx->pipe_busy = true;
+    for (int l = 0; l < kPipeDepth - 1 && l < (int)ctx->lanes.size(); ++l) {
+      saved[l] = ctx->lanes[l]->stream;
+      ctx->lanes[l]->stream = ctx->stream;
+    }
+  }
+  ~PipeScope() {
+    for (int l = 0; l < kPipeDepth - 1 && l < (int)ctx->lanes.size(); ++l) ctx->lanes[l]->stream = saved[l];
+    ctx->pipe_busy = false;
+  }
+};
+
+// one tick: the occupancy role of `fresh` (nullable) and the next role of every batch in
+// flight; afterwards every batch is one stage older and finished batches leave
+int pipe_tick(c3h_ctx* ctx, const c3h_ctx::PipeBatch* fresh) {
+  c3h::TickParts tp;
+  tp.prof = &ctx->prof;
+  if (fresh) tp.occ = &fresh->l;
+  for (auto& b : ctx->pipe) {
+    if (b.age == 1) tp.tile = &b.l;
+    if (b.age == 2) {
+      tp.gate = &b.q;
+      tp.comp = &b.sc;
+    }
+    if (b.age == 3) tp.score = &b.q;
+  }
+  {
+    Timed tm(ctx, 5, fresh ? fresh->nf : 0);
+    hipError_t e = c3h::launch_tick(tp, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, "launch_tick", e);
+  }
+  std::vector<c3h_ctx::PipeBatch> next;
+  for (auto& b : ctx->pipe)
+    if (b.age < 3) {
+      next.push_back(b);
+      next.back().age++;
+    }
+  if (fresh) {
+    next.push_back(*fresh);
+    next.back().age = 1;
+  }
+  ctx->pipe.swap(next);
+  return C3H_OK;
+}
+
+int pipe_flush(c3h_ctx* ctx) {
+  if (ctx->pipe.empty()) return C3H_OK;
+  PipeScope scope(ctx);
+  while (!ctx->pipe.empty()) {
+    int rc = pipe_tick(ctx, nullptr);
+    if (rc != C3H_OK) {
+      ctx->pipe.clear();
+      return rc;
+    }
+  }
+  return C3H_OK;
+}
+
+// public entry points that touch this context's buffers drain an open stream first
+int pipe_quiesce(c3h_ctx* ctx) {
+  if (ctx->pipe_busy || ctx->pipe.empty()) return C3H_OK;
+  return pipe_flush(ctx);
+}
+
+// Prepares nb frames as the next batch on its buffer set and launches its first tick.
+// Returns > 0 (modes searched), 0 when the configuration does not fit the tick (only
+// possible for the first batch of a stream: the caller then runs the lanes), < 0 on error.
+int pipe_push(c3h_ctx* ctx, const uint32_t* const* grids, c3h_det* const* outs, int nb,
+              const c3h_ctx::PipeKey& k) {
+  c3h_ctx* c = pipe_set(ctx, ctx->pipe_seq);
+  c->capture = true;
+  c->cap_c3_valid = c->cap_search_valid = false;
+  int rc = c3h_set_grid(c, grids[0], k.div_b, k.min_b, k.leaf, 1);
+  if (rc == C3H_OK) rc = extract_frames(c, grids, nb, &k.p, nullptr, nullptr);
+  if (rc == C3H_OK) rc = search_frames(c, nb, k.range, k.thr, k.rotate, outs, 2);
+  c->capture = false;
+  if (rc < 0) {
+    if (c != ctx) ctx->err = c->err;
+    return rc;
+  }
+  const bool fits = c->cap_c3_valid && c->cap_search_valid && c->cap_sparse_g && c->cap_argmax &&
+                    c3h::tick_ok(c->cap_c3);
+  if (!fits) {  // one geometry per stream: decided on its first batch
+    if (!ctx->pipe.empty()) return fail(ctx, C3H_ERR_STATE, "pipeline: internal: geometry changed");
+    return 0;
+  }
+  c->nframes_feat = 1;  // slot 0 is the context's view from here on
+  const c3h_ctx::PipeBatch fresh{c->cap_c3, c->cap_q, c->cap_sc, nb, 0};
+  int trc = pipe_tick(ctx, &fresh);
+  if (trc != C3H_OK) return trc;
+  ctx->pipe_seq++;
+  ctx->pipe_key = k;
+  ctx->pipe_nm = rc;
+  return rc;
+}
+
+c3h_ctx::PipeKey pipe_key(c3h_ctx* ctx, const int32_t div_b[3], const int32_t min_b[3], float leaf,
+                          const c3h_extract_params* p, const int32_t range[3], int32_t thr, int32_t rotate,
+                          int B) {
+  c3h_ctx::PipeKey k;
+  memset(&k, 0, sizeof(k));  // compared bytewise
+  memcpy(k.div_b, div_b, sizeof(k.div_b));
+  memcpy(k.min_b, min_b, sizeof(k.min_b));
+  k.leaf = leaf;
+  k.p = *p;
+  memcpy(k.range, range, sizeof(k.range));
+  k.thr = thr;
+  k.rotate = rotate ? 1 : 0;
+  k.batch = B;
+  k.rank = ctx->rank;
+  k.setup_version = ctx->setup_version;
+  return k;
+}
+
+bool pipelinable(const c3h_ctx* ctx) {
+  return ctx->pipeline && ctx->rank == 1 && c3h::score_fast_ok(ctx->D, ctx->r);
+}
+
+// Runs nframes through the pipeline in batches of B.  drain: run the fill/drain ticks so
+// every result is complete on return (c3h_run_frames); the last batch is then placed on
+// set 0 with its last frame in slot 0, so this context holds the last frame's state.
+// Returns as pipe_push.
 int run_frames_pipelined(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes,
                          const int32_t div_b[3], const int32_t min_b[3], float leaf,
                          const c3h_extract_params* p, const int32_t range[3], int32_t exist_threshold,
-                         int32_t rotate, c3h_det* d_out, int B) {
+                         int32_t rotate, c3h_det* d_out, int B, bool drain) {
   const size_t per_frame = (size_t)std::max(ctx->M, 1) * ctx->rank;
   const int nchunks = (nframes + B - 1) / B;
   int rc = ensure_lanes(ctx, kPipeDepth - 1);
   if (rc != C3H_OK) return rc;
-  auto set_ctx = [&](int b) {
-    const int set = (nchunks - 1 - b) % kPipeDepth;
-    return set == 0 ? ctx : ctx->lanes[set - 1];
-  };
-  hipStream_t saved[kPipeDepth - 1];
-  for (int l = 0; l < kPipeDepth - 1; ++l) {
-    saved[l] = ctx->lanes[l]->stream;
-    ctx->lanes[l]->stream = ctx->stream;
+  const c3h_ctx::PipeKey k = pipe_key(ctx, div_b, min_b, leaf, p, range, exist_threshold, rotate, B);
+  if (!ctx->pipe.empty() && memcmp(&k, &ctx->pipe_key, sizeof(k)) != 0) {
+    rc = pipe_flush(ctx);  // a different stream: drain the open one first
+    if (rc != C3H_OK) return rc;
   }
-  struct Batch {
-    c3h::C3Launch l;
-    c3h::SparseSearch q;
-    c3h::SparseCompress sc;
-    int nf;
-  };
-  std::vector<Batch> bt(nchunks);
+  PipeScope scope(ctx);
+  if (drain && ctx->pipe.empty())  // the last batch lands on set 0
+    ctx->pipe_seq = (uint64_t)((kPipeDepth - (nchunks - 1) % kPipeDepth) % kPipeDepth);
   int nm = 0;
-  for (int t = 0; t < nchunks + kPipeDepth - 1 && rc >= 0; ++t) {
-    if (t < nchunks) {  // prepare batch t (host state, first-use buffer clears on the stream)
-      c3h_ctx* c = set_ctx(t);
-      const uint32_t* grids[c3h::kMaxBatch];
-      c3h_det* outs[c3h::kMaxBatch];
-      const int nb = chunk_frames(d_grids, d_out, per_frame, nframes, B, nchunks, t, grids, outs);
-      c->capture = true;
-      c->cap_c3_valid = c->cap_search_valid = false;
-      rc = c3h_set_grid(c, grids[0], div_b, min_b, leaf, 1);
-      if (rc == C3H_OK) rc = extract_frames(c, grids, nb, p, nullptr, nullptr);
-      if (rc == C3H_OK) rc = search_frames(c, nb, range, exist_threshold, rotate, outs, 2);
-      c->capture = false;
-      if (rc < 0) {
-        if (c != ctx) ctx->err = c->err;
-        break;
-      }
-      const bool fits = c->cap_c3_valid && c->cap_search_valid && c->cap_sparse_g && c->cap_argmax &&
-                        c3h::tick_ok(c->cap_c3);
-      if (!fits) {  // same geometry for every batch: decided on the first
-        if (t != 0) rc = fail(ctx, C3H_ERR_STATE, "c3h_run_frames: internal: pipeline geometry changed");
-        else rc = 0;
-        break;
-      }
-      nm = rc;
-      bt[t] = Batch{c->cap_c3, c->cap_q, c->cap_sc, nb};
-      c->nframes_feat = 1;  // slot 0 is the context's view from here on
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const uint32_t* grids[c3h::kMaxBatch];
+    c3h_det* outs[c3h::kMaxBatch];
+    const int nb = chunk_frames(d_grids, d_out, per_frame, nframes, B, drain ? nchunks : -1, ch, grids, outs);
+    rc = pipe_push(ctx, grids, outs, nb, k);
+    if (rc <= 0) {
+      if (rc == 0 && ch == 0) return 0;
+      ctx->pipe.clear();
+      return rc == 0 ? fail(ctx, C3H_ERR_STATE, "pipeline: internal: batch does not fit") : rc;
     }
-    c3h::TickParts tp;
-    if (t < nchunks) tp.occ = &bt[t].l;
-    if (t >= 1 && t - 1 < nchunks) tp.tile = &bt[t - 1].l;
-    if (t >= 2 && t - 2 < nchunks) {
-      tp.gate = &bt[t - 2].q;
-      tp.comp = &bt[t - 2].sc;
-    }
-    if (t >= 3 && t - 3 < nchunks) tp.score = &bt[t - 3].q;
-    Timed tm(ctx, 5, t < nchunks ? bt[t].nf : 0);
-    hipError_t e = c3h::launch_tick(tp, ctx->stream);
-    if (e != hipSuccess) rc = hip_fail(ctx, "launch_tick", e);
+    nm = rc;
   }
-  for (int l = 0; l < kPipeDepth - 1; ++l) ctx->lanes[l]->stream = saved[l];
-  if (rc < 0) return rc;
-  if (rc == 0) return 0;
-  // the lane contexts' stream work was enqueued on ctx->stream: nothing to join
+  if (drain) {
+    while (!ctx->pipe.empty()) {
+      rc = pipe_tick(ctx, nullptr);
+      if (rc != C3H_OK) {
+        ctx->pipe.clear();
+        return rc;
+      }
+    }
+  }
   return nm;
 }
 
@@ -1429,15 +1554,19 @@ int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes
   if (!ctx || !d_grids || nframes < 0 || !div_b || !min_b || !p || !range || !d_out)
     return C3H_ERR_ARG;
   if (!ctx->have_setup) return fail(ctx, C3H_ERR_STATE, "c3h_run_frames: no axes (call c3h_search_setup)");
-  if (nframes == 0) return 0;
   HIPCHK(hipSetDevice(ctx->device));
+  {
+    int rc = pipe_flush(ctx);  // an open stream completes first
+    if (rc != C3H_OK) return rc;
+  }
+  if (nframes == 0) return 0;
   const size_t per_frame = (size_t)std::max(ctx->M, 1) * ctx->rank;
   // frames go in chunks of B (one set of launches per chunk, frame = launch y / z index)
   const int B = c3h::score_fast_ok(ctx->D, ctx->r) ? std::max(1, std::min(ctx->nbatch, c3h::kMaxBatch)) : 1;
   const int nchunks = (nframes + B - 1) / B;
-  if (ctx->pipeline && ctx->rank == 1 && c3h::score_fast_ok(ctx->D, ctx->r)) {
+  if (pipelinable(ctx)) {
     const int rc = run_frames_pipelined(ctx, d_grids, nframes, div_b, min_b, leaf, p, range, exist_threshold,
-                                        rotate, d_out, B);
+                                        rotate, d_out, B, true);
     if (rc != 0) return rc;
   }
   // lanes: chunks are spread over K child contexts on their own streams and host threads
@@ -1485,14 +1614,41 @@ int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes
   return lane_rc[0];
 }
 
+int c3h_stream_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes,
+                      const int32_t div_b[3], const int32_t min_b[3], float leaf,
+                      const c3h_extract_params* p, const int32_t range[3], int32_t exist_threshold,
+                      int32_t rotate, c3h_det* d_out) {
+  if (!ctx || !d_grids || nframes < 0 || !div_b || !min_b || !p || !range || !d_out)
+    return C3H_ERR_ARG;
+  if (!ctx->have_setup) return fail(ctx, C3H_ERR_STATE, "c3h_stream_frames: no axes (call c3h_search_setup)");
+  if (nframes == 0) return ctx->pipe_nm;
+  HIPCHK(hipSetDevice(ctx->device));
+  const int B = std::max(1, std::min(ctx->nbatch, c3h::kMaxBatch));
+  if (pipelinable(ctx)) {
+    const int rc = run_frames_pipelined(ctx, d_grids, nframes, div_b, min_b, leaf, p, range, exist_threshold,
+                                        rotate, d_out, B, false);
+    if (rc != 0) return rc;
+  }
+  // not pipelinable: the frames complete as in c3h_run_frames
+  return c3h_run_frames(ctx, d_grids, nframes, div_b, min_b, leaf, p, range, exist_threshold, rotate, d_out);
+}
+
+int c3h_stream_flush(c3h_ctx* ctx) {
+  if (!ctx) return C3H_ERR_ARG;
+  HIPCHK(hipSetDevice(ctx->device));
+  return pipe_flush(ctx);
+}
+
 int c3h_set_pipeline(c3h_ctx* ctx, int32_t enable) {
   if (!ctx) return C3H_ERR_ARG;
+  QUIESCE(ctx);
   ctx->pipeline = enable != 0;
   return C3H_OK;
 }
 
 int c3h_get_compressed(c3h_ctx* ctx, float* out, int on_device) {
   if (!ctx || !out) return C3H_ERR_ARG;
+  QUIESCE(ctx);
   if (!ctx->g_valid) return fail(ctx, C3H_ERR_STATE, "no compressed features (run a search)");
   HIPCHK(hipSetDevice(ctx->device));
   const size_t n = (size_t)ctx->hist_num * ctx->D;
@@ -1507,6 +1663,7 @@ int c3h_get_compressed(c3h_ctx* ctx, float* out, int on_device) {
 
 int c3h_get_scores(c3h_ctx* ctx, double* out, int64_t* n_out, int on_device) {
   if (!ctx) return C3H_ERR_ARG;
+  QUIESCE(ctx);
   if (n_out) *n_out = ctx->scores_n;
   if (!out) return C3H_OK;
   HIPCHK(hipSetDevice(ctx->device));

@@ -22,7 +22,7 @@
 #include <vector>
 
 #include "c3hlac_dev.h"
-#include "search2_dev.h"
+#include "search_dev.h"
 
 namespace c3h {
 namespace {
@@ -33,7 +33,7 @@ struct TickArgs {
   int s_gx, s_groups;
   SparseSearch gq;                   // compress + gate role
   CompressRows cr;
-  int g_ngate, g_ncomp, g_comp2;
+  int g_ngate, g_ncomp;
   KArgs ka;                          // tile role
   int t_grid;
   OccArgs oa;                        // occupancy role
@@ -78,14 +78,12 @@ __device__ __forceinline__ void tick_roles(const TickArgs& t, uint32_t* tick_sme
   if (b < t.n_cg) {
     const int per = t.g_ngate + t.g_ncomp, f = b / per, r = b - f * per;
     if (r < t.g_ngate) gate_body(t.gq, r, f);
-    else if (t.g_comp2) compress2_body(t.cr, r - t.g_ngate, t.g_ncomp, f, reinterpret_cast<float*>(tick_smem));
     else compress_rows_body(t.cr, r - t.g_ngate, t.g_ncomp, f, reinterpret_cast<float*>(tick_smem));
     return;
   }
   b -= t.n_cg;
   const int per = t.s_gx * t.s_groups, f = b / per, r = b - f * per;
-  if (t.sq.v2) score2_body(t.sq, r, f, t.s_gx, reinterpret_cast<float*>(tick_smem));
-  else score_list_body(t.sq, r % t.s_gx, r / t.s_gx, f, t.s_gx, t.s_groups, reinterpret_cast<float*>(tick_smem));
+  score_list_body(t.sq, r % t.s_gx, r / t.s_gx, f, t.s_gx, t.s_groups, reinterpret_cast<float*>(tick_smem));
 }
 
 // waves per SIMD the register allocation must allow (4: the 128-VGPR cap); diagnostics builds
@@ -109,7 +107,7 @@ void tick_prof_dump(const TickArgs& t, long long* d_prof, int total, hipStream_t
   std::vector<long long> v((size_t)2 * total);
   if (hipMemcpyAsync(v.data(), d_prof, v.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess) return;
   if (hipStreamSynchronize(s) != hipSuccess) return;
-  FILE* fp = fopen(getenv("C3H_TICK_PROF"), "a");
+  FILE* fp = fopen(diag_env("C3H_TICK_PROF"), "a");
   if (!fp) return;
   long long t0 = LLONG_MAX;
   for (int b = 0; b < total; ++b) t0 = std::min(t0, v[2 * b]);
@@ -152,7 +150,7 @@ void tick_prof_dump(const TickArgs& t, long long* d_prof, int total, hipStream_t
 }
 
 int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
+  const char* v = diag_env(name);
   return v && *v ? atoi(v) : dflt;
 }
 
@@ -170,7 +168,7 @@ hipError_t launch_tick(const TickParts& p, hipStream_t s) {
   // then tile, compress+gate and scoring in the remaining workgroup slots.
   // C3H_TICK_ORDER="3210" etc. (diagnostics) lists role ids first-dispatched first.
   t.order = 0x3210;
-  if (const char* o = getenv("C3H_TICK_ORDER"))
+  if (const char* o = diag_env("C3H_TICK_ORDER"))
     if (strlen(o) == 4) {
       t.order = 0;
       for (int i = 0; i < 4; ++i) t.order |= (o[i] - '0') << (4 * i);
@@ -178,16 +176,9 @@ hipError_t launch_tick(const TickParts& p, hipStream_t s) {
   if (p.score) {
     const SparseSearch& a = *p.score;
     t.sq = a;
-    if (a.v2) {  // lane = position: one workgroup per 64 listed positions, all models
-      t.s_gx = (int)std::max<int64_t>(1, std::min<int64_t>(score2_chunks(a.pstart[a.nmodes]),
-                                                           env_int("C3H_TICK_SCORE", 24)));
-      t.s_groups = 1;
-      lds = std::max(lds, score2_lds_bytes(a.D));
-    } else {
-      t.s_gx = (int)std::max<int64_t>(1, std::min<int64_t>(sparse_score_blocks(a), env_int("C3H_TICK_SCORE", 16)));
-      t.s_groups = (a.M + a.mpg - 1) / a.mpg;
-      lds = std::max(lds, score_list_lds_bytes(a.D, a.mpg));
-    }
+    t.s_gx = (int)std::max<int64_t>(1, std::min<int64_t>(sparse_score_blocks(a), env_int("C3H_TICK_SCORE", 16)));
+    t.s_groups = (a.M + a.mpg - 1) / a.mpg;
+    lds = std::max(lds, score_list_lds_bytes(a.D, a.mpg));
     t.n_score = t.s_gx * t.s_groups * a.nframes;
   }
   if (p.gate) {
@@ -195,16 +186,10 @@ hipError_t launch_tick(const TickParts& p, hipStream_t s) {
     const SparseCompress& sc = *p.comp;
     t.gq = a;
     t.cr = CompressRows{sc.feat, sc.PT, sc.fmax, sc.G, sc.rows, sc.nrows, sc.F, sc.D, sc.Dpad,
-                        sc.fmax_len, sc.s_feat, sc.s_G, sc.s_rows, sc.s_nrows, sc.PW};
+                        sc.fmax_len, sc.s_feat, sc.s_G, sc.s_rows, sc.s_nrows};
     t.g_ngate = (int)((a.pstart[a.nmodes] + kBlock - 1) / kBlock);
-    t.g_comp2 = sc.PW && compress2_ok(sc.F, sc.D) ? 1 : 0;
-    if (t.g_comp2) {
-      t.g_ncomp = (int)std::max<int64_t>(1, std::min<int64_t>((sc.H + kC2Rows - 1) / kC2Rows, env_int("C3H_TICK_COMP", 16)));
-      lds = std::max(lds, compress2_lds_bytes(sc.F));
-    } else {
-      t.g_ncomp = (int)std::max<int64_t>(1, std::min<int64_t>((sc.H + kRR - 1) / kRR, env_int("C3H_TICK_COMP", 32)));
-      lds = std::max(lds, sizeof(float) * ((size_t)kRK * sc.Dpad + (size_t)kRR * sc.F));
-    }
+    t.g_ncomp = (int)std::max<int64_t>(1, std::min<int64_t>((sc.H + kRR - 1) / kRR, env_int("C3H_TICK_COMP", 32)));
+    lds = std::max(lds, sizeof(float) * ((size_t)kRK * sc.Dpad + (size_t)kRR * sc.F));
     t.n_cg = (t.g_ngate + t.g_ncomp) * a.nframes;
   }
   if (p.tile) {
@@ -228,7 +213,7 @@ hipError_t launch_tick(const TickParts& p, hipStream_t s) {
     t.n_occ = t.o_grid * c.nframes;
     lds = std::max(lds, c.occ_lds);
   }
-  if (const char* m = getenv("C3H_TICK_ROLES")) {  // diagnostics only: bit mask of roles run
+  if (const char* m = diag_env("C3H_TICK_ROLES")) {  // diagnostics only: bit mask of roles run
     const int mask = atoi(m);                       // 1 score, 2 compress+gate, 4 tile, 8 occupancy
     if (!(mask & 1)) t.n_score = 0;
     if (!(mask & 2)) t.n_cg = 0;
@@ -237,18 +222,19 @@ hipError_t launch_tick(const TickParts& p, hipStream_t s) {
   }
   const int total = t.n_score + t.n_cg + t.n_tile + t.n_occ;
   if (total == 0) return hipSuccess;
-  static long long* d_prof = nullptr;  // diagnostics only
-  static int d_prof_n = 0;
-  if (getenv("C3H_TICK_PROF")) {
-    if (d_prof_n < total) {
-      if (d_prof) (void)hipFree(d_prof);
-      if (hipMalloc(&d_prof, (size_t)2 * total * 8) != hipSuccess) return hipErrorOutOfMemory;
-      d_prof_n = total;
+  if (diag_env("C3H_TICK_PROF") && p.prof) {  // diagnostics builds only; synchronises
+    DevBuf<long long>& b = *p.prof;
+    if (b.n < (size_t)2 * total) {
+      if (b.p) (void)hipFree(b.p);
+      b.p = nullptr;
+      b.n = 0;
+      if (hipMalloc(&b.p, (size_t)2 * total * 8) != hipSuccess) return hipErrorOutOfMemory;
+      b.n = (size_t)2 * total;
     }
-    t.prof = d_prof;
+    t.prof = b.p;
   }
   c3h_tick_kernel<<<(unsigned)total, kBlock, lds, s>>>(t);
-  if (t.prof) tick_prof_dump(t, d_prof, total, s);
+  if (t.prof) tick_prof_dump(t, t.prof, total, s);
   return hipGetLastError();
 }
 

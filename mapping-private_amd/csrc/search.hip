@@ -16,7 +16,7 @@
 //   reference's (mode, z, y, x) order; only candidates above the current rank-th score
 //   (the lists only grow) are visited serially.
 #include "c3h_internal.h"
-#include "search2_dev.h"
+#include "search_dev.h"
 
 namespace c3h {
 namespace {
@@ -189,17 +189,6 @@ __global__ __launch_bounds__(kBlock) void compress_gate_kernel(CompressRows cr, 
   else compress_rows_body(cr, blockIdx.x - ngate, gridDim.x - ngate, blockIdx.y, cg_smem);
 }
 
-__global__ __launch_bounds__(kBlock) void compress2_gate_kernel(CompressRows cr, SparseSearch b, int ngate) {
-  extern __shared__ __attribute__((aligned(16))) float cg2_smem[];
-  if ((int)blockIdx.x < ngate) gate_body(b, blockIdx.x, blockIdx.y);
-  else compress2_body(cr, blockIdx.x - ngate, gridDim.x - ngate, blockIdx.y, cg2_smem);
-}
-
-__global__ __launch_bounds__(kBlock) void score2_kernel(SparseSearch b) {
-  extern __shared__ __attribute__((aligned(16))) float s2_smem[];
-  score2_body(b, blockIdx.x, blockIdx.y, gridDim.x, s2_smem);
-}
-
 __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch b) {
   extern __shared__ __attribute__((aligned(16))) float sl_smem[];
   score_list_body(b, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y, sl_smem);
@@ -311,21 +300,6 @@ __global__ __launch_bounds__(64) void replay_kernel(const double* __restrict__ s
 
 }  // namespace
 
-// The lane-per-item bodies of search2_dev.h are opt-in (C3H_LANE_BODIES=1, read at search
-// setup): measured on MI355X at 256^3 / S=10 / 10 models, they made the pipeline tick 2.5x
-// slower (67.8 vs 27.2 us/frame, profiles/r1/ab1_lane_bodies.log) -- the block bodies of
-// search_dev.h stay the default.
-static bool lane_bodies() {
-  const char* e = getenv("C3H_LANE_BODIES");
-  return e && atoi(e) != 0;
-}
-bool compress2_fits(int F, int D) { return lane_bodies() && compress2_ok(F, D); }
-bool score2_fits(int D, int M, int r) { return lane_bodies() && score2_ok(D, M, r); }
-size_t compress2_pw_floats(int F) { return (size_t)F * kC2W; }
-void compress2_pack_host(const float* PT, int F, int D, int Dpad, float* PW) { compress2_pack(PT, F, D, Dpad, PW); }
-size_t score2_qw_floats(int D) { return (size_t)D * kSW; }
-void score2_pack_host(const float* axis_q, int M, int r, int D, float* QW) { score2_pack(axis_q, M, r, D, QW); }
-
 bool compress_rows_ok(int F, int Dpad) {
   return Dpad <= 128 && ((size_t)kRK * Dpad + (size_t)kRR * F) * 4 <= 65536;
 }
@@ -399,23 +373,13 @@ hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc,
   const unsigned nf = (unsigned)a.nframes;
   if (sc) {  // compress (non-empty rows) and gate in one launch
     const CompressRows cr{sc->feat, sc->PT, sc->fmax, sc->G, sc->rows, sc->nrows, sc->F, sc->D, sc->Dpad,
-                          sc->fmax_len, sc->s_feat, sc->s_G, sc->s_rows, sc->s_nrows, sc->PW};
-    if (sc->PW && compress2_ok(sc->F, sc->D)) {  // lane = row: ~700 non-empty rows are ~11 workgroups
-      const unsigned ncomp = (unsigned)std::min<int64_t>((sc->H + kC2Rows - 1) / kC2Rows, 32);
-      compress2_gate_kernel<<<dim3(ngate + ncomp, nf), kBlock, compress2_lds_bytes(sc->F), s>>>(cr, a, (int)ngate);
-    } else {
-      const size_t lds = sizeof(float) * ((size_t)kRK * sc->Dpad + (size_t)kRR * sc->F);
-      // compress workgroups: surface frames have ~700 non-empty rows (~44 row blocks)
-      const unsigned ncomp = (unsigned)std::min<int64_t>((sc->H + kRR - 1) / kRR, kCompressGridCap);
-      compress_gate_kernel<<<dim3(ngate + ncomp, nf), kBlock, lds, s>>>(cr, a, (int)ngate);
-    }
+                          sc->fmax_len, sc->s_feat, sc->s_G, sc->s_rows, sc->s_nrows};
+    const size_t lds = sizeof(float) * ((size_t)kRK * sc->Dpad + (size_t)kRR * sc->F);
+    // compress workgroups: surface frames have ~700 non-empty rows (~44 row blocks)
+    const unsigned ncomp = (unsigned)std::min<int64_t>((sc->H + kRR - 1) / kRR, kCompressGridCap);
+    compress_gate_kernel<<<dim3(ngate + ncomp, nf), kBlock, lds, s>>>(cr, a, (int)ngate);
   } else {
     gate_kernel<<<dim3(ngate, nf), kBlock, 0, s>>>(a);
-  }
-  if (a.v2) {  // lane = position; surface frames pass ~1k positions (~15 chunks)
-    const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(score2_chunks(ptot), 64));
-    score2_kernel<<<dim3(gx, nf), kBlock, score2_lds_bytes(a.D), s>>>(a);
-    return hipGetLastError();
   }
   const size_t lds = score_list_lds_bytes(a.D, a.mpg);
   const unsigned groups = (unsigned)((a.M + a.mpg - 1) / a.mpg);

@@ -24,7 +24,6 @@ struct CompressRows {
   const uint32_t* nrows;
   int F, D, Dpad, fmax_len;
   int64_t s_feat, s_G, s_rows, s_nrows;  // per-frame strides (frame = launch y / z index)
-  const float* PW;                       // per-wave column slices of P (compress2_pack)
 };
 
 __device__ __forceinline__ void compress_rows_body(const CompressRows& cr, int bid, int nblk, int64_t f,

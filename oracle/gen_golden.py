@@ -64,6 +64,10 @@ def one(name, pts, leaf, subdiv, offset, D, M, r, ranges, rank, thr_exist, seed,
 
 def main():
     OUT.mkdir(parents=True, exist_ok=True)
+    # BASELINE configs[0] at its stated size: 50k-point parity cloud -> 64^3, C3-HLAC-981,
+    # subdivision 10 (7^3 = 343 subdivisions), 1-model search
+    one("cfg0_parity_64", synth.parity_cloud(50_000, grid=64, leaf=0.01, seed=0xC3A1AC), 0.01, 10, (0, 0, 0),
+        D=100, M=1, r=20, ranges=(2, 2, 2), rank=1, thr_exist=100, seed=10)
     one("cfg1_parity_24", synth.parity_cloud(4000, grid=24, leaf=0.01, seed=101), 0.01, 8, (0, 0, 0),
         D=12, M=2, r=4, ranges=(1, 1, 2), rank=1, thr_exist=10, seed=11)
     one("kinect_40_offsets", synth.kinect_scene(25_000, grid=40, leaf=0.02, seed=202), 0.02, 6, (1, 2, 0),

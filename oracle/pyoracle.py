@@ -190,3 +190,34 @@ def pca_read(path, ascii=False, max_dim=4096):
     if dim < 0:
         raise RuntimeError("orc_pca_read failed %d" % dim)
     return buf[: dim * dim].reshape(dim, dim).T.copy(), var[:dim].copy(), (mean[:dim].copy() if hm.value else None)
+
+
+def grid_inputs(words, div_b, leaf, min_b=(0, 0, 0)):
+    """(grid dict, leaf_layout, cloud) for a packed colour/occupancy grid (uint32 words in
+    z, y, x order, 0 = empty, else 1<<24 | rgb): the inputs getVoxelGrid would leave for a
+    cloud with one point at the centre of every occupied cell, so centroid-derived and
+    index-derived cells coincide (the grid-only entry points' definition)."""
+    words = np.ascontiguousarray(words, np.uint32).reshape(-1)
+    dx, dy, dz = (int(v) for v in div_b)
+    assert words.size == dx * dy * dz
+    occ = words != 0
+    layout = np.full(words.size, -1, np.int32)
+    idx = np.flatnonzero(occ)
+    layout[idx] = np.arange(idx.size, dtype=np.int32)
+    x, y, z = idx % dx, (idx // dx) % dy, idx // (dx * dy)
+    lf = np.float64(np.float32(leaf))
+    cloud = np.empty((idx.size, 4), np.float32)
+    cloud[:, 0] = ((x + int(min_b[0]) + 0.5) * lf).astype(np.float32)
+    cloud[:, 1] = ((y + int(min_b[1]) + 0.5) * lf).astype(np.float32)
+    cloud[:, 2] = ((z + int(min_b[2]) + 0.5) * lf).astype(np.float32)
+    cloud[:, 3] = (words[idx] & np.uint32(0xFFFFFF)).view(np.float32)
+    g = OrcGrid()
+    for a, (d, m) in enumerate(zip((dx, dy, dz), min_b)):
+        g.div_b[a] = d
+        g.min_b[a] = int(m)
+        g.max_b[a] = int(m) + d - 1
+    g.n_valid = idx.size
+    g.n_occ = idx.size
+    g.leaf = float(leaf)
+    g.inv_leaf = float(np.float32(1) / np.float32(leaf))
+    return g, layout, cloud

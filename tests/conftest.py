@@ -38,4 +38,4 @@ def load_golden(name):
         return {k: z[k] for k in z.files}
 
 
-GOLDEN_CASES = ["cfg1_parity_24", "kinect_40_offsets", "kinect_32_whole"]
+GOLDEN_CASES = ["cfg0_parity_64", "cfg1_parity_24", "kinect_40_offsets", "kinect_32_whole"]

@@ -381,9 +381,10 @@ def test_run_frames_lanes_match_sequential(ctx, lanes, batch, rank, pipe):
     ctx.set_lanes(lanes)
     ctx.set_batch(batch)
     ctx.set_pipeline(pipe)
+    torch.cuda.synchronize()  # d_out / grids were written on torch's stream, the library runs on its own
     ctx.run_frames(np.array([g.data_ptr() for g in d_grids], np.uint64), (G, G, G), (0, 0, 0), 0.01, 117,
                    THR, S, rng_box, 20, True, d_out.data_ptr())
-    torch.cuda.synchronize()
+    ctx.synchronize()
     got = d_out.cpu().numpy().view(c3hlac.DET_DTYPE).reshape(len(words), 4, rank)
     for i in range(len(words)):
         np.testing.assert_array_equal(got[i], ref[i])
@@ -494,9 +495,10 @@ def test_run_frames_pipelined_many_batches(ctx, batch):
     d_out = torch.zeros((len(words), 4 * 3), dtype=torch.int64, device=dev)
     ctx.set_batch(batch)
     ctx.set_pipeline(1)
+    torch.cuda.synchronize()  # d_out / grids were written on torch's stream, the library runs on its own
     ctx.run_frames(np.array([g.data_ptr() for g in d_grids], np.uint64), (G, G, G), (0, 0, 0), 0.01, 117,
                    THR, S, rng_box, 20, True, d_out.data_ptr())
-    torch.cuda.synchronize()
+    ctx.synchronize()
     got = d_out.cpu().numpy().view(c3hlac.DET_DTYPE).reshape(len(words), 4, 1)
     for i in range(len(words)):
         np.testing.assert_array_equal(got[i], ref[i], err_msg="frame %d" % i)

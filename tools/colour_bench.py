@@ -7,7 +7,7 @@ import os
 import sys
 import time
 
-sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), "mapping-private_amd")]
+sys.path[:0] = [os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mapping-private_amd")]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import c3hlac  # noqa: E402

@@ -1,4 +1,4 @@
-"""Per-launch HBM traffic of the C3 stage from rocprofv3 --pmc passes (scripts_pmc.sh).
+"""Per-launch HBM traffic of the C3 stage from rocprofv3 --pmc passes (tools/pmc.sh).
 
 FETCH_SIZE / WRITE_SIZE are in KB per dispatch.  gfx950 correction
 (MI355X_MICROARCH.md, HBM/rocprofv3): FETCH_SIZE reports exactly half of the bytes of a
@@ -8,7 +8,7 @@ tick dispatches and divided by the frames that went through the pipeline (each f
 passes every role exactly once).  Gathers (tile halos, box sums) are 4-16 B per lane and
 uncalibrated: the x2 correction is exact only for the occupancy stream, which is ~90 %
 of the bytes.
-Usage: python tools_pmc_summary.py <pmc_dir> <out.json> [frames_per_dispatch] [pipeline_frames]"""
+Usage: python tools/pmc_summary.py <pmc_dir> <out.json> [frames_per_dispatch] [pipeline_frames]"""
 import collections
 import csv
 import json
