@@ -137,6 +137,9 @@ int c3h_feature_pcd_write(const char* path, const float* feat, int64_t rows, int
  * the reference's silent-empty cases: offsets >= grid or a negative threshold). */
 int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3],
                 int64_t* hist_num);
+/* the features the context holds (the last extract, or after c3h_run_frames the last
+ * frame's): getSubdivNum, hist_num and the dimension (981 / 117; 0 before any extract) */
+int c3h_get_feature_info(c3h_ctx* ctx, int32_t subdiv_out[3], int64_t* hist_num, int32_t* dim);
 /* hist_num x variant floats of the last extract */
 int c3h_get_features(c3h_ctx* ctx, float* out, int on_device);
 /* exist_voxel_num of SearchC3HLAC::setC3HLAC

@@ -202,8 +202,22 @@ class Context:
         nm = self._chk(fn(self.h, ptr(gp), gp.size, i32x3(div_b), i32x3(min_b), float(leaf),
                           C.byref(p), i32x3(ranges), int(exist_threshold),
                           int(bool(rotate)), ptr(d_out)), "run_frames")
-        self.variant = int(variant)
+        if not stream:  # the context holds the last frame's grid, features and search
+            self._refresh()
         return nm
+
+    def _refresh(self):
+        """Re-read the grid / feature state the library holds (after run_frames)."""
+        gi = _capi.GridInfo()
+        if self.lib.c3h_get_grid_info(self.h, C.byref(gi)) == 0:
+            self.info = gi
+        sb = (C.c_int32 * 3)()
+        hn = C.c_int64()
+        dim = C.c_int32()
+        self._chk(self.lib.c3h_get_feature_info(self.h, sb, C.byref(hn), C.byref(dim)), "get_feature_info")
+        self.subdiv = tuple(int(x) for x in sb)
+        self.hist_num = int(hn.value)
+        self.variant = int(dim.value) or self.variant
 
     def stream_flush(self):
         """c3h_stream_flush: the remaining ticks of an open frame stream (no host sync)."""

@@ -63,6 +63,7 @@ _SIGS = {
     "c3h_feature_pcd_read": (C.c_int, [C.c_char_p, _P, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
     "c3h_feature_pcd_write": (C.c_int, [C.c_char_p, _P, C.c_int64, C.c_int32, C.c_int32, C.c_char_p]),
     "c3h_extract": (C.c_int, [_P, C.POINTER(ExtractParams), C.POINTER(C.c_int32), C.POINTER(C.c_int64)]),
+    "c3h_get_feature_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
     "c3h_get_features": (C.c_int, [_P, _P, C.c_int]),
     "c3h_get_exist": (C.c_int, [_P, _P, C.c_int]),
     "c3h_search_setup": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int32, _P, C.c_int32, C.c_int32, _P, C.c_int32]),

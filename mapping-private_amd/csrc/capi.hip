@@ -1140,6 +1140,17 @@ static int masked_readback(c3h_ctx* ctx, const float* src, int W, float* out, in
   return C3H_OK;
 }
 
+int c3h_get_feature_info(c3h_ctx* ctx, int32_t subdiv_out[3], int64_t* hist_num, int32_t* dim) {
+  if (!ctx) return C3H_ERR_ARG;
+  QUIESCE(ctx);
+  const bool h = ctx->have_feat;
+  if (subdiv_out)
+    for (int a = 0; a < 3; ++a) subdiv_out[a] = h ? ctx->subdiv_b[a] : 0;
+  if (hist_num) *hist_num = h ? ctx->hist_num : 0;
+  if (dim) *dim = h ? ctx->feat_dim : 0;
+  return C3H_OK;
+}
+
 int c3h_get_features(c3h_ctx* ctx, float* out, int on_device) {
   if (!ctx || !out) return C3H_ERR_ARG;
   QUIESCE(ctx);
