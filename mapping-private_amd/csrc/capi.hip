@@ -387,11 +387,13 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
   const bool sparse_g = !ctx->g_valid && fast && ctx->rows_valid &&
                         c3h::compress_rows_ok(ctx->F, ctx->Dpad);
   if (ctx->capture && !sparse_g) return 0;  // not pipelinable: the caller falls back
-  if (!ctx->g_valid && !sparse_g) {  // nf == 1 here
-    Timed t(ctx, 2);
-    HIPCHK(c3h::launch_compress(ctx->feat.p, H, ctx->F, ctx->axis_pt.p, ctx->D, ctx->Dpad,
-                                ctx->fmax.p, ctx->fmax_len, ctx->G.p, nullptr, nullptr,
-                                ctx->feat_sparse ? ctx->exist.p : nullptr, ctx->stream));
+  if (!ctx->g_valid && !sparse_g) {  // dense compress of every frame of the extract
+    Timed t(ctx, 2, nf);
+    for (int f = 0; f < nf; ++f)
+      HIPCHK(c3h::launch_compress(ctx->feat.p + (size_t)f * H * ctx->F, H, ctx->F, ctx->axis_pt.p, ctx->D,
+                                  ctx->Dpad, ctx->fmax.p, ctx->fmax_len, ctx->G.p + (size_t)f * H * ctx->D,
+                                  nullptr, nullptr, ctx->feat_sparse ? ctx->exist.p + (size_t)f * H : nullptr,
+                                  ctx->stream));
     ctx->g_valid = true;
     ctx->g_sparse = false;
   }

@@ -189,7 +189,7 @@ hipError_t launch_tick(const TickParts& p, hipStream_t s) {
                         sc.fmax_len, sc.s_feat, sc.s_G, sc.s_rows, sc.s_nrows};
     t.g_ngate = (int)((a.pstart[a.nmodes] + kBlock - 1) / kBlock);
     t.g_ncomp = (int)std::max<int64_t>(1, std::min<int64_t>((sc.H + kRR - 1) / kRR, env_int("C3H_TICK_COMP", 32)));
-    lds = std::max(lds, sizeof(float) * ((size_t)kRK * sc.Dpad + (size_t)kRR * sc.F));
+    lds = std::max(lds, compress_rows_lds_bytes(sc.Dpad));
     t.n_cg = (t.g_ngate + t.g_ncomp) * a.nframes;
   }
   if (p.tile) {

@@ -301,7 +301,8 @@ __global__ __launch_bounds__(64) void replay_kernel(const double* __restrict__ s
 }  // namespace
 
 bool compress_rows_ok(int F, int Dpad) {
-  return Dpad <= 128 && ((size_t)kRK * Dpad + (size_t)kRR * F) * 4 <= 65536;
+  (void)F;
+  return Dpad <= 128;
 }
 
 hipError_t launch_compress(const float* feat, int64_t H, int F, const float* axis_pt, int D,
@@ -309,7 +310,7 @@ hipError_t launch_compress(const float* feat, int64_t H, int F, const float* axi
                            const int32_t* rows, const uint32_t* nrows, const int32_t* exist,
                            hipStream_t s) {
   if (rows && compress_rows_ok(F, Dpad)) {  // sparse list
-    const size_t lds = sizeof(float) * ((size_t)kRK * Dpad + (size_t)kRR * F);
+    const size_t lds = compress_rows_lds_bytes(Dpad);
     const CompressRows cr{feat, axis_pt, fmax, G, rows, nrows, F, D, Dpad, fmax_len, 0, 0, 0, 0};
     compress_rows_kernel<<<(unsigned)((H + kRR - 1) / kRR), kBlock, lds, s>>>(cr);
     return hipGetLastError();
@@ -374,7 +375,7 @@ hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc,
   if (sc) {  // compress (non-empty rows) and gate in one launch
     const CompressRows cr{sc->feat, sc->PT, sc->fmax, sc->G, sc->rows, sc->nrows, sc->F, sc->D, sc->Dpad,
                           sc->fmax_len, sc->s_feat, sc->s_G, sc->s_rows, sc->s_nrows};
-    const size_t lds = sizeof(float) * ((size_t)kRK * sc->Dpad + (size_t)kRR * sc->F);
+    const size_t lds = compress_rows_lds_bytes(sc->Dpad);
     // compress workgroups: surface frames have ~700 non-empty rows (~44 row blocks)
     const unsigned ncomp = (unsigned)std::min<int64_t>((sc->H + kRR - 1) / kRR, kCompressGridCap);
     compress_gate_kernel<<<dim3(ngate + ncomp, nf), kBlock, lds, s>>>(cr, a, (int)ngate);

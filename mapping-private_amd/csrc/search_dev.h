@@ -8,12 +8,17 @@
 namespace c3h {
 
 // Sparse compress (row list from the extract): 16 listed rows per workgroup x all
-// columns (Dpad <= 128).  The 16 feature rows (max-normalised) and 32-row chunks of P
-// are staged in LDS, P prefetched one chunk ahead into registers so only the first
-// load's latency is exposed; thread = (row, 8 columns); the fma chain per output runs
-// in ascending j exactly like compress_kernel, so both paths give identical G rows.
+// columns (Dpad <= 128).  Per 32-feature chunk, the 16 rows' feature slice (max-
+// normalised) and the 32 x Dpad slice of P are staged in LDS, both prefetched one chunk
+// ahead into registers so only the first load's latency is exposed; LDS use does not
+// depend on F (981 fits the tick).  Thread = (row, 8 columns); the fma chain per output
+// runs in ascending j exactly like compress_kernel, so both paths give identical G rows.
 constexpr int kRR = 16, kRK = 32;
+constexpr int kRS = kRK + 1;  // feature slice row stride (4 rows per wave: no bank conflict)
 constexpr int kCompressGridCap = 128;  // row-block workgroups per frame of the fused launch
+__host__ __device__ inline size_t compress_rows_lds_bytes(int Dpad) {
+  return sizeof(float) * ((size_t)kRK * Dpad + (size_t)kRR * kRS);
+}
 
 struct CompressRows {
   const float* feat;
@@ -34,7 +39,7 @@ __device__ __forceinline__ void compress_rows_body(const CompressRows& cr, int b
   const int32_t* __restrict__ rows = cr.rows + f * cr.s_rows;
   const int F = cr.F, D = cr.D, Dpad = cr.Dpad, fmax_len = cr.fmax_len;
   float* pc = csm;                 // kRK x Dpad
-  float* fs = csm + kRK * Dpad;    // kRR x F
+  float* fs = csm + kRK * Dpad;    // kRR x kRS (one 32-feature slice of the 16 rows)
   const int tid = threadIdx.x;
   const int nq4 = kRK * Dpad / 4, tot4 = F * Dpad / 4;
   const float4* P4 = reinterpret_cast<const float4*>(cr.PT);
@@ -46,6 +51,26 @@ __device__ __forceinline__ void compress_rows_body(const CompressRows& cr, int b
       pre[j] = (e < nq4 && g < tot4) ? P4[g] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
+  // feature slice: element e = tid + i * kBlock -> row e / kRK, feature c * kRK + e % kRK
+  float fpre[kRR * kRK / kBlock];
+  int64_t rbase[kRR * kRK / kBlock];
+  auto load_feat = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < kRR * kRK / kBlock; ++i) {
+      const int e = tid + i * kBlock, j = c * kRK + (e & (kRK - 1));
+      float v = 0.0f;
+      if (rbase[i] >= 0 && j < F) {
+        v = feat[rbase[i] + j];
+        if (j < fmax_len) {  // setData max-normalisation (search.cpp:563-570)
+          const float mx = fmax[j];
+          if (mx == 0.0f) v = 0.0f;
+          else if (v == mx) v = 1.0f;
+          else v = __fdiv_rn(v, mx);
+        }
+      }
+      fpre[i] = v;
+    }
+  };
   // P's first chunk is independent of the row count: in flight before the count arrives
   load_chunk(0);
   const int n = (int)cr.nrows[f * cr.s_nrows];
@@ -55,20 +80,12 @@ __device__ __forceinline__ void compress_rows_body(const CompressRows& cr, int b
   // row blocks bid, bid + nblk, ... (the launch holds few workgroups; dense scenes loop)
   for (int r0 = bid * kRR; r0 < n; r0 += nblk * kRR) {
     if (r0 != bid * kRR) load_chunk(0);
-    for (int e = tid; e < kRR * F; e += kBlock) {
-      const int r = e / F, j = e - r * F;
-      float v = 0.0f;
-      if (r0 + r < n) {
-        v = feat[(int64_t)rows[r0 + r] * F + j];
-        if (j < fmax_len) {  // setData max-normalisation (search.cpp:563-570)
-          const float mx = fmax[j];
-          if (mx == 0.0f) v = 0.0f;
-          else if (v == mx) v = 1.0f;
-          else v = __fdiv_rn(v, mx);
-        }
-      }
-      fs[e] = v;
+#pragma unroll
+    for (int i = 0; i < kRR * kRK / kBlock; ++i) {
+      const int r = (tid + i * kBlock) / kRK;
+      rbase[i] = r0 + r < n ? (int64_t)rows[r0 + r] * F : -1;
     }
+    load_feat(0);
     float acc[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) acc[q] = 0.0f;
@@ -79,11 +96,19 @@ __device__ __forceinline__ void compress_rows_body(const CompressRows& cr, int b
         const int e = tid + j * kBlock;
         if (e < nq4) reinterpret_cast<float4*>(pc)[e] = pre[j];
       }
-      if (c + 1 < nch) load_chunk(c + 1);
+#pragma unroll
+      for (int i = 0; i < kRR * kRK / kBlock; ++i) {
+        const int e = tid + i * kBlock;
+        fs[(e / kRK) * kRS + (e & (kRK - 1))] = fpre[i];
+      }
+      if (c + 1 < nch) {
+        load_chunk(c + 1);
+        load_feat(c + 1);
+      }
       lds_barrier();
       if (active) {
         const int kn = min(kRK, F - c * kRK);
-        const float* fr = fs + row * F + c * kRK;
+        const float* fr = fs + row * kRS;
         for (int k = 0; k < kn; ++k) {
           const float fv = fr[k];
           const float4 p0 = *reinterpret_cast<const float4*>(&pc[k * Dpad + 8 * cg]);
