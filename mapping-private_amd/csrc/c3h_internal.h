@@ -84,22 +84,46 @@ inline const char* diag_env(const char* name) {
 }
 
 // ---- launchers (defined in the .hip files) ----------------------------------------
-hipError_t launch_minmax(const float4* pts, int64_t n, float z_limit, uint32_t* out,
-                         hipStream_t s);
-hipError_t launch_voxel_accum(const float4* pts, int64_t n, float z_limit, float inv,
-                              const int32_t min_b[3], const int32_t div_b[3], uint32_t* keys,
-                              uint32_t* cnt, uint32_t* sr, uint32_t* sg, uint32_t* sb,
-                              float* sx, float* sy, float* sz, uint64_t table_size,
-                              uint32_t* overflow, hipStream_t s);
-hipError_t launch_voxel_scatter(const uint32_t* keys, const uint32_t* cnt, const uint32_t* sr,
-                                const uint32_t* sg, const uint32_t* sb, uint64_t table_size,
-                                uint32_t* grid, uint32_t* n_occ, hipStream_t s);
+// voxeliser (voxelize.hip): counters are uint32 words of VoxArgs::cnt
+enum {
+  kVcMin = 0,     // int32[3] min cell
+  kVcMax = 3,     // int32[3] max cell
+  kVcValid = 6,   // u64 valid points
+  kVcSlots = 8,   // [2] voxels listed by the frame of each epoch parity
+  kVcFlag = 10,   // voxels whose centroid may leave their cell
+  kVcErr = 11,    // cell range / table overflow
+  kVcOver = 12,   // grid buffer too small (scatter not run)
+  kVcOff = 13,    // off-cell voxels recorded by the exact pass
+  kVcWords = 16
+};
+struct VoxArgs {
+  const float4* pts;
+  int64_t n;
+  float z_limit, inv, leaf;
+  unsigned long long* key;  // global hash table: absolute cell key (~0 = empty)
+  unsigned long long* sa;   // count << 40 | sum r
+  unsigned long long* sb;   // sum b << 32 | sum g
+  uint32_t* margin;         // min distance (cells, float bits) of a member point to the cell boundary
+  uint32_t* slotpos;        // slot -> position in the frame's slot list
+  uint64_t tmask;           // table size - 1 (power of two)
+  uint32_t* lists;          // [slots parity 0 | slots parity 1 | grid words parity 0 | parity 1] x lcap
+  uint64_t lcap;
+  uint32_t* cnt;            // kVcWords counters
+  uint32_t* grid;           // packed grid buffer (capacity grid_cap words)
+  int64_t grid_cap;
+  int par;                  // epoch parity of this frame
+  int clear_tables, clear_grid;  // clear what the previous frame listed
+};
+hipError_t launch_voxelize(const VoxArgs& a, int64_t list_hint, hipStream_t s);
+hipError_t launch_vox_scatter(const VoxArgs& a, hipStream_t s);
+hipError_t launch_vox_centroids(const VoxArgs& a, int64_t ns, uint32_t* counts, uint32_t* offs, uint32_t* cur,
+                                uint32_t* block_sums, uint32_t* bucket, float4* cent, int32_t* offcell,
+                                hipStream_t s);
+hipError_t launch_vox_downsampled(const VoxArgs& a, int64_t ns, const float4* cent, const int32_t* leaf,
+                                  float* out, hipStream_t s);
+int64_t scan_blocks(int64_t n);
 hipError_t launch_leaf_layout(const uint32_t* grid, int64_t nvox, int32_t* leaf,
                               uint32_t* block_sums, int64_t nblocks, hipStream_t s);
-hipError_t launch_downsampled(const int32_t* leaf, const uint32_t* grid, int64_t nvox,
-                              const int32_t div_b[3], const uint32_t* keys, const uint32_t* cnt,
-                              const float* sx, const float* sy, const float* sz,
-                              uint64_t table_size, float* out, hipStream_t s);
 
 #ifndef C3H_MAX_BATCH
 #define C3H_MAX_BATCH 64
@@ -140,6 +164,9 @@ int64_t c3hlac_grid(const C3Launch& a);  // persistent grid of the tile kernel
 hipError_t launch_c3hlac(const C3Launch& a, hipStream_t s);
 // colour.hip: per-channel 256-bin histograms of the occupied voxels (adds into out[768])
 hipError_t launch_colour_hist(const uint32_t* grid, int64_t nvox, unsigned long long* out, hipStream_t s);
+// voxels whose centroid cells differ from their own (exact 64-bit sums, before finalize)
+hipError_t launch_offcell_delta(const int32_t* rec, int nrec, const C3Launch& l, int hist1, const int off[3],
+                                const int sb[3], float inv_s, hipStream_t s);
 hipError_t launch_c3_finalize(const unsigned long long* acc64, int64_t hist_num, int variant,
                               float* feat, int32_t* exist, int nframes, hipStream_t s);
 
@@ -275,9 +302,23 @@ struct c3h_ctx {
   c3h::DevBuf<uint32_t> grid;       // owned packed grid
   const uint32_t* grid_ptr = nullptr;  // the grid in use (owned or bound)
   c3h::DevBuf<float> pts;           // staging copy of host points
-  c3h::DevBuf<uint32_t> keys, cnt, sr, sg, sb;  // voxel hash table
-  c3h::DevBuf<float> sx, sy, sz;
-  uint64_t table_size = 0;          // power of two
+  // voxeliser state (voxelize.hip): global hash table, slot / grid-word lists by epoch
+  // parity, counters; what the previous frame listed is cleared by the next frame
+  c3h::DevBuf<unsigned long long> vkey, vsa, vsb;
+  c3h::DevBuf<uint32_t> vmargin, vslotpos, vlists, vcnt;
+  uint64_t vtsize = 0, vlcap = 0;
+  int vpar = 0;
+  int64_t vns_prev = 0;             // voxels the previous frame listed
+  bool vgrid_tracked = false;       // grid buffer is zero outside the previous frame's list
+  c3h::VoxArgs vargs{};             // the last voxelize (exact centroid pass, downsampled)
+  int64_t vns = 0;                  // voxels of the last voxelize
+  // exact centroid pass: per-voxel counts / offsets / cursors, point buckets, centroids,
+  // off-cell records {idx, neighbour-base cell xyz, subdivision cell xyz, 0}
+  c3h::DevBuf<uint32_t> vcounts, voffs, vcur, vbucket;
+  c3h::DevBuf<float4> vcent;
+  c3h::DevBuf<int32_t> voffcell;
+  bool vcent_valid = false;
+  int64_t n_offcell = 0;
   c3h::DevBuf<uint32_t> scratch;    // minmax / counters
   c3h::DevBuf<uint32_t> tmp_u32;    // leaf-layout block sums
   c3h::DevBuf<int32_t> tmp_i32;     // leaf layout for host copies

@@ -174,7 +174,124 @@ __global__ __launch_bounds__(kBlock) void c3_finalize_kernel(const unsigned long
   if (threadIdx.x == 0) exist[h] = exist_from((float)hist[0], (float)hist[1]);
 }
 
+// Centroid-derived cells (voxelize.hip vox_centroid_kernel).  The tile pass adds every
+// occupied voxel's centre contribution at its own cell; the reference takes the voxel's
+// subdivision (floor(c / voxel_size) - min_b - offset, c3_hlac.cpp:349-354, skipped when
+// negative) and its 13 neighbours (PCL getNeighborCentroidIndices: floor(c * inv_leaf) +
+// relative coordinates, in-bounds only, c3_hlac.cpp:377) from its centroid c.  For each
+// recorded off-cell voxel this adds the centroid-based contribution and subtracts the
+// cell-based one in the exact 64-bit sums (two's complement), before c3_finalize_kernel.
+// One thread per record (there are few).  A subdivision past the last one (a centroid
+// rounding beyond max_b, out of bounds in the reference) contributes nothing.
+struct OffcellArgs {
+  const int32_t* rec;  // {linear index, neighbour-base cell xyz, subdivision cell xyz, 0}
+  int nrec;
+  const uint32_t* grid;
+  int gx, gy, gz;
+  int hist1;           // hist_num == 1: every voxel feeds histogram 0
+  int off[3], sb[3];
+  float inv_s;
+  const uint32_t* lut;
+  int thr[3];
+  unsigned long long* acc64;
+};
+
+__device__ __forceinline__ void channels(uint32_t word, const uint32_t* lut, const int thr[3], int a[6], int beta[6]) {
+  const int v[3] = {(int)((word >> 16) & 0xff), (int)((word >> 8) & 0xff), (int)(word & 0xff)};
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    const uint32_t l = lut[v[ch]];
+    a[2 * ch] = (int)(l & 0xff);
+    a[2 * ch + 1] = (int)((l >> 8) & 0xff);
+    beta[2 * ch] = v[ch] > thr[ch] ? 1 : 0;
+    beta[2 * ch + 1] = 1 - beta[2 * ch];
+  }
+}
+
+// sign * (contribution of centre word `w` with subdivision cell `sc` and neighbour base `nb`)
+__device__ void offcell_contrib(const OffcellArgs& o, uint32_t w, const int sc[3], const int nb[3], long long sign) {
+  int64_t h = 0;
+  if (!o.hist1) {
+    int ijk[3];
+    for (int ax = 0; ax < 3; ++ax) {
+      const int t = sc[ax] - o.off[ax];
+      if (t < 0) return;  // c3_hlac.cpp:355: voxels below the offset are skipped
+      ijk[ax] = (int)floorf((float)t * o.inv_s);
+      if (ijk[ax] >= o.sb[ax]) return;
+    }
+    h = ijk[0] + (int64_t)o.sb[0] * (ijk[1] + (int64_t)o.sb[1] * ijk[2]);
+  }
+  unsigned long long* hist = o.acc64 + h * 981;
+  const unsigned long long sg = (unsigned long long)sign;
+  int a[6], be[6];
+  channels(w, o.lut, o.thr, a, be);
+  for (int c = 0; c < 6; ++c) {
+    if (be[c]) atomicAdd(&hist[495 + c], sg);
+    atomicAdd(&hist[c], sg * (unsigned long long)a[c]);
+    for (int n = c; n < 6; ++n) atomicAdd(&hist[474 + tri6(c, n)], sg * (unsigned long long)(a[c] * a[n]));
+  }
+  for (int c = 0; c < 4; ++c)
+    for (int n = (c < 2 ? 2 : 4); n < 6; ++n)
+      if (be[c] && be[n]) atomicAdd(&hist[c < 2 ? 969 + 4 * c + (n - 2) : 977 + 2 * (c - 2) + (n - 4)], sg);
+  const int dims[3] = {o.gx, o.gy, o.gz};
+  for (int k = 0; k < 13; ++k) {  // relative coordinates, c3_hlac.cpp:177-202
+    const int rel[3] = {k < 9 ? k / 3 - 1 : (k < 12 ? k - 10 : -1), k < 9 ? k % 3 - 1 : (k < 12 ? -1 : 0),
+                        k < 9 ? -1 : 0};
+    int q[3];
+    bool in = true;
+    for (int ax = 0; ax < 3; ++ax) {
+      q[ax] = nb[ax] + rel[ax];
+      in = in && q[ax] >= 0 && q[ax] < dims[ax];
+    }
+    if (!in) continue;
+    const uint32_t nw = o.grid[q[0] + (int64_t)o.gx * (q[1] + (int64_t)o.gy * q[2])];
+    if (!nw) continue;
+    int na[6], nbe[6];
+    channels(nw, o.lut, o.thr, na, nbe);
+    for (int c = 0; c < 6; ++c)
+      for (int n = 0; n < 6; ++n) {
+        atomicAdd(&hist[bin981(k, c, n)], sg * (unsigned long long)(a[c] * na[n]));
+        if (be[c] && nbe[n]) atomicAdd(&hist[495 + bin981(k, c, n)], sg);
+      }
+  }
+}
+
+__global__ __launch_bounds__(64) void offcell_delta_kernel(OffcellArgs o) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= o.nrec) return;
+  const int32_t* r = o.rec + 8 * (int64_t)i;
+  const int64_t idx = r[0];
+  const uint32_t w = o.grid[idx];
+  const int own[3] = {(int)(idx % o.gx), (int)((idx / o.gx) % o.gy), (int)(idx / ((int64_t)o.gx * o.gy))};
+  offcell_contrib(o, w, own, own, -1);
+  const int nb[3] = {r[1], r[2], r[3]}, sc[3] = {r[4], r[5], r[6]};
+  offcell_contrib(o, w, sc, nb, 1);
+}
+
 }  // namespace
+
+hipError_t launch_offcell_delta(const int32_t* rec, int nrec, const C3Launch& l, int hist1, const int off[3],
+                                const int sb[3], float inv_s, hipStream_t s) {
+  if (nrec <= 0) return hipSuccess;
+  OffcellArgs o{};
+  o.rec = rec;
+  o.nrec = nrec;
+  o.grid = l.grid[0];
+  o.gx = l.gx;
+  o.gy = l.gy;
+  o.gz = l.gz;
+  o.hist1 = hist1;
+  for (int ax = 0; ax < 3; ++ax) {
+    o.off[ax] = off[ax];
+    o.sb[ax] = sb[ax];
+    o.thr[ax] = l.thr[ax];
+  }
+  o.inv_s = inv_s;
+  o.lut = l.lut;
+  o.acc64 = l.acc64;
+  offcell_delta_kernel<<<(nrec + 63) / 64, 64, 0, s>>>(o);
+  return hipGetLastError();
+}
 
 size_t c3hlac_lds_bytes(int tw_max, int list_max) {
   return sizeof(uint32_t) * (256 + tw_max + ((list_max + 7) / 8) * 4 + kGroups * kArrStride + 4 + 9 * kSegLds);

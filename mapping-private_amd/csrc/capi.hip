@@ -122,13 +122,6 @@ void host_lut(int lut_double, uint32_t* out) {
   }
 }
 
-float dec_f(uint32_t e) {
-  const uint32_t u = (e & 0x80000000u) ? (e & 0x7fffffffu) : ~e;
-  float f;
-  memcpy(&f, &u, 4);
-  return f;
-}
-
 // search.cpp:218-251
 void get_range(int mode, int r1, int r2, int r3, int* xr, int* yr, int* zr) {
   switch (mode) {
@@ -557,6 +550,28 @@ int run_search(c3h_ctx* ctx, const int32_t range[3], int32_t thr, int32_t rotate
   return search_frames(ctx, 1, range, thr, rotate, &d_out, 0);
 }
 
+// Exact centroids of the last voxelize (voxelize.hip vox_centroid_kernel): the fp32
+// sequential means in input order, and the off-cell records (read back to the host count).
+int exact_centroids(c3h_ctx* ctx) {
+  if (ctx->vcent_valid) return C3H_OK;
+  const int64_t ns = ctx->vns;
+  const c3h::VoxArgs& a = ctx->vargs;
+  ENSURE(ctx->vcounts, (size_t)ns);
+  ENSURE(ctx->voffs, (size_t)ns);
+  ENSURE(ctx->vcur, (size_t)ns);
+  ENSURE(ctx->tmp_u32, (size_t)c3h::scan_blocks(ns));
+  ENSURE(ctx->vbucket, (size_t)std::max<int64_t>(ctx->info.n_valid, 1));
+  ENSURE(ctx->vcent, (size_t)ns);
+  ENSURE(ctx->voffcell, (size_t)ns * 8);
+  HIPCHK(c3h::launch_vox_centroids(a, ns, ctx->vcounts.p, ctx->voffs.p, ctx->vcur.p, ctx->tmp_u32.p,
+                                   ctx->vbucket.p, ctx->vcent.p, ctx->voffcell.p, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->h_small, ctx->vcnt.p, c3h::kVcWords * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  ctx->n_offcell = ctx->h_small[c3h::kVcOff];
+  ctx->vcent_valid = true;
+  return C3H_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -604,14 +619,19 @@ void c3h_destroy(c3h_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   release(ctx->grid);
   release(ctx->pts);
-  release(ctx->keys);
-  release(ctx->cnt);
-  release(ctx->sr);
-  release(ctx->sg);
-  release(ctx->sb);
-  release(ctx->sx);
-  release(ctx->sy);
-  release(ctx->sz);
+  release(ctx->vkey);
+  release(ctx->vsa);
+  release(ctx->vsb);
+  release(ctx->vmargin);
+  release(ctx->vslotpos);
+  release(ctx->vlists);
+  release(ctx->vcnt);
+  release(ctx->vcounts);
+  release(ctx->voffs);
+  release(ctx->vcur);
+  release(ctx->vbucket);
+  release(ctx->vcent);
+  release(ctx->voffcell);
   release(ctx->scratch);
   release(ctx->tmp_u32);
   release(ctx->tmp_i32);
@@ -668,11 +688,15 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
   QUIESCE(ctx);
   if (n < 0 || (n > 0 && !xyzrgb) || !(leaf > 0))
     return fail(ctx, C3H_ERR_ARG, "c3h_voxelize: bad arguments");
+  if (n >= (int64_t)1 << 24)
+    return fail(ctx, C3H_ERR_RANGE, "c3h_voxelize: at most 16,777,215 points per call");
   HIPCHK(hipSetDevice(ctx->device));
   ctx->have_grid = false;
   ctx->have_feat = false;
   ctx->g_valid = false;
   ctx->table_valid = false;
+  ctx->vcent_valid = false;
+  ctx->n_offcell = 0;
   c3h_grid_info gi{};
   gi.leaf = leaf;
   gi.inv_leaf = 1.0f / leaf;
@@ -686,67 +710,113 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
       d_pts = reinterpret_cast<const float4*>(ctx->pts.p);
     }
   }
-  Timed t(ctx, 0);
-  uint32_t init[16] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  memcpy(ctx->h_small, init, sizeof(init));
-  HIPCHK(hipMemcpyAsync(ctx->scratch.p, ctx->h_small, sizeof(init), hipMemcpyHostToDevice, ctx->stream));
-  if (n > 0) HIPCHK(c3h::launch_minmax(d_pts, n, z_limit, ctx->scratch.p, ctx->stream));
-  HIPCHK(hipMemcpyAsync(ctx->h_small, ctx->scratch.p, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+  // tables: >= 2x the points (load <= 1/2); (re)allocation starts from all-empty state
+  uint64_t ts = 1024;
+  while (ts < 2 * (uint64_t)n) ts <<= 1;
+  if (ctx->vtsize < ts || !ctx->vcnt.p) {
+    ctx->vtsize = 0;
+    ENSURE(ctx->vkey, ts);
+    ENSURE(ctx->vsa, ts);
+    ENSURE(ctx->vsb, ts);
+    ENSURE(ctx->vmargin, ts);
+    ENSURE(ctx->vslotpos, ts);
+    ENSURE(ctx->vlists, 4 * (ts / 2));
+    ENSURE(ctx->vcnt, c3h::kVcWords);
+    HIPCHK(hipMemsetAsync(ctx->vkey.p, 0xff, ts * 8, ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->vsa.p, 0, ts * 8, ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->vsb.p, 0, ts * 8, ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->vmargin.p, 0xff, ts * 4, ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->vcnt.p, 0, c3h::kVcWords * 4, ctx->stream));
+    ctx->vtsize = ts;
+    ctx->vlcap = ts / 2;
+    ctx->vns_prev = 0;
+    ctx->vgrid_tracked = false;
+  }
+  // the previous frame's grid words are cleared through its list only when its scatter
+  // completed (tracked); otherwise the whole buffer is zeroed once
+  const bool clear_grid = ctx->vgrid_tracked && ctx->grid.n;
+  if (!ctx->vgrid_tracked && ctx->grid.n) HIPCHK(hipMemsetAsync(ctx->grid.p, 0, ctx->grid.n * 4, ctx->stream));
+  ctx->vgrid_tracked = false;  // until this frame's scatter completes
+  c3h::VoxArgs a{};
+  a.pts = d_pts;
+  a.n = n;
+  a.z_limit = z_limit;
+  a.inv = gi.inv_leaf;
+  a.leaf = leaf;
+  a.key = ctx->vkey.p;
+  a.sa = ctx->vsa.p;
+  a.sb = ctx->vsb.p;
+  a.margin = ctx->vmargin.p;
+  a.slotpos = ctx->vslotpos.p;
+  a.tmask = ctx->vtsize - 1;
+  a.lists = ctx->vlists.p;
+  a.lcap = ctx->vlcap;
+  a.cnt = ctx->vcnt.p;
+  a.grid = ctx->grid.p;
+  a.grid_cap = (int64_t)ctx->grid.n;
+  a.par = ctx->vpar;
+  a.clear_tables = 1;
+  a.clear_grid = clear_grid ? 1 : 0;
+  {
+    Timed t(ctx, 0);
+    HIPCHK(c3h::launch_voxelize(a, ctx->vns_prev, ctx->stream));
+  }
+  uint32_t* hc = ctx->h_small;
+  HIPCHK(hipMemcpyAsync(hc, ctx->vcnt.p, c3h::kVcWords * 4, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  // from here the tables hold this frame's entries (listed under parity a.par)
+  ctx->vpar ^= 1;
+  ctx->vns_prev = hc[c3h::kVcSlots + a.par];
+  if (hc[c3h::kVcErr]) {
+    return fail(ctx, C3H_ERR_RANGE, "c3h_voxelize: leaf size too small (cell coordinates beyond +-2^20)");
+  }
   uint64_t nvalid;
-  memcpy(&nvalid, ctx->h_small + 6, 8);
+  memcpy(&nvalid, hc + c3h::kVcValid, 8);
   gi.n_valid = (int64_t)nvalid;
-  if (nvalid == 0) {
+  if (nvalid == 0) {  // nothing scattered, and the previous frame's words are cleared
+    ctx->vgrid_tracked = true;
     ctx->info = gi;
     ctx->have_grid = true;
     ctx->grid_ptr = nullptr;
+    ctx->vns = 0;
     if (info) *info = gi;
     return C3H_OK;
   }
   int64_t nvox = 1;
-  for (int a = 0; a < 3; ++a) {
-    const float mn = dec_f(ctx->h_small[a]), mx = dec_f(ctx->h_small[3 + a]);
-    gi.min_b[a] = (int)floorf(mn * gi.inv_leaf);
-    gi.max_b[a] = (int)floorf(mx * gi.inv_leaf);
-    gi.div_b[a] = gi.max_b[a] - gi.min_b[a] + 1;
-    nvox *= gi.div_b[a];
+  for (int ax = 0; ax < 3; ++ax) {
+    gi.min_b[ax] = (int32_t)hc[c3h::kVcMin + ax];
+    gi.max_b[ax] = (int32_t)hc[c3h::kVcMax + ax];
+    gi.div_b[ax] = gi.max_b[ax] - gi.min_b[ax] + 1;
+    nvox *= gi.div_b[ax];
   }
-  if (nvox > 2147483647LL)
+  if (nvox > 2147483647LL) {
     return fail(ctx, C3H_ERR_RANGE, "c3h_voxelize: leaf size too small for int32 voxel indices");
-  uint64_t ts = 1024;
-  while (ts < 2 * nvalid) ts <<= 1;
-  ctx->table_size = ts;
-  ENSURE(ctx->keys, ts);
-  ENSURE(ctx->cnt, ts);
-  ENSURE(ctx->sr, ts);
-  ENSURE(ctx->sg, ts);
-  ENSURE(ctx->sb, ts);
-  ENSURE(ctx->sx, ts);
-  ENSURE(ctx->sy, ts);
-  ENSURE(ctx->sz, ts);
-  ENSURE(ctx->grid, (size_t)nvox);
-  HIPCHK(hipMemsetAsync(ctx->keys.p, 0xff, ts * 4, ctx->stream));
-  HIPCHK(hipMemsetAsync(ctx->cnt.p, 0, ts * 4, ctx->stream));
-  HIPCHK(hipMemsetAsync(ctx->sr.p, 0, ts * 4, ctx->stream));
-  HIPCHK(hipMemsetAsync(ctx->sg.p, 0, ts * 4, ctx->stream));
-  HIPCHK(hipMemsetAsync(ctx->sb.p, 0, ts * 4, ctx->stream));
-  HIPCHK(hipMemsetAsync(ctx->sx.p, 0, ts * 4, ctx->stream));
-  HIPCHK(hipMemsetAsync(ctx->sy.p, 0, ts * 4, ctx->stream));
-  HIPCHK(hipMemsetAsync(ctx->sz.p, 0, ts * 4, ctx->stream));
-  HIPCHK(hipMemsetAsync(ctx->grid.p, 0, (size_t)nvox * 4, ctx->stream));
-  HIPCHK(c3h::launch_voxel_accum(d_pts, n, z_limit, gi.inv_leaf, gi.min_b, gi.div_b, ctx->keys.p,
-                                 ctx->cnt.p, ctx->sr.p, ctx->sg.p, ctx->sb.p, ctx->sx.p, ctx->sy.p,
-                                 ctx->sz.p, ts, ctx->scratch.p + 8, ctx->stream));
-  HIPCHK(c3h::launch_voxel_scatter(ctx->keys.p, ctx->cnt.p, ctx->sr.p, ctx->sg.p, ctx->sb.p, ts,
-                                   ctx->grid.p, ctx->scratch.p + 9, ctx->stream));
-  HIPCHK(hipMemcpyAsync(ctx->h_small + 8, ctx->scratch.p + 8, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(hipStreamSynchronize(ctx->stream));
-  if (ctx->h_small[8]) return fail(ctx, C3H_ERR_HIP, "c3h_voxelize: hash table overflow");
-  gi.n_occ = ctx->h_small[9];
+  }
+  if (hc[c3h::kVcOver]) {  // the grid buffer grows (zeroed) and the scatter runs again
+    ENSURE(ctx->grid, (size_t)nvox);
+    HIPCHK(hipMemsetAsync(ctx->grid.p, 0, ctx->grid.n * 4, ctx->stream));
+    a.grid = ctx->grid.p;
+    a.grid_cap = (int64_t)ctx->grid.n;
+    {
+      Timed t(ctx, 0);
+      HIPCHK(c3h::launch_vox_scatter(a, ctx->stream));
+    }
+    HIPCHK(hipMemcpyAsync(hc, ctx->vcnt.p, c3h::kVcWords * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (hc[c3h::kVcOver]) return fail(ctx, C3H_ERR_HIP, "c3h_voxelize: internal: grid still too small");
+  }
+  ctx->vgrid_tracked = true;
+  ctx->vargs = a;
+  ctx->vns = hc[c3h::kVcSlots + a.par];
+  gi.n_occ = ctx->vns;
   ctx->info = gi;
   ctx->grid_ptr = ctx->grid.p;
   ctx->have_grid = true;
   ctx->table_valid = true;
+  if (hc[c3h::kVcFlag]) {  // centroids may leave their cells: the exact pass decides
+    int rc = exact_centroids(ctx);
+    if (rc != C3H_OK) return rc;
+  }
   if (info) *info = gi;
   return C3H_OK;
 }
@@ -872,17 +942,17 @@ int c3h_get_downsampled(c3h_ctx* ctx, float* out, int on_device) {
   HIPCHK(hipSetDevice(ctx->device));
   const int64_t nvox = grid_voxels(ctx);
   if (nvox == 0 || ctx->info.n_occ == 0) return C3H_OK;
+  int rc = exact_centroids(ctx);
+  if (rc != C3H_OK) return rc;
   ENSURE(ctx->tmp_i32, (size_t)nvox);
-  int rc = compute_leaf_layout(ctx, ctx->tmp_i32.p);
+  rc = compute_leaf_layout(ctx, ctx->tmp_i32.p);
   if (rc != C3H_OK) return rc;
   float* dst = out;
   if (!on_device) {
     ENSURE(ctx->pts, (size_t)ctx->info.n_occ * 4);
     dst = ctx->pts.p;
   }
-  HIPCHK(c3h::launch_downsampled(ctx->tmp_i32.p, ctx->grid_ptr, nvox, ctx->info.div_b, ctx->keys.p,
-                                 ctx->cnt.p, ctx->sx.p, ctx->sy.p, ctx->sz.p, ctx->table_size, dst,
-                                 ctx->stream));
+  HIPCHK(c3h::launch_vox_downsampled(ctx->vargs, ctx->vns, ctx->vcent.p, ctx->tmp_i32.p, dst, ctx->stream));
   if (!on_device)
     HIPCHK(hipMemcpyAsync(out, dst, (size_t)ctx->info.n_occ * 16, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -916,6 +986,7 @@ int c3h_set_grid(c3h_ctx* ctx, const uint32_t* words, const int32_t div_b[3],
   } else {
     ENSURE(ctx->grid, (size_t)nvox);
     HIPCHK(hipMemcpyAsync(ctx->grid.p, words, (size_t)nvox * 4, hipMemcpyHostToDevice, ctx->stream));
+    ctx->vgrid_tracked = false;  // the next voxelize zeroes the buffer first
     ctx->grid_ptr = ctx->grid.p;
   }
   ctx->info = gi;
@@ -982,7 +1053,11 @@ int extract_frames(c3h_ctx* ctx, const uint32_t* const* grids, int nf, const c3h
       ctx->err = "c3h_extract: more than 32767 tile segments along one axis";
       return C3H_ERR_RANGE;
     }
-  const bool atomic = split[0] || split[1] || split[2];
+  // voxels whose centroid leaves their cell (voxelize's exact pass) are corrected in the
+  // exact 64-bit sums: the extract then runs in the atomic mode
+  const bool offcell = nf == 1 && !ctx->capture && ctx->table_valid && ctx->n_offcell > 0 &&
+                       ctx->grid_ptr == ctx->grid.p;
+  const bool atomic = split[0] || split[1] || split[2] || offcell;
   const bool all_covered = covered[0] && covered[1] && covered[2] && ntiles > 0;
   ENSURE(ctx->feat, (size_t)nf * hist_num * F);
   ENSURE(ctx->exist, (size_t)nf * hist_num);
@@ -1099,6 +1174,11 @@ int extract_frames(c3h_ctx* ctx, const uint32_t* const* grids, int nf, const c3h
       if (l.prof) {
         int rc = prof_dump(ctx, "c3hlac_tile_kernel", tgrid);
         if (rc != C3H_OK) return rc;
+      }
+      if (offcell) {
+        const int sbv[3] = {l.sbx, l.sby, mode1 ? 1 : sb[2]};
+        HIPCHK(c3h::launch_offcell_delta(ctx->voffcell.p, (int)ctx->n_offcell, l, mode1 ? 1 : 0, p->offset, sbv,
+                                         inv_s, ctx->stream));
       }
       if (atomic)
         HIPCHK(c3h::launch_c3_finalize(ctx->acc64.p, hist_num, F, ctx->feat.p, ctx->exist.p, nf, ctx->stream));

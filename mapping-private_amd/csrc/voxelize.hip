@@ -1,27 +1,54 @@
-// voxelize.hip -- hash-and-scatter voxeliser for gfx950 (PCL VoxelGrid semantics).
+// voxelize.hip -- LDS-privatised voxeliser for gfx950 (PCL VoxelGrid semantics).
 //
 // Replaces getVoxelGrid (c3_hlac/include/c3_hlac/c3_hlac_tools.hpp:124-130 -> PCL
 // VoxelGrid::filter, semantics restated in SURVEY.md App. B) and limitPoint
 // (color_voxel_recognition/test/detect_object.cpp:68-87).
 //
-// Pass 1 (minmax): one coalesced 16-B read per point; finite && z < z_limit filter;
-//   wave/block reduction of the bounds, one atomic per block.
-// Pass 2 (accum): voxel index = floor(p * inv_leaf) - min_b (float multiply + floor,
-//   exactly PCL's), inserted into an open-addressing hash table sized >= 2x the valid
-//   points; integer atomics accumulate count and r/g/b sums (exact), float atomics the
-//   xyz sums (only used for the optional downsampled cloud).
-// Pass 3 (scatter): one word per occupied voxel into the dense packed grid:
-//   kOcc | r<<16 | g<<8 | b with r = (int)(float(sum_r) / float(count)) (IEEE divide,
-//   the canonical PCL >= 1.2 colour rule).
+// Hot path: three launches, no host round trip between them.
+//   vox_reset   clears what the previous frame left: its hash-table slots and its grid
+//               words (both listed by that frame), and the frame counters.  The grid
+//               buffer is therefore all-zero outside the voxels a frame writes, without
+//               a 4 B/voxel memset per frame.
+//   vox_accum   one workgroup per 2,048 consecutive points (a depth camera's pixel order
+//               is spatially coherent: a voxel is hit by runs of neighbouring pixels):
+//               coalesced 16-B loads, the bounds (block-reduced, one atomic per block and
+//               field), and per point an LDS hash insert of the absolute cell with LDS
+//               atomics for count + r (one u32), g | b (one u64) and the point's distance
+//               to the cell boundary (min).  Each (workgroup, voxel) then leaves one
+//               global hash insert and three global atomics; new slots are appended to
+//               the frame's slot list with one global atomic per workgroup.
+//   vox_scatter one thread per listed voxel: cell - min_b -> linear index (PCL's
+//               (floor(p * inv) - min_b) . divb_mul), the canonical colour mean
+//               kOcc | r<<16 | g<<8 | b with r = (int)(float(sum_r) / float(count)), the
+//               grid word, and the safety test below.
+// Integer sums are exact and order-independent, so the grid is deterministic.
+//
+// Centroids.  C3-HLAC takes a voxel's subdivision (floor(c / voxel_size)) and neighbour
+// base (PCL getNeighborCentroidIndices: floor(c * inv_leaf)) from its float centroid c,
+// the fp32 sequential mean of its points in input order (the oracle's reading of PCL's
+// sort-then-sum).  That can leave the voxel's own cell only when c lies within the sum's
+// rounding of a cell boundary; vox_scatter flags a voxel when its closest point's margin
+// is below (count + 4) * 2^-22 * (|cell| + 1) cells (4x the error bound of the mean, the
+// multiply and the divide).  Only then (and for c3h_get_downsampled) the exact pass runs:
+// points are bucketed per voxel (counting sort over the slot list), each bucket sorted by
+// point index and summed sequentially in fp32 -- bit-identical to the oracle -- and voxels
+// whose centroid cells differ from their own cell are recorded (c3h_extract corrects
+// their C3-HLAC contribution, c3hlac.hip offcell_delta_kernel).
+#include <climits>
+
 #include "c3h_internal.h"
 
 namespace c3h {
 namespace {
 
-__device__ __forceinline__ uint32_t enc_f(float f) {
-  const uint32_t u = __float_as_uint(f);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr unsigned long long kNoKey = ~0ull;
+constexpr uint32_t kNoMargin = 0xffffffffu;  // above every float's bits: "no point yet"
+constexpr int kVoxChunk = 2048;  // points per workgroup (8 per thread)
+constexpr int kVoxPer = kVoxChunk / kBlock;
+constexpr int kLSlots = 1024;    // LDS hash slots per workgroup
+constexpr int kLProbe = 48;      // LDS probes before a point goes straight to the global table
+constexpr int kCellBias = 1 << 20;
 
 __device__ __forceinline__ bool point_valid(const float4& p, float z_limit) {
   return isfinite(p.x) && isfinite(p.y) && isfinite(p.z) && p.z < z_limit;
@@ -34,137 +61,375 @@ __device__ __forceinline__ T wave_reduce(T v, Op op) {
   return v;
 }
 
-__global__ __launch_bounds__(kBlock) void minmax_kernel(const float4* __restrict__ pts,
-                                                        int64_t n, float z_limit,
-                                                        uint32_t* __restrict__ out) {
-  uint32_t mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
-  uint32_t cnt = 0;
-  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
+__device__ __forceinline__ unsigned long long pack_cell(int x, int y, int z) {
+  return (unsigned long long)(uint32_t)(x + kCellBias) |
+         ((unsigned long long)(uint32_t)(y + kCellBias) << 21) |
+         ((unsigned long long)(uint32_t)(z + kCellBias) << 42);
+}
+
+__device__ __forceinline__ void unpack_cell(unsigned long long k, int& x, int& y, int& z) {
+  x = (int)(k & 0x1fffff) - kCellBias;
+  y = (int)((k >> 21) & 0x1fffff) - kCellBias;
+  z = (int)((k >> 42) & 0x1fffff) - kCellBias;
+}
+
+__device__ __forceinline__ uint32_t mix64(unsigned long long k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return (uint32_t)k;
+}
+
+// global table insert: returns the slot (or -1 when the table is full, which the host
+// sizing at >= 2x the point count excludes); *fresh = this call inserted the key
+__device__ __forceinline__ int64_t global_slot(const VoxArgs& a, unsigned long long key, bool* fresh) {
+  uint64_t h = mix64(key) & a.tmask;
+  for (uint64_t probes = 0; probes <= a.tmask; ++probes) {
+    const unsigned long long prev = atomicCAS(&a.key[h], kNoKey, key);
+    if (prev == kNoKey) {
+      *fresh = true;
+      return (int64_t)h;
+    }
+    if (prev == key) {
+      *fresh = false;
+      return (int64_t)h;
+    }
+    h = (h + 1) & a.tmask;
+  }
+  return -1;
+}
+
+// existing key -> slot (the key must be in the table)
+__device__ __forceinline__ int64_t find_slot(const VoxArgs& a, unsigned long long key) {
+  uint64_t h = mix64(key) & a.tmask;
+  for (uint64_t probes = 0; probes <= a.tmask; ++probes) {
+    const unsigned long long k = a.key[h];
+    if (k == key) return (int64_t)h;
+    if (k == kNoKey) return -1;
+    h = (h + 1) & a.tmask;
+  }
+  return -1;
+}
+
+__device__ __forceinline__ bool point_cell(const VoxArgs& a, const float4& p, int c[3], float* margin) {
+  const float f[3] = {p.x * a.inv, p.y * a.inv, p.z * a.inv};
+  float m = 1.0f;
+  bool ok = true;
+#pragma unroll
+  for (int ax = 0; ax < 3; ++ax) {
+    const float fl = floorf(f[ax]);  // PCL: static_cast<int> (floor (p * inverse_leaf_size))
+    ok = ok && fl > (float)(-kCellBias) && fl < (float)(kCellBias - 1);
+    c[ax] = ok ? (int)fl : 0;
+    m = fminf(m, fminf(f[ax] - fl, fl + 1.0f - f[ax]));
+  }
+  *margin = fmaxf(m, 0.0f);
+  return ok;
+}
+
+__global__ __launch_bounds__(kBlock) void vox_reset_kernel(VoxArgs a) {
+  const int pp = a.par ^ 1;
+  uint32_t* cnt = a.cnt;
+  const uint32_t np = cnt[kVcSlots + pp];
+  const uint32_t* sl = a.lists + (size_t)pp * a.lcap;
+  const uint32_t* tl = a.lists + (size_t)(2 + pp) * a.lcap;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < (int64_t)np;
        i += (int64_t)gridDim.x * kBlock) {
-    const float4 p = pts[i];
-    if (!point_valid(p, z_limit)) continue;
-    ++cnt;
-    const uint32_t e[3] = {enc_f(p.x), enc_f(p.y), enc_f(p.z)};
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      mn[a] = min(mn[a], e[a]);
-      mx[a] = max(mx[a], e[a]);
+    if (a.clear_tables) {
+      const uint32_t s = sl[i];
+      a.key[s] = kNoKey;
+      a.sa[s] = 0;
+      a.sb[s] = 0;
+      a.margin[s] = kNoMargin;
     }
+    if (a.clear_grid) a.grid[tl[i]] = 0;
   }
-  auto umin = [](uint32_t a, uint32_t b) { return a < b ? a : b; };
-  auto umax = [](uint32_t a, uint32_t b) { return a > b ? a : b; };
-  auto uadd = [](uint32_t a, uint32_t b) { return a + b; };
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    mn[a] = wave_reduce(mn[a], umin);
-    mx[a] = wave_reduce(mx[a], umax);
-  }
-  cnt = wave_reduce(cnt, uadd);
-  // block reduction in LDS, then one set of atomics per block (same-address atomics
-  // from every wave serialise at the memory side)
-  __shared__ uint32_t red[kBlock / 64][7];
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    for (int a = 0; a < 3; ++a) {
-      red[w][a] = mn[a];
-      red[w][3 + a] = mx[a];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    for (int ax = 0; ax < 3; ++ax) {
+      reinterpret_cast<int32_t*>(cnt)[kVcMin + ax] = INT_MAX;
+      reinterpret_cast<int32_t*>(cnt)[kVcMax + ax] = INT_MIN;
     }
-    red[w][6] = cnt;
+    cnt[kVcValid] = cnt[kVcValid + 1] = 0;
+    cnt[kVcSlots + a.par] = 0;
+    cnt[kVcFlag] = cnt[kVcErr] = cnt[kVcOver] = cnt[kVcOff] = 0;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void vox_accum_kernel(VoxArgs a) {
+  __shared__ unsigned long long s_key[kLSlots];
+  __shared__ unsigned long long s_gb[kLSlots];  // b << 32 | g
+  __shared__ uint32_t s_cr[kLSlots];            // count << 20 | r (chunk sums: r < 2^20, count <= 2^11)
+  __shared__ uint32_t s_m[kLSlots];
+  __shared__ uint32_t s_new[kVoxChunk];         // global slots this workgroup inserted
+  __shared__ uint32_t s_nnew, s_base;
+  __shared__ int s_red[kBlock / 64][7];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int s = tid; s < kLSlots; s += kBlock) {
+    s_key[s] = kNoKey;
+    s_gb[s] = 0;
+    s_cr[s] = 0;
+    s_m[s] = kNoMargin;
+  }
+  if (tid == 0) s_nnew = 0;
+  const int64_t base = blockIdx.x * (int64_t)kVoxChunk;
+  float4 p[kVoxPer];
+#pragma unroll
+  for (int j = 0; j < kVoxPer; ++j) {  // all loads first: bytes in flight, not latency
+    const int64_t i = base + j * kBlock + tid;
+    if (i < a.n) {  // streamed once: non-temporal
+      const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.pts) + i);
+      p[j] = make_float4(v.x, v.y, v.z, v.w);
+    } else {
+      p[j] = make_float4(NAN, NAN, NAN, 0.0f);
+    }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int i = 1; i < kBlock / 64; ++i) {
-      for (int a = 0; a < 3; ++a) {
-        red[0][a] = umin(red[0][a], red[i][a]);
-        red[0][3 + a] = umax(red[0][3 + a], red[i][3 + a]);
-      }
-      red[0][6] += red[i][6];
+  int mn[3] = {INT_MAX, INT_MAX, INT_MAX}, mx[3] = {INT_MIN, INT_MIN, INT_MIN};
+  int nv = 0;
+  bool err = false;
+  auto add_global = [&](unsigned long long key, unsigned long long A, unsigned long long B, uint32_t m) {
+    bool fresh = false;
+    const int64_t s = global_slot(a, key, &fresh);
+    if (s < 0) {
+      err = true;
+      return;
     }
-    for (int a = 0; a < 3; ++a) {
-      atomicMin(&out[a], red[0][a]);
-      atomicMax(&out[3 + a], red[0][3 + a]);
+    if (fresh) s_new[atomicAdd(&s_nnew, 1u)] = (uint32_t)s;
+    atomicAdd(&a.sa[s], A);
+    atomicAdd(&a.sb[s], B);
+    atomicMin(&a.margin[s], m);
+  };
+#pragma unroll
+  for (int j = 0; j < kVoxPer; ++j) {
+    if (!point_valid(p[j], a.z_limit)) continue;
+    int c[3];
+    float margin;
+    if (!point_cell(a, p[j], c, &margin)) {
+      err = true;
+      continue;
     }
-    atomicAdd(reinterpret_cast<unsigned long long*>(out + 6), (unsigned long long)red[0][6]);
-  }
-}
-
-__device__ __forceinline__ uint32_t hash_key(uint32_t k) {
-  k ^= k >> 16;
-  k *= 0x7feb352du;
-  k ^= k >> 15;
-  k *= 0x846ca68bu;
-  k ^= k >> 16;
-  return k;
-}
-
-__global__ __launch_bounds__(kBlock) void accum_kernel(
-    const float4* __restrict__ pts, int64_t n, float z_limit, float inv, int mbx, int mby,
-    int mbz, int dx, int dy, uint32_t* __restrict__ keys, uint32_t* __restrict__ cnt,
-    uint32_t* __restrict__ sr, uint32_t* __restrict__ sg, uint32_t* __restrict__ sb,
-    float* __restrict__ sx, float* __restrict__ sy, float* __restrict__ sz, uint64_t mask,
-    uint32_t* __restrict__ overflow) {
-  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * kBlock) {
-    const float4 p = pts[i];
-    if (!point_valid(p, z_limit)) continue;
-    // PCL: static_cast<int>(floor(p * inverse_leaf_size) - static_cast<float>(min_b))
-    const int ix = (int)(floorf(p.x * inv) - (float)mbx);
-    const int iy = (int)(floorf(p.y * inv) - (float)mby);
-    const int iz = (int)(floorf(p.z * inv) - (float)mbz);
-    const uint32_t key = (uint32_t)ix + (uint32_t)iy * (uint32_t)dx + (uint32_t)iz * (uint32_t)dx * (uint32_t)dy;
-    uint64_t h = hash_key(key) & mask;
-    uint64_t probes = 0;
-    for (;;) {
-      const uint32_t prev = atomicCAS(&keys[h], kEmptyKey, key);
-      if (prev == kEmptyKey || prev == key) break;
-      h = (h + 1) & mask;
-      if (++probes > mask) {
-        atomicOr(overflow, 1u);
+    ++nv;
+#pragma unroll
+    for (int ax = 0; ax < 3; ++ax) {
+      mn[ax] = min(mn[ax], c[ax]);
+      mx[ax] = max(mx[ax], c[ax]);
+    }
+    const unsigned long long key = pack_cell(c[0], c[1], c[2]);
+    const uint32_t rgb = __float_as_uint(p[j].w);
+    const uint32_t r = (rgb >> 16) & 0xffu, g = (rgb >> 8) & 0xffu, b = rgb & 0xffu;
+    const uint32_t mb = __float_as_uint(margin);
+    uint32_t h = mix64(key) & (kLSlots - 1);
+    bool done = false;
+    for (int probe = 0; probe < kLProbe; ++probe) {
+      const unsigned long long prev = atomicCAS(&s_key[h], kNoKey, key);
+      if (prev == kNoKey || prev == key) {
+        atomicAdd(&s_cr[h], (1u << 20) | r);
+        atomicAdd(&s_gb[h], ((unsigned long long)b << 32) | g);
+        atomicMin(&s_m[h], mb);
+        done = true;
         break;
       }
+      h = (h + 1) & (kLSlots - 1);
     }
-    if (probes > mask) continue;
-    const uint32_t rgb = __float_as_uint(p.w);
-    atomicAdd(&cnt[h], 1u);
-    atomicAdd(&sr[h], (rgb >> 16) & 0xffu);
-    atomicAdd(&sg[h], (rgb >> 8) & 0xffu);
-    atomicAdd(&sb[h], rgb & 0xffu);
-    if (sx) {
-      atomicAdd(&sx[h], p.x);
-      atomicAdd(&sy[h], p.y);
-      atomicAdd(&sz[h], p.z);
+    if (!done) add_global(key, (1ull << 40) | r, ((unsigned long long)b << 32) | g, mb);  // LDS table full
+  }
+  // bounds: wave, then block reduction; one atomic per block and field
+#pragma unroll
+  for (int ax = 0; ax < 3; ++ax) {
+    mn[ax] = wave_reduce(mn[ax], [](int x, int y) { return min(x, y); });
+    mx[ax] = wave_reduce(mx[ax], [](int x, int y) { return max(x, y); });
+  }
+  nv = wave_reduce(nv, [](int x, int y) { return x + y; });
+  if (lane == 0) {
+    for (int ax = 0; ax < 3; ++ax) {
+      s_red[w][ax] = mn[ax];
+      s_red[w][3 + ax] = mx[ax];
+    }
+    s_red[w][6] = nv;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int i = 1; i < kBlock / 64; ++i) {
+      for (int ax = 0; ax < 3; ++ax) {
+        s_red[0][ax] = min(s_red[0][ax], s_red[i][ax]);
+        s_red[0][3 + ax] = max(s_red[0][3 + ax], s_red[i][3 + ax]);
+      }
+      s_red[0][6] += s_red[i][6];
+    }
+    if (s_red[0][6]) {
+      int32_t* ci = reinterpret_cast<int32_t*>(a.cnt);
+      for (int ax = 0; ax < 3; ++ax) {
+        atomicMin(&ci[kVcMin + ax], s_red[0][ax]);
+        atomicMax(&ci[kVcMax + ax], s_red[0][3 + ax]);
+      }
+      atomicAdd(reinterpret_cast<unsigned long long*>(a.cnt + kVcValid), (unsigned long long)s_red[0][6]);
+    }
+  }
+  // flush: one global insert + three atomics per (workgroup, voxel)
+  for (int s = tid; s < kLSlots; s += kBlock) {
+    const unsigned long long key = s_key[s];
+    if (key == kNoKey) continue;
+    const uint32_t cr = s_cr[s];
+    add_global(key, ((unsigned long long)(cr >> 20) << 40) | (cr & 0xfffffu), s_gb[s], s_m[s]);
+  }
+  if (err) atomicOr(a.cnt + kVcErr, 1u);
+  __syncthreads();
+  if (tid == 0) s_base = s_nnew ? atomicAdd(a.cnt + kVcSlots + a.par, s_nnew) : 0;
+  __syncthreads();
+  uint32_t* sl = a.lists + (size_t)a.par * a.lcap;
+  for (uint32_t i = tid; i < s_nnew; i += kBlock) sl[s_base + i] = s_new[i];
+}
+
+__device__ __forceinline__ bool vox_bounds(const VoxArgs& a, int mn[3], int dv[3], int64_t* nvox) {
+  const int32_t* ci = reinterpret_cast<const int32_t*>(a.cnt);
+  int64_t n = 1;
+  for (int ax = 0; ax < 3; ++ax) {
+    mn[ax] = ci[kVcMin + ax];
+    dv[ax] = ci[kVcMax + ax] - mn[ax] + 1;
+    n *= dv[ax];
+  }
+  *nvox = n;
+  return ci[kVcMax] >= ci[kVcMin];
+}
+
+__global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
+  const uint32_t ns = a.cnt[kVcSlots + a.par];
+  int mn[3], dv[3];
+  int64_t nvox;
+  if (!vox_bounds(a, mn, dv, &nvox)) return;
+  if (nvox > a.grid_cap || nvox > INT_MAX) {  // the host grows the grid and runs this again
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.cnt[kVcOver] = 1;
+    return;
+  }
+  const uint32_t* sl = a.lists + (size_t)a.par * a.lcap;
+  uint32_t* tl = a.lists + (size_t)(2 + a.par) * a.lcap;
+  uint32_t flagged = 0;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < (int64_t)ns;
+       i += (int64_t)gridDim.x * kBlock) {
+    const uint32_t s = sl[i];
+    int x, y, z;
+    unpack_cell(a.key[s], x, y, z);
+    const int64_t idx = (x - mn[0]) + (int64_t)dv[0] * ((y - mn[1]) + (int64_t)dv[1] * (z - mn[2]));
+    const unsigned long long A = a.sa[s], B = a.sb[s];
+    const uint32_t count = (uint32_t)(A >> 40);
+    const float c = (float)count;
+    const uint32_t r = (uint32_t)(int)__fdiv_rn((float)(A & 0xffffffffffull), c);
+    const uint32_t g = (uint32_t)(int)__fdiv_rn((float)(B & 0xffffffffull), c);
+    const uint32_t b = (uint32_t)(int)__fdiv_rn((float)(B >> 32), c);
+    a.grid[idx] = kOcc | (r << 16) | (g << 8) | b;
+    tl[i] = (uint32_t)idx;
+    a.slotpos[s] = (uint32_t)i;
+    const int cmag = max(max(abs(x), abs(y)), abs(z)) + 1;
+    const float eps = (float)(count + 4) * (float)cmag * 0x1p-22f;
+    if (__uint_as_float(a.margin[s]) < eps) ++flagged;
+  }
+  flagged = wave_reduce(flagged, [](uint32_t u, uint32_t v) { return u + v; });
+  if ((threadIdx.x & 63) == 0 && flagged) atomicAdd(a.cnt + kVcFlag, flagged);
+}
+
+// ---- exact centroids (flagged frames and c3h_get_downsampled) ----------------------
+__global__ __launch_bounds__(kBlock) void vox_counts_kernel(VoxArgs a, uint32_t* __restrict__ counts) {
+  const uint32_t ns = a.cnt[kVcSlots + a.par];
+  const uint32_t* sl = a.lists + (size_t)a.par * a.lcap;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < (int64_t)ns;
+       i += (int64_t)gridDim.x * kBlock)
+    counts[i] = (uint32_t)(a.sa[sl[i]] >> 40);
+}
+
+__global__ __launch_bounds__(kBlock) void vox_bucket_kernel(VoxArgs a, const uint32_t* __restrict__ off,
+                                                            uint32_t* __restrict__ cur,
+                                                            uint32_t* __restrict__ bucket) {
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * kBlock) {
+    const float4 p = a.pts[i];
+    if (!point_valid(p, a.z_limit)) continue;
+    int c[3];
+    float m;
+    if (!point_cell(a, p, c, &m)) continue;
+    const int64_t s = find_slot(a, pack_cell(c[0], c[1], c[2]));
+    if (s < 0) continue;
+    const uint32_t lp = a.slotpos[s];
+    bucket[off[lp] + atomicAdd(&cur[lp], 1u)] = (uint32_t)i;
+  }
+}
+
+// per voxel: its points in input order (shell sort of the bucket), the fp32 sequential
+// sum and the IEEE mean (the oracle's orc_voxel_fill); off-cell voxels are recorded as
+// {linear index, neighbour-base cell xyz, subdivision cell xyz} relative to min_b
+__global__ __launch_bounds__(kBlock) void vox_centroid_kernel(VoxArgs a, const uint32_t* __restrict__ off,
+                                                              const uint32_t* __restrict__ counts,
+                                                              uint32_t* __restrict__ bucket,
+                                                              float4* __restrict__ cent,
+                                                              int32_t* __restrict__ offcell) {
+  const uint32_t ns = a.cnt[kVcSlots + a.par];
+  int mn[3], dv[3];
+  int64_t nvox;
+  vox_bounds(a, mn, dv, &nvox);
+  const uint32_t* sl = a.lists + (size_t)a.par * a.lcap;
+  const uint32_t* tl = a.lists + (size_t)(2 + a.par) * a.lcap;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < (int64_t)ns;
+       i += (int64_t)gridDim.x * kBlock) {
+    uint32_t* bk = bucket + off[i];
+    const int m = (int)counts[i];
+    const int gaps[8] = {701, 301, 132, 57, 23, 10, 4, 1};
+    for (int gi = 0; gi < 8; ++gi) {
+      const int gap = gaps[gi];
+      for (int u = gap; u < m; ++u) {
+        const uint32_t t = bk[u];
+        int v = u;
+        for (; v >= gap && bk[v - gap] > t; v -= gap) bk[v] = bk[v - gap];
+        bk[v] = t;
+      }
+    }
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f;
+    for (int u = 0; u < m; ++u) {
+      const float4 p = a.pts[bk[u]];
+      sx += p.x;
+      sy += p.y;
+      sz += p.z;
+    }
+    const float fc = (float)m;
+    const float c[3] = {__fdiv_rn(sx, fc), __fdiv_rn(sy, fc), __fdiv_rn(sz, fc)};
+    const uint32_t idx = tl[i];
+    cent[i] = make_float4(c[0], c[1], c[2], __uint_as_float(a.grid[idx] & 0x00ffffffu));
+    int own[3];
+    unpack_cell(a.key[sl[i]], own[0], own[1], own[2]);
+    int nb[3], sb[3];
+    bool moved = false;
+#pragma unroll
+    for (int ax = 0; ax < 3; ++ax) {
+      nb[ax] = (int)floorf(c[ax] * a.inv);          // getNeighborCentroidIndices
+      sb[ax] = (int)floorf(__fdiv_rn(c[ax], a.leaf));  // c3_hlac.cpp:349-354
+      moved = moved || nb[ax] != own[ax] || sb[ax] != own[ax];
+    }
+    if (moved) {
+      const uint32_t k = atomicAdd(a.cnt + kVcOff, 1u);
+      int32_t* o = offcell + 8 * (int64_t)k;
+      o[0] = (int32_t)idx;
+      for (int ax = 0; ax < 3; ++ax) {
+        o[1 + ax] = nb[ax] - mn[ax];
+        o[4 + ax] = sb[ax] - mn[ax];
+      }
+      o[7] = 0;
     }
   }
 }
 
-__global__ __launch_bounds__(kBlock) void scatter_kernel(
-    const uint32_t* __restrict__ keys, const uint32_t* __restrict__ cnt,
-    const uint32_t* __restrict__ sr, const uint32_t* __restrict__ sg,
-    const uint32_t* __restrict__ sb, uint64_t table_size, uint32_t* __restrict__ grid,
-    uint32_t* __restrict__ n_occ) {
-  uint32_t local = 0;
-  for (uint64_t s = blockIdx.x * (uint64_t)kBlock + threadIdx.x; s < table_size;
-       s += (uint64_t)gridDim.x * kBlock) {
-    const uint32_t key = keys[s];
-    if (key == kEmptyKey) continue;
-    const float c = (float)cnt[s];
-    const uint32_t r = (uint32_t)(int)__fdiv_rn((float)sr[s], c);
-    const uint32_t g = (uint32_t)(int)__fdiv_rn((float)sg[s], c);
-    const uint32_t b = (uint32_t)(int)__fdiv_rn((float)sb[s], c);
-    grid[key] = kOcc | (r << 16) | (g << 8) | b;
-    ++local;
-  }
-  auto uadd = [](uint32_t a, uint32_t b) { return a + b; };
-  local = wave_reduce(local, uadd);
-  if ((threadIdx.x & 63) == 0 && local) atomicAdd(n_occ, local);
+__global__ __launch_bounds__(kBlock) void vox_downsampled_kernel(VoxArgs a, const float4* __restrict__ cent,
+                                                                 const int32_t* __restrict__ leaf,
+                                                                 float4* __restrict__ out) {
+  const uint32_t ns = a.cnt[kVcSlots + a.par];
+  const uint32_t* tl = a.lists + (size_t)(2 + a.par) * a.lcap;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < (int64_t)ns;
+       i += (int64_t)gridDim.x * kBlock)
+    out[leaf[tl[i]]] = cent[i];
 }
 
-// ---- leaf layout: exclusive scan of occupancy over the grid (not on the timed path)
-constexpr int kScanItems = 4;  // voxels per thread
+// ---- exclusive scans (leaf layout, bucket offsets) --------------------------------
+constexpr int kScanItems = 4;  // items per thread
 constexpr int kScanBlock = kBlock * kScanItems;
 
-__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds,
-                                                         uint32_t* total) {
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds, uint32_t* total) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint32_t x = v;
 #pragma unroll
@@ -184,22 +449,27 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* l
   return wbase + x - v;
 }
 
-__global__ __launch_bounds__(kBlock) void occ_count_kernel(const uint32_t* __restrict__ grid,
-                                                           int64_t nvox,
-                                                           uint32_t* __restrict__ sums) {
+// item value: grid word occupancy (leaf layout) or a count array
+template <bool kOccupancy>
+__device__ __forceinline__ uint32_t scan_item(const uint32_t* src, int64_t i, int64_t n) {
+  if (i >= n) return 0;
+  return kOccupancy ? (src[i] ? 1u : 0u) : src[i];
+}
+
+template <bool kOccupancy>
+__global__ __launch_bounds__(kBlock) void scan_count_kernel(const uint32_t* __restrict__ src, int64_t n,
+                                                            uint32_t* __restrict__ sums) {
   __shared__ uint32_t lds[kBlock / 64];
   const int64_t base = blockIdx.x * (int64_t)kScanBlock + threadIdx.x * kScanItems;
   uint32_t c = 0;
 #pragma unroll
-  for (int j = 0; j < kScanItems; ++j)
-    if (base + j < nvox && grid[base + j]) ++c;
+  for (int j = 0; j < kScanItems; ++j) c += scan_item<kOccupancy>(src, base + j, n);
   uint32_t tot;
   block_exclusive_scan(c, lds, &tot);
   if (threadIdx.x == 0) sums[blockIdx.x] = tot;
 }
 
-__global__ __launch_bounds__(kBlock) void scan_sums_kernel(uint32_t* __restrict__ sums,
-                                                           int64_t nblocks) {
+__global__ __launch_bounds__(kBlock) void scan_sums_kernel(uint32_t* __restrict__ sums, int64_t nblocks) {
   __shared__ uint32_t lds[kBlock / 64];
   uint32_t carry = 0;
   for (int64_t b0 = 0; b0 < nblocks; b0 += kBlock) {
@@ -212,51 +482,27 @@ __global__ __launch_bounds__(kBlock) void scan_sums_kernel(uint32_t* __restrict_
   }
 }
 
-__global__ __launch_bounds__(kBlock) void leaf_write_kernel(const uint32_t* __restrict__ grid,
-                                                            int64_t nvox,
+// kOccupancy: leaf layout (rank or -1 per voxel); else exclusive offsets of the counts
+template <bool kOccupancy>
+__global__ __launch_bounds__(kBlock) void scan_write_kernel(const uint32_t* __restrict__ src, int64_t n,
                                                             const uint32_t* __restrict__ sums,
-                                                            int32_t* __restrict__ leaf) {
+                                                            int32_t* __restrict__ out) {
   __shared__ uint32_t lds[kBlock / 64];
   const int64_t base = blockIdx.x * (int64_t)kScanBlock + threadIdx.x * kScanItems;
-  uint32_t occ[kScanItems];
+  uint32_t v[kScanItems];
   uint32_t c = 0;
 #pragma unroll
   for (int j = 0; j < kScanItems; ++j) {
-    occ[j] = (base + j < nvox && grid[base + j]) ? 1u : 0u;
-    c += occ[j];
+    v[j] = scan_item<kOccupancy>(src, base + j, n);
+    c += v[j];
   }
   uint32_t tot;
   uint32_t rank = sums[blockIdx.x] + block_exclusive_scan(c, lds, &tot);
 #pragma unroll
   for (int j = 0; j < kScanItems; ++j) {
-    if (base + j >= nvox) break;
-    leaf[base + j] = occ[j] ? (int32_t)rank : -1;
-    rank += occ[j];
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void downsampled_kernel(
-    const int32_t* __restrict__ leaf, const uint32_t* __restrict__ grid, int64_t nvox,
-    const uint32_t* __restrict__ keys, const uint32_t* __restrict__ cnt,
-    const float* __restrict__ sx, const float* __restrict__ sy, const float* __restrict__ sz,
-    uint64_t mask, float* __restrict__ out) {
-  for (int64_t v = blockIdx.x * (int64_t)kBlock + threadIdx.x; v < nvox;
-       v += (int64_t)gridDim.x * kBlock) {
-    const int32_t rk = leaf[v];
-    if (rk < 0) continue;
-    const uint32_t key = (uint32_t)v;
-    uint64_t h = hash_key(key) & mask;
-    for (uint64_t probes = 0; probes <= mask; ++probes) {
-      if (keys[h] == key) break;
-      h = (h + 1) & mask;
-    }
-    const float c = (float)cnt[h];
-    float4 o;
-    o.x = __fdiv_rn(sx[h], c);
-    o.y = __fdiv_rn(sy[h], c);
-    o.z = __fdiv_rn(sz[h], c);
-    o.w = __uint_as_float(grid[v] & 0x00ffffffu);
-    reinterpret_cast<float4*>(out)[rk] = o;
+    if (base + j >= n) break;
+    out[base + j] = kOccupancy ? (v[j] ? (int32_t)rank : -1) : (int32_t)rank;
+    rank += v[j];
   }
 }
 
@@ -268,49 +514,49 @@ int grid_for(int64_t n, int cap = 4096) {
 
 }  // namespace
 
-hipError_t launch_minmax(const float4* pts, int64_t n, float z_limit, uint32_t* out,
-                         hipStream_t s) {
-  minmax_kernel<<<grid_for(n, 512), kBlock, 0, s>>>(pts, n, z_limit, out);
+int64_t scan_blocks(int64_t n) { return (n + kScanBlock - 1) / kScanBlock; }
+int64_t leaf_layout_blocks(int64_t nvox) { return scan_blocks(nvox); }
+
+hipError_t launch_voxelize(const VoxArgs& a, int64_t list_hint, hipStream_t s) {
+  vox_reset_kernel<<<grid_for(list_hint, 1024), kBlock, 0, s>>>(a);
+  if (a.n > 0) vox_accum_kernel<<<(unsigned)((a.n + kVoxChunk - 1) / kVoxChunk), kBlock, 0, s>>>(a);
+  vox_scatter_kernel<<<grid_for(a.n / 8 + 1, 2048), kBlock, 0, s>>>(a);
   return hipGetLastError();
 }
 
-hipError_t launch_voxel_accum(const float4* pts, int64_t n, float z_limit, float inv,
-                              const int32_t min_b[3], const int32_t div_b[3], uint32_t* keys,
-                              uint32_t* cnt, uint32_t* sr, uint32_t* sg, uint32_t* sb,
-                              float* sx, float* sy, float* sz, uint64_t table_size,
-                              uint32_t* overflow, hipStream_t s) {
-  accum_kernel<<<grid_for(n, 8192), kBlock, 0, s>>>(pts, n, z_limit, inv, min_b[0], min_b[1],
-                                                     min_b[2], div_b[0], div_b[1], keys, cnt,
-                                                     sr, sg, sb, sx, sy, sz, table_size - 1,
-                                                     overflow);
+hipError_t launch_vox_scatter(const VoxArgs& a, hipStream_t s) {
+  vox_scatter_kernel<<<grid_for(a.n / 8 + 1, 2048), kBlock, 0, s>>>(a);
   return hipGetLastError();
 }
 
-hipError_t launch_voxel_scatter(const uint32_t* keys, const uint32_t* cnt, const uint32_t* sr,
-                                const uint32_t* sg, const uint32_t* sb, uint64_t table_size,
-                                uint32_t* grid, uint32_t* n_occ, hipStream_t s) {
-  scatter_kernel<<<grid_for((int64_t)table_size), kBlock, 0, s>>>(keys, cnt, sr, sg, sb,
-                                                                  table_size, grid, n_occ);
+hipError_t launch_vox_centroids(const VoxArgs& a, int64_t ns, uint32_t* counts, uint32_t* offs, uint32_t* cur,
+                                uint32_t* block_sums, uint32_t* bucket, float4* cent, int32_t* offcell,
+                                hipStream_t s) {
+  if (ns <= 0) return hipSuccess;
+  vox_counts_kernel<<<grid_for(ns), kBlock, 0, s>>>(a, counts);
+  const int64_t nb = scan_blocks(ns);
+  scan_count_kernel<false><<<(unsigned)nb, kBlock, 0, s>>>(counts, ns, block_sums);
+  scan_sums_kernel<<<1, kBlock, 0, s>>>(block_sums, nb);
+  scan_write_kernel<false><<<(unsigned)nb, kBlock, 0, s>>>(counts, ns, block_sums, reinterpret_cast<int32_t*>(offs));
+  hipError_t e = hipMemsetAsync(cur, 0, (size_t)ns * 4, s);
+  if (e != hipSuccess) return e;
+  vox_bucket_kernel<<<grid_for(a.n, 8192), kBlock, 0, s>>>(a, offs, cur, bucket);
+  vox_centroid_kernel<<<grid_for(ns), kBlock, 0, s>>>(a, offs, counts, bucket, cent, offcell);
+  return hipGetLastError();
+}
+
+hipError_t launch_vox_downsampled(const VoxArgs& a, int64_t ns, const float4* cent, const int32_t* leaf,
+                                  float* out, hipStream_t s) {
+  if (ns <= 0) return hipSuccess;
+  vox_downsampled_kernel<<<grid_for(ns), kBlock, 0, s>>>(a, cent, leaf, reinterpret_cast<float4*>(out));
   return hipGetLastError();
 }
 
 hipError_t launch_leaf_layout(const uint32_t* grid, int64_t nvox, int32_t* leaf,
                               uint32_t* block_sums, int64_t nblocks, hipStream_t s) {
-  occ_count_kernel<<<(unsigned)nblocks, kBlock, 0, s>>>(grid, nvox, block_sums);
+  scan_count_kernel<true><<<(unsigned)nblocks, kBlock, 0, s>>>(grid, nvox, block_sums);
   scan_sums_kernel<<<1, kBlock, 0, s>>>(block_sums, nblocks);
-  leaf_write_kernel<<<(unsigned)nblocks, kBlock, 0, s>>>(grid, nvox, block_sums, leaf);
-  return hipGetLastError();
-}
-
-int64_t leaf_layout_blocks(int64_t nvox) { return (nvox + kScanBlock - 1) / kScanBlock; }
-
-hipError_t launch_downsampled(const int32_t* leaf, const uint32_t* grid, int64_t nvox,
-                              const int32_t div_b[3], const uint32_t* keys, const uint32_t* cnt,
-                              const float* sx, const float* sy, const float* sz,
-                              uint64_t table_size, float* out, hipStream_t s) {
-  (void)div_b;
-  downsampled_kernel<<<grid_for(nvox, 8192), kBlock, 0, s>>>(leaf, grid, nvox, keys, cnt, sx,
-                                                             sy, sz, table_size - 1, out);
+  scan_write_kernel<true><<<(unsigned)nblocks, kBlock, 0, s>>>(grid, nvox, block_sums, leaf);
   return hipGetLastError();
 }
 

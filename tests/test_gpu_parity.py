@@ -30,9 +30,8 @@ def test_golden_voxelize(ctx, name):
     assert gi.n_occ == z["cloud"].shape[0]
     assert np.array_equal(ctx.grid(), z["grid_words"])
     assert np.array_equal(ctx.leaf_layout(), z["leaf_layout"])
-    ds = ctx.downsampled()
-    assert np.array_equal(ds[:, 3].view(np.uint32), z["cloud"][:, 3].view(np.uint32))
-    np.testing.assert_allclose(ds[:, :3], z["cloud"][:, :3], rtol=1e-6, atol=1e-7)
+    ds = ctx.downsampled()  # centroids: fp32 sequential sums in input order, bit-exact
+    assert np.array_equal(ds.view(np.uint32), z["cloud"].view(np.uint32))
 
 
 @pytest.mark.parametrize("name", GOLDEN_CASES)
@@ -183,7 +182,7 @@ def test_multipoint_voxel_colour_mean(ctx):
     exp = (1 << 24) | cloud[layout[occ], 3].view(np.uint32)
     assert np.array_equal(words[occ], exp) and not words[~occ].any()
     ds = ctx.downsampled()
-    np.testing.assert_allclose(ds[:, :3], cloud[:, :3], rtol=2e-6)
+    assert np.array_equal(ds.view(np.uint32), cloud.view(np.uint32))
 
 
 def test_config2_kinect_128(ctx):
@@ -442,31 +441,76 @@ def test_config5_dense_512_periodic(ctx):
             np.unravel_index(p, (n - 1,) * 3)
 
 
-# bowl1_0000.pcd is a real Kinect capture, its coordinates quantised to 1 mm: at leaf 4 mm
-# 10 of its 945 voxel centroids round across a cell boundary (floor(c * inv_leaf) is not the
-# voxel's own index).  The reference takes the subdivision (c3_hlac.cpp:177-178) and the
-# neighbour base (PCL getNeighborCentroidIndices) of such a voxel from its float centroid;
-# the GPU path takes both from the voxel index.  Known parity gap, see DESIGN.md §5.
-_CENTROID_GAP = pytest.mark.xfail(strict=True, reason="centroid-boundary voxels (DESIGN.md §5)")
+REF_CLOUDS = ["noisy_torus_blue.pcd", "bowl1_0000.pcd", "tmp_normal.pcd", "obj_torus_black.pcd",
+              "noiseless_cone_red.pcd", "noisy_sphere_green.pcd", "noiseless_cylinder_yellow.pcd",
+              "noisy_plane_purple.pcd", "noiseless_torus_black.pcd", "plastic-cup1_0000.pcd",
+              "assam_blend_tea_0000.pcd", "messmer_tea_0000.pcd", "bouillon_0000.pcd", "marker_red_0000.pcd",
+              "bowl1_0015.pcd"]
 
 
-@pytest.mark.parametrize("name,leaf", [("noisy_torus_blue.pcd", 0.005),
-                                       pytest.param("bowl1_0000.pcd", 0.004, marks=_CENTROID_GAP),
-                                       ("tmp_normal.pcd", 0.005), ("obj_torus_black.pcd", 0.004)])
-def test_reference_clouds_end_to_end(ctx, name, leaf):
-    """The reference's own demo clouds (tests/golden/ref_fixtures/pcd): c3h_pcd_read_xyzrgb ->
-    voxelise -> C3-HLAC-981/117 on the GPU, against the oracle on the same points (voxel
-    indices, leaf layout, packed colours bit-exact; exact-integer features bit-exact)."""
+def _pcd(name):
     from pathlib import Path
-    pts = c3hlac.read_pcd(Path(__file__).resolve().parent / "golden" / "ref_fixtures" / "pcd" / name)
+    return c3hlac.read_pcd(Path(__file__).resolve().parent / "golden" / "ref_fixtures" / "pcd" / name)
+
+
+def _check_cloud(ctx, pts, leaf, cases):
+    """voxelise + C3-HLAC on the GPU vs the oracle on the same points: voxel indices, leaf
+    layout, packed colours and the downsampled centroids bit-exact; exact-integer features
+    bit-exact, including voxels whose float centroid rounds across a cell boundary (the
+    reference takes their subdivision, c3_hlac.cpp:349-354, and neighbour base, PCL
+    getNeighborCentroidIndices, from the centroid)."""
     gi = ctx.voxelize(pts, leaf)
     g, layout, cloud = po.voxelize(pts, leaf)
     assert list(gi.div_b) == list(g.div_b) and gi.n_occ == g.n_occ
     assert np.array_equal(ctx.leaf_layout(), layout)
-    for variant in (981, 117):
-        sb, hn = ctx.extract(variant, THR, 5)
-        fe, _, _ = po.c3hlac(g, layout, cloud, variant, THR, leaf, 5, exact=True)
-        assert np.array_equal(ctx.features(), fe)
+    assert np.array_equal(ctx.downsampled().view(np.uint32), cloud.view(np.uint32))
+    checked = 0
+    for variant, S, off in cases:
+        fe, sbo, hn = po.c3hlac(g, layout, cloud, variant, THR, leaf, S, off, exact=True)
+        if hn < 0:  # a centroid past the last subdivision: out of bounds in the reference
+            continue
+        sb, hn2 = ctx.extract(variant, THR, S, off)
+        assert tuple(sb) == tuple(sbo) and hn2 == hn
+        assert np.array_equal(ctx.features(), fe), (variant, S, off)
+        fa, _, _ = po.c3hlac(g, layout, cloud, 981, THR, leaf, S, off, exact=False)
+        assert np.array_equal(ctx.exist(), po.exist(fa))
+        checked += 1
+    return checked
+
+
+@pytest.mark.parametrize("leaf", [0.004, 0.005, 0.01])
+@pytest.mark.parametrize("name", REF_CLOUDS)
+def test_reference_clouds_end_to_end(ctx, name, leaf):
+    """The reference's own demo clouds (tests/golden/ref_fixtures/pcd: synthetic shapes and
+    real Kinect object views) read with c3h_pcd_read_xyzrgb, at three leaf sizes."""
+    cases = [(981, 5, (0, 0, 0)), (117, 5, (0, 0, 0)), (981, 0, (0, 0, 0)), (117, 4, (1, 0, 2))]
+    assert _check_cloud(ctx, _pcd(name), leaf, cases) >= 2
+
+
+def test_points_on_cell_boundaries(ctx):
+    """Every point on (or one ulp beside) a cell boundary, several points per voxel: the
+    centroids of most voxels round across a boundary in some direction, so the exact
+    centroid pass and the off-cell correction of the C3-HLAC sums carry the whole result."""
+    rng = np.random.default_rng(11)
+    leaf = np.float32(0.005)
+    n = 30000
+    cells = rng.integers(0, 24, (n, 3)).astype(np.float32)
+    xyz = cells * leaf
+    ulp = rng.integers(-1, 2, (n, 3))
+    xyz = np.nextafter(xyz, np.where(ulp < 0, -np.inf, np.inf).astype(np.float32)) * (ulp != 0) + xyz * (ulp == 0)
+    col = rng.integers(0, 256, (n, 3))
+    pts = np.concatenate([xyz.astype(np.float32), synth.pack_rgb(col[:, 0], col[:, 1], col[:, 2])[:, None]], 1)
+    pts = np.ascontiguousarray(pts, np.float32)
+    g, layout, cloud = po.voxelize(pts, leaf)
+    occ = np.flatnonzero(layout >= 0)
+    d = np.array(g.div_b)
+    own = np.stack([occ % d[0], (occ // d[0]) % d[1], occ // (d[0] * d[1])], 1) + np.array(g.min_b)
+    c = cloud[layout[occ], :3]
+    moved = ((np.floor(c * (np.float32(1) / leaf)) != own) | (np.floor(c / leaf) != own)).any(1)
+    assert moved.sum() > 100  # the case under test is there
+    cases = [(981, 6, (0, 0, 0)), (117, 6, (0, 0, 0)), (981, 0, (0, 0, 0)), (117, 5, (2, 1, 0)),
+             (981, 20, (0, 0, 0))]
+    assert _check_cloud(ctx, pts, float(leaf), cases) >= 3
 
 
 @pytest.mark.parametrize("batch", [32, 64])
