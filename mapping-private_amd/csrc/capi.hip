@@ -797,6 +797,7 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
     HIPCHK(hipMemsetAsync(ctx->grid.p, 0, ctx->grid.n * 4, ctx->stream));
     a.grid = ctx->grid.p;
     a.grid_cap = (int64_t)ctx->grid.n;
+    HIPCHK(hipMemsetAsync(ctx->vcnt.p + c3h::kVcOver, 0, 4, ctx->stream));
     {
       Timed t(ctx, 0);
       HIPCHK(c3h::launch_vox_scatter(a, ctx->stream));
