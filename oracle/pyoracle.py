@@ -90,6 +90,8 @@ def c3hlac(g, layout, cloud, variant, thr, voxel_size, subdiv=0, offset=(0, 0, 0
         return np.zeros((0, variant), np.float32), tuple(int(x) for x in sb), int(hn)
     feat = np.zeros((max(hn, 1), variant), np.float32)
     hn2 = lib.orc_c3hlac(*args, _p(feat), _p(sb))
+    if hn2 < 0:  # -5: a centroid's subdivision past the last one (out of bounds in the reference)
+        return np.zeros((0, variant), np.float32), tuple(int(x) for x in sb), int(hn2)
     assert hn2 == hn
     return feat[:hn], tuple(int(x) for x in sb), int(hn)
 
