@@ -80,7 +80,14 @@ const char* c3h_last_error(const c3h_ctx* ctx);
 /* getVoxelGrid (c3_hlac/include/c3_hlac/c3_hlac_tools.hpp:124-130) preceded by
  * limitPoint (color_voxel_recognition/test/detect_object.cpp:68-87): points with a
  * non-finite coordinate or z >= z_limit are dropped (pass INFINITY for no limit).
- * xyzrgb: n x 4 floats (x, y, z, rgb packed in the float bits as in PCL). */
+ * xyzrgb: n x 4 floats (x, y, z, rgb packed in the float bits as in PCL); at most
+ * 16,777,215 points per call and cell coordinates within +-2^20 (C3H_ERR_RANGE).
+ * The grid (indices, occupancy, colour means) is deterministic and exact.  Voxel
+ * centroids are the fp32 sums of the voxel's points in input order divided by the count
+ * (c3h_get_downsampled); where a centroid rounds across its cell boundary, the next
+ * c3h_extract takes that voxel's subdivision and neighbour base from the centroid, as
+ * c3_hlac.cpp:349-377 does.  With on_device = 1, c3h_get_downsampled reads the points
+ * again: keep the buffer alive until then. */
 int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, float leaf,
                  float z_limit, c3h_grid_info* info);
 /* VoxelGrid::getLeafLayout (setSaveLeafLayout(true)): div_b product int32, -1 = empty. */

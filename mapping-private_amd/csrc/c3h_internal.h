@@ -96,30 +96,40 @@ enum {
   kVcOff = 13,    // off-cell voxels recorded by the exact pass
   kVcWords = 16
 };
+// one voxel of the voxeliser's global hash table (32 B: one load / clear)
+struct VoxSlot {
+  unsigned long long key;  // absolute cell (21 bits per axis, biased), ~0 = empty
+  unsigned long long a;    // count << 40 | sum r
+  unsigned long long b;    // sum b << 32 | sum g
+  uint32_t margin;         // min distance (cells, float bits) of a member point to the cell boundary
+  uint32_t pos;            // position (accum block * 2048 + i) in the frame's slot list
+};
 struct VoxArgs {
   const float4* pts;
   int64_t n;
   float z_limit, inv, leaf;
-  unsigned long long* key;  // global hash table: absolute cell key (~0 = empty)
-  unsigned long long* sa;   // count << 40 | sum r
-  unsigned long long* sb;   // sum b << 32 | sum g
-  uint32_t* margin;         // min distance (cells, float bits) of a member point to the cell boundary
-  uint32_t* slotpos;        // slot -> position in the frame's slot list
+  VoxSlot* tab;             // this frame's hash table (the two tables alternate by parity)
+  VoxSlot* tab_prev;        // the previous frame's, cleared by this frame's accum launch
   uint64_t tmask;           // table size - 1 (power of two)
-  uint32_t* lists;          // [slots parity 0 | slots parity 1 | grid words parity 0 | parity 1] x lcap
-  uint64_t lcap;
-  uint32_t* cnt;            // kVcWords counters
+  uint32_t* lists;          // [slots parity 0 | slots parity 1 | grid words parity 0 | parity 1] x lcap,
+  uint64_t lcap;            //   each a segment of 2048 per accum block
+  int32_t* part;            // per parity, per accum block: bounds, counts (vox_part_words() ints)
+  int nblk, nblk_prev, nblk_cap;  // accum blocks of this / the previous frame, capacity
+  uint32_t* cnt;            // kVcWords counters (totals published by the scatter)
   uint32_t* grid;           // packed grid buffer (capacity grid_cap words)
   int64_t grid_cap;
   int par;                  // epoch parity of this frame
   int clear_tables, clear_grid;  // clear what the previous frame listed
 };
-hipError_t launch_voxelize(const VoxArgs& a, int64_t list_hint, hipStream_t s);
+hipError_t launch_voxelize(const VoxArgs& a, hipStream_t s);
 hipError_t launch_vox_scatter(const VoxArgs& a, hipStream_t s);
-hipError_t launch_vox_centroids(const VoxArgs& a, int64_t ns, uint32_t* counts, uint32_t* offs, uint32_t* cur,
+int64_t vox_blocks(int64_t n);
+int64_t vox_positions(int64_t n);
+int vox_part_words();
+hipError_t launch_vox_centroids(const VoxArgs& a, uint32_t* counts, uint32_t* offs, uint32_t* cur,
                                 uint32_t* block_sums, uint32_t* bucket, float4* cent, int32_t* offcell,
                                 hipStream_t s);
-hipError_t launch_vox_downsampled(const VoxArgs& a, int64_t ns, const float4* cent, const int32_t* leaf,
+hipError_t launch_vox_downsampled(const VoxArgs& a, const float4* cent, const uint32_t* counts, const int32_t* leaf,
                                   float* out, hipStream_t s);
 int64_t scan_blocks(int64_t n);
 hipError_t launch_leaf_layout(const uint32_t* grid, int64_t nvox, int32_t* leaf,
@@ -304,11 +314,12 @@ struct c3h_ctx {
   c3h::DevBuf<float> pts;           // staging copy of host points
   // voxeliser state (voxelize.hip): global hash table, slot / grid-word lists by epoch
   // parity, counters; what the previous frame listed is cleared by the next frame
-  c3h::DevBuf<unsigned long long> vkey, vsa, vsb;
-  c3h::DevBuf<uint32_t> vmargin, vslotpos, vlists, vcnt;
+  c3h::DevBuf<c3h::VoxSlot> vtab[2];
+  c3h::DevBuf<uint32_t> vlists, vcnt;
+  c3h::DevBuf<int32_t> vpart;
   uint64_t vtsize = 0, vlcap = 0;
-  int vpar = 0;
-  int64_t vns_prev = 0;             // voxels the previous frame listed
+  int vpar = 0, vblk_cap = 0;
+  int vblk_prev = 0;                // accum blocks of the previous frame (its lists to clear)
   bool vgrid_tracked = false;       // grid buffer is zero outside the previous frame's list
   c3h::VoxArgs vargs{};             // the last voxelize (exact centroid pass, downsampled)
   int64_t vns = 0;                  // voxels of the last voxelize

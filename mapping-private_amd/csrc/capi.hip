@@ -556,14 +556,15 @@ int exact_centroids(c3h_ctx* ctx) {
   if (ctx->vcent_valid) return C3H_OK;
   const int64_t ns = ctx->vns;
   const c3h::VoxArgs& a = ctx->vargs;
-  ENSURE(ctx->vcounts, (size_t)ns);
-  ENSURE(ctx->voffs, (size_t)ns);
-  ENSURE(ctx->vcur, (size_t)ns);
-  ENSURE(ctx->tmp_u32, (size_t)c3h::scan_blocks(ns));
+  const int64_t np = (int64_t)a.nblk * c3h::vox_positions(1);  // segmented list positions
+  ENSURE(ctx->vcounts, (size_t)np);
+  ENSURE(ctx->voffs, (size_t)np);
+  ENSURE(ctx->vcur, (size_t)np);
+  ENSURE(ctx->tmp_u32, (size_t)c3h::scan_blocks(np));
   ENSURE(ctx->vbucket, (size_t)std::max<int64_t>(ctx->info.n_valid, 1));
-  ENSURE(ctx->vcent, (size_t)ns);
-  ENSURE(ctx->voffcell, (size_t)ns * 8);
-  HIPCHK(c3h::launch_vox_centroids(a, ns, ctx->vcounts.p, ctx->voffs.p, ctx->vcur.p, ctx->tmp_u32.p,
+  ENSURE(ctx->vcent, (size_t)np);
+  ENSURE(ctx->voffcell, (size_t)std::max<int64_t>(ns, 1) * 8);
+  HIPCHK(c3h::launch_vox_centroids(a, ctx->vcounts.p, ctx->voffs.p, ctx->vcur.p, ctx->tmp_u32.p,
                                    ctx->vbucket.p, ctx->vcent.p, ctx->voffcell.p, ctx->stream));
   HIPCHK(hipMemcpyAsync(ctx->h_small, ctx->vcnt.p, c3h::kVcWords * 4, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -619,13 +620,11 @@ void c3h_destroy(c3h_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   release(ctx->grid);
   release(ctx->pts);
-  release(ctx->vkey);
-  release(ctx->vsa);
-  release(ctx->vsb);
-  release(ctx->vmargin);
-  release(ctx->vslotpos);
+  release(ctx->vtab[0]);
+  release(ctx->vtab[1]);
   release(ctx->vlists);
   release(ctx->vcnt);
+  release(ctx->vpart);
   release(ctx->vcounts);
   release(ctx->voffs);
   release(ctx->vcur);
@@ -713,23 +712,26 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
   // tables: >= 2x the points (load <= 1/2); (re)allocation starts from all-empty state
   uint64_t ts = 1024;
   while (ts < 2 * (uint64_t)n) ts <<= 1;
-  if (ctx->vtsize < ts || !ctx->vcnt.p) {
+  const int nblk = (int)c3h::vox_blocks(n);
+  if (ctx->vtsize < ts || !ctx->vcnt.p || ctx->vblk_cap < nblk) {
     ctx->vtsize = 0;
-    ENSURE(ctx->vkey, ts);
-    ENSURE(ctx->vsa, ts);
-    ENSURE(ctx->vsb, ts);
-    ENSURE(ctx->vmargin, ts);
-    ENSURE(ctx->vslotpos, ts);
-    ENSURE(ctx->vlists, 4 * (ts / 2));
+    const int bcap = (int)c3h::vox_blocks((int64_t)(ts / 2));
+    ENSURE(ctx->vtab[0], ts);
+    ENSURE(ctx->vtab[1], ts);
+    ENSURE(ctx->vlists, 4 * (size_t)c3h::vox_positions((int64_t)(ts / 2)));
+    ENSURE(ctx->vpart, 2 * (size_t)bcap * c3h::vox_part_words());
     ENSURE(ctx->vcnt, c3h::kVcWords);
-    HIPCHK(hipMemsetAsync(ctx->vkey.p, 0xff, ts * 8, ctx->stream));
-    HIPCHK(hipMemsetAsync(ctx->vsa.p, 0, ts * 8, ctx->stream));
-    HIPCHK(hipMemsetAsync(ctx->vsb.p, 0, ts * 8, ctx->stream));
-    HIPCHK(hipMemsetAsync(ctx->vmargin.p, 0xff, ts * 4, ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->vpart.p, 0, ctx->vpart.n * 4, ctx->stream));
+    for (int t = 0; t < 2; ++t) {  // empty slots: key ~0, sums 0, margin ~0
+      HIPCHK(hipMemset2DAsync(&ctx->vtab[t].p[0].key, sizeof(c3h::VoxSlot), 0xff, 8, ts, ctx->stream));
+      HIPCHK(hipMemset2DAsync(&ctx->vtab[t].p[0].a, sizeof(c3h::VoxSlot), 0, 16, ts, ctx->stream));
+      HIPCHK(hipMemset2DAsync(&ctx->vtab[t].p[0].margin, sizeof(c3h::VoxSlot), 0xff, 8, ts, ctx->stream));
+    }
     HIPCHK(hipMemsetAsync(ctx->vcnt.p, 0, c3h::kVcWords * 4, ctx->stream));
     ctx->vtsize = ts;
-    ctx->vlcap = ts / 2;
-    ctx->vns_prev = 0;
+    ctx->vlcap = (uint64_t)c3h::vox_positions((int64_t)(ts / 2));
+    ctx->vblk_cap = bcap;
+    ctx->vblk_prev = 0;
     ctx->vgrid_tracked = false;
   }
   // the previous frame's grid words are cleared through its list only when its scatter
@@ -743,14 +745,15 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
   a.z_limit = z_limit;
   a.inv = gi.inv_leaf;
   a.leaf = leaf;
-  a.key = ctx->vkey.p;
-  a.sa = ctx->vsa.p;
-  a.sb = ctx->vsb.p;
-  a.margin = ctx->vmargin.p;
-  a.slotpos = ctx->vslotpos.p;
+  a.tab = ctx->vtab[ctx->vpar].p;
+  a.tab_prev = ctx->vtab[ctx->vpar ^ 1].p;
   a.tmask = ctx->vtsize - 1;
   a.lists = ctx->vlists.p;
   a.lcap = ctx->vlcap;
+  a.part = ctx->vpart.p;
+  a.nblk = nblk;
+  a.nblk_prev = ctx->vblk_prev;
+  a.nblk_cap = ctx->vblk_cap;
   a.cnt = ctx->vcnt.p;
   a.grid = ctx->grid.p;
   a.grid_cap = (int64_t)ctx->grid.n;
@@ -759,14 +762,14 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
   a.clear_grid = clear_grid ? 1 : 0;
   {
     Timed t(ctx, 0);
-    HIPCHK(c3h::launch_voxelize(a, ctx->vns_prev, ctx->stream));
+    HIPCHK(c3h::launch_voxelize(a, ctx->stream));
   }
   uint32_t* hc = ctx->h_small;
   HIPCHK(hipMemcpyAsync(hc, ctx->vcnt.p, c3h::kVcWords * 4, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   // from here the tables hold this frame's entries (listed under parity a.par)
   ctx->vpar ^= 1;
-  ctx->vns_prev = hc[c3h::kVcSlots + a.par];
+  ctx->vblk_prev = nblk;
   if (hc[c3h::kVcErr]) {
     return fail(ctx, C3H_ERR_RANGE, "c3h_voxelize: leaf size too small (cell coordinates beyond +-2^20)");
   }
@@ -953,7 +956,7 @@ int c3h_get_downsampled(c3h_ctx* ctx, float* out, int on_device) {
     ENSURE(ctx->pts, (size_t)ctx->info.n_occ * 4);
     dst = ctx->pts.p;
   }
-  HIPCHK(c3h::launch_vox_downsampled(ctx->vargs, ctx->vns, ctx->vcent.p, ctx->tmp_i32.p, dst, ctx->stream));
+  HIPCHK(c3h::launch_vox_downsampled(ctx->vargs, ctx->vcent.p, ctx->vcounts.p, ctx->tmp_i32.p, dst, ctx->stream));
   if (!on_device)
     HIPCHK(hipMemcpyAsync(out, dst, (size_t)ctx->info.n_occ * 16, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));

@@ -4,20 +4,22 @@
 // VoxelGrid::filter, semantics restated in SURVEY.md App. B) and limitPoint
 // (color_voxel_recognition/test/detect_object.cpp:68-87).
 //
-// Hot path: three launches, no host round trip between them.
-//   vox_reset   clears what the previous frame left: its hash-table slots and its grid
-//               words (both listed by that frame), and the frame counters.  The grid
-//               buffer is therefore all-zero outside the voxels a frame writes, without
-//               a 4 B/voxel memset per frame.
+// Hot path: two launches, no host round trip between them.
 //   vox_accum   one workgroup per 2,048 consecutive points (a depth camera's pixel order
 //               is spatially coherent: a voxel is hit by runs of neighbouring pixels):
-//               coalesced 16-B loads, the bounds (block-reduced, one atomic per block and
-//               field), and per point an LDS hash insert of the absolute cell with LDS
-//               atomics for count + r (one u32), g | b (one u64) and the point's distance
+//               coalesced 16-B loads; per point an LDS hash insert of the absolute cell
+//               with LDS atomics for count | r, b | g (u64 each) and the point's distance
 //               to the cell boundary (min).  Each (workgroup, voxel) then leaves one
-//               global hash insert and three global atomics; new slots are appended to
-//               the frame's slot list with one global atomic per workgroup.
-//   vox_scatter one thread per listed voxel: cell - min_b -> linear index (PCL's
+//               global hash insert and two global atomics on one 32-B slot; the new slots
+//               go to the workgroup's own segment of the frame's slot list, and bounds /
+//               counts to its partial record (no same-address atomics across workgroups:
+//               they serialise at the memory side).  The same launch clears what the
+//               previous frame left: its grid words and its hash-table slots (listed by
+//               it).  Two tables alternate by frame parity, so the clear of one never
+//               races the inserts into the other; the grid buffer stays all-zero outside
+//               the voxels a frame writes, without a 4 B/voxel memset per frame.
+//   vox_scatter every block reduces the partial records (bounds, totals), then converts
+//               its segment's voxels: cell - min_b -> linear index (PCL's
 //               (floor(p * inv) - min_b) . divb_mul), the canonical colour mean
 //               kOcc | r<<16 | g<<8 | b with r = (int)(float(sum_r) / float(count)), the
 //               grid word, and the safety test below.
@@ -34,6 +36,7 @@
 // point index and summed sequentially in fp32 -- bit-identical to the oracle -- and voxels
 // whose centroid cells differ from their own cell are recorded (c3h_extract corrects
 // their C3-HLAC contribution, c3hlac.hip offcell_delta_kernel).
+#include <algorithm>
 #include <climits>
 
 #include "c3h_internal.h"
@@ -44,11 +47,16 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr unsigned long long kNoKey = ~0ull;
 constexpr uint32_t kNoMargin = 0xffffffffu;  // above every float's bits: "no point yet"
-constexpr int kVoxChunk = 2048;  // points per workgroup (8 per thread)
+constexpr int kVoxChunk = 2048;               // points per workgroup (8 per thread)
 constexpr int kVoxPer = kVoxChunk / kBlock;
-constexpr int kLSlots = 1024;    // LDS hash slots per workgroup
-constexpr int kLProbe = 48;      // LDS probes before a point goes straight to the global table
+constexpr int kVoxRound = kVoxPer;             // loads in flight per thread (one round)
+constexpr int kLSlots = 1024;                 // LDS hash slots per workgroup
+constexpr int kLProbe = 48;                   // LDS probes before a point goes straight to the global table
 constexpr int kCellBias = 1 << 20;
+// point margins (cells) at or above this are not recorded per voxel: the scatter's bound
+// is below it except for very dense far voxels, which it then flags conservatively
+constexpr uint32_t kMarginFlush = 0x3c800000u;  // 1/64
+static_assert(sizeof(VoxSlot) == 32, "one 32-B slot per voxel");
 
 __device__ __forceinline__ bool point_valid(const float4& p, float z_limit) {
   return isfinite(p.x) && isfinite(p.y) && isfinite(p.z) && p.z < z_limit;
@@ -87,7 +95,7 @@ __device__ __forceinline__ uint32_t mix64(unsigned long long k) {
 __device__ __forceinline__ int64_t global_slot(const VoxArgs& a, unsigned long long key, bool* fresh) {
   uint64_t h = mix64(key) & a.tmask;
   for (uint64_t probes = 0; probes <= a.tmask; ++probes) {
-    const unsigned long long prev = atomicCAS(&a.key[h], kNoKey, key);
+    const unsigned long long prev = atomicCAS(&a.tab[h].key, kNoKey, key);
     if (prev == kNoKey) {
       *fresh = true;
       return (int64_t)h;
@@ -105,7 +113,7 @@ __device__ __forceinline__ int64_t global_slot(const VoxArgs& a, unsigned long l
 __device__ __forceinline__ int64_t find_slot(const VoxArgs& a, unsigned long long key) {
   uint64_t h = mix64(key) & a.tmask;
   for (uint64_t probes = 0; probes <= a.tmask; ++probes) {
-    const unsigned long long k = a.key[h];
+    const unsigned long long k = a.tab[h].key;
     if (k == key) return (int64_t)h;
     if (k == kNoKey) return -1;
     h = (h + 1) & a.tmask;
@@ -128,42 +136,39 @@ __device__ __forceinline__ bool point_cell(const VoxArgs& a, const float4& p, in
   return ok;
 }
 
-__global__ __launch_bounds__(kBlock) void vox_reset_kernel(VoxArgs a) {
+// per accum block: {min xyz, max xyz, valid points, new slots, error} at part[par][b]
+constexpr int kPartW = 12;
+enum { kPMin = 0, kPMax = 3, kPValid = 6, kPNew = 7, kPErr = 8 };
+
+__device__ __forceinline__ const int32_t* part_of(const VoxArgs& a, int par) {
+  return a.part + (size_t)par * a.nblk_cap * kPartW;
+}
+
+// the previous frame's grid words and its table's slots (its segments b, b + nblk, ...)
+__device__ __forceinline__ void vox_clear_prev(const VoxArgs& a) {
   const int pp = a.par ^ 1;
-  uint32_t* cnt = a.cnt;
-  const uint32_t np = cnt[kVcSlots + pp];
-  const uint32_t* sl = a.lists + (size_t)pp * a.lcap;
-  const uint32_t* tl = a.lists + (size_t)(2 + pp) * a.lcap;
-  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < (int64_t)np;
-       i += (int64_t)gridDim.x * kBlock) {
-    if (a.clear_tables) {
-      const uint32_t s = sl[i];
-      a.key[s] = kNoKey;
-      a.sa[s] = 0;
-      a.sb[s] = 0;
-      a.margin[s] = kNoMargin;
+  for (int b = blockIdx.x; b < a.nblk_prev; b += gridDim.x) {
+    const int nn = part_of(a, pp)[(size_t)b * kPartW + kPNew];
+    const uint32_t* sl = a.lists + (size_t)pp * a.lcap + (size_t)b * kVoxChunk;
+    const uint32_t* tl = a.lists + (size_t)(2 + pp) * a.lcap + (size_t)b * kVoxChunk;
+    for (int i = threadIdx.x; i < nn; i += kBlock) {
+      if (a.clear_tables) {
+        VoxSlot& t = a.tab_prev[sl[i]];
+        *reinterpret_cast<ulonglong2*>(&t.key) = make_ulonglong2(kNoKey, 0ull);
+        *reinterpret_cast<ulonglong2*>(&t.b) = make_ulonglong2(0ull, (unsigned long long)kNoMargin);
+      }
+      if (a.clear_grid) a.grid[tl[i]] = 0;
     }
-    if (a.clear_grid) a.grid[tl[i]] = 0;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    for (int ax = 0; ax < 3; ++ax) {
-      reinterpret_cast<int32_t*>(cnt)[kVcMin + ax] = INT_MAX;
-      reinterpret_cast<int32_t*>(cnt)[kVcMax + ax] = INT_MIN;
-    }
-    cnt[kVcValid] = cnt[kVcValid + 1] = 0;
-    cnt[kVcSlots + a.par] = 0;
-    cnt[kVcFlag] = cnt[kVcErr] = cnt[kVcOver] = cnt[kVcOff] = 0;
   }
 }
 
 __global__ __launch_bounds__(kBlock) void vox_accum_kernel(VoxArgs a) {
   __shared__ unsigned long long s_key[kLSlots];
   __shared__ unsigned long long s_gb[kLSlots];  // b << 32 | g
-  __shared__ uint32_t s_cr[kLSlots];            // count << 20 | r (chunk sums: r < 2^20, count <= 2^11)
+  __shared__ unsigned long long s_cr[kLSlots];  // count << 32 | r
   __shared__ uint32_t s_m[kLSlots];
-  __shared__ uint32_t s_new[kVoxChunk];         // global slots this workgroup inserted
-  __shared__ uint32_t s_nnew, s_base;
-  __shared__ int s_red[kBlock / 64][7];
+  __shared__ uint32_t s_nnew;                   // global slots this workgroup inserted (its list segment)
+  __shared__ int s_red[kBlock / 64][8];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   for (int s = tid; s < kLSlots; s += kBlock) {
     s_key[s] = kNoKey;
@@ -172,18 +177,18 @@ __global__ __launch_bounds__(kBlock) void vox_accum_kernel(VoxArgs a) {
     s_m[s] = kNoMargin;
   }
   if (tid == 0) s_nnew = 0;
-  const int64_t base = blockIdx.x * (int64_t)kVoxChunk;
-  float4 p[kVoxPer];
-#pragma unroll
-  for (int j = 0; j < kVoxPer; ++j) {  // all loads first: bytes in flight, not latency
-    const int64_t i = base + j * kBlock + tid;
-    if (i < a.n) {  // streamed once: non-temporal
-      const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.pts) + i);
-      p[j] = make_float4(v.x, v.y, v.z, v.w);
-    } else {
-      p[j] = make_float4(NAN, NAN, NAN, 0.0f);
+  if (blockIdx.x == 0 && tid == 0) {  // totals of an empty frame (the scatter publishes the others)
+    for (int ax = 0; ax < 3; ++ax) {
+      reinterpret_cast<int32_t*>(a.cnt)[kVcMin + ax] = INT_MAX;
+      reinterpret_cast<int32_t*>(a.cnt)[kVcMax + ax] = INT_MIN;
     }
+    a.cnt[kVcValid] = a.cnt[kVcValid + 1] = 0;
+    a.cnt[kVcSlots + a.par] = 0;
+    a.cnt[kVcFlag] = a.cnt[kVcErr] = a.cnt[kVcOver] = a.cnt[kVcOff] = 0;
   }
+  vox_clear_prev(a);
+  const int64_t base = blockIdx.x * (int64_t)kVoxChunk;
+  uint32_t* sl = a.lists + (size_t)a.par * a.lcap + (size_t)blockIdx.x * kVoxChunk;
   __syncthreads();
   int mn[3] = {INT_MAX, INT_MAX, INT_MAX}, mx[3] = {INT_MIN, INT_MIN, INT_MIN};
   int nv = 0;
@@ -195,13 +200,25 @@ __global__ __launch_bounds__(kBlock) void vox_accum_kernel(VoxArgs a) {
       err = true;
       return;
     }
-    if (fresh) s_new[atomicAdd(&s_nnew, 1u)] = (uint32_t)s;
-    atomicAdd(&a.sa[s], A);
-    atomicAdd(&a.sb[s], B);
-    atomicMin(&a.margin[s], m);
+    if (fresh) sl[atomicAdd(&s_nnew, 1u)] = (uint32_t)s;
+    atomicAdd(&a.tab[s].a, A);
+    atomicAdd(&a.tab[s].b, B);
+    if (m < kMarginFlush) atomicMin(&a.tab[s].margin, m);
   };
+  for (int j0 = 0; j0 < kVoxPer; j0 += kVoxRound) {
+  float4 p[kVoxRound];
 #pragma unroll
-  for (int j = 0; j < kVoxPer; ++j) {
+  for (int j = 0; j < kVoxRound; ++j) {  // a round of loads in flight together
+    const int64_t i = base + (j0 + j) * kBlock + tid;
+    if (i < a.n) {  // streamed once: non-temporal
+      const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.pts) + i);
+      p[j] = make_float4(v.x, v.y, v.z, v.w);
+    } else {
+      p[j] = make_float4(NAN, NAN, NAN, 0.0f);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kVoxRound; ++j) {
     if (!point_valid(p[j], a.z_limit)) continue;
     int c[3];
     float margin;
@@ -224,9 +241,9 @@ __global__ __launch_bounds__(kBlock) void vox_accum_kernel(VoxArgs a) {
     for (int probe = 0; probe < kLProbe; ++probe) {
       const unsigned long long prev = atomicCAS(&s_key[h], kNoKey, key);
       if (prev == kNoKey || prev == key) {
-        atomicAdd(&s_cr[h], (1u << 20) | r);
+        atomicAdd(&s_cr[h], (1ull << 32) | r);
         atomicAdd(&s_gb[h], ((unsigned long long)b << 32) | g);
-        atomicMin(&s_m[h], mb);
+        if (mb < kMarginFlush) atomicMin(&s_m[h], mb);
         done = true;
         break;
       }
@@ -234,51 +251,163 @@ __global__ __launch_bounds__(kBlock) void vox_accum_kernel(VoxArgs a) {
     }
     if (!done) add_global(key, (1ull << 40) | r, ((unsigned long long)b << 32) | g, mb);  // LDS table full
   }
-  // bounds: wave, then block reduction; one atomic per block and field
+  }
+  // flush: one global insert + two (three near a cell boundary) atomics per (workgroup, voxel)
+  __syncthreads();  // every point's LDS update is in
+  for (int s = tid; s < kLSlots; s += kBlock) {
+    const unsigned long long key = s_key[s];
+    if (key == kNoKey) continue;
+    const unsigned long long cr = s_cr[s];
+    add_global(key, ((cr >> 32) << 40) | (cr & 0xffffffffull), s_gb[s], s_m[s]);
+  }
+  // bounds, counts and the slot list go to this block's partial record: no same-address
+  // atomics across blocks (they serialise at the memory side)
 #pragma unroll
   for (int ax = 0; ax < 3; ++ax) {
     mn[ax] = wave_reduce(mn[ax], [](int x, int y) { return min(x, y); });
     mx[ax] = wave_reduce(mx[ax], [](int x, int y) { return max(x, y); });
   }
   nv = wave_reduce(nv, [](int x, int y) { return x + y; });
+  const int e = wave_reduce(err ? 1 : 0, [](int x, int y) { return x | y; });
   if (lane == 0) {
     for (int ax = 0; ax < 3; ++ax) {
       s_red[w][ax] = mn[ax];
       s_red[w][3 + ax] = mx[ax];
     }
     s_red[w][6] = nv;
+    s_red[w][7] = e;
   }
   __syncthreads();
-  if (tid == 0) {
+  int32_t* pr = a.part + ((size_t)a.par * a.nblk_cap + blockIdx.x) * kPartW;
+  if (tid < 8) {
+    int v = s_red[0][tid];
     for (int i = 1; i < kBlock / 64; ++i) {
-      for (int ax = 0; ax < 3; ++ax) {
-        s_red[0][ax] = min(s_red[0][ax], s_red[i][ax]);
-        s_red[0][3 + ax] = max(s_red[0][3 + ax], s_red[i][3 + ax]);
-      }
-      s_red[0][6] += s_red[i][6];
+      const int u = s_red[i][tid];
+      v = tid < 3 ? min(v, u) : (tid < 6 ? max(v, u) : (tid == 6 ? v + u : (v | u)));
     }
-    if (s_red[0][6]) {
-      int32_t* ci = reinterpret_cast<int32_t*>(a.cnt);
+    pr[tid < 7 ? tid : kPErr] = v;
+  }
+  if (tid == 8) pr[kPNew] = (int)s_nnew;
+}
+
+// every block reduces the accum blocks' partial records (a few KB, from L2); block 0
+// publishes the totals for the host and the later kernels
+struct VoxTotals {
+  int mn[3], dv[3];
+  int64_t nvox;
+  bool any;
+};
+
+__device__ VoxTotals vox_reduce(const VoxArgs& a, bool publish) {
+  __shared__ int s_r[kBlock / 64][10];
+  const int32_t* pt = part_of(a, a.par);
+  int mn[3] = {INT_MAX, INT_MAX, INT_MAX}, mx[3] = {INT_MIN, INT_MIN, INT_MIN};
+  int nv = 0, nn = 0, er = 0;
+  for (int b = threadIdx.x; b < a.nblk; b += kBlock) {
+    const int32_t* r = pt + (size_t)b * kPartW;
+    if (r[kPValid]) {
       for (int ax = 0; ax < 3; ++ax) {
-        atomicMin(&ci[kVcMin + ax], s_red[0][ax]);
-        atomicMax(&ci[kVcMax + ax], s_red[0][3 + ax]);
+        mn[ax] = min(mn[ax], r[kPMin + ax]);
+        mx[ax] = max(mx[ax], r[kPMax + ax]);
       }
-      atomicAdd(reinterpret_cast<unsigned long long*>(a.cnt + kVcValid), (unsigned long long)s_red[0][6]);
     }
+    nv += r[kPValid];
+    nn += r[kPNew];
+    er |= r[kPErr];
   }
-  // flush: one global insert + three atomics per (workgroup, voxel)
-  for (int s = tid; s < kLSlots; s += kBlock) {
-    const unsigned long long key = s_key[s];
-    if (key == kNoKey) continue;
-    const uint32_t cr = s_cr[s];
-    add_global(key, ((unsigned long long)(cr >> 20) << 40) | (cr & 0xfffffu), s_gb[s], s_m[s]);
+  for (int ax = 0; ax < 3; ++ax) {
+    mn[ax] = wave_reduce(mn[ax], [](int x, int y) { return min(x, y); });
+    mx[ax] = wave_reduce(mx[ax], [](int x, int y) { return max(x, y); });
   }
-  if (err) atomicOr(a.cnt + kVcErr, 1u);
+  nv = wave_reduce(nv, [](int x, int y) { return x + y; });
+  nn = wave_reduce(nn, [](int x, int y) { return x + y; });
+  er = wave_reduce(er, [](int x, int y) { return x | y; });
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    for (int ax = 0; ax < 3; ++ax) {
+      s_r[w][ax] = mn[ax];
+      s_r[w][3 + ax] = mx[ax];
+    }
+    s_r[w][6] = nv;
+    s_r[w][7] = nn;
+    s_r[w][8] = er;
+  }
   __syncthreads();
-  if (tid == 0) s_base = s_nnew ? atomicAdd(a.cnt + kVcSlots + a.par, s_nnew) : 0;
-  __syncthreads();
-  uint32_t* sl = a.lists + (size_t)a.par * a.lcap;
-  for (uint32_t i = tid; i < s_nnew; i += kBlock) sl[s_base + i] = s_new[i];
+  VoxTotals t;
+  int64_t nvox = 1;
+  for (int ax = 0; ax < 3; ++ax) {
+    int lo = s_r[0][ax], hi = s_r[0][3 + ax];
+    for (int i = 1; i < kBlock / 64; ++i) {
+      lo = min(lo, s_r[i][ax]);
+      hi = max(hi, s_r[i][3 + ax]);
+    }
+    t.mn[ax] = lo;
+    t.dv[ax] = hi - lo + 1;
+    nvox *= t.dv[ax];
+  }
+  int tv = 0, tn = 0, te = 0;
+  for (int i = 0; i < kBlock / 64; ++i) {
+    tv += s_r[i][6];
+    tn += s_r[i][7];
+    te |= s_r[i][8];
+  }
+  t.any = tv > 0;
+  t.nvox = t.any ? nvox : 0;
+  if (publish && threadIdx.x == 0) {
+    int32_t* ci = reinterpret_cast<int32_t*>(a.cnt);
+    for (int ax = 0; ax < 3; ++ax) {
+      ci[kVcMin + ax] = t.mn[ax];
+      ci[kVcMax + ax] = t.mn[ax] + t.dv[ax] - 1;
+    }
+    a.cnt[kVcValid] = (uint32_t)tv;
+    a.cnt[kVcValid + 1] = 0;
+    a.cnt[kVcSlots + a.par] = (uint32_t)tn;
+    if (te) a.cnt[kVcErr] = 1;
+  }
+  return t;
+}
+
+__device__ __forceinline__ int seg_count(const VoxArgs& a, int b) {
+  return part_of(a, a.par)[(size_t)b * kPartW + kPNew];
+}
+
+// one block per accum block: its listed voxels (the block's segment of the slot list)
+__global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
+  const VoxTotals t = vox_reduce(a, blockIdx.x == 0);
+  if (!t.any) return;
+  if (t.nvox > a.grid_cap || t.nvox > INT_MAX) {  // the host grows the grid and runs this again
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.cnt[kVcOver] = 1;
+    return;
+  }
+  const int b = blockIdx.x;
+  const int nn = seg_count(a, b);
+  const size_t seg = (size_t)b * kVoxChunk;
+  const uint32_t* sl = a.lists + (size_t)a.par * a.lcap + seg;
+  uint32_t* tl = a.lists + (size_t)(2 + a.par) * a.lcap + seg;
+  uint32_t flagged = 0;
+  for (int i = threadIdx.x; i < nn; i += kBlock) {
+    const uint32_t s = sl[i];
+    const ulonglong2 ka = *reinterpret_cast<const ulonglong2*>(&a.tab[s].key);
+    const ulonglong2 bm = *reinterpret_cast<const ulonglong2*>(&a.tab[s].b);
+    int x, y, z;
+    unpack_cell(ka.x, x, y, z);
+    const int64_t idx = (x - t.mn[0]) + (int64_t)t.dv[0] * ((y - t.mn[1]) + (int64_t)t.dv[1] * (z - t.mn[2]));
+    const unsigned long long A = ka.y, B = bm.x;
+    const uint32_t count = (uint32_t)(A >> 40);
+    const float c = (float)count;
+    const uint32_t r = (uint32_t)(int)__fdiv_rn((float)(A & 0xffffffffffull), c);
+    const uint32_t g = (uint32_t)(int)__fdiv_rn((float)(B & 0xffffffffull), c);
+    const uint32_t bl = (uint32_t)(int)__fdiv_rn((float)(B >> 32), c);
+    a.grid[idx] = kOcc | (r << 16) | (g << 8) | bl;
+    tl[i] = (uint32_t)idx;
+    a.tab[s].pos = (uint32_t)(seg + i);
+    // margins >= kMarginFlush were not recorded: conservative when the bound exceeds it
+    const int cmag = max(max(abs(x), abs(y)), abs(z)) + 1;
+    const float eps = (float)(count + 4) * (float)cmag * 0x1p-22f;
+    if (__uint_as_float((uint32_t)bm.y) < eps || eps >= __uint_as_float(kMarginFlush)) ++flagged;
+  }
+  flagged = wave_reduce(flagged, [](uint32_t u, uint32_t v) { return u + v; });
+  if ((threadIdx.x & 63) == 0 && flagged) atomicAdd(a.cnt + kVcFlag, flagged);
 }
 
 __device__ __forceinline__ bool vox_bounds(const VoxArgs& a, int mn[3], int dv[3], int64_t* nvox) {
@@ -293,48 +422,16 @@ __device__ __forceinline__ bool vox_bounds(const VoxArgs& a, int mn[3], int dv[3
   return ci[kVcMax] >= ci[kVcMin];
 }
 
-__global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
-  const uint32_t ns = a.cnt[kVcSlots + a.par];
-  int mn[3], dv[3];
-  int64_t nvox;
-  if (!vox_bounds(a, mn, dv, &nvox)) return;
-  if (nvox > a.grid_cap || nvox > INT_MAX) {  // the host grows the grid and runs this again
-    if (blockIdx.x == 0 && threadIdx.x == 0) a.cnt[kVcOver] = 1;
-    return;
-  }
-  const uint32_t* sl = a.lists + (size_t)a.par * a.lcap;
-  uint32_t* tl = a.lists + (size_t)(2 + a.par) * a.lcap;
-  uint32_t flagged = 0;
-  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < (int64_t)ns;
-       i += (int64_t)gridDim.x * kBlock) {
-    const uint32_t s = sl[i];
-    int x, y, z;
-    unpack_cell(a.key[s], x, y, z);
-    const int64_t idx = (x - mn[0]) + (int64_t)dv[0] * ((y - mn[1]) + (int64_t)dv[1] * (z - mn[2]));
-    const unsigned long long A = a.sa[s], B = a.sb[s];
-    const uint32_t count = (uint32_t)(A >> 40);
-    const float c = (float)count;
-    const uint32_t r = (uint32_t)(int)__fdiv_rn((float)(A & 0xffffffffffull), c);
-    const uint32_t g = (uint32_t)(int)__fdiv_rn((float)(B & 0xffffffffull), c);
-    const uint32_t b = (uint32_t)(int)__fdiv_rn((float)(B >> 32), c);
-    a.grid[idx] = kOcc | (r << 16) | (g << 8) | b;
-    tl[i] = (uint32_t)idx;
-    a.slotpos[s] = (uint32_t)i;
-    const int cmag = max(max(abs(x), abs(y)), abs(z)) + 1;
-    const float eps = (float)(count + 4) * (float)cmag * 0x1p-22f;
-    if (__uint_as_float(a.margin[s]) < eps) ++flagged;
-  }
-  flagged = wave_reduce(flagged, [](uint32_t u, uint32_t v) { return u + v; });
-  if ((threadIdx.x & 63) == 0 && flagged) atomicAdd(a.cnt + kVcFlag, flagged);
-}
-
 // ---- exact centroids (flagged frames and c3h_get_downsampled) ----------------------
+// positions p = b * kVoxChunk + i of the segmented slot list; gaps (i >= the segment's
+// count) hold count 0
 __global__ __launch_bounds__(kBlock) void vox_counts_kernel(VoxArgs a, uint32_t* __restrict__ counts) {
-  const uint32_t ns = a.cnt[kVcSlots + a.par];
+  const int64_t np = (int64_t)a.nblk * kVoxChunk;
   const uint32_t* sl = a.lists + (size_t)a.par * a.lcap;
-  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < (int64_t)ns;
-       i += (int64_t)gridDim.x * kBlock)
-    counts[i] = (uint32_t)(a.sa[sl[i]] >> 40);
+  for (int64_t q = blockIdx.x * (int64_t)kBlock + threadIdx.x; q < np; q += (int64_t)gridDim.x * kBlock) {
+    const int b = (int)(q / kVoxChunk), i = (int)(q % kVoxChunk);
+    counts[q] = i < seg_count(a, b) ? (uint32_t)(a.tab[sl[q]].a >> 40) : 0u;
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void vox_bucket_kernel(VoxArgs a, const uint32_t* __restrict__ off,
@@ -348,7 +445,7 @@ __global__ __launch_bounds__(kBlock) void vox_bucket_kernel(VoxArgs a, const uin
     if (!point_cell(a, p, c, &m)) continue;
     const int64_t s = find_slot(a, pack_cell(c[0], c[1], c[2]));
     if (s < 0) continue;
-    const uint32_t lp = a.slotpos[s];
+    const uint32_t lp = a.tab[s].pos;
     bucket[off[lp] + atomicAdd(&cur[lp], 1u)] = (uint32_t)i;
   }
 }
@@ -361,16 +458,16 @@ __global__ __launch_bounds__(kBlock) void vox_centroid_kernel(VoxArgs a, const u
                                                               uint32_t* __restrict__ bucket,
                                                               float4* __restrict__ cent,
                                                               int32_t* __restrict__ offcell) {
-  const uint32_t ns = a.cnt[kVcSlots + a.par];
   int mn[3], dv[3];
   int64_t nvox;
   vox_bounds(a, mn, dv, &nvox);
+  const int64_t np = (int64_t)a.nblk * kVoxChunk;
   const uint32_t* sl = a.lists + (size_t)a.par * a.lcap;
   const uint32_t* tl = a.lists + (size_t)(2 + a.par) * a.lcap;
-  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < (int64_t)ns;
-       i += (int64_t)gridDim.x * kBlock) {
-    uint32_t* bk = bucket + off[i];
-    const int m = (int)counts[i];
+  for (int64_t q = blockIdx.x * (int64_t)kBlock + threadIdx.x; q < np; q += (int64_t)gridDim.x * kBlock) {
+    const int m = (int)counts[q];
+    if (m == 0) continue;
+    uint32_t* bk = bucket + off[q];
     const int gaps[8] = {701, 301, 132, 57, 23, 10, 4, 1};
     for (int gi = 0; gi < 8; ++gi) {
       const int gap = gaps[gi];
@@ -390,15 +487,15 @@ __global__ __launch_bounds__(kBlock) void vox_centroid_kernel(VoxArgs a, const u
     }
     const float fc = (float)m;
     const float c[3] = {__fdiv_rn(sx, fc), __fdiv_rn(sy, fc), __fdiv_rn(sz, fc)};
-    const uint32_t idx = tl[i];
-    cent[i] = make_float4(c[0], c[1], c[2], __uint_as_float(a.grid[idx] & 0x00ffffffu));
+    const uint32_t idx = tl[q];
+    cent[q] = make_float4(c[0], c[1], c[2], __uint_as_float(a.grid[idx] & 0x00ffffffu));
     int own[3];
-    unpack_cell(a.key[sl[i]], own[0], own[1], own[2]);
+    unpack_cell(a.tab[sl[q]].key, own[0], own[1], own[2]);
     int nb[3], sb[3];
     bool moved = false;
 #pragma unroll
     for (int ax = 0; ax < 3; ++ax) {
-      nb[ax] = (int)floorf(c[ax] * a.inv);          // getNeighborCentroidIndices
+      nb[ax] = (int)floorf(c[ax] * a.inv);             // getNeighborCentroidIndices
       sb[ax] = (int)floorf(__fdiv_rn(c[ax], a.leaf));  // c3_hlac.cpp:349-354
       moved = moved || nb[ax] != own[ax] || sb[ax] != own[ax];
     }
@@ -416,13 +513,13 @@ __global__ __launch_bounds__(kBlock) void vox_centroid_kernel(VoxArgs a, const u
 }
 
 __global__ __launch_bounds__(kBlock) void vox_downsampled_kernel(VoxArgs a, const float4* __restrict__ cent,
+                                                                 const uint32_t* __restrict__ counts,
                                                                  const int32_t* __restrict__ leaf,
                                                                  float4* __restrict__ out) {
-  const uint32_t ns = a.cnt[kVcSlots + a.par];
+  const int64_t np = (int64_t)a.nblk * kVoxChunk;
   const uint32_t* tl = a.lists + (size_t)(2 + a.par) * a.lcap;
-  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < (int64_t)ns;
-       i += (int64_t)gridDim.x * kBlock)
-    out[leaf[tl[i]]] = cent[i];
+  for (int64_t q = blockIdx.x * (int64_t)kBlock + threadIdx.x; q < np; q += (int64_t)gridDim.x * kBlock)
+    if (counts[q]) out[leaf[tl[q]]] = cent[q];
 }
 
 // ---- exclusive scans (leaf layout, bucket offsets) --------------------------------
@@ -517,38 +614,44 @@ int grid_for(int64_t n, int cap = 4096) {
 int64_t scan_blocks(int64_t n) { return (n + kScanBlock - 1) / kScanBlock; }
 int64_t leaf_layout_blocks(int64_t nvox) { return scan_blocks(nvox); }
 
-hipError_t launch_voxelize(const VoxArgs& a, int64_t list_hint, hipStream_t s) {
-  vox_reset_kernel<<<grid_for(list_hint, 1024), kBlock, 0, s>>>(a);
-  if (a.n > 0) vox_accum_kernel<<<(unsigned)((a.n + kVoxChunk - 1) / kVoxChunk), kBlock, 0, s>>>(a);
-  vox_scatter_kernel<<<grid_for(a.n / 8 + 1, 2048), kBlock, 0, s>>>(a);
+hipError_t launch_voxelize(const VoxArgs& a, hipStream_t s) {
+  // at least one accum block: it also clears the previous frame and resets the totals
+  vox_accum_kernel<<<(unsigned)std::max(a.nblk, 1), kBlock, 0, s>>>(a);
+  if (a.nblk > 0) vox_scatter_kernel<<<(unsigned)a.nblk, kBlock, 0, s>>>(a);
   return hipGetLastError();
 }
 
 hipError_t launch_vox_scatter(const VoxArgs& a, hipStream_t s) {
-  vox_scatter_kernel<<<grid_for(a.n / 8 + 1, 2048), kBlock, 0, s>>>(a);
+  if (a.nblk > 0) vox_scatter_kernel<<<(unsigned)a.nblk, kBlock, 0, s>>>(a);
   return hipGetLastError();
 }
 
-hipError_t launch_vox_centroids(const VoxArgs& a, int64_t ns, uint32_t* counts, uint32_t* offs, uint32_t* cur,
+int64_t vox_blocks(int64_t n) { return (n + kVoxChunk - 1) / kVoxChunk; }
+int64_t vox_positions(int64_t n) { return vox_blocks(n) * kVoxChunk; }
+int vox_part_words() { return kPartW; }
+
+hipError_t launch_vox_centroids(const VoxArgs& a, uint32_t* counts, uint32_t* offs, uint32_t* cur,
                                 uint32_t* block_sums, uint32_t* bucket, float4* cent, int32_t* offcell,
                                 hipStream_t s) {
-  if (ns <= 0) return hipSuccess;
-  vox_counts_kernel<<<grid_for(ns), kBlock, 0, s>>>(a, counts);
-  const int64_t nb = scan_blocks(ns);
-  scan_count_kernel<false><<<(unsigned)nb, kBlock, 0, s>>>(counts, ns, block_sums);
+  const int64_t np = (int64_t)a.nblk * kVoxChunk;
+  if (np <= 0) return hipSuccess;
+  vox_counts_kernel<<<grid_for(np), kBlock, 0, s>>>(a, counts);
+  const int64_t nb = scan_blocks(np);
+  scan_count_kernel<false><<<(unsigned)nb, kBlock, 0, s>>>(counts, np, block_sums);
   scan_sums_kernel<<<1, kBlock, 0, s>>>(block_sums, nb);
-  scan_write_kernel<false><<<(unsigned)nb, kBlock, 0, s>>>(counts, ns, block_sums, reinterpret_cast<int32_t*>(offs));
-  hipError_t e = hipMemsetAsync(cur, 0, (size_t)ns * 4, s);
+  scan_write_kernel<false><<<(unsigned)nb, kBlock, 0, s>>>(counts, np, block_sums, reinterpret_cast<int32_t*>(offs));
+  hipError_t e = hipMemsetAsync(cur, 0, (size_t)np * 4, s);
   if (e != hipSuccess) return e;
   vox_bucket_kernel<<<grid_for(a.n, 8192), kBlock, 0, s>>>(a, offs, cur, bucket);
-  vox_centroid_kernel<<<grid_for(ns), kBlock, 0, s>>>(a, offs, counts, bucket, cent, offcell);
+  vox_centroid_kernel<<<grid_for(np), kBlock, 0, s>>>(a, offs, counts, bucket, cent, offcell);
   return hipGetLastError();
 }
 
-hipError_t launch_vox_downsampled(const VoxArgs& a, int64_t ns, const float4* cent, const int32_t* leaf,
+hipError_t launch_vox_downsampled(const VoxArgs& a, const float4* cent, const uint32_t* counts, const int32_t* leaf,
                                   float* out, hipStream_t s) {
-  if (ns <= 0) return hipSuccess;
-  vox_downsampled_kernel<<<grid_for(ns), kBlock, 0, s>>>(a, cent, leaf, reinterpret_cast<float4*>(out));
+  const int64_t np = (int64_t)a.nblk * kVoxChunk;
+  if (np <= 0) return hipSuccess;
+  vox_downsampled_kernel<<<grid_for(np), kBlock, 0, s>>>(a, cent, counts, leaf, reinterpret_cast<float4*>(out));
   return hipGetLastError();
 }
 

@@ -33,11 +33,14 @@ def main():
             n_pts += frames[i % 4].shape[0]
         ms, cnt = ctx.kernel_times(reset=True)["voxelize"]
         ctx.timing(False)
+        ctx.voxelize(frames[0], 0.01)
+        w = ctx.grid()
+        check = int((w.astype(np.uint64) * (np.arange(w.size, dtype=np.uint64) | np.uint64(1))).sum() & np.uint64(2**63 - 1))
         per = ms / reps
         occ = int(gi.n_occ)
         alg = 16 * 1_000_000 + 4 * 256 ** 3  # 16 B/point read + 4 B/voxel grid
         out = {"frames": reps, "us_per_frame": per * 1e3, "mpoints_per_s": n_pts / (ms / 1e3) / 1e6,
-               "occupied_voxels": occ, "algorithmic_bytes": alg,
+               "occupied_voxels": occ, "grid_checksum": check, "algorithmic_bytes": alg,
                "algorithmic_GBps": alg / (per / 1e3) / 1e9, "frac_of_8TBps": alg / (per / 1e3) / 8e12}
     print(json.dumps(out))
 
