@@ -43,6 +43,7 @@
 #include "c3h_internal.h"
 
 #include "c3hlac_dev.h"
+#include "c3hlac_mfma.h"
 
 namespace c3h {
 namespace {
@@ -154,6 +155,12 @@ __global__ __launch_bounds__(kBlock) void c3_occupancy_kernel(OccArgs oa) {
       if (fresh[j]) work[base + __popcll(m & ((1ull << lane) - 1))] = ts[j];
     }
   }
+}
+
+// dense frames: one tile per wave on the i8 matrix cores (c3hlac_mfma.h)
+__global__ __launch_bounds__(kBlock, 2) void c3hlac_mfma_kernel(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t mf_smem[];
+  c3hlac_mfma_body(a, blockIdx.x * kMfWaves + (threadIdx.x >> 6), gridDim.x * kMfWaves, blockIdx.y, mf_smem);
 }
 
 // multi-tile subdivisions: 64-bit exact partial sums -> features
@@ -417,6 +424,8 @@ C3Args build_c3_args(const C3Launch& l) {
   a.debug = l.debug;
   a.prof = l.prof;
   a.wave117 = wave117_ok(l) ? 1 : 0;
+  a.mf_ty = l.lmax[1] + 2;
+  a.mfma = 0;  // set by launch_c3hlac (the stand-alone path), never in the tick
   if (a.wave117) a.tw_max = w117_halo_words(l.lmax[0], l.lmax[1], l.lmax[2]);
   c.tile_lds = a.wave117 ? w117_lds_bytes(a.tw_max, a.list_max) : c3hlac_lds_bytes(a.tw_max, a.list_max);
   c.tgrid = (int)c3hlac_grid(l);
@@ -424,9 +433,36 @@ C3Args build_c3_args(const C3Launch& l) {
   return c;
 }
 
+// dense-tile MFMA kernel: tiles up to 16 x 16 per layer, resident persistent grid
+static bool mfma_ok(const C3Launch& l) { return l.lmax[0] <= 16 && l.lmax[1] <= 16 && l.debug == 0; }
+
+static int64_t mfma_grid(const C3Launch& l, size_t lds) {
+  static thread_local size_t c_lds = 0;
+  static thread_local int c_per_cu = 0, c_ncu = 0, c_dev = -1;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (lds != c_lds || dev != c_dev) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c3hlac_mfma_kernel, kBlock, lds) != hipSuccess ||
+        per_cu < 1)
+      per_cu = 1;
+    int n_cu = 256;
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    c_lds = lds;
+    c_per_cu = per_cu;
+    c_ncu = n_cu;
+    c_dev = dev;
+  }
+  const int64_t tiles_per_block = kMfWaves;
+  return std::max<int64_t>(1, std::min<int64_t>((l.ntiles + tiles_per_block - 1) / tiles_per_block,
+                                                 (int64_t)c_ncu * c_per_cu));
+}
+
 hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
   if (l.nframes < 1 || l.nframes > kMaxBatch) return hipErrorInvalidValue;
-  const C3Args c = build_c3_args(l);
+  C3Args c = build_c3_args(l);
+  const bool mf = mfma_ok(l);
+  c.ka.mfma = mf ? 1 : 0;
   const dim3 g1d((unsigned)c.g1, (unsigned)l.nframes);
   if (c.bits) {
     if (c.ax)
@@ -442,6 +478,10 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
   else
     c3_occupancy_kernel<false, false><<<g1d, kBlock, 0, s>>>(c.oa);
   c3hlac_tile_kernel<<<dim3((unsigned)c.tgrid, (unsigned)l.nframes), kBlock, c.tile_lds, s>>>(c.ka);
+  if (mf) {  // both kernels read the frame's work count; each takes the frames of its kind
+    const size_t lds = mf_lds_bytes(c.ka.mf_ty);
+    c3hlac_mfma_kernel<<<dim3((unsigned)mfma_grid(l, lds), (unsigned)l.nframes), kBlock, lds, s>>>(c.ka);
+  }
   return hipGetLastError();
 }
 

@@ -426,6 +426,9 @@ struct KArgs {
                           // (direct mode, every subdivision one tile: h == tile), else 0
   long long* prof;  // diagnostics only (C3H_PROF): per-block phase timestamps [grid][8]
   int wave117;      // C3-HLAC-117 per-wave tiles (c3hlac_wave117_body), else the block body
+  int mfma;         // the dense-tile MFMA kernel runs beside (c3hlac_mfma.h): frames with
+                    // >= half of their tiles non-empty are left to it
+  int mf_ty;        // its largest tile row count (ly + 2)
   int debug;  // diagnostics only (C3H_C3_DEBUG): 1 stop after the loads, 2 after compaction,
              // 3 skip the tile kernel
 };
@@ -506,6 +509,7 @@ __device__ __forceinline__ void c3hlac_tile_body(const KArgs& a, int bx, int fy_
   lds_barrier();
   C3H_PROF(1, true);
 
+  if (a.mfma && 2 * nwork >= a.ntiles) return;  // dense frame: c3hlac_mfma_body takes it
   for (; wi < (a.debug == 4 ? 0 : nwork); wi += G) {
     const int tile = tile_next;
     if (wi + G < nwork) tile_next = fwork[wi + G];
