@@ -189,6 +189,11 @@ __global__ __launch_bounds__(kBlock) void compress_gate_kernel(CompressRows cr, 
   else compress_rows_body(cr, blockIdx.x - ngate, gridDim.x - ngate, blockIdx.y, cg_smem);
 }
 
+__global__ __launch_bounds__(kBlock) void compress_mfma_kernel(CompressRows cr) {
+  extern __shared__ __attribute__((aligned(16))) float cm_smem[];
+  compress_mfma_body(cr, blockIdx.x, gridDim.x, blockIdx.y, cm_smem);
+}
+
 __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch b) {
   extern __shared__ __attribute__((aligned(16))) float sl_smem[];
   score_list_body(b, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y, sl_smem);
@@ -300,6 +305,10 @@ __global__ __launch_bounds__(64) void replay_kernel(const double* __restrict__ s
 
 }  // namespace
 
+// subdivision counts from which the stand-alone search compresses on the matrix cores
+// (512^3 at S = 10: 140,608; the bench's 256^3 frames, 17,576, keep the fused VALU launch)
+constexpr int64_t kCompressMfmaRows = 65536;
+
 bool compress_rows_ok(int F, int Dpad) {
   (void)F;
   return Dpad <= 128;
@@ -375,10 +384,16 @@ hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc,
   if (sc) {  // compress (non-empty rows) and gate in one launch
     const CompressRows cr{sc->feat, sc->PT, sc->fmax, sc->G, sc->rows, sc->nrows, sc->F, sc->D, sc->Dpad,
                           sc->fmax_len, sc->s_feat, sc->s_G, sc->s_rows, sc->s_nrows};
-    const size_t lds = compress_rows_lds_bytes(sc->Dpad);
-    // compress workgroups: surface frames have ~700 non-empty rows (~44 row blocks)
-    const unsigned ncomp = (unsigned)std::min<int64_t>((sc->H + kRR - 1) / kRR, kCompressGridCap);
-    compress_gate_kernel<<<dim3(ngate + ncomp, nf), kBlock, lds, s>>>(cr, a, (int)ngate);
+    if (sc->H >= kCompressMfmaRows) {  // large grids: the f32 matrix-core compress, then the gate
+      const unsigned ncomp = (unsigned)std::min<int64_t>((sc->H + kMR - 1) / kMR, 2048);
+      compress_mfma_kernel<<<dim3(ncomp, nf), kBlock, compress_mfma_lds_bytes(), s>>>(cr);
+      gate_kernel<<<dim3(ngate, nf), kBlock, 0, s>>>(a);
+    } else {
+      const size_t lds = compress_rows_lds_bytes(sc->Dpad);
+      // compress workgroups: surface frames have ~700 non-empty rows (~44 row blocks)
+      const unsigned ncomp = (unsigned)std::min<int64_t>((sc->H + kRR - 1) / kRR, kCompressGridCap);
+      compress_gate_kernel<<<dim3(ngate + ncomp, nf), kBlock, lds, s>>>(cr, a, (int)ngate);
+    }
   } else {
     gate_kernel<<<dim3(ngate, nf), kBlock, 0, s>>>(a);
   }

@@ -134,6 +134,111 @@ __device__ __forceinline__ void compress_rows_body(const CompressRows& cr, int b
   }
 }
 
+// Dense frames (tens of thousands of listed rows): the same G = f' * P on the f32 matrix
+// cores.  v_mfma_f32_32x32x2_f32 is bit-for-bit a k-ordered fmaf chain
+// (D = fma(a_k1, b_k1, fma(a_k0, b_k0, C))), so feeding j in ascending order gives the
+// VALU body's G exactly (one extra fma with a = 0 pads an odd F).  128 listed rows per
+// workgroup (wave = 32 rows x 4 column tiles of 32 = Dpad <= 128); per 32-feature chunk
+// the rows' feature slice and P's slice are staged in LDS (prefetched one chunk ahead in
+// registers), then 16 k-pair steps of 4 MFMAs (one A float, four B floats per lane).
+constexpr int kMR = 128, kMK = 32;
+constexpr int kMAS = kMK + 1;  // A slice row stride (lanes read 32 rows of one column)
+__host__ __device__ inline size_t compress_mfma_lds_bytes() {
+  return sizeof(float) * ((size_t)kMR * kMAS + (size_t)kMK * 128);
+}
+typedef float mf_f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ void compress_mfma_body(const CompressRows& cr, int bid, int nblk, int64_t f,
+                                                   float* csm) {
+  const float* __restrict__ feat = cr.feat + f * cr.s_feat;
+  const float* __restrict__ fmax = cr.fmax;
+  float* __restrict__ G = cr.G + f * cr.s_G;
+  const int32_t* __restrict__ rows = cr.rows + f * cr.s_rows;
+  const int F = cr.F, D = cr.D, Dpad = cr.Dpad, fmax_len = cr.fmax_len;
+  float* sa = csm;                 // kMR x kMAS feature slice
+  float* sbm = csm + kMR * kMAS;   // kMK x 128 slice of P (columns >= Dpad zero)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = (int)cr.nrows[f * cr.s_nrows];
+  const int nch = (F + kMK - 1) / kMK;
+  constexpr int kFE = kMR * kMK / kBlock;   // feature-slice elements per thread (16)
+  constexpr int kPE = kMK * 128 / kBlock;   // P-slice elements per thread (16)
+  for (int r0 = bid * kMR; r0 < n; r0 += nblk * kMR) {
+    int64_t rbase[kFE / 4];  // 4 consecutive features per thread share a row
+#pragma unroll
+    for (int i = 0; i < kFE / 4; ++i) {
+      const int e = 4 * (tid + i * kBlock), r = e / kMK;
+      rbase[i] = r0 + r < n ? (int64_t)rows[r0 + r] * F : -1;
+    }
+    float fa[kFE], pb[kPE];
+    auto load = [&](int c) {
+#pragma unroll
+      for (int i = 0; i < kFE / 4; ++i) {
+        const int e = 4 * (tid + i * kBlock), jb = c * kMK + (e % kMK);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int j = jb + u;
+          float v = 0.0f;
+          if (rbase[i] >= 0 && j < F) {
+            v = feat[rbase[i] + j];
+            if (j < fmax_len) {  // setData max-normalisation (search.cpp:563-570)
+              const float mx = fmax[j];
+              if (mx == 0.0f) v = 0.0f;
+              else if (v == mx) v = 1.0f;
+              else v = __fdiv_rn(v, mx);
+            }
+          }
+          fa[4 * i + u] = v;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < kPE; ++i) {
+        const int e = tid + i * kBlock, j = c * kMK + e / 128, col = e % 128;
+        pb[i] = (j < F && col < Dpad) ? cr.PT[(int64_t)j * Dpad + col] : 0.0f;
+      }
+    };
+    load(0);
+    mf_f32x16 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[t][q] = 0.0f;
+    for (int c = 0; c < nch; ++c) {
+      lds_barrier();
+#pragma unroll
+      for (int i = 0; i < kFE / 4; ++i) {
+        const int e = 4 * (tid + i * kBlock), r = e / kMK, j = e % kMK;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sa[r * kMAS + j + u] = fa[4 * i + u];
+      }
+#pragma unroll
+      for (int i = 0; i < kPE; ++i) sbm[tid + i * kBlock] = pb[i];
+      if (c + 1 < nch) load(c + 1);
+      lds_barrier();
+      const int kn = min(kMK, F - c * kMK);
+      const float* arow = sa + (wave * 32 + (lane & 31)) * kMAS + (lane >> 5);
+      const float* bcol = sbm + (lane >> 5) * 128 + (lane & 31);
+      for (int k = 0; k < kn; k += 2) {
+        const float av = arow[k];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bcol[k * 128 + 32 * t], acc[t], 0, 0, 0);
+      }
+    }
+    // C/D map: column lane & 31 (+ 32 t), row (q & 3) + 8 (q >> 2) + 4 (lane >> 5)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int rr = r0 + wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
+      if (rr >= n) continue;
+      const int64_t hh = rows[rr];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int col = 32 * t + (lane & 31);
+        if (col < D) G[hh * D + col] = acc[t][q];
+      }
+    }
+  }
+}
+
 // Fast path (D <= 256, D % 4 == 0, M*r <= 256) = the sparse search below: 32 list
 // entries per workgroup.  Box features are summed with float4 loads and staged k-major in
 // LDS (lanes = positions: conflict-free); the projection onto all M*r basis rows is a
