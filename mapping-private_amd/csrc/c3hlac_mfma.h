@@ -34,34 +34,16 @@ constexpr int kMfWaves = kBlock / 64;
 constexpr int kMfRowB = 32;  // bytes per plane row
 constexpr int kMfCh = 12;
 constexpr int kMfK = 14;     // 13 offsets + the centre's own channels
-constexpr int kMfLoad = 2;   // (row, dword) pairs per lane of a layer (<= 18 rows x 5 dwords)
+constexpr int kMfRaw = 384;  // dwords of one raw layer slot (<= 18 x 18 words, 6 DMA rounds)
+constexpr int kMfRawSlots = 4;
 
 __host__ __device__ inline int mf_slot_bytes(int ty) { return kMfCh * ty * kMfRowB; }
 __host__ __device__ inline int mf_wave_bytes(int ty) {
-  const int ring = 3 * mf_slot_bytes(ty), epi = (kMfK * 256 + 984) * 4;
-  return ((ring > epi ? ring : epi) + 15) & ~15;
+  const int work = kMfRawSlots * kMfRaw * 4 + 3 * mf_slot_bytes(ty), epi = (kMfK * 256 + 984) * 4;
+  return ((work > epi ? work : epi) + 15) & ~15;
 }
-__host__ __device__ inline size_t mf_lds_bytes(int ty) { return 1024 + (size_t)kMfWaves * mf_wave_bytes(ty); }
-
-// 12 channel bytes (offset by -128) of 4 voxels, packed one dword per channel
-__device__ __forceinline__ void mf_channels(const uint32_t w[4], const uint32_t* s_lut, const KArgs& a,
-                                            uint32_t ch[kMfCh]) {
-#pragma unroll
-  for (int c = 0; c < kMfCh; ++c) ch[c] = 0x80808080u;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (!w[j]) continue;
-    const uint32_t r = (w[j] >> 16) & 0xffu, g = (w[j] >> 8) & 0xffu, b = w[j] & 0xffu;
-    const uint32_t lr = s_lut[r], lg = s_lut[g], lb = s_lut[b];
-    const uint32_t sh = 8 * j, clr = ~(0xffu << sh);
-    const uint32_t v[12] = {lr & 0xffu, (lr >> 8) & 0xffu, lg & 0xffu, (lg >> 8) & 0xffu, lb & 0xffu,
-                            (lb >> 8) & 0xffu, (int)r > a.thr_r ? 1u : 0u, (int)r > a.thr_r ? 0u : 1u,
-                            (int)g > a.thr_g ? 1u : 0u, (int)g > a.thr_g ? 0u : 1u,
-                            (int)b > a.thr_b ? 1u : 0u, (int)b > a.thr_b ? 0u : 1u};
-#pragma unroll
-    for (int c = 0; c < kMfCh; ++c) ch[c] = (ch[c] & clr) | ((v[c] ^ 0x80u) << sh);
-  }
-}
+// 3 x 256 channel-byte tables | per-wave regions
+__host__ __device__ inline size_t mf_lds_bytes(int ty) { return 3072 + (size_t)kMfWaves * mf_wave_bytes(ty); }
 
 // 16 bytes starting at byte s (0..2) of a 32-byte plane row held as two uint4
 __device__ __forceinline__ mf_v4i mf_frag(const uint4& lo, const uint4& hi, int s) {
@@ -75,15 +57,31 @@ __device__ __forceinline__ mf_v4i mf_frag(const uint4& lo, const uint4& hi, int 
 }
 
 __device__ __forceinline__ void wave_lds_sync() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// wait until at most n of this wave's vector-memory operations (LDS DMA) are outstanding
+__device__ __forceinline__ void wait_vm(int n) {
+  switch (n) {
+    case 0: __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: __asm__ volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: __asm__ volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: __asm__ volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: __asm__ volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: __asm__ volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    default: __asm__ volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+  }
+}
 
-// corrected exact sum of tile T at (c, n)
+// channel plane of (type t: 0 colour LUT / 1 binary, reference channel c in 0..5): the
+// planes hold per colour col the bytes {sin, cos, beta, 1 - beta} (4 col + s)
+__device__ __forceinline__ int mf_plane(int t, int c) { return 4 * (c >> 1) + 2 * t + (c & 1); }
+
+// corrected exact sum of tile T at (plane c, plane n)
 __device__ __forceinline__ uint32_t mf_corr(const int32_t* T, int c, int n) {
   const long long v = (long long)T[c * 16 + n] + 128ll * ((long long)T[c * 16 + 15] + T[15 * 16 + n]) +
                       16384ll * T[15 * 16 + 15];
   return (uint32_t)v;
 }
 
-// wave wid of nw (all frames' waves of this launch for frame fy); smem = mf_lds_bytes(TYmax)
+// wave wid of nw (all waves of this launch for frame fy); smem = mf_lds_bytes(TYmax)
 __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw, int fy_, uint32_t* smem) {
   const int64_t fy = fy_;
   const uint32_t* __restrict__ fgrid = a.grids[fy];
@@ -94,15 +92,24 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
   const int32_t* __restrict__ fwork = a.work + fy * a.s_work;
   int32_t* frows = a.rows ? a.rows + fy * a.s_h : nullptr;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t* s_lut = smem;
-  for (int i = threadIdx.x; i < 256; i += kBlock) s_lut[i] = a.lut[i];
+  // channel-byte tables: T_col[v] = {sin, cos, beta, 1 - beta} ^ 0x80 (setColor LUT, thresholds)
+  uint32_t* s_tab = smem;
+  for (int i = threadIdx.x; i < 768; i += kBlock) {
+    const int col = i >> 8, v = i & 255;
+    const uint32_t l = a.lut[v];
+    const int thr = col == 0 ? a.thr_r : (col == 1 ? a.thr_g : a.thr_b);
+    const uint32_t be = v > thr ? 1u : 0u;
+    s_tab[i] = ((l & 0xffu) | (l & 0xff00u) | (be << 16) | ((be ^ 1u) << 24)) ^ 0x80808080u;
+  }
   __syncthreads();
   const int nwork = (int)ftf[2 + (a.epoch & 1)];
   if (2 * nwork < a.ntiles) return;  // sparse frame: the dot4 tile body takes it
-  const int tymax = a.mf_ty;
-  uint8_t* wl = reinterpret_cast<uint8_t*>(smem + 256) + (size_t)wave * mf_wave_bytes(tymax);
+  uint8_t* wl = reinterpret_cast<uint8_t*>(smem + 768) + (size_t)wave * mf_wave_bytes(a.mf_ty);
+  uint32_t* raw = reinterpret_cast<uint32_t*>(wl);                       // kMfRawSlots x kMfRaw
+  uint8_t* planes = wl + kMfRawSlots * kMfRaw * 4;                       // 3 layer slots
   const int F = a.variant;
   const int h4 = lane >> 4, n = lane & 15;
+  const bool real = n < kMfCh;
   const mf_v4i kConst = n == 15 ? mf_v4i{0x01010101, 0x01010101, 0x01010101, 0x01010101} : mf_v4i{0, 0, 0, 0};
 
   for (int wi = wid; wi < nwork; wi += nw) {
@@ -113,36 +120,55 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
     const int32_t* sz = a.segs + 3 * (2 * a.seg_stride + iz);
     const int x0 = sx[0], lx = sx[1], y0 = sy[0], ly = sy[1], z0 = sz[0], lz = sz[1];
     const int64_t h = sx[2] + (int64_t)sy[2] * a.sbx + (int64_t)sz[2] * a.sbx * a.sby;
-    const int TY = ly + 2, nks = (ly + 3) >> 2, npair = TY * 5;
+    const int TY = ly + 2, TX = lx + 2, nks = (ly + 3) >> 2;
+    const int nraw = TY * TX, ndma = (nraw + 63) >> 6;
     const int sb = mf_slot_bytes(TY);
-    // layer loads: (row, dword q) pairs e = lane + 64 i; x = x0 - 1 + 4 q + j
-    uint32_t wv[kMfLoad][4];
-    auto load_layer = [&](int L) {
+    // layer L (z = z0 - 1 + L) -> raw slot L % 4 by LDS DMA: element e = row * TX + xo
+    // (off-grid elements read word 0 and are masked at conversion)
+    auto dma = [&](int L) {
       const int gz = z0 - 1 + L;
-#pragma unroll
-      for (int i = 0; i < kMfLoad; ++i) {
-        const int e = lane + 64 * i, row = e / 5, q = e - row * 5;
-        const int gy = y0 - 1 + row;
-        const bool rowin = e < npair && (unsigned)gy < (unsigned)a.gy && (unsigned)gz < (unsigned)a.gz;
-        const uint32_t* src = fgrid + ((int64_t)gz * a.gy + gy) * a.gx;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int gxx = x0 - 1 + 4 * q + j;
-          wv[i][j] = rowin && (unsigned)gxx < (unsigned)a.gx ? src[gxx] : 0u;
-        }
+      uint32_t* dst = raw + (L % kMfRawSlots) * kMfRaw;
+      for (int i = 0; i < ndma; ++i) {
+        const int e = 64 * i + lane, row = e / TX, xo = e - row * TX;
+        const int gy = y0 - 1 + row, gxx = x0 - 1 + xo;
+        const bool in = e < nraw && (unsigned)gz < (unsigned)a.gz && (unsigned)gy < (unsigned)a.gy &&
+                        (unsigned)gxx < (unsigned)a.gx;
+        const uint32_t* src = in ? fgrid + ((int64_t)gz * a.gy + gy) * a.gx + gxx : fgrid;
+        __builtin_amdgcn_global_load_lds(src, dst + 64 * i, 4, 0, 0);
       }
     };
-    auto store_layer = [&](int L) {
-      uint8_t* slot = wl + (size_t)(L % 3) * sb;
+    // raw layer -> 12 channel planes: (row, dword q) pairs, 4 voxels x = -1 + 4 q + j each;
+    // table reads give 4 channel bytes per voxel and colour, a 4 x 4 byte transpose packs
+    // them per channel
+    auto convert = [&](int L) {
+      const int gz = z0 - 1 + L;
+      const uint32_t* src = raw + (L % kMfRawSlots) * kMfRaw;
+      uint8_t* slot = planes + (size_t)(L % 3) * sb;
+      for (int e = lane; e < TY * 5; e += 64) {
+        const int row = e / 5, q = e - row * 5;
+        const int gy = y0 - 1 + row;
+        const bool rin = (unsigned)gz < (unsigned)a.gz && (unsigned)gy < (unsigned)a.gy;
+        uint32_t t[3][4];
 #pragma unroll
-      for (int i = 0; i < kMfLoad; ++i) {
-        const int e = lane + 64 * i, row = e / 5, q = e - row * 5;
-        if (e >= npair) continue;
-        uint32_t ch[kMfCh];
-        mf_channels(wv[i], s_lut, a, ch);
+        for (int j = 0; j < 4; ++j) {
+          const int xo = 4 * q + j, gxx = x0 - 1 + xo;
+          const uint32_t w = (rin && xo < TX && (unsigned)gxx < (unsigned)a.gx) ? src[row * TX + xo] : 0u;
 #pragma unroll
-        for (int c = 0; c < kMfCh; ++c)
-          *reinterpret_cast<uint32_t*>(slot + ((size_t)c * TY + row) * kMfRowB + 4 * q) = ch[c];
+          for (int col = 0; col < 3; ++col)
+            t[col][j] = w ? s_tab[col * 256 + ((w >> (16 - 8 * col)) & 0xffu)] : 0x80808080u;
+        }
+#pragma unroll
+        for (int col = 0; col < 3; ++col) {
+          const uint32_t u0 = __builtin_amdgcn_perm(t[col][1], t[col][0], 0x05010400u);
+          const uint32_t u1 = __builtin_amdgcn_perm(t[col][1], t[col][0], 0x07030602u);
+          const uint32_t u2 = __builtin_amdgcn_perm(t[col][3], t[col][2], 0x05010400u);
+          const uint32_t u3 = __builtin_amdgcn_perm(t[col][3], t[col][2], 0x07030602u);
+          const uint32_t o[4] = {__builtin_amdgcn_perm(u2, u0, 0x05040100u), __builtin_amdgcn_perm(u2, u0, 0x07060302u),
+                                 __builtin_amdgcn_perm(u3, u1, 0x05040100u), __builtin_amdgcn_perm(u3, u1, 0x07060302u)};
+#pragma unroll
+          for (int s2 = 0; s2 < 4; ++s2)
+            *reinterpret_cast<uint32_t*>(slot + ((size_t)(4 * col + s2) * TY + row) * kMfRowB + 4 * q) = o[s2];
+        }
       }
     };
     // centre mask of A: bytes j >= lx are no centre (a = 0 -> 0x80)
@@ -157,26 +183,22 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
     mf_v4i acc[kMfK];
 #pragma unroll
     for (int k = 0; k < kMfK; ++k) acc[k] = mf_v4i{0, 0, 0, 0};
-    load_layer(0);
-    store_layer(0);
-    load_layer(1);
-    store_layer(1);
+    // prologue: layers 0..3 in flight, 0 and 1 converted
+    wait_vm(0);
+    for (int L = 0; L <= min(3, lz); ++L) dma(L);
+    wait_vm(0);
+    convert(0);
+    convert(1);
     for (int z = 0; z < lz; ++z) {
-      // layers z (dz = -1) and z + 1 (dz = 0) are in LDS; layer z + 2 loads meanwhile
-      const bool more = z + 2 <= lz;
-      if (more) load_layer(z + 2);
       wave_lds_sync();
-      const uint8_t* sp = wl + (size_t)(z % 3) * sb;        // dz = -1
-      const uint8_t* sc = wl + (size_t)((z + 1) % 3) * sb;  // dz = 0
+      const uint8_t* sp = planes + (size_t)(z % 3) * sb;        // dz = -1
+      const uint8_t* sc = planes + (size_t)((z + 1) % 3) * sb;  // dz = 0
+      const uint8_t* pc = sc + (size_t)(real ? n : 0) * TY * kMfRowB;
+      const uint8_t* pp = sp + (size_t)(real ? n : 0) * TY * kMfRowB;
       for (int ks = 0; ks < nks; ++ks) {
         const int y = 4 * ks + h4;
         const bool ymask = y < ly;
         const int rm = min(y, TY - 1), rc = min(y + 1, TY - 1), rp = min(y + 2, TY - 1);
-        // rows of the 5 (dz, dy) offsets; padding lanes (n >= 12) read plane 0 and take
-        // the constant fragment instead (no divergence around the MFMAs)
-        const bool real = n < kMfCh;
-        const uint8_t* pc = sc + (size_t)(real ? n : 0) * TY * kMfRowB;
-        const uint8_t* pp = sp + (size_t)(real ? n : 0) * TY * kMfRowB;
         auto row = [&](const uint8_t* plane, int r, uint4& lo, uint4& hi) {
           lo = *reinterpret_cast<const uint4*>(plane + r * kMfRowB);
           hi = *reinterpret_cast<const uint4*>(plane + r * kMfRowB + 16);
@@ -205,7 +227,12 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
                 __builtin_amdgcn_mfma_i32_16x16x64_i8(A, sel(mf_frag(lo, hi, dxi)), acc[3 * dxi + dyi], 0, 0, 0);
         }
       }
-      if (more) store_layer(z + 2);  // the slot of layer z - 1, no longer read
+      // layer z + 2 into the plane slot of layer z - 1; its DMA was issued two layers ago
+      if (z + 2 <= lz) {
+        wait_vm(z + 3 <= lz ? ndma : 0);
+        convert(z + 2);
+        if (z + 4 <= lz) dma(z + 4);
+      }
     }
     wave_lds_sync();
     // epilogue: accumulator tiles -> LDS (C/D map: row 4 (lane >> 4) + r, column lane & 15)
@@ -224,23 +251,23 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
       if (e < 936) {  // first order: k, type (colour / binary), c, n
         const int k = e / 72, rem = e - 72 * k, ty = rem / 36, c = (rem % 36) / 6, nn = rem % 6;
         bin = 495 * ty + bin981(k, c, nn);
-        v = mf_corr(T + k * 256, 6 * ty + c, 6 * ty + nn);
+        v = mf_corr(T + k * 256, mf_plane(ty, c), mf_plane(ty, nn));
       } else if (e < 957) {  // centre auto products (c <= n)
         const int q = e - 936;
         int c = 0;
         while (q >= tri6(c + 1, c + 1)) ++c;
         const int nn = c + (q - tri6(c, c));
         bin = 474 + q;
-        v = mf_corr(T13, c, nn);
+        v = mf_corr(T13, mf_plane(0, c), mf_plane(0, nn));
       } else if (e < 969) {  // centre bin-pair counts
         const int q = e - 957;
         const int c = q < 8 ? q / 4 : 2 + (q - 8) / 2, nn = q < 8 ? 2 + q % 4 : 4 + (q - 8) % 2;
         bin = 969 + q;
-        v = mf_corr(T13, 6 + c, 6 + nn);
+        v = mf_corr(T13, mf_plane(1, c), mf_plane(1, nn));
       } else {  // zero order: colour channels, then binary counts
         const int q = e - 969;
         bin = q < 6 ? q : 495 + (q - 6);
-        v = (uint32_t)((long long)T13[(q < 6 ? q : 6 + (q - 6)) * 16 + 15] + 128ll * K);
+        v = (uint32_t)((long long)T13[mf_plane(q < 6 ? 0 : 1, q < 6 ? q : q - 6) * 16 + 15] + 128ll * K);
       }
       hist[bin] = v;
     }
@@ -262,6 +289,7 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
     if (frows && lane == 0) frows[wi] = (int32_t)h;
     wave_lds_sync();  // the tile's LDS is rebuilt by the next tile
   }
+  wait_vm(0);  // no LDS DMA outlives the wave
 }
 
 }  // namespace c3h
