@@ -34,16 +34,21 @@ constexpr int kMfWaves = kBlock / 64;
 constexpr int kMfRowB = 32;  // bytes per plane row
 constexpr int kMfCh = 12;
 constexpr int kMfK = 14;     // 13 offsets + the centre's own channels
-constexpr int kMfRaw = 384;  // dwords of one raw layer slot (<= 18 x 18 words, 6 DMA rounds)
-constexpr int kMfRawSlots = 4;
+constexpr int kMfLoad = 2;  // (row, dword) pairs per lane of a layer (<= 18 rows x 5 dwords)
+constexpr int kMfTyMax = 18;
+#ifndef C3H_MF_EXP
+#define C3H_MF_EXP 0  // diagnostics variants: 1 no K steps, 2 no conversion
+#endif
 
 __host__ __device__ inline int mf_slot_bytes(int ty) { return kMfCh * ty * kMfRowB; }
+// per wave: 3 plane slots + 4 constant planes (rows 12..15 of A / columns 12..15 of B:
+// zeros, and ones in 15), or the epilogue's accumulator tiles + histogram
 __host__ __device__ inline int mf_wave_bytes(int ty) {
-  const int work = kMfRawSlots * kMfRaw * 4 + 3 * mf_slot_bytes(ty), epi = (kMfK * 256 + 984) * 4;
+  const int work = 3 * mf_slot_bytes(ty) + 4 * kMfTyMax * kMfRowB, epi = (kMfK * 256 + 984) * 4;
   return ((work > epi ? work : epi) + 15) & ~15;
 }
-// 3 x 256 channel-byte tables | per-wave regions
-__host__ __device__ inline size_t mf_lds_bytes(int ty) { return 3072 + (size_t)kMfWaves * mf_wave_bytes(ty); }
+// 3 x 256 channel-byte tables | 984 epilogue bin codes | per-wave regions
+__host__ __device__ inline size_t mf_lds_bytes(int ty) { return 3072 + 3936 + (size_t)kMfWaves * mf_wave_bytes(ty); }
 
 // 16 bytes starting at byte s (0..2) of a 32-byte plane row held as two uint4
 __device__ __forceinline__ mf_v4i mf_frag(const uint4& lo, const uint4& hi, int s) {
@@ -57,28 +62,42 @@ __device__ __forceinline__ mf_v4i mf_frag(const uint4& lo, const uint4& hi, int 
 }
 
 __device__ __forceinline__ void wave_lds_sync() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-// wait until at most n of this wave's vector-memory operations (LDS DMA) are outstanding
-__device__ __forceinline__ void wait_vm(int n) {
-  switch (n) {
-    case 0: __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: __asm__ volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: __asm__ volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: __asm__ volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: __asm__ volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: __asm__ volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    default: __asm__ volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-  }
-}
 
 // channel plane of (type t: 0 colour LUT / 1 binary, reference channel c in 0..5): the
 // planes hold per colour col the bytes {sin, cos, beta, 1 - beta} (4 col + s)
-__device__ __forceinline__ int mf_plane(int t, int c) { return 4 * (c >> 1) + 2 * t + (c & 1); }
+__host__ __device__ inline int mf_plane(int t, int c) { return 4 * (c >> 1) + 2 * t + (c & 1); }
 
-// corrected exact sum of tile T at (plane c, plane n)
-__device__ __forceinline__ uint32_t mf_corr(const int32_t* T, int c, int n) {
-  const long long v = (long long)T[c * 16 + n] + 128ll * ((long long)T[c * 16 + 15] + T[15 * 16 + n]) +
-                      16384ll * T[15 * 16 + 15];
-  return (uint32_t)v;
+// epilogue code of bin e (0..980): bin | kind << 10 | k << 12 | c << 16 | n << 20, kind 0 =
+// product bin (offset k's tile at plane c, plane n), 1 = zero order (plane c's row sum)
+__device__ inline uint32_t mf_bin_code(int e) {
+  int bin, kind = 0, k = 13, c, nn;
+  if (e < 936) {  // first order: k, type (colour / binary), c, n
+    k = e / 72;
+    const int rem = e - 72 * k, ty = rem / 36, cc = (rem % 36) / 6, n6 = rem % 6;
+    bin = 495 * ty + bin981(k, cc, n6);
+    c = mf_plane(ty, cc);
+    nn = mf_plane(ty, n6);
+  } else if (e < 957) {  // centre auto products (c <= n)
+    const int q = e - 936;
+    int cc = 0;
+    while (q >= tri6(cc + 1, cc + 1)) ++cc;
+    bin = 474 + q;
+    c = mf_plane(0, cc);
+    nn = mf_plane(0, cc + (q - tri6(cc, cc)));
+  } else if (e < 969) {  // centre bin-pair counts
+    const int q = e - 957;
+    const int cc = q < 8 ? q / 4 : 2 + (q - 8) / 2, n6 = q < 8 ? 2 + q % 4 : 4 + (q - 8) % 2;
+    bin = 969 + q;
+    c = mf_plane(1, cc);
+    nn = mf_plane(1, n6);
+  } else {  // zero order: colour channels, then binary counts
+    const int q = e - 969;
+    bin = q < 6 ? q : 495 + (q - 6);
+    kind = 1;
+    c = mf_plane(q < 6 ? 0 : 1, q < 6 ? q : q - 6);
+    nn = 15;
+  }
+  return (uint32_t)bin | ((uint32_t)kind << 10) | ((uint32_t)k << 12) | ((uint32_t)c << 16) | ((uint32_t)nn << 20);
 }
 
 // wave wid of nw (all waves of this launch for frame fy); smem = mf_lds_bytes(TYmax)
@@ -94,6 +113,7 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // channel-byte tables: T_col[v] = {sin, cos, beta, 1 - beta} ^ 0x80 (setColor LUT, thresholds)
   uint32_t* s_tab = smem;
+  uint32_t* s_bins = smem + 768;
   for (int i = threadIdx.x; i < 768; i += kBlock) {
     const int col = i >> 8, v = i & 255;
     const uint32_t l = a.lut[v];
@@ -101,16 +121,18 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
     const uint32_t be = v > thr ? 1u : 0u;
     s_tab[i] = ((l & 0xffu) | (l & 0xff00u) | (be << 16) | ((be ^ 1u) << 24)) ^ 0x80808080u;
   }
+  for (int e = threadIdx.x; e < 981; e += kBlock) s_bins[e] = mf_bin_code(e);
+  uint8_t* wl = reinterpret_cast<uint8_t*>(smem + 768 + 984) + (size_t)wave * mf_wave_bytes(a.mf_ty);
+  uint8_t* planes = wl;                                   // 3 layer slots
+  uint8_t* cplanes = wl + 3 * mf_slot_bytes(a.mf_ty);    // planes 12..15 (constant)
+  for (int i = lane; i < 4 * kMfTyMax * kMfRowB / 4; i += 64)
+    reinterpret_cast<uint32_t*>(cplanes)[i] = i >= 3 * kMfTyMax * kMfRowB / 4 ? 0x01010101u : 0u;
   __syncthreads();
   const int nwork = (int)ftf[2 + (a.epoch & 1)];
   if (2 * nwork < a.ntiles) return;  // sparse frame: the dot4 tile body takes it
-  uint8_t* wl = reinterpret_cast<uint8_t*>(smem + 768) + (size_t)wave * mf_wave_bytes(a.mf_ty);
-  uint32_t* raw = reinterpret_cast<uint32_t*>(wl);                       // kMfRawSlots x kMfRaw
-  uint8_t* planes = wl + kMfRawSlots * kMfRaw * 4;                       // 3 layer slots
   const int F = a.variant;
   const int h4 = lane >> 4, n = lane & 15;
   const bool real = n < kMfCh;
-  const mf_v4i kConst = n == 15 ? mf_v4i{0x01010101, 0x01010101, 0x01010101, 0x01010101} : mf_v4i{0, 0, 0, 0};
 
   for (int wi = wid; wi < nwork; wi += nw) {
     const int tile = fwork[wi];
@@ -120,43 +142,43 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
     const int32_t* sz = a.segs + 3 * (2 * a.seg_stride + iz);
     const int x0 = sx[0], lx = sx[1], y0 = sy[0], ly = sy[1], z0 = sz[0], lz = sz[1];
     const int64_t h = sx[2] + (int64_t)sy[2] * a.sbx + (int64_t)sz[2] * a.sbx * a.sby;
-    const int TY = ly + 2, TX = lx + 2, nks = (ly + 3) >> 2;
-    const int nraw = TY * TX, ndma = (nraw + 63) >> 6;
+    const int TY = ly + 2, nks = (ly + 3) >> 2, npair = TY * 5;
     const int sb = mf_slot_bytes(TY);
-    // layer L (z = z0 - 1 + L) -> raw slot L % 4 by LDS DMA: element e = row * TX + xo
-    // (off-grid elements read word 0 and are masked at conversion)
-    auto dma = [&](int L) {
+    // layer words in registers: (row, dword q) pairs e = lane + 64 i, x = x0 - 1 + 4 q + j;
+    // two layers in flight
+    uint32_t wv[2][kMfLoad][4];
+    auto load_layer = [&](int L, uint32_t (&w)[kMfLoad][4]) {
       const int gz = z0 - 1 + L;
-      uint32_t* dst = raw + (L % kMfRawSlots) * kMfRaw;
-      for (int i = 0; i < ndma; ++i) {
-        const int e = 64 * i + lane, row = e / TX, xo = e - row * TX;
-        const int gy = y0 - 1 + row, gxx = x0 - 1 + xo;
-        const bool in = e < nraw && (unsigned)gz < (unsigned)a.gz && (unsigned)gy < (unsigned)a.gy &&
-                        (unsigned)gxx < (unsigned)a.gx;
-        const uint32_t* src = in ? fgrid + ((int64_t)gz * a.gy + gy) * a.gx + gxx : fgrid;
-        __builtin_amdgcn_global_load_lds(src, dst + 64 * i, 4, 0, 0);
-      }
-    };
-    // raw layer -> 12 channel planes: (row, dword q) pairs, 4 voxels x = -1 + 4 q + j each;
-    // table reads give 4 channel bytes per voxel and colour, a 4 x 4 byte transpose packs
-    // them per channel
-    auto convert = [&](int L) {
-      const int gz = z0 - 1 + L;
-      const uint32_t* src = raw + (L % kMfRawSlots) * kMfRaw;
-      uint8_t* slot = planes + (size_t)(L % 3) * sb;
-      for (int e = lane; e < TY * 5; e += 64) {
-        const int row = e / 5, q = e - row * 5;
+#pragma unroll
+      for (int i = 0; i < kMfLoad; ++i) {
+        const int e = lane + 64 * i, row = e / 5, q = e - row * 5;
         const int gy = y0 - 1 + row;
-        const bool rin = (unsigned)gz < (unsigned)a.gz && (unsigned)gy < (unsigned)a.gy;
-        uint32_t t[3][4];
+        const bool rowin = e < npair && (unsigned)gy < (unsigned)a.gy && (unsigned)gz < (unsigned)a.gz;
+        const uint32_t* src = fgrid + ((int64_t)gz * a.gy + gy) * a.gx;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int xo = 4 * q + j, gxx = x0 - 1 + xo;
-          const uint32_t w = (rin && xo < TX && (unsigned)gxx < (unsigned)a.gx) ? src[row * TX + xo] : 0u;
+          const int gxx = x0 - 1 + 4 * q + j;
+          w[i][j] = rowin && (unsigned)gxx < (unsigned)a.gx ? src[gxx] : 0u;
+        }
+      }
+    };
+    // 12 channel planes of layer L: per voxel and colour one table read gives the 4 channel
+    // bytes, a 4 x 4 byte transpose packs them per channel (4 voxels per dword)
+    auto store_layer = [&](int L, const uint32_t (&w)[kMfLoad][4]) {
+#if C3H_MF_EXP & 2
+      return;
+#endif
+      uint8_t* slot = planes + (size_t)(L % 3) * sb;
+#pragma unroll
+      for (int i = 0; i < kMfLoad; ++i) {
+        const int e = lane + 64 * i, row = e / 5, q = e - row * 5;
+        if (e >= npair) continue;
+        uint32_t t[3][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
           for (int col = 0; col < 3; ++col)
-            t[col][j] = w ? s_tab[col * 256 + ((w >> (16 - 8 * col)) & 0xffu)] : 0x80808080u;
-        }
+            t[col][j] = w[i][j] ? s_tab[col * 256 + ((w[i][j] >> (16 - 8 * col)) & 0xffu)] : 0x80808080u;
 #pragma unroll
         for (int col = 0; col < 3; ++col) {
           const uint32_t u0 = __builtin_amdgcn_perm(t[col][1], t[col][0], 0x05010400u);
@@ -171,52 +193,53 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
         }
       }
     };
-    // centre mask of A: bytes j >= lx are no centre (a = 0 -> 0x80)
+    // centre mask of A: bytes j >= lx are no centre (a = 0 -> 0x80); the constant lanes keep all
     uint32_t keep[4];
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       uint32_t m = 0;
 #pragma unroll
       for (int b = 0; b < 4; ++b) m |= (4 * d + b < lx ? 0xffu : 0u) << (8 * b);
-      keep[d] = m;
+      keep[d] = real ? m : 0xffffffffu;
     }
     mf_v4i acc[kMfK];
 #pragma unroll
     for (int k = 0; k < kMfK; ++k) acc[k] = mf_v4i{0, 0, 0, 0};
-    // prologue: layers 0..3 in flight, 0 and 1 converted
-    wait_vm(0);
-    for (int L = 0; L <= min(3, lz); ++L) dma(L);
-    wait_vm(0);
-    convert(0);
-    convert(1);
+    load_layer(0, wv[0]);
+    load_layer(1, wv[1]);
+    store_layer(0, wv[0]);
+    store_layer(1, wv[1]);
+    if (2 <= lz) load_layer(2, wv[0]);
+    if (3 <= lz) load_layer(3, wv[1]);
     for (int z = 0; z < lz; ++z) {
       wave_lds_sync();
       const uint8_t* sp = planes + (size_t)(z % 3) * sb;        // dz = -1
       const uint8_t* sc = planes + (size_t)((z + 1) % 3) * sb;  // dz = 0
-      const uint8_t* pc = sc + (size_t)(real ? n : 0) * TY * kMfRowB;
-      const uint8_t* pp = sp + (size_t)(real ? n : 0) * TY * kMfRowB;
-      for (int ks = 0; ks < nks; ++ks) {
+      // padding lanes read the constant planes (their rows are the same for every layer)
+      const uint8_t* pc = real ? sc + (size_t)n * TY * kMfRowB : cplanes + (size_t)(n - kMfCh) * kMfTyMax * kMfRowB;
+      const uint8_t* pp = real ? sp + (size_t)n * TY * kMfRowB : pc;
+      for (int ks = 0; ks < ((C3H_MF_EXP & 1) ? 0 : nks); ++ks) {
         const int y = 4 * ks + h4;
-        const bool ymask = y < ly;
+        const bool ym = y < ly;
         const int rm = min(y, TY - 1), rc = min(y + 1, TY - 1), rp = min(y + 2, TY - 1);
         auto row = [&](const uint8_t* plane, int r, uint4& lo, uint4& hi) {
           lo = *reinterpret_cast<const uint4*>(plane + r * kMfRowB);
           hi = *reinterpret_cast<const uint4*>(plane + r * kMfRowB + 16);
         };
-        auto sel = [&](const mf_v4i& f) { return real ? f : kConst; };
         uint4 lo, hi;
         row(pc, rc, lo, hi);
         mf_v4i A = mf_frag(lo, hi, 1);
 #pragma unroll
-        for (int d = 0; d < 4; ++d)
-          A[d] = ymask ? (int)(((uint32_t)A[d] & keep[d]) | (0x80808080u & ~keep[d])) : (int)0x80808080u;
-        A = sel(A);
+        for (int d = 0; d < 4; ++d) {
+          const uint32_t m = (ym || !real) ? keep[d] : 0u;
+          A[d] = (int)(((uint32_t)A[d] & m) | (0x80808080u & ~m));
+        }
         acc[13] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, A, acc[13], 0, 0, 0);  // own channels
-        acc[12] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, sel(mf_frag(lo, hi, 0)), acc[12], 0, 0, 0);  // (-1, 0, 0)
+        acc[12] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, mf_frag(lo, hi, 0), acc[12], 0, 0, 0);  // (-1, 0, 0)
         row(pc, rm, lo, hi);  // (dx, -1, 0): k = 9 + dx + 1
 #pragma unroll
         for (int dxi = 0; dxi < 3; ++dxi)
-          acc[9 + dxi] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, sel(mf_frag(lo, hi, dxi)), acc[9 + dxi], 0, 0, 0);
+          acc[9 + dxi] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, mf_frag(lo, hi, dxi), acc[9 + dxi], 0, 0, 0);
         // (dx, dy, -1): k = 3 (dx + 1) + (dy + 1)
 #pragma unroll
         for (int dyi = 0; dyi < 3; ++dyi) {
@@ -224,14 +247,19 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
 #pragma unroll
           for (int dxi = 0; dxi < 3; ++dxi)
             acc[3 * dxi + dyi] =
-                __builtin_amdgcn_mfma_i32_16x16x64_i8(A, sel(mf_frag(lo, hi, dxi)), acc[3 * dxi + dyi], 0, 0, 0);
+                __builtin_amdgcn_mfma_i32_16x16x64_i8(A, mf_frag(lo, hi, dxi), acc[3 * dxi + dyi], 0, 0, 0);
         }
       }
-      // layer z + 2 into the plane slot of layer z - 1; its DMA was issued two layers ago
+      // layer z + 2 into the plane slot of layer z - 1 (loaded two layers ago), then the
+      // loads of layer z + 4 into its registers
       if (z + 2 <= lz) {
-        wait_vm(z + 3 <= lz ? ndma : 0);
-        convert(z + 2);
-        if (z + 4 <= lz) dma(z + 4);
+        if (z & 1) {
+          store_layer(z + 2, wv[1]);
+          if (z + 4 <= lz) load_layer(z + 4, wv[1]);
+        } else {
+          store_layer(z + 2, wv[0]);
+          if (z + 4 <= lz) load_layer(z + 4, wv[0]);
+        }
       }
     }
     wave_lds_sync();
@@ -243,33 +271,16 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
 #pragma unroll
       for (int r = 0; r < 4; ++r) T[k * 256 + (4 * h4 + r) * 16 + n] = acc[k][r];
     wave_lds_sync();
-    const int32_t* T13 = T + 13 * 256;
-    const long long K = T13[255];
+    const long long K = T[13 * 256 + 255];
     for (int e = lane; e < 981; e += 64) {
-      int bin;
-      uint32_t v;
-      if (e < 936) {  // first order: k, type (colour / binary), c, n
-        const int k = e / 72, rem = e - 72 * k, ty = rem / 36, c = (rem % 36) / 6, nn = rem % 6;
-        bin = 495 * ty + bin981(k, c, nn);
-        v = mf_corr(T + k * 256, mf_plane(ty, c), mf_plane(ty, nn));
-      } else if (e < 957) {  // centre auto products (c <= n)
-        const int q = e - 936;
-        int c = 0;
-        while (q >= tri6(c + 1, c + 1)) ++c;
-        const int nn = c + (q - tri6(c, c));
-        bin = 474 + q;
-        v = mf_corr(T13, mf_plane(0, c), mf_plane(0, nn));
-      } else if (e < 969) {  // centre bin-pair counts
-        const int q = e - 957;
-        const int c = q < 8 ? q / 4 : 2 + (q - 8) / 2, nn = q < 8 ? 2 + q % 4 : 4 + (q - 8) % 2;
-        bin = 969 + q;
-        v = mf_corr(T13, mf_plane(1, c), mf_plane(1, nn));
-      } else {  // zero order: colour channels, then binary counts
-        const int q = e - 969;
-        bin = q < 6 ? q : 495 + (q - 6);
-        v = (uint32_t)((long long)T13[mf_plane(q < 6 ? 0 : 1, q < 6 ? q : q - 6) * 16 + 15] + 128ll * K);
-      }
-      hist[bin] = v;
+      const uint32_t code = s_bins[e];
+      const int bin = code & 1023, kind = (code >> 10) & 3, k = (code >> 12) & 15, c = (code >> 16) & 15,
+                nn = (code >> 20) & 15;
+      const int32_t* Tk = T + k * 256;
+      const long long v = kind ? (long long)Tk[c * 16 + 15] + 128ll * K
+                               : (long long)Tk[c * 16 + nn] + 128ll * ((long long)Tk[c * 16 + 15] + Tk[15 * 16 + nn]) +
+                                     16384ll * K;
+      hist[bin] = (uint32_t)v;
     }
     wave_lds_sync();
     if (a.atomic) {
@@ -289,7 +300,6 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
     if (frows && lane == 0) frows[wi] = (int32_t)h;
     wave_lds_sync();  // the tile's LDS is rebuilt by the next tile
   }
-  wait_vm(0);  // no LDS DMA outlives the wave
 }
 
 }  // namespace c3h
