@@ -41,11 +41,12 @@ constexpr int kMfTyMax = 18;
 #endif
 
 __host__ __device__ inline int mf_slot_bytes(int ty) { return kMfCh * ty * kMfRowB; }
-// per wave: 3 plane slots + 4 constant planes (rows 12..15 of A / columns 12..15 of B:
-// zeros, and ones in 15), or the epilogue's accumulator tiles + histogram
+// per wave: 4 constant planes (rows 12..15 of A / columns 12..15 of B: zeros, and ones
+// in 15), then 3 plane slots or (aliasing them) the epilogue's accumulator tiles + histogram
+constexpr int kMfConstBytes = 4 * kMfTyMax * kMfRowB;
 __host__ __device__ inline int mf_wave_bytes(int ty) {
-  const int work = 3 * mf_slot_bytes(ty) + 4 * kMfTyMax * kMfRowB, epi = (kMfK * 256 + 984) * 4;
-  return ((work > epi ? work : epi) + 15) & ~15;
+  const int work = 3 * mf_slot_bytes(ty), epi = (kMfK * 256 + 984) * 4;
+  return kMfConstBytes + (((work > epi ? work : epi) + 15) & ~15);
 }
 // 3 x 256 channel-byte tables | 984 epilogue bin codes | per-wave regions
 __host__ __device__ inline size_t mf_lds_bytes(int ty) { return 3072 + 3936 + (size_t)kMfWaves * mf_wave_bytes(ty); }
@@ -122,9 +123,9 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
     s_tab[i] = ((l & 0xffu) | (l & 0xff00u) | (be << 16) | ((be ^ 1u) << 24)) ^ 0x80808080u;
   }
   for (int e = threadIdx.x; e < 981; e += kBlock) s_bins[e] = mf_bin_code(e);
-  uint8_t* wl = reinterpret_cast<uint8_t*>(smem + 768 + 984) + (size_t)wave * mf_wave_bytes(a.mf_ty);
-  uint8_t* planes = wl;                                   // 3 layer slots
-  uint8_t* cplanes = wl + 3 * mf_slot_bytes(a.mf_ty);    // planes 12..15 (constant)
+  uint8_t* cplanes = reinterpret_cast<uint8_t*>(smem + 768 + 984) + (size_t)wave * mf_wave_bytes(a.mf_ty);
+  uint8_t* wl = cplanes + kMfConstBytes;  // 3 layer slots, or the epilogue
+  uint8_t* planes = wl;
   for (int i = lane; i < 4 * kMfTyMax * kMfRowB / 4; i += 64)
     reinterpret_cast<uint32_t*>(cplanes)[i] = i >= 3 * kMfTyMax * kMfRowB / 4 ? 0x01010101u : 0u;
   __syncthreads();
