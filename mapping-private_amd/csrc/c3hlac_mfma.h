@@ -41,11 +41,11 @@ constexpr int kMfTyMax = 18;
 #endif
 
 __host__ __device__ inline int mf_slot_bytes(int ty) { return kMfCh * ty * kMfRowB; }
-// per wave: 4 constant planes (rows 12..15 of A / columns 12..15 of B: zeros, and ones
-// in 15), then 3 plane slots or (aliasing them) the epilogue's accumulator tiles + histogram
-constexpr int kMfConstBytes = 4 * kMfTyMax * kMfRowB;
+// per wave: 2 constant planes (rows 12..15 of A / columns 12..15 of B: zeros, and ones
+// in 15), then 3 plane slots or (aliasing them) the epilogue's accumulator tiles
+constexpr int kMfConstBytes = 2 * kMfTyMax * kMfRowB;
 __host__ __device__ inline int mf_wave_bytes(int ty) {
-  const int work = 3 * mf_slot_bytes(ty), epi = (kMfK * 256 + 984) * 4;
+  const int work = 3 * mf_slot_bytes(ty), epi = kMfK * 256 * 4;
   return kMfConstBytes + (((work > epi ? work : epi) + 15) & ~15);
 }
 // 3 x 256 channel-byte tables | 984 epilogue bin codes | per-wave regions
@@ -126,8 +126,8 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
   uint8_t* cplanes = reinterpret_cast<uint8_t*>(smem + 768 + 984) + (size_t)wave * mf_wave_bytes(a.mf_ty);
   uint8_t* wl = cplanes + kMfConstBytes;  // 3 layer slots, or the epilogue
   uint8_t* planes = wl;
-  for (int i = lane; i < 4 * kMfTyMax * kMfRowB / 4; i += 64)
-    reinterpret_cast<uint32_t*>(cplanes)[i] = i >= 3 * kMfTyMax * kMfRowB / 4 ? 0x01010101u : 0u;
+  for (int i = lane; i < 2 * kMfTyMax * kMfRowB / 4; i += 64)
+    reinterpret_cast<uint32_t*>(cplanes)[i] = i >= kMfTyMax * kMfRowB / 4 ? 0x01010101u : 0u;
   __syncthreads();
   const int nwork = (int)ftf[2 + (a.epoch & 1)];
   if (2 * nwork < a.ntiles) return;  // sparse frame: the dot4 tile body takes it
@@ -217,7 +217,7 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
       const uint8_t* sp = planes + (size_t)(z % 3) * sb;        // dz = -1
       const uint8_t* sc = planes + (size_t)((z + 1) % 3) * sb;  // dz = 0
       // padding lanes read the constant planes (their rows are the same for every layer)
-      const uint8_t* pc = real ? sc + (size_t)n * TY * kMfRowB : cplanes + (size_t)(n - kMfCh) * kMfTyMax * kMfRowB;
+      const uint8_t* pc = real ? sc + (size_t)n * TY * kMfRowB : cplanes + (n == 15 ? kMfTyMax * kMfRowB : 0);
       const uint8_t* pp = real ? sp + (size_t)n * TY * kMfRowB : pc;
       for (int ks = 0; ks < ((C3H_MF_EXP & 1) ? 0 : nks); ++ks) {
         const int y = 4 * ks + h4;
@@ -264,39 +264,59 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
       }
     }
     wave_lds_sync();
-    // epilogue: accumulator tiles -> LDS (C/D map: row 4 (lane >> 4) + r, column lane & 15)
+    // epilogue: accumulator tiles -> LDS (C/D map: row 4 (lane >> 4) + r, column lane & 15);
+    // the bins are formed from them directly (exact corrected sums, then the reference's
+    // normalisation / the 117 fold)
     int32_t* T = reinterpret_cast<int32_t*>(wl);
-    uint32_t* hist = reinterpret_cast<uint32_t*>(wl) + kMfK * 256;
 #pragma unroll
     for (int k = 0; k < kMfK; ++k)
 #pragma unroll
       for (int r = 0; r < 4; ++r) T[k * 256 + (4 * h4 + r) * 16 + n] = acc[k][r];
     wave_lds_sync();
     const long long K = T[13 * 256 + 255];
-    for (int e = lane; e < 981; e += 64) {
-      const uint32_t code = s_bins[e];
-      const int bin = code & 1023, kind = (code >> 10) & 3, k = (code >> 12) & 15, c = (code >> 16) & 15,
-                nn = (code >> 20) & 15;
+    auto corr = [&](int k, int c, int nn) -> long long {
       const int32_t* Tk = T + k * 256;
-      const long long v = kind ? (long long)Tk[c * 16 + 15] + 128ll * K
-                               : (long long)Tk[c * 16 + nn] + 128ll * ((long long)Tk[c * 16 + 15] + Tk[15 * 16 + nn]) +
-                                     16384ll * K;
-      hist[bin] = (uint32_t)v;
-    }
-    wave_lds_sync();
+      return (long long)Tk[c * 16 + nn] + 128ll * ((long long)Tk[c * 16 + 15] + Tk[15 * 16 + nn]) + 16384ll * K;
+    };
+    auto code_value = [&](uint32_t code) -> uint32_t {
+      const int kind = (code >> 10) & 3, k = (code >> 12) & 15, c = (code >> 16) & 15, nn = (code >> 20) & 15;
+      return (uint32_t)(kind ? (long long)T[k * 256 + c * 16 + 15] + 128ll * K : corr(k, c, nn));
+    };
     if (a.atomic) {
-      for (int i = lane; i < 981; i += 64) {
-        const uint32_t v = hist[i];
-        if (v) atomicAdd(&facc[h * 981 + i], (unsigned long long)v);
+      for (int e = lane; e < 981; e += 64) {
+        const uint32_t code = s_bins[e], v = code_value(code);
+        if (v) atomicAdd(&facc[h * 981 + (code & 1023)], (unsigned long long)v);
       }
     } else {
       float* out = ffeat + h * F;
       if (F == 981) {
-        for (int i = lane; i < 981; i += 64) out[i] = (float)hist[i] * norm981(i);
-      } else {
-        for (int i = lane; i < 117; i += 64) out[i] = (float)fold117(hist, i) * norm117(i);
+        for (int e = lane; e < 981; e += 64) {
+          const uint32_t code = s_bins[e];
+          const int bin = code & 1023;
+          out[bin] = (float)code_value(code) * norm981(bin);
+        }
+      } else {  // color_chlac.hpp:1647-1743: first-order bins summed over the 13 offsets
+        for (int i = lane; i < 117; i += 64) {
+          uint32_t v;
+          if (i < 6 || (i >= 63 && i < 69)) {  // zero order
+            const int t = i < 6 ? 0 : 1, c = i < 6 ? i : i - 63;
+            v = (uint32_t)((long long)T[13 * 256 + mf_plane(t, c) * 16 + 15] + 128ll * K);
+          } else if (i < 42 || (i >= 69 && i < 105)) {  // first order, all offsets
+            const int t = i < 42 ? 0 : 1, q = i < 42 ? i - 6 : i - 69, c = q / 6, nn = q % 6;
+            long long sum = 0;
+            for (int k = 0; k < 13; ++k) sum += corr(k, mf_plane(t, c), mf_plane(t, nn));
+            v = (uint32_t)sum;
+          } else {  // centre auto products / bin-pair counts: codes 936.. / 957..
+            v = code_value(s_bins[i < 63 ? 936 + (i - 42) : 957 + (i - 105)]);
+          }
+          out[i] = (float)v * norm117(i);
+        }
       }
-      if (lane == 0) fexist[h] = exist_from((float)hist[0], (float)hist[1]);
+      if (lane == 0) {  // exist_voxel_num from the zero-order r sums (search_c3_hlac.h:60-61)
+        const uint32_t s0 = (uint32_t)((long long)T[13 * 256 + mf_plane(0, 0) * 16 + 15] + 128ll * K);
+        const uint32_t s1 = (uint32_t)((long long)T[13 * 256 + mf_plane(0, 1) * 16 + 15] + 128ll * K);
+        fexist[h] = exist_from((float)s0, (float)s1);
+      }
     }
     if (frows && lane == 0) frows[wi] = (int32_t)h;
     wave_lds_sync();  // the tile's LDS is rebuilt by the next tile
