@@ -231,6 +231,49 @@ int c3h_remove_overlap(int32_t M, int32_t rank, const int32_t range[3], c3h_det*
  * axis = var = NULL queries the dimension (header only; max_dim ignored). */
 int c3h_pca_read(const char* path, int32_t ascii, float* axis, float* var, float* mean,
                  int32_t* has_mean, int32_t max_dim);
+/* PCA::write (pca.cpp:190-240): the same layout c3h_pca_read reads; mean may be NULL
+ * (mean_flg false).  Host arrays. */
+int c3h_pca_write(const char* path, int32_t ascii, int32_t dim, const float* axis, const float* var,
+                  const float* mean);
+
+/* ---- PCA training on the GPU --------------------------------------
+ * class PCA (color_voxel_recognition/include/color_voxel_recognition/pca.h:45-81) as
+ * used by pca_scene.cpp (scene compress axis) and pca_models.cpp (model subspaces: every
+ * feature compressed by the scene axis, plus its 23 rotateFeature90 images).  The
+ * correlation accumulates in f64 on the device; solve runs rocSOLVER dsyevd (loaded at
+ * the first solve) and sortVecAndVal's stable descending order.  Differences from the
+ * reference: sums are f64 (the reference accumulates in f32), and solve leaves the
+ * accumulated sums untouched (it can be called again after more addData). */
+typedef struct c3h_pca c3h_pca;
+/* PCA::PCA(bool _mean_flg = true) (pca.cpp:40-44) on a HIP device */
+int c3h_pca_create(int hip_device, int32_t mean_flg, c3h_pca** out);
+void c3h_pca_destroy(c3h_pca* pca);
+const char* c3h_pca_last_error(c3h_pca* pca);
+int c3h_pca_set_stream(c3h_pca* pca, void* hip_stream); /* NULL = the object's own stream */
+/* compressFeature (pca_models.cpp:48-63) applied to every added vector: axis = the first
+ * D eigenvectors of the scene PCA, F x D column-major (PCA::getAxis().block(0,0,F,D));
+ * var = its variances (WHITENING, FILE_MODE) or NULL.  Host arrays; before any addData. */
+int c3h_pca_set_compress(c3h_pca* pca, const float* axis, const float* var, int32_t F, int32_t D);
+/* PCA::addData (pca.cpp:48-69) for n rows of F floats (row stride ld).  rotate24 = 1
+ * adds, per row, the 24 vectors of pca_models.cpp:109-171 (the row and its 23
+ * rotateFeature90 compositions; F = 981, 495 or 486).  A differing F is an error
+ * (pca.cpp:54-57).  Rows on the device (on_device = 1) or the host. */
+int c3h_pca_add_data(c3h_pca* pca, const float* rows, int64_t n, int64_t ld, int32_t F, int32_t rotate24,
+                     int on_device);
+/* PCA::solve(regularization_flg, regularization_nolm) (pca.cpp:73-105) + sortVecAndVal */
+int c3h_pca_solve(c3h_pca* pca, int32_t regularization_flg, float regularization_nolm);
+/* getAxis / getVariance / getMean after solve: axis dim x dim column-major (eigenvector i
+ * contiguous, by descending variance), var dim, mean dim (error without mean_flg, as
+ * pca.cpp:110-113); any pointer may be NULL.  Returns dim (D if compressing, else F). */
+int c3h_pca_get(c3h_pca* pca, float* axis, float* var, float* mean, int64_t* nsample, int on_device);
+/* the normalised correlation matrix solve decomposed (dim x dim doubles, host) */
+int c3h_pca_get_correlation(c3h_pca* pca, double* corr);
+/* pcl::rotateFeature90 (c3_hlac/src/c3_hlac.cpp:49-172) on n device rows (stride ld) on a
+ * HIP stream; dim 981 / 495 / 486, mode 0..3 = R_MODE_1..4; in != out. */
+int c3h_rotate_feature90(const float* in, float* out, int64_t n, int64_t ld, int32_t dim, int32_t mode,
+                         void* hip_stream);
+/* the same rotation as a gather map: map_out[o] = input index of output o (host). */
+int c3h_rotate_map(int32_t dim, int32_t mode, int32_t* map_out);
 
 /* per-kernel device time (ms) accumulated since the last reset with HIP events on the
  * context stream; slots: 0 voxelize, 1 C3-HLAC, 2 compress, 3 score, 4 rank replay,

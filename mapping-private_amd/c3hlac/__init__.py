@@ -345,3 +345,113 @@ def box_size(size_m, region_size):
     if (t - s) >= 0.5 or s == 0:
         s += 1
     return s
+
+
+R_MODE_1, R_MODE_2, R_MODE_3, R_MODE_4 = 0, 1, 2, 3
+
+
+def rotate_map(dim, mode):
+    """pcl::rotateFeature90 (c3_hlac.cpp:49-172) as a gather map: out[o] = in[map[o]]."""
+    out = np.zeros(dim, np.int32)
+    check(_capi.load().c3h_rotate_map(dim, mode, ptr(out)), None, "rotate_map")
+    return out
+
+
+def rotate_feature90(d_in, d_out, mode, stream=None):
+    """pcl::rotateFeature90 on device rows: d_in / d_out torch float32 tensors (n, dim)."""
+    n, dim = d_in.shape
+    assert d_out.shape == d_in.shape and d_in.is_contiguous() and d_out.is_contiguous()
+    s = None if stream is None else C.c_void_p(stream)
+    check(_capi.load().c3h_rotate_feature90(ptr(d_in), ptr(d_out), n, dim, dim, mode, s), None,
+          "rotate_feature90")
+
+
+def pca_write(path, axis, var, mean=None, ascii=False):
+    """PCA::write (pca.cpp:190-240); axis (dim, dim) with axis[:, i] = eigenvector i."""
+    dim = len(var)
+    a = np.ascontiguousarray(np.asarray(axis, np.float32).T)  # eigenvector i contiguous
+    v = np.ascontiguousarray(var, np.float32)
+    m = None if mean is None else np.ascontiguousarray(mean, np.float32)
+    check(_capi.load().c3h_pca_write(str(path).encode(), int(bool(ascii)), dim, ptr(a), ptr(v), ptr(m)), None,
+          "pca_write")
+
+
+class PCA:
+    """class PCA (color_voxel_recognition/include/color_voxel_recognition/pca.h:45-81) with
+    the correlation accumulated on the GPU (csrc/pca.hip).
+
+    add_data takes a batch of rows (numpy host array or torch device tensor) instead of
+    one std::vector per call; set_compress + rotate24 give pca_models.cpp's augmented,
+    compressed training in one pass (see c3h_pca_add_data)."""
+
+    def __init__(self, mean_flg=True, device=0):
+        self.lib = _capi.load()
+        h = C.c_void_p()
+        check(self.lib.c3h_pca_create(device, int(bool(mean_flg)), C.byref(h)), None, "pca_create")
+        self.h = h
+        self.mean_flg = bool(mean_flg)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.c3h_pca_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def _check(self, rc, what):
+        if rc < 0:
+            m = self.lib.c3h_pca_last_error(self.h)
+            raise _capi.C3HError("%s failed: %s %s" % (what, _capi.ERRORS.get(rc, rc), m.decode() if m else ""))
+        return rc
+
+    def set_compress(self, axis, var, dim):
+        """compressFeature's projection: the first dim columns of axis (F, F'), whitened by var."""
+        F = axis.shape[0]
+        a = np.ascontiguousarray(np.asarray(axis, np.float32)[:, :dim].T)  # column d contiguous
+        v = None if var is None else np.ascontiguousarray(np.asarray(var, np.float32)[:dim])
+        self._check(self.lib.c3h_pca_set_compress(self.h, ptr(a), ptr(v), F, dim), "pca_set_compress")
+
+    def add_data(self, rows, rotate24=False):
+        on_dev = hasattr(rows, "data_ptr")
+        if not on_dev:
+            rows = np.ascontiguousarray(rows, np.float32)
+            if rows.ndim == 1:
+                rows = rows[None, :]
+        else:
+            assert rows.is_contiguous()
+        n, F = rows.shape
+        self._check(self.lib.c3h_pca_add_data(self.h, ptr(rows), n, F, F, int(bool(rotate24)), int(on_dev)),
+                    "pca_add_data")
+
+    addData = add_data
+
+    def solve(self, regularization_flg=False, regularization_nolm=0.0001):
+        self._check(self.lib.c3h_pca_solve(self.h, int(bool(regularization_flg)), regularization_nolm), "pca_solve")
+        d = self._check(self.lib.c3h_pca_get(self.h, None, None, None, None, 0), "pca_get")
+        a = np.zeros((d, d), np.float32)
+        v = np.zeros(d, np.float32)
+        m = np.zeros(d, np.float32) if self.mean_flg else None
+        n = C.c_int64()
+        self._check(self.lib.c3h_pca_get(self.h, ptr(a), ptr(v), ptr(m), C.byref(n), 0), "pca_get")
+        self.axis, self.variance, self.mean, self.nsample = a.T.copy(), v, m, n.value
+        return self
+
+    def correlation(self):
+        d = self.axis.shape[0]
+        out = np.zeros((d, d), np.float64)
+        self._check(self.lib.c3h_pca_get_correlation(self.h, ptr(out)), "pca_get_correlation")
+        return out
+
+    def getAxis(self):
+        return self.axis
+
+    def getVariance(self):
+        return self.variance
+
+    def getMean(self):
+        if not self.mean_flg:
+            raise _capi.C3HError("getMean: There is no mean vector (mean_flg=false).")
+        return self.mean
+
+    def write(self, path, ascii=False):
+        pca_write(path, self.axis, self.variance, self.mean if self.mean_flg else None, ascii)

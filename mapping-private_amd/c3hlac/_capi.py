@@ -83,6 +83,18 @@ _SIGS = {
     "c3h_get_scores": (C.c_int, [_P, _P, C.POINTER(C.c_int64), C.c_int]),
     "c3h_remove_overlap": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(C.c_int32), _P]),
     "c3h_pca_read": (C.c_int, [C.c_char_p, C.c_int32, _P, _P, _P, C.POINTER(C.c_int32), C.c_int32]),
+    "c3h_pca_write": (C.c_int, [C.c_char_p, C.c_int32, C.c_int32, _P, _P, _P]),
+    "c3h_pca_create": (C.c_int, [C.c_int, C.c_int32, C.POINTER(_P)]),
+    "c3h_pca_destroy": (None, [_P]),
+    "c3h_pca_last_error": (C.c_char_p, [_P]),
+    "c3h_pca_set_stream": (C.c_int, [_P, _P]),
+    "c3h_pca_set_compress": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int32]),
+    "c3h_pca_add_data": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int]),
+    "c3h_pca_solve": (C.c_int, [_P, C.c_int32, C.c_float]),
+    "c3h_pca_get": (C.c_int, [_P, _P, _P, _P, C.POINTER(C.c_int64), C.c_int]),
+    "c3h_pca_get_correlation": (C.c_int, [_P, _P]),
+    "c3h_rotate_feature90": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _P]),
+    "c3h_rotate_map": (C.c_int, [C.c_int32, C.c_int32, _P]),
     "c3h_timing": (C.c_int, [_P, C.c_int32]),
     "c3h_kernel_times": (C.c_int, [_P, _P, _P, C.c_int32]),
 }
