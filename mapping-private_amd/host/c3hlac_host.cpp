@@ -257,8 +257,93 @@ void PCA::read(const char* filename, bool ascii) {
 }
 
 const std::vector<float>& PCA::getMean() const {
-  if (!mean_flg_) throw Error(C3H_ERR_STATE, "PCA::getMean: no mean vector in the file");
+  if (!mean_flg_) throw Error(C3H_ERR_STATE, "PCA::getMean: There is no mean vector (mean_flg=false).");
   return mean_;
+}
+
+namespace {
+constexpr size_t kPcaBatchRows = 4096;  // host rows per c3h_pca_add_data call
+}
+
+PCA::~PCA() { c3h_pca_destroy(h_); }
+
+c3h_pca* PCA::handle() {
+  if (!h_) {
+    int rc = c3h_pca_create(device_, mean_flg_ ? 1 : 0, &h_);
+    if (rc != C3H_OK) throw Error(rc, "PCA: c3h_pca_create failed");
+  }
+  return h_;
+}
+
+void PCA::flush(bool rotated) {
+  std::vector<float>& r = rows_[rotated ? 1 : 0];
+  if (r.empty()) return;
+  const int64_t n = (int64_t)(r.size() / F_);
+  int rc = c3h_pca_add_data(handle(), r.data(), n, F_, F_, rotated ? 1 : 0, 0);
+  r.clear();
+  if (rc != C3H_OK) throw Error(rc, std::string("PCA::addData: ") + c3h_pca_last_error(h_));
+}
+
+void PCA::addData(const std::vector<float>& feature) {
+  if (F_ == -1) F_ = (int)feature.size();
+  if ((int)feature.size() != F_) throw Error(C3H_ERR_ARG, "PCA::addData: vector size differs");
+  rows_[0].insert(rows_[0].end(), feature.begin(), feature.end());
+  if (rows_[0].size() >= kPcaBatchRows * F_) flush(false);
+}
+
+void PCA::addDataRotated24(const std::vector<float>& feature) {
+  if (F_ == -1) F_ = (int)feature.size();
+  if ((int)feature.size() != F_) throw Error(C3H_ERR_ARG, "PCA::addData: vector size differs");
+  rows_[1].insert(rows_[1].end(), feature.begin(), feature.end());
+  if (rows_[1].size() >= kPcaBatchRows * F_) flush(true);
+}
+
+void PCA::setCompress(const MatrixXf& axis, const std::vector<float>& variance, int dim, bool whitening) {
+  const int F = axis.rows;
+  if (dim <= 0 || dim > axis.cols || (whitening && (int)variance.size() < dim))
+    throw Error(C3H_ERR_ARG, "PCA::setCompress: bad dimension");
+  std::vector<float> col((size_t)F * dim);  // column d contiguous
+  for (int d = 0; d < dim; ++d)
+    for (int f = 0; f < F; ++f) col[(size_t)d * F + f] = axis(f, d);
+  int rc = c3h_pca_set_compress(handle(), col.data(), whitening ? variance.data() : nullptr, F, dim);
+  if (rc != C3H_OK) throw Error(rc, std::string("PCA::setCompress: ") + c3h_pca_last_error(h_));
+}
+
+void PCA::solve(bool regularization_flg, float regularization_nolm) {
+  flush(false);
+  flush(true);
+  c3h_pca* h = handle();
+  int rc = c3h_pca_solve(h, regularization_flg ? 1 : 0, regularization_nolm);
+  if (rc != C3H_OK) throw Error(rc, std::string("PCA::solve: ") + c3h_pca_last_error(h));
+  const int dim = c3h_pca_get(h, nullptr, nullptr, nullptr, nullptr, 0);
+  if (dim < 0) throw Error(dim, "PCA::solve: get");
+  std::vector<float> col((size_t)dim * dim);
+  variance_.assign(dim, 0.f);
+  mean_.assign(mean_flg_ ? dim : 0, 0.f);
+  rc = c3h_pca_get(h, col.data(), variance_.data(), mean_flg_ ? mean_.data() : nullptr, nullptr, 0);
+  if (rc < 0) throw Error(rc, "PCA::solve: get");
+  axis_ = MatrixXf(dim, dim);
+  for (int i = 0; i < dim; ++i)
+    for (int j = 0; j < dim; ++j) axis_(j, i) = col[(size_t)i * dim + j];
+}
+
+void PCA::write(const char* filename, bool ascii) const {
+  const int dim = (int)variance_.size();
+  std::vector<float> col((size_t)dim * dim);
+  for (int i = 0; i < dim; ++i)
+    for (int j = 0; j < dim; ++j) col[(size_t)i * dim + j] = axis_(j, i);
+  int rc = c3h_pca_write(filename, ascii ? 1 : 0, dim, col.data(), variance_.data(),
+                         mean_flg_ ? mean_.data() : nullptr);
+  if (rc != C3H_OK) throw Error(rc, std::string("PCA::write: cannot write ") + filename);
+}
+
+void rotateFeature90(std::vector<float>& output, const std::vector<float>& input, RotateMode mode) {
+  const int dim = (int)input.size();
+  std::vector<int32_t> map(dim);
+  int rc = c3h_rotate_map(dim, (int32_t)mode, map.data());
+  if (rc != C3H_OK) throw Error(rc, "rotateFeature90: improper dimension");
+  output.resize(dim);
+  for (int o = 0; o < dim; ++o) output[o] = input[map[o]];
 }
 
 // ------------------------------------------------------------------------- Param

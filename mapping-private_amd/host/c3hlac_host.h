@@ -146,18 +146,42 @@ class ColorThreshold {
 // column i, as Eigen holds it.
 class PCA {
  public:
-  explicit PCA(bool mean_flg = true) : mean_flg_(mean_flg) {}
+  // PCA(bool _mean_flg = true) (pca.h:49); training runs on HIP device `hip_device`
+  explicit PCA(bool mean_flg = true, int hip_device = 0) : mean_flg_(mean_flg), device_(hip_device) {}
+  ~PCA();
+  PCA(const PCA&) = delete;
+  PCA& operator=(const PCA&) = delete;
+  // addData (pca.cpp:48-69): rows are batched on the host and accumulated on the GPU
+  void addData(const std::vector<float>& feature);
+  // pca_models.cpp's training in one call: compressFeature with the scene axis (first
+  // dim columns, whitened by variance unless whitening = false) applied to every vector
+  // added afterwards (setCompress), and the 24 rotateFeature90 images of a feature
+  // (addDataRotated24 = the 24 addData calls of pca_models.cpp:109-171)
+  void setCompress(const MatrixXf& axis, const std::vector<float>& variance, int dim, bool whitening = true);
+  void addDataRotated24(const std::vector<float>& feature);
+  void solve(bool regularization_flg = false, float regularization_nolm = 0.0001f);
   void read(const char* filename, bool ascii = false);
+  void write(const char* filename, bool ascii = false) const;
   const MatrixXf& getAxis() const { return axis_; }
   const std::vector<float>& getVariance() const { return variance_; }
   const std::vector<float>& getMean() const;
   int dim() const { return axis_.rows; }
 
  private:
+  void flush(bool rotated);
+  c3h_pca* handle();
   bool mean_flg_;
+  int device_;
+  c3h_pca* h_ = nullptr;
+  int F_ = -1;
+  std::vector<float> rows_[2];  // pending plain / rotated rows
   MatrixXf axis_;
   std::vector<float> variance_, mean_;
 };
+
+// pcl::rotateFeature90 (c3_hlac.cpp:49-172) on one host vector (an index gather)
+enum RotateMode { R_MODE_1, R_MODE_2, R_MODE_3, R_MODE_4 };
+void rotateFeature90(std::vector<float>& output, const std::vector<float>& input, RotateMode mode);
 
 // Param (param.h): the same keys, defaults and -1 error returns.
 struct Param {

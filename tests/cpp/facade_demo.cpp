@@ -6,6 +6,8 @@
 //   facade_demo run <xyzrgb.bin> <out_features.bin>   (GPU: the detection pipeline)
 //   facade_demo io <cloud.pcd> <feature.pcd> <out.pcd>  (host only: loadPCDFile, read/writeFeature)
 //   facade_demo thr <cloud.pcd> <leaf>                  (GPU: calc_scene_auto_threshold flow)
+//   facade_demo rot <dim> <mode>                        (host only: rotateFeature90 of 0..dim-1)
+//   facade_demo train <rows.bin> <out_dir> <D> <n_model> (GPU: pca_scene.cpp + pca_models.cpp)
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -145,12 +147,50 @@ static int thr(const char* cloud_pcd, float leaf) {
   return 0;
 }
 
+static int rot(int dim, int mode) {
+  std::vector<float> in(dim), out;
+  for (int i = 0; i < dim; ++i) in[i] = (float)i;
+  rotateFeature90(out, in, (RotateMode)mode);
+  printf("[");
+  for (int i = 0; i < dim; ++i) printf(i ? ", %d" : "%d", (int)out[i]);
+  printf("]\n");
+  return 0;
+}
+
+// pca_scene.cpp (every row, mean_flg false) then pca_models.cpp (the first n_model rows,
+// compressed by the scene axis to D dims, each with its 23 rotations); rows.bin = int32
+// n, int32 F, n x F float32
+static int train(const char* rows_path, const std::string& out, int D, int n_model) {
+  std::ifstream f(rows_path, std::ios::binary);
+  int32_t n = 0, F = 0;
+  f.read((char*)&n, 4);
+  f.read((char*)&F, 4);
+  std::vector<float> X((size_t)n * F);
+  f.read((char*)X.data(), X.size() * 4);
+  if (!f) throw Error(C3H_ERR_FORMAT, "train: short rows file");
+  PCA scene(false);
+  for (int h = 0; h < n; ++h) scene.addData(std::vector<float>(X.begin() + (size_t)h * F, X.begin() + (size_t)(h + 1) * F));
+  scene.solve();
+  scene.write((out + "/scene_pca").c_str(), false);
+  PCA model(false);
+  model.setCompress(scene.getAxis(), scene.getVariance(), D);
+  for (int h = 0; h < n_model; ++h)
+    model.addDataRotated24(std::vector<float>(X.begin() + (size_t)h * F, X.begin() + (size_t)(h + 1) * F));
+  model.solve();
+  model.write((out + "/model_pca").c_str(), false);
+  printf("{\"scene_dim\": %d, \"model_dim\": %d, \"scene_var0\": %.9g, \"model_var0\": %.9g}\n", scene.dim(),
+         model.dim(), scene.getVariance()[0], model.getVariance()[0]);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   try {
     if (argc == 4 && !strcmp(argv[1], "params")) return params(argv[2], argv[3]);
     if (argc == 4 && !strcmp(argv[1], "run")) return run(argv[2], argv[3]);
     if (argc == 5 && !strcmp(argv[1], "io")) return io(argv[2], argv[3], argv[4]);
     if (argc == 4 && !strcmp(argv[1], "thr")) return thr(argv[2], (float)atof(argv[3]));
+    if (argc == 4 && !strcmp(argv[1], "rot")) return rot(atoi(argv[2]), atoi(argv[3]));
+    if (argc == 6 && !strcmp(argv[1], "train")) return train(argv[2], argv[3], atoi(argv[4]), atoi(argv[5]));
   } catch (const Error& e) {
     fprintf(stderr, "c3hlac::Error %d: %s\n", e.code, e.what());
     return 2;

@@ -137,3 +137,38 @@ def test_facade_auto_threshold(demo, ctx):
     t, ave = npr.auto_threshold(h)
     assert j["n_occ"] == h[0].sum() // 2 and j["h_sum"] == h[0].sum()
     assert j["thr"] == list(t) and j["ave"] == list(ave)
+
+
+@pytest.mark.parametrize("dim", [981, 495])
+def test_facade_rotate_feature90(demo, dim):
+    import pca_oracle as pco
+    for mode in range(4):
+        out = subprocess.run([str(demo), "rot", str(dim), str(mode)], check=True, capture_output=True,
+                             text=True).stdout
+        assert json.loads(out) == pco.rotate_map(dim, mode).tolist()
+
+
+@pytest.mark.gpu
+def test_facade_pca_training(ctx, demo, tmp_path):
+    """pca_scene + pca_models through the facade (host rows batched into the GPU
+    accumulator) against the oracle: variances, subspaces and the file format."""
+    import pca_oracle as pco
+    rng = np.random.default_rng(11)
+    n, F, D, nm = 1200, 981, 40, 60
+    X = (rng.random((n, 8)) @ rng.random((8, F)) + 0.01 * rng.random((n, F))).astype(np.float32)
+    rows = tmp_path / "rows.bin"
+    rows.write_bytes(np.array([n, F], np.int32).tobytes() + X.tobytes())
+    out = subprocess.run([str(demo), "train", str(rows), str(tmp_path), str(D), str(nm)], check=True,
+                         capture_output=True, text=True).stdout
+    j = json.loads(out)
+    assert (j["scene_dim"], j["model_dim"]) == (F, D)
+    sa, sv, sm = c3hlac.pca_read(tmp_path / "scene_pca")
+    assert sm is None
+    ref_s = pco.train(X)
+    np.testing.assert_allclose(sv, ref_s[1].astype(np.float32), rtol=0, atol=1e-9 * ref_s[1][0])
+    ma, mv, _ = c3hlac.pca_read(tmp_path / "model_pca")
+    ref_m = pco.train(X[:nm], sa[:, :D], sv[:D], rotate=True, exact=True)
+    np.testing.assert_allclose(mv, ref_m[1].astype(np.float32), rtol=1e-6, atol=1e-9 * ref_m[1][0])
+    # leading model subspace (r = 10 as in the demos) equals the oracle's
+    P1, P2 = ma[:, :10].astype(np.float64), ref_m[0][:, :10]
+    assert np.abs(P1 @ P1.T - P2 @ P2.T).max() < 1e-4
