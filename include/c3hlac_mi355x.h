@@ -90,6 +90,22 @@ const char* c3h_last_error(const c3h_ctx* ctx);
  * again: keep the buffer alive until then. */
 int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, float leaf,
                  float z_limit, c3h_grid_info* info);
+/* sensor_msgs/PointCloud2 ingestion: pcl::fromROSMsg(*msg, cloud) into PointXYZRGB
+ * (color_voxel_recognition/test/detect_object.cpp:142) followed by c3h_voxelize.  data =
+ * the message's data[] (host, or device with on_device = 1), height x width points,
+ * point_step / row_step / is_bigendian as in the message; offsets = the byte offsets of
+ * the FLOAT32 fields x, y, z and rgb (rgb < 0: absent, read as 0), i.e. the `offset` of
+ * the PointField named "x", "y", "z", "rgb" (or "rgba").  Every point is converted (NaN
+ * ones too, limitPoint drops them) on the device.  c3h_get_downsampled stays valid until
+ * the next ingestion. */
+int c3h_voxelize_pointcloud2(c3h_ctx* ctx, const void* data, uint32_t height, uint32_t width,
+                             uint32_t point_step, uint32_t row_step, const int32_t offsets[4],
+                             int32_t is_bigendian, int on_device, float leaf, float z_limit,
+                             c3h_grid_info* info);
+/* the conversion alone, device to device on a HIP stream: d_out = height*width x 4 floats */
+int c3h_pointcloud2_to_xyzrgb(const void* d_data, uint32_t height, uint32_t width, uint32_t point_step,
+                              uint32_t row_step, const int32_t offsets[4], int32_t is_bigendian,
+                              float* d_out, void* hip_stream);
 /* VoxelGrid::getLeafLayout (setSaveLeafLayout(true)): div_b product int32, -1 = empty. */
 int c3h_get_leaf_layout(c3h_ctx* ctx, int32_t* out, int on_device);
 /* the downsampled cloud of getVoxelGrid: n_occ x 4 floats in ascending voxel index. */
@@ -147,6 +163,19 @@ int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3]
 /* the features the context holds (the last extract, or after c3h_run_frames the last
  * frame's): getSubdivNum, hist_num and the dimension (981 / 117; 0 before any extract) */
 int c3h_get_feature_info(c3h_ctx* ctx, int32_t subdiv_out[3], int64_t* hist_num, int32_t* dim);
+/* SearchObj::setData(subdiv_b, feature) (search.cpp:539-658) with features computed
+ * elsewhere (VOSCH / ConVOSCH / GRSD extractors, search_new.h:34-76, or stored C3-HLAC
+ * rows): subdiv_b[0]*[1]*[2] rows of dim floats, row h = x + y*xn + z*xn*yn.  exist =
+ * the rows' exist_voxel_num, or NULL to derive it by exist_rule with the reference's
+ * arithmetic: C3H_EXIST_C3HLAC (int)((f0+f1)*2+0.001) (setC3HLAC), C3H_EXIST_VOSCH
+ * (int)((f20+f21)*2+0.001) (setVOSCH / setConVOSCH), C3H_EXIST_GRSD an int summing
+ * f0..f19, then / 26 (setGRSD).  The next c3h_search / c3h_search_async uses them
+ * (dim must equal the F of c3h_search_setup). */
+#define C3H_EXIST_C3HLAC 0
+#define C3H_EXIST_VOSCH 1
+#define C3H_EXIST_GRSD 2
+int c3h_set_features(c3h_ctx* ctx, const float* feat, const int32_t subdiv_b[3], int32_t dim,
+                     const int32_t* exist, int32_t exist_rule, int on_device);
 /* hist_num x variant floats of the last extract */
 int c3h_get_features(c3h_ctx* ctx, float* out, int on_device);
 /* exist_voxel_num of SearchC3HLAC::setC3HLAC

@@ -82,6 +82,23 @@ class Context:
         self.info = gi
         return gi
 
+    def voxelize_pointcloud2(self, msg, leaf, z_limit=float("inf")):
+        """sensor_msgs/PointCloud2 as a dict {height, width, point_step, row_step,
+        is_bigendian, fields: {name: offset}, data: bytes / uint8 array / device tensor}."""
+        f = msg["fields"]
+        off = (C.c_int32 * 4)(f["x"], f["y"], f["z"], f.get("rgb", f.get("rgba", -1)))
+        data = msg["data"]
+        on_dev = hasattr(data, "data_ptr")
+        if not on_dev:
+            data = np.frombuffer(data, np.uint8) if isinstance(data, (bytes, bytearray)) else np.ascontiguousarray(data)
+        gi = _capi.GridInfo()
+        self._chk(self.lib.c3h_voxelize_pointcloud2(self.h, ptr(data), msg["height"], msg["width"], msg["point_step"],
+                                                    msg["row_step"], off, int(bool(msg.get("is_bigendian", 0))),
+                                                    int(on_dev), float(leaf), float(z_limit), C.byref(gi)),
+                  "voxelize_pointcloud2")
+        self.info = gi
+        return gi
+
     def set_grid(self, words, div_b, min_b=(0, 0, 0), leaf=0.01):
         on_dev = not isinstance(words, np.ndarray)
         if not on_dev:
@@ -136,6 +153,22 @@ class Context:
         if out.size:
             self._chk(self.lib.c3h_get_features(self.h, ptr(out), 0), "get_features")
         return out
+
+    def set_features(self, feat, subdiv, exist=None, rule=0):
+        """SearchObj::setData with caller-computed features (c3h_set_features): feat
+        (hist_num, dim) numpy or torch device tensor, exist None -> derived by rule
+        (0 setC3HLAC, 1 setVOSCH / setConVOSCH, 2 setGRSD)."""
+        on_dev = hasattr(feat, "data_ptr")
+        if not on_dev:
+            feat = np.ascontiguousarray(feat, np.float32)
+            if exist is not None:
+                exist = np.ascontiguousarray(exist, np.int32)
+        sb = (C.c_int32 * 3)(*[int(v) for v in subdiv])
+        self._chk(self.lib.c3h_set_features(self.h, ptr(feat), sb, int(feat.shape[1]), ptr(exist), int(rule),
+                                            int(on_dev)), "set_features")
+        self.hist_num = int(feat.shape[0])
+        self.subdiv = tuple(int(v) for v in subdiv)
+        self.variant = int(feat.shape[1])
 
     def exist(self):
         out = np.zeros(self.hist_num, np.int32)

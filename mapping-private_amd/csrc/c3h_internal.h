@@ -179,6 +179,10 @@ hipError_t launch_offcell_delta(const int32_t* rec, int nrec, const C3Launch& l,
                                 const int sb[3], float inv_s, hipStream_t s);
 hipError_t launch_c3_finalize(const unsigned long long* acc64, int64_t hist_num, int variant,
                               float* feat, int32_t* exist, int nframes, hipStream_t s);
+// sensor_msgs/PointCloud2 bytes -> n x float4 (x, y, z, rgb bits) (ingest.hip)
+hipError_t launch_pc2_convert(const void* data, uint32_t height, uint32_t width, uint32_t point_step,
+                              uint32_t row_step, const int32_t off[4], int big, float* out, hipStream_t s);
+hipError_t launch_exist_rule(const float* feat, int64_t H, int dim, int rule, int32_t* exist, hipStream_t s);
 
 // rows/nrows (device): compress only the listed rows (sparse mode), else all H rows
 hipError_t launch_compress(const float* feat, int64_t H, int F, const float* axis_pt, int D,
@@ -312,6 +316,7 @@ struct c3h_ctx {
   c3h::DevBuf<uint32_t> grid;       // owned packed grid
   const uint32_t* grid_ptr = nullptr;  // the grid in use (owned or bound)
   c3h::DevBuf<float> pts;           // staging copy of host points
+  c3h::DevBuf<uint32_t> raw;        // staging copy of host PointCloud2 bytes
   // voxeliser state (voxelize.hip): global hash table, slot / grid-word lists by epoch
   // parity, counters; what the previous frame listed is cleared by the next frame
   c3h::DevBuf<c3h::VoxSlot> vtab[2];

@@ -485,6 +485,34 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
   return hipGetLastError();
 }
 
+// exist_voxel_num of caller-supplied feature rows (c3h_set_features), with the reference's
+// float / int arithmetic: rule 0 setC3HLAC ((f0 + f1) * 2 + 0.001, search_c3_hlac.h:60-61),
+// 1 setVOSCH / setConVOSCH ((f20 + f21) * 2 + 0.001, search_new.h:41-43), 2 setGRSD (an
+// int accumulating f0..f19 one float add at a time, then / 26, search_new.h:69-74)
+__global__ void exist_rule_kernel(const float* __restrict__ feat, int64_t H, int dim, int rule,
+                                  int32_t* __restrict__ exist) {
+  for (int64_t h = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; h < H; h += (int64_t)gridDim.x * blockDim.x) {
+    const float* f = feat + h * dim;
+    int32_t e;
+    if (rule == 2) {
+      e = 0;
+      for (int i = 0; i < 20; ++i) e = (int32_t)((float)e + f[i]);
+      e /= 26;
+    } else {
+      const int i0 = rule == 1 ? 20 : 0;
+      const float t = (f[i0] + f[i0 + 1]) * 2.0f;
+      e = (int32_t)((double)t + 0.001);
+    }
+    exist[h] = e;
+  }
+}
+
+hipError_t launch_exist_rule(const float* feat, int64_t H, int dim, int rule, int32_t* exist, hipStream_t s) {
+  const int64_t blocks = std::min<int64_t>((H + 255) / 256, 4096);
+  exist_rule_kernel<<<(unsigned)std::max<int64_t>(blocks, 1), 256, 0, s>>>(feat, H, dim, rule, exist);
+  return hipGetLastError();
+}
+
 hipError_t launch_c3_finalize(const unsigned long long* acc64, int64_t hist_num, int variant,
                               float* feat, int32_t* exist, int nframes, hipStream_t s) {
   c3_finalize_kernel<<<dim3((unsigned)hist_num, (unsigned)nframes), kBlock, 0, s>>>(acc64, variant, feat, exist,

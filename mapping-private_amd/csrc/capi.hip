@@ -620,6 +620,7 @@ void c3h_destroy(c3h_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   release(ctx->grid);
   release(ctx->pts);
+  release(ctx->raw);
   release(ctx->vtab[0]);
   release(ctx->vtab[1]);
   release(ctx->vlists);
@@ -1206,6 +1207,91 @@ int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3]
   QUIESCE(ctx);
   const uint32_t* g = ctx->grid_ptr;
   return extract_frames(ctx, &g, 1, p, subdiv_out, hist_num_out);
+}
+
+// sensor_msgs/PointCloud2 ingestion (pcl::fromROSMsg, detect_object.cpp:142)
+static int pc2_check(c3h_ctx* ctx, uint32_t height, uint32_t width, uint32_t point_step, uint32_t row_step,
+                     const int32_t off[4]) {
+  if (!off) return fail(ctx, C3H_ERR_ARG, "pointcloud2: no field offsets");
+  for (int k = 0; k < 4; ++k)
+    if ((k < 3 && off[k] < 0) || off[k] + 4 > (int64_t)point_step)
+      return fail(ctx, C3H_ERR_ARG, "pointcloud2: field x/y/z missing or outside point_step");
+  if (height > 1 && (uint64_t)row_step < (uint64_t)width * point_step)
+    return fail(ctx, C3H_ERR_ARG, "pointcloud2: row_step < width * point_step");
+  return C3H_OK;
+}
+
+int c3h_pointcloud2_to_xyzrgb(const void* d_data, uint32_t height, uint32_t width, uint32_t point_step,
+                              uint32_t row_step, const int32_t offsets[4], int32_t is_bigendian, float* d_out,
+                              void* hip_stream) {
+  if ((!d_data || !d_out) && (uint64_t)height * width > 0) return C3H_ERR_ARG;
+  int rc = pc2_check(nullptr, height, width, point_step, row_step, offsets);
+  if (rc != C3H_OK) return rc;
+  return c3h::launch_pc2_convert(d_data, height, width, point_step, row_step, offsets, is_bigendian ? 1 : 0, d_out,
+                                 (hipStream_t)hip_stream) == hipSuccess
+             ? C3H_OK
+             : C3H_ERR_HIP;
+}
+
+int c3h_voxelize_pointcloud2(c3h_ctx* ctx, const void* data, uint32_t height, uint32_t width, uint32_t point_step,
+                             uint32_t row_step, const int32_t offsets[4], int32_t is_bigendian, int on_device,
+                             float leaf, float z_limit, c3h_grid_info* info) {
+  if (!ctx) return C3H_ERR_ARG;
+  QUIESCE(ctx);
+  int rc = pc2_check(ctx, height, width, point_step, row_step, offsets);
+  if (rc != C3H_OK) return rc;
+  const int64_t n = (int64_t)height * width;
+  if (n > 0 && !data) return fail(ctx, C3H_ERR_ARG, "pointcloud2: no data");
+  if (n >= (int64_t)1 << 24) return fail(ctx, C3H_ERR_RANGE, "c3h_voxelize: at most 16,777,215 points per call");
+  HIPCHK(hipSetDevice(ctx->device));
+  const void* src = data;
+  if (n > 0 && !on_device) {  // the message bytes: rows of row_step (the last one may be short)
+    const size_t bytes = (size_t)(height - 1) * (height > 1 ? row_step : 0) + (size_t)width * point_step;
+    ENSURE(ctx->raw, (bytes + 3) / 4);
+    HIPCHK(hipMemcpyAsync(ctx->raw.p, data, bytes, hipMemcpyHostToDevice, ctx->stream));
+    src = ctx->raw.p;
+  }
+  ENSURE(ctx->pts, (size_t)std::max<int64_t>(n, 1) * 4);
+  HIPCHK(c3h::launch_pc2_convert(src, height, width, point_step, height > 1 ? row_step : width * point_step, offsets,
+                                 is_bigendian ? 1 : 0, ctx->pts.p, ctx->stream));
+  return c3h_voxelize(ctx, ctx->pts.p, n, 1, leaf, z_limit, info);
+}
+
+// SearchObj::setData (search.cpp:539-658) with caller-computed features (VOSCH, GRSD,
+// ConVOSCH, or C3-HLAC rows from elsewhere): the next search consumes them
+int c3h_set_features(c3h_ctx* ctx, const float* feat, const int32_t subdiv_b[3], int32_t dim,
+                     const int32_t* exist, int32_t exist_rule, int on_device) {
+  if (!ctx || !subdiv_b || dim <= 0) return C3H_ERR_ARG;
+  if (subdiv_b[0] < 0 || subdiv_b[1] < 0 || subdiv_b[2] < 0) return fail(ctx, C3H_ERR_ARG, "set_features: subdiv_b");
+  if (!exist && (exist_rule < 0 || exist_rule > 2)) return fail(ctx, C3H_ERR_ARG, "set_features: exist rule");
+  if (exist_rule == C3H_EXIST_VOSCH && dim < 22) return fail(ctx, C3H_ERR_ARG, "set_features: VOSCH rule needs dim >= 22");
+  if (exist_rule == C3H_EXIST_GRSD && dim < 20) return fail(ctx, C3H_ERR_ARG, "set_features: GRSD rule needs dim >= 20");
+  if (exist_rule == C3H_EXIST_C3HLAC && dim < 2) return fail(ctx, C3H_ERR_ARG, "set_features: bad dim");
+  QUIESCE(ctx);
+  HIPCHK(hipSetDevice(ctx->device));
+  const int64_t H = (int64_t)subdiv_b[0] * subdiv_b[1] * subdiv_b[2];
+  if (H > 0 && !feat) return C3H_ERR_ARG;
+  ctx->have_feat = false;
+  ctx->g_valid = false;
+  ctx->rows_valid = false;
+  ENSURE(ctx->feat, (size_t)H * dim);
+  ENSURE(ctx->exist, (size_t)H);
+  if (H > 0) {
+    const hipMemcpyKind k = on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    HIPCHK(hipMemcpyAsync(ctx->feat.p, feat, (size_t)H * dim * sizeof(float), k, ctx->stream));
+    if (exist)
+      HIPCHK(hipMemcpyAsync(ctx->exist.p, exist, (size_t)H * sizeof(int32_t), k, ctx->stream));
+    else
+      HIPCHK(c3h::launch_exist_rule(ctx->feat.p, H, dim, exist_rule, ctx->exist.p, ctx->stream));
+  }
+  if (!on_device) HIPCHK(hipStreamSynchronize(ctx->stream));  // host arrays may be freed on return
+  ctx->hist_num = H;
+  ctx->feat_dim = dim;
+  for (int a = 0; a < 3; ++a) ctx->subdiv_b[a] = subdiv_b[a];
+  ctx->nframes_feat = 1;
+  ctx->feat_sparse = false;
+  ctx->have_feat = true;
+  return C3H_OK;
 }
 
 // rows h with exist[h] == 0 read as 0 (buffers whose empty rows are left stale)

@@ -1,0 +1,86 @@
+"""c3h_set_features: SearchObj::setData with caller-computed features (search.cpp:539-658)
+as the VOSCH / ConVOSCH / GRSD searches of color_voxel_recognition_2 feed it
+(search_new.h:34-76).
+
+- C3-HLAC rows of an extract fed back (host and device, explicit exist) give the same
+  scores and lists as the search right after the extract.
+- 137-dim VOSCH-shaped rows with feature_max normalisation and the setVOSCH exist rule,
+  and 20+-dim GRSD-shaped rows with the setGRSD rule: exist bit-exact against the
+  reference arithmetic restated in numpy, scores within 1e-5 of the float64 oracle."""
+import numpy as np
+import pytest
+
+import pyoracle as po
+from c3hlac import synth
+from conftest import THR
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-5
+
+
+def _vosch_exist(f):
+    t = (f[:, 20] + f[:, 21]).astype(np.float32) * np.float32(2)
+    return (t.astype(np.float64) + 0.001).astype(np.int32)
+
+
+def _grsd_exist(f):
+    e = np.zeros(f.shape[0], np.int32)
+    for i in range(20):
+        e = (e.astype(np.float32) + f[:, i]).astype(np.int32)
+    return e // 26
+
+
+def test_roundtrip_of_extracted_rows(ctx):
+    import torch
+    pts = synth.kinect_scene(200_000, grid=64, leaf=0.02, seed=21)
+    ctx.voxelize(pts, 0.02)
+    sb, hn = ctx.extract(981, THR, 6)
+    f, ex = ctx.features(), ctx.exist()
+    axis_t, var, axis_q = synth.random_bases(981, 40, 3, 8, seed=22)
+    ctx.search_setup(axis_t, var, axis_q)
+    ctx.set_rank(2)
+    l0, _ = ctx.search((2, 2, 2), 20)
+    s0 = ctx.scores()
+    for src, exist, rule in ((f, ex, 0), (torch.from_numpy(f).cuda(), torch.from_numpy(ex).cuda(), 0), (f, None, 0)):
+        ctx.set_features(src, sb, exist, rule)
+        assert np.array_equal(ctx.exist(), ex)
+        ctx.set_rank(2)
+        l1, _ = ctx.search((2, 2, 2), 20)
+        assert np.array_equal(ctx.scores(), s0)
+        assert np.array_equal(l1, l0)
+
+
+@pytest.mark.parametrize("kind", ["vosch", "grsd"])
+def test_external_features_with_reference_exist_rules(ctx, kind):
+    rng = np.random.default_rng(7 if kind == "vosch" else 8)
+    sb = (9, 7, 6)
+    H = int(np.prod(sb))
+    if kind == "vosch":  # 137 = GRSD 20 + colour 117-style bins; f20, f21 = zero-order colour
+        F = 137
+        f = (rng.random((H, F)) * 3).astype(np.float32)
+        f[rng.random(H) < 0.3] = 0
+        exp = _vosch_exist(f)
+        rule = 1
+        fmax = (f.max(0) * np.float32(0.9)).astype(np.float32)
+        fmax[5] = 0
+    else:  # GRSD-21: 20 surface-type pair counts + 1
+        F = 21
+        f = np.floor(rng.random((H, F)) * 60).astype(np.float32)
+        exp = _grsd_exist(f)
+        rule = 2
+        fmax = None
+    ctx.set_features(f, sb, None, rule)
+    assert np.array_equal(ctx.exist(), exp)
+    D = min(F, 30)
+    axis_t, var, axis_q = synth.random_bases(F, D, 2, 5, seed=9)
+    ctx.search_setup(axis_t, var, axis_q, feature_max=fmax)
+    ctx.set_rank(1)
+    thr = int(np.median(exp))
+    lists, nm = ctx.search((2, 2, 2), thr, rotate=False)
+    _, _, scd = po.search(sb, f, exp, synth.whiten(axis_t, var), axis_q, (2, 2, 2), 1, thr, rotate=False,
+                          dbl=True, fmax=fmax, want_scores=True)
+    sc = ctx.scores()
+    assert np.array_equal(sc < 0, scd < 0)
+    ok = scd > 0
+    assert ok.any()
+    np.testing.assert_allclose(sc[ok], scd[ok], rtol=RTOL)
