@@ -264,7 +264,7 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
   // wave-uniform: its two lookups per j are uniform-address LDS reads, all 2 x unroll issued
   // together and moved to SGPRs, and a lane's 4 x-segments are loop invariant.  The general
   // path below steps and looks up (x, y, z) per lane and per j.
-  if (kAx && !kOccPipe && (gx & 255) == 0 && 1024 % gx == 0) {
+  if (kAx && (gx & 255) == 0 && 1024 % gx == 0) {
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int rpj = (kBlock * 4) / gx;                 // rows per j step
     const int xl = (wv * 256) % gx + 4 * (tid & 63);   // this lane's x (every chunk, every j)
@@ -278,11 +278,19 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
     const int lg = gx == 256 ? 8 : gx == 512 ? 9 : 10;
     const int64_t nch = (n4 + kChunk4 - 1) / kChunk4;
     uint4 w[kOccBitsUnroll];
+    auto chunk_of = [&](int64_t i) { return i * gdx + (bx + i) % gdx; };
+    if (kOccPipe && chunk_of(0) < nch) load_chunk(w, chunk_of(0) * kChunk4);
     for (int64_t i = 0; i * gdx < nch; ++i) {
-      const int64_t cidx = i * gdx + (bx + i) % gdx;
+      const int64_t cidx = chunk_of(i);
       if (cidx >= nch) continue;  // uniform: the last, partial round of chunks
       const int64_t c0 = cidx * kChunk4;
-      load_chunk(w, c0);
+      uint4 nx[kOccBitsUnroll];
+      if constexpr (kOccPipe) {  // the next chunk's loads in flight while this one is processed
+        const int64_t cn = chunk_of(i + 1);
+        if (cn < nch) load_chunk(nx, cn * kChunk4);
+      } else {
+        load_chunk(w, c0);
+      }
       // uniform 32-bit row arithmetic (rows < 2^24: nvox < 2^32 is host-checked): the
       // chunk's first row, then (y, z) stepped by whole rows per j
       const uint32_t row0 = (uint32_t)(((uint64_t)c0 * 4 + (uint64_t)wv * 256) >> lg);
@@ -321,6 +329,10 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
             }
           }
         }
+      }
+      if constexpr (kOccPipe) {
+#pragma unroll
+        for (int j = 0; j < kOccBitsUnroll; ++j) w[j] = nx[j];
       }
     }
     __syncthreads();

@@ -141,7 +141,7 @@ __device__ __forceinline__ void compress_rows_body(const CompressRows& cr, int b
 // workgroup (wave = 32 rows x 4 column tiles of 32 = Dpad <= 128); per 32-feature chunk
 // the rows' feature slice and P's slice are staged in LDS (prefetched one chunk ahead in
 // registers), then 16 k-pair steps of 4 MFMAs (one A float, four B floats per lane).
-constexpr int kMR = 128, kMK = 32;
+constexpr int kMR = 128, kMK = 16;
 constexpr int kMAS = kMK + 1;  // A slice row stride (lanes read 32 rows of one column)
 __host__ __device__ inline size_t compress_mfma_lds_bytes() {
   return sizeof(float) * ((size_t)kMR * kMAS + (size_t)kMK * 128);
@@ -214,14 +214,18 @@ __device__ __forceinline__ void compress_mfma_body(const CompressRows& cr, int b
       for (int i = 0; i < kPE; ++i) sbm[tid + i * kBlock] = pb[i];
       if (c + 1 < nch) load(c + 1);
       lds_barrier();
-      const int kn = min(kMK, F - c * kMK);
+      // the slice is zero past F (A and P), so every chunk runs all kMK: the k loop unrolls
+      // and its LDS reads are issued ahead of the MFMAs that use them
       const float* arow = sa + (wave * 32 + (lane & 31)) * kMAS + (lane >> 5);
       const float* bcol = sbm + (lane >> 5) * 128 + (lane & 31);
-      for (int k = 0; k < kn; k += 2) {
-        const float av = arow[k];
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bcol[k * 128 + 32 * t], acc[t], 0, 0, 0);
+      for (int k = 0; k < kMK; k += 2) {
+        const float av = arow[k];
+        float bv[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bv[t] = bcol[k * 128 + 32 * t];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[t], acc[t], 0, 0, 0);
       }
     }
     // C/D map: column lane & 31 (+ 32 t), row (q & 3) + 8 (q >> 2) + 4 (lane >> 5)
@@ -237,6 +241,92 @@ __device__ __forceinline__ void compress_mfma_body(const CompressRows& cr, int b
       }
     }
   }
+}
+
+// The same GEMM with the slices moved by LDS DMA (global_load_lds, no VGPR staging) into a
+// ring of three chunk buffers, two chunks ahead of the MFMAs: the row gather's HBM latency
+// is covered by two chunks of matrix work instead of one, and the registers stay with the
+// accumulators.  Without setNormalizeVal only (the DMA cannot divide by feature_max); lanes
+// past F / past the row list / past Dpad read a zero word.  A chunk buffer is the
+// kMR x kMAS feature slice (pad column: a zero) then the kMK x 128 P slice.
+constexpr int kMDA = (kMR * kMAS + kBlock - 1) / kBlock;  // A-slice DMA dwords per lane
+constexpr int kMDP = kMK * 128 / kBlock;                  // P-slice DMA dwords per lane
+constexpr int kMDBuf = kMDA * kBlock + kMK * 128;         // floats per ring buffer
+__host__ __device__ inline size_t compress_dma_lds_bytes() { return sizeof(float) * 3 * (size_t)kMDBuf; }
+
+__device__ __forceinline__ void compress_mfma_dma_body(const CompressRows& cr, int bid, int nblk, int64_t f,
+                                                       float* csm, const float* zero) {
+  const float* __restrict__ feat = cr.feat + f * cr.s_feat;
+  float* __restrict__ G = cr.G + f * cr.s_G;
+  const int32_t* __restrict__ rows = cr.rows + f * cr.s_rows;
+  const int F = cr.F, D = cr.D, Dpad = cr.Dpad;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = (int)cr.nrows[f * cr.s_nrows];
+  const int nch = (F + kMK - 1) / kMK;
+  for (int r0 = bid * kMR; r0 < n; r0 += nblk * kMR) {
+    // this lane's DMA sources: A dword i = j * kBlock + tid -> (row i / kMAS, k i % kMAS)
+    int32_t arow_h[kMDA];  // subdivision of this lane's A dword j, -1 = padding
+#pragma unroll
+    for (int j = 0; j < kMDA; ++j) {
+      const int i = j * kBlock + tid, r = i / kMAS, k = i - r * kMAS;
+      arow_h[j] = (i < kMR * kMAS && k < kMK && r0 + r < n) ? rows[r0 + r] : -1;
+    }
+    auto issue = [&](int c) {
+      float* buf = csm + (c % 3) * kMDBuf;
+#pragma unroll
+      for (int j = 0; j < kMDA; ++j) {
+        const int i = j * kBlock + tid, col = c * kMK + (i % kMAS);
+        const float* src = (arow_h[j] >= 0 && col < F) ? feat + (int64_t)arow_h[j] * F + col : zero;
+        __builtin_amdgcn_global_load_lds(src, buf + j * kBlock + wave * 64, 4, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < kMDP; ++j) {
+        const int e = j * kBlock + tid, k = c * kMK + e / 128, col = e % 128;
+        const float* src = (k < F && col < Dpad) ? cr.PT + (int64_t)k * Dpad + col : zero;
+        __builtin_amdgcn_global_load_lds(src, buf + kMDA * kBlock + j * kBlock + wave * 64, 4, 0, 0);
+      }
+    };
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // row indices in; no stores in flight
+    issue(0);
+    if (nch > 1) issue(1);
+    mf_f32x16 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[t][q] = 0.0f;
+    for (int c = 0; c < nch; ++c) {
+      // chunk c landed (the next chunk's kMDA + kMDP DMAs may still be in flight), in every wave
+      if (c + 1 < nch) __asm__ volatile("s_waitcnt vmcnt(%0)" ::"n"(kMDA + kMDP) : "memory");
+      else __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();
+      if (c + 2 < nch) issue(c + 2);  // into the buffer chunk c - 1 used (every wave is past it)
+      const float* buf = csm + (c % 3) * kMDBuf;
+      const float* arow = buf + (wave * 32 + (lane & 31)) * kMAS + (lane >> 5);
+      const float* bcol = buf + kMDA * kBlock + (lane >> 5) * 128 + (lane & 31);
+#pragma unroll 2
+      for (int k = 0; k < kMK; k += 2) {
+        const float av = arow[k];
+        float bv[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bv[t] = bcol[k * 128 + 32 * t];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[t], acc[t], 0, 0, 0);
+      }
+    }
+    lds_barrier();  // the ring is refilled by the next row block
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int rr = r0 + wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
+      if (rr >= n) continue;
+      const int64_t hh = rows[rr];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int col = 32 * t + (lane & 31);
+        if (col < D) G[hh * D + col] = acc[t][q];
+      }
+    }
+  }
+  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS DMA outlives the workgroup
 }
 
 // Fast path (D <= 256, D % 4 == 0, M*r <= 256) = the sparse search below: 32 list
