@@ -192,6 +192,12 @@ int c3h_get_exist(c3h_ctx* ctx, int32_t* out, int on_device);
 int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_t D,
                      int32_t F, const float* axis_q, int32_t M, int32_t r,
                      const float* feature_max, int32_t feature_max_len);
+/* Search precision of the matrix-core compress (grids of >= 65,536 subdivisions, e.g.
+ * BASELINE config 5; D <= 128): fp16 = 1 rounds the normalised features and the whitened
+ * axis to f16 and accumulates in f32 on v_mfma_f32_32x32x16_f16; scores then agree with
+ * the float64 oracle within 2e-3 relative (fp16 = 0, the default: fp32, 1e-5).  Smaller
+ * grids and the pipelined c3h_run_frames path always compress in fp32. */
+int c3h_set_search_precision(c3h_ctx* ctx, int32_t fp16);
 /* SearchObj::setRank / SearchObjMulti::setRank (search.cpp:130-143, 778-815):
  * (re)allocates the per-model lists; modes start at S_MODE_1. */
 int c3h_set_rank(c3h_ctx* ctx, int32_t rank);

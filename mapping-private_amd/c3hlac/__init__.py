@@ -154,6 +154,10 @@ class Context:
             self._chk(self.lib.c3h_get_features(self.h, ptr(out), 0), "get_features")
         return out
 
+    def set_search_precision(self, fp16):
+        """c3h_set_search_precision: fp16 matrix-core compress for large grids."""
+        self._chk(self.lib.c3h_set_search_precision(self.h, int(bool(fp16))), "set_search_precision")
+
     def set_features(self, feat, subdiv, exist=None, rule=0):
         """SearchObj::setData with caller-computed features (c3h_set_features): feat
         (hist_num, dim) numpy or torch device tensor, exist None -> derived by rule

@@ -254,6 +254,8 @@ struct SparseCompress {
   int F, D, Dpad, fmax_len;
   int64_t H;
   int64_t s_feat, s_G, s_rows, s_nrows;  // per-frame strides
+  const _Float16* PT16 = nullptr;         // fp16 search precision: f16 axis, 128 x Fp16
+  int Fp16 = 0;
 };
 bool compress_rows_ok(int F, int Dpad);
 hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc, hipStream_t s);
@@ -379,6 +381,9 @@ struct c3h_ctx {
   int D = 0, F = 0, M = 0, r = 0, Dpad = 0;
   bool compress = true;
   c3h::DevBuf<float> axis_pt;       // F x Dpad (transposed, whitened)
+  c3h::DevBuf<_Float16> axis_pt16;  // 128 x Fp16 f16 copy (column-major) for the fp16 compress
+  int Fp16 = 0;
+  bool prec16 = false;              // c3h_set_search_precision: fp16 matrix-core compress
   c3h::DevBuf<float> axis_q;        // M x r x D
   c3h::DevBuf<float> fmax;
   int fmax_len = 0;

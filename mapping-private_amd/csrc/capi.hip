@@ -489,6 +489,10 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
       sc = c3h::SparseCompress{ctx->feat.p, ctx->axis_pt.p, ctx->fmax.p, ctx->G.p, ctx->rows.p,
                                ctx->tileflags.p + 2 + (ctx->tile_epoch & 1), ctx->F, ctx->D, ctx->Dpad,
                                ctx->fmax_len, H, H * ctx->F, H * ctx->D, H, ctx->tf_stride};
+      if (ctx->prec16 && ctx->Fp16 > 0) {
+        sc.PT16 = ctx->axis_pt16.p;
+        sc.Fp16 = ctx->Fp16;
+      }
       ctx->g_valid = true;
       ctx->g_sparse = true;
     }
@@ -647,6 +651,7 @@ void c3h_destroy(c3h_ctx* ctx) {
   release(ctx->gcnt);
   release(ctx->lut);
   release(ctx->axis_pt);
+  release(ctx->axis_pt16);
   release(ctx->axis_q);
   release(ctx->fmax);
   release(ctx->G);
@@ -1346,6 +1351,14 @@ int c3h_get_exist(c3h_ctx* ctx, int32_t* out, int on_device) {
   return C3H_OK;
 }
 
+int c3h_set_search_precision(c3h_ctx* ctx, int32_t fp16) {
+  if (!ctx) return C3H_ERR_ARG;
+  QUIESCE(ctx);
+  ctx->prec16 = fp16 != 0;
+  ctx->g_valid = false;
+  return C3H_OK;
+}
+
 int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_t D, int32_t F,
                      const float* axis_q, int32_t M, int32_t r, const float* feature_max,
                      int32_t feature_max_len) {
@@ -1374,6 +1387,18 @@ int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_
   }
   ENSURE(ctx->axis_pt, pt.size());
   HIPCHK(hipMemcpy(ctx->axis_pt.p, pt.data(), pt.size() * 4, hipMemcpyHostToDevice));
+  // f16 copy for the fp16 matrix-core compress: 128 columns x Fp16, column-major
+  if (D <= 128) {
+    const int Fp16 = (F + 15) / 16 * 16;
+    std::vector<_Float16> p16((size_t)128 * Fp16, (_Float16)0.0f);
+    for (int d = 0; d < D; ++d)
+      for (int j = 0; j < F; ++j) p16[(size_t)d * Fp16 + j] = (_Float16)pt[(size_t)j * Dpad + d];
+    ENSURE(ctx->axis_pt16, p16.size());
+    HIPCHK(hipMemcpy(ctx->axis_pt16.p, p16.data(), p16.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    ctx->Fp16 = Fp16;
+  } else {
+    ctx->Fp16 = 0;
+  }
   ENSURE(ctx->axis_q, (size_t)M * r * D);
   HIPCHK(hipMemcpy(ctx->axis_q.p, axis_q, (size_t)M * r * D * 4, hipMemcpyHostToDevice));
   // transposed basis for the fast score path: qt[d][m*r + i] = axis_q[m][i][d]

@@ -201,6 +201,10 @@ __global__ __launch_bounds__(kBlock, 3) void compress_dma_kernel(CompressRows cr
   compress_mfma_dma_body(cr, blockIdx.x, gridDim.x, blockIdx.y, cd_smem, g_zero_word);
 }
 
+__global__ __launch_bounds__(kBlock) void compress_f16_kernel(CompressRows cr, const _Float16* PT16, int Fp16) {
+  compress_f16_body(cr, PT16, Fp16, blockIdx.x, gridDim.x, blockIdx.y);
+}
+
 __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch b) {
   extern __shared__ __attribute__((aligned(16))) float sl_smem[];
   score_list_body(b, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y, sl_smem);
@@ -394,6 +398,14 @@ hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc,
     if (sc->H >= kCompressMfmaRows) {  // large grids: the f32 matrix-core compress, then the gate
       // persistent: every workgroup resident (row blocks b, b + grid, ...), so no partial
       // last round of workgroups
+      if (sc->PT16) {  // fp16 search precision
+        const int64_t rblocks = (sc->H + kMR - 1) / kMR;
+        const unsigned ncomp = (unsigned)std::min<int64_t>(rblocks, 2048);
+        compress_f16_kernel<<<dim3(ncomp, nf), kBlock, 0, s>>>(cr, sc->PT16, sc->Fp16);
+        gate_kernel<<<dim3(ngate, nf), kBlock, 0, s>>>(a);
+        goto score;
+      }
+      {
       const bool dma = sc->fmax_len == 0;  // the DMA ring cannot normalise by feature_max
       static thread_local int c_slots[2] = {0, 0}, c_dev = -1;
       int dev = 0;
@@ -421,6 +433,7 @@ hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc,
       else
         compress_mfma_kernel<<<dim3(ncomp, nf), kBlock, compress_mfma_lds_bytes(), s>>>(cr);
       gate_kernel<<<dim3(ngate, nf), kBlock, 0, s>>>(a);
+      }
     } else {
       const size_t lds = compress_rows_lds_bytes(sc->Dpad);
       // compress workgroups: surface frames have ~700 non-empty rows (~44 row blocks)
@@ -430,6 +443,7 @@ hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc,
   } else {
     gate_kernel<<<dim3(ngate, nf), kBlock, 0, s>>>(a);
   }
+score:
   const size_t lds = score_list_lds_bytes(a.D, a.mpg);
   const unsigned groups = (unsigned)((a.M + a.mpg - 1) / a.mpg);
   // workgroups per (group, frame): list chunks beyond the cap loop (dense scenes only);

@@ -329,6 +329,87 @@ __device__ __forceinline__ void compress_mfma_dma_body(const CompressRows& cr, i
   __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS DMA outlives the workgroup
 }
 
+// fp16 variant of the matrix-core compress (c3h_set_search_precision): the normalised
+// features are rounded to f16 on load, the whitened axis is kept as f16 (PT16: 128
+// columns x Fp16 = F rounded up to 16, column-major so a lane's 8 consecutive k are one
+// 16-B load), products accumulate in f32 on v_mfma_f32_32x32x16_f16.  No LDS: each wave
+// reads its 32 rows' features and the (L2-resident) f16 axis straight into its operand
+// registers, one k step ahead.  Stated tolerance: scores within 2e-3 relative of the
+// float64 oracle (tests/test_gpu_parity.py::test_config5_dense_512_periodic).
+typedef _Float16 mf_f16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void compress_f16_body(const CompressRows& cr, const _Float16* __restrict__ PT16,
+                                                  int Fp16, int bid, int nblk, int64_t f) {
+  const float* __restrict__ feat = cr.feat + f * cr.s_feat;
+  const float* __restrict__ fmax = cr.fmax;
+  float* __restrict__ G = cr.G + f * cr.s_G;
+  const int32_t* __restrict__ rows = cr.rows + f * cr.s_rows;
+  const int F = cr.F, D = cr.D, fmax_len = cr.fmax_len;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = (int)cr.nrows[f * cr.s_nrows];
+  const int kh = 8 * (lane >> 5);
+  for (int r0 = bid * kMR; r0 < n; r0 += nblk * kMR) {
+    const int myrow = r0 + wave * 32 + (lane & 31);
+    const int64_t abase = myrow < n ? (int64_t)rows[myrow] * F : -1;
+    auto load_a = [&](int k0, mf_f16x8& av) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = k0 + kh + j;
+        float v = 0.0f;
+        if (abase >= 0 && k < F) {
+          v = feat[abase + k];
+          if (k < fmax_len) {  // setData max-normalisation (search.cpp:563-570)
+            const float mx = fmax[k];
+            if (mx == 0.0f) v = 0.0f;
+            else if (v == mx) v = 1.0f;
+            else v = __fdiv_rn(v, mx);
+          }
+        }
+        av[j] = (_Float16)v;
+      }
+    };
+    auto load_b = [&](int k0, mf_f16x8 (&bv)[4]) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        bv[t] = *reinterpret_cast<const mf_f16x8*>(PT16 + (int64_t)(32 * t + (lane & 31)) * Fp16 + k0 + kh);
+    };
+    mf_f32x16 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[t][q] = 0.0f;
+    mf_f16x8 a_cur, b_cur[4];
+    load_a(0, a_cur);
+    load_b(0, b_cur);
+    for (int k0 = 0; k0 < Fp16; k0 += 16) {
+      mf_f16x8 a_nxt, b_nxt[4];
+      const bool more = k0 + 16 < Fp16;
+      if (more) {
+        load_a(k0 + 16, a_nxt);
+        load_b(k0 + 16, b_nxt);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_cur, b_cur[t], acc[t], 0, 0, 0);
+      if (more) {
+        a_cur = a_nxt;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) b_cur[t] = b_nxt[t];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int rr = r0 + wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
+      if (rr >= n) continue;
+      const int64_t hh = rows[rr];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int col = 32 * t + (lane & 31);
+        if (col < D) G[hh * D + col] = acc[t][q];
+      }
+    }
+  }
+}
+
 // Fast path (D <= 256, D % 4 == 0, M*r <= 256) = the sparse search below: 32 list
 // entries per workgroup.  Box features are summed with float4 loads and staged k-major in
 // LDS (lanes = positions: conflict-free); the projection onto all M*r basis rows is a

@@ -439,6 +439,22 @@ def test_config5_dense_512_periodic(ctx):
         assert float(lists[m, 0]["score"]) == flat[m, p]
         assert (int(lists[m, 0]["z"]), int(lists[m, 0]["y"]), int(lists[m, 0]["x"])) == \
             np.unravel_index(p, (n - 1,) * 3)
+    # fp16 matrix-core compress (c3h_set_search_precision): stated tolerance 2e-3 relative
+    ctx.set_search_precision(True)
+    try:
+        ctx.set_rank(1)
+        lists16, _ = ctx.search((2, 2, 2), 100)
+        sc16 = ctx.scores().reshape(M, n - 1, n - 1, n - 1)
+        assert (sc16 > 0).all()
+        inner16 = sc16[:, 1:n - 2, 1:n - 2, 1:n - 2].reshape(M, -1)
+        assert (inner16 == inner16[:, :1]).all()
+        np.testing.assert_allclose(inner16[:, 0], s64, rtol=2e-3)
+        assert not np.array_equal(inner16[:, 0], inner[:, 0])  # the f16 path really ran
+        flat16 = sc16.reshape(M, -1)
+        for m in range(M):
+            assert float(lists16[m, 0]["score"]) == flat16[m].max()
+    finally:
+        ctx.set_search_precision(False)
 
 
 REF_CLOUDS = ["noisy_torus_blue.pcd", "bowl1_0000.pcd", "tmp_normal.pcd", "obj_torus_black.pcd",

@@ -23,6 +23,8 @@ with c3hlac.Context(0) as ctx:
     axis_t, var, axis_q = synth.random_bases(981, D, M, R, seed=synth.BASE_SEED)
     ctx.search_setup(axis_t, var, axis_q)
     ctx.set_rank(1)
+    if "--fp16" in sys.argv:
+        ctx.set_search_precision(True)
     res = []
     for rep in range(4):
         ctx.timing(True)
