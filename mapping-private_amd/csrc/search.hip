@@ -394,7 +394,7 @@ hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc,
   const unsigned nf = (unsigned)a.nframes;
   if (sc) {  // compress (non-empty rows) and gate in one launch
     const CompressRows cr{sc->feat, sc->PT, sc->fmax, sc->G, sc->rows, sc->nrows, sc->F, sc->D, sc->Dpad,
-                          sc->fmax_len, sc->s_feat, sc->s_G, sc->s_rows, sc->s_nrows};
+                          sc->fmax_len, sc->s_feat, sc->s_G, sc->s_rows, sc->s_nrows, sc->H};
     if (sc->H >= kCompressMfmaRows) {  // large grids: the f32 matrix-core compress, then the gate
       // persistent: every workgroup resident (row blocks b, b + grid, ...), so no partial
       // last round of workgroups

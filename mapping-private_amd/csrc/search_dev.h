@@ -29,6 +29,7 @@ struct CompressRows {
   const uint32_t* nrows;
   int F, D, Dpad, fmax_len;
   int64_t s_feat, s_G, s_rows, s_nrows;  // per-frame strides (frame = launch y / z index)
+  int64_t H = 0;  // subdivisions per frame: a list of all H rows is read as rows 0..H-1 in order
 };
 
 __device__ __forceinline__ void compress_rows_body(const CompressRows& cr, int bid, int nblk, int64_t f,
@@ -265,11 +266,12 @@ __device__ __forceinline__ void compress_mfma_dma_body(const CompressRows& cr, i
   const int nch = (F + kMK - 1) / kMK;
   for (int r0 = bid * kMR; r0 < n; r0 += nblk * kMR) {
     // this lane's DMA sources: A dword i = j * kBlock + tid -> (row i / kMAS, k i % kMAS)
+    const bool ident = n == cr.H;  // dense frame: the list is a permutation, read in memory order
     int32_t arow_h[kMDA];  // subdivision of this lane's A dword j, -1 = padding
 #pragma unroll
     for (int j = 0; j < kMDA; ++j) {
       const int i = j * kBlock + tid, r = i / kMAS, k = i - r * kMAS;
-      arow_h[j] = (i < kMR * kMAS && k < kMK && r0 + r < n) ? rows[r0 + r] : -1;
+      arow_h[j] = (i < kMR * kMAS && k < kMK && r0 + r < n) ? (ident ? r0 + r : rows[r0 + r]) : -1;
     }
     auto issue = [&](int c) {
       float* buf = csm + (c % 3) * kMDBuf;
@@ -318,7 +320,7 @@ __device__ __forceinline__ void compress_mfma_dma_body(const CompressRows& cr, i
     for (int q = 0; q < 16; ++q) {
       const int rr = r0 + wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
       if (rr >= n) continue;
-      const int64_t hh = rows[rr];
+      const int64_t hh = ident ? rr : rows[rr];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int col = 32 * t + (lane & 31);
@@ -349,8 +351,11 @@ __device__ __forceinline__ void compress_f16_body(const CompressRows& cr, const 
   const int n = (int)cr.nrows[f * cr.s_nrows];
   const int kh = 8 * (lane >> 5);
   for (int r0 = bid * kMR; r0 < n; r0 += nblk * kMR) {
+    // every subdivision listed (dense frame): the list is a permutation of 0..H-1, so row
+    // block r0 covers subdivisions r0.. in memory order instead (contiguous feature rows)
+    const bool ident = n == cr.H;
     const int myrow = r0 + wave * 32 + (lane & 31);
-    const int64_t abase = myrow < n ? (int64_t)rows[myrow] * F : -1;
+    const int64_t abase = myrow < n ? (int64_t)(ident ? myrow : rows[myrow]) * F : -1;
     auto load_a = [&](int k0, mf_f16x8& av) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -400,7 +405,7 @@ __device__ __forceinline__ void compress_f16_body(const CompressRows& cr, const 
     for (int q = 0; q < 16; ++q) {
       const int rr = r0 + wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
       if (rr >= n) continue;
-      const int64_t hh = rows[rr];
+      const int64_t hh = ident ? rr : rows[rr];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int col = 32 * t + (lane & 31);
