@@ -163,6 +163,38 @@ int c3h_extract(c3h_ctx* ctx, const c3h_extract_params* p, int32_t subdiv_out[3]
 /* the features the context holds (the last extract, or after c3h_run_frames the last
  * frame's): getSubdivNum, hist_num and the dimension (981 / 117; 0 before any extract) */
 int c3h_get_feature_info(c3h_ctx* ctx, int32_t subdiv_out[3], int64_t* hist_num, int32_t* dim);
+/* ---- VOSCH / GRSD features (color_chlac/include/color_chlac/
+ * grsd_colorCHLAC_tools.hpp), on the points and grid of the last c3h_voxelize (the points
+ * it kept; a device input buffer must stay alive).
+ * c3h_compute_normals: pcl::NormalEstimation with radius search (computeNormal, :63-87;
+ * normals_radius_search = 0.02, grsd_colorCHLAC_tools.h:28): covariance of the points
+ * within `radius` (float distances, the point included), smallest-eigenvalue eigenvector
+ * (double), flipped towards `viewpoint` (NULL = origin), curvature; < 3 neighbours -> NaN.
+ * c3h_get_normals: n x 4 floats (nx, ny, nz, curvature) in input order.
+ * c3h_extract_grsd: extractGRSDSignature21 (:131-296): per occupied voxel PCL's
+ * PrincipalRadiiRSD (computeRSD: nr_subdiv 5, plane radius 0.2) over the points within
+ * max(rsd_radius, leaf sqrt(3)/2) of its centroid, get_type (:99-118), and the 6 x 6 type
+ * transitions with its 26 neighbour voxels per subdivision (setVoxelFilter's subdivision
+ * rules); features = the first 20 upper-triangle bins (x 20/26 with normalize), exist by
+ * the setGRSD rule.  c3h_get_rsd: r_min / r_max and the type per occupied voxel (leaf
+ * layout order); returns their count.
+ * c3h_extract_vosch: extractVOSCH (:832-843): [GRSD-20 | C3-HLAC-117] = 137 floats per
+ * subdivision (the C3 part as c3h_extract with variant 117, thr, lut_double), exist by
+ * the setVOSCH rule; the next c3h_search uses them (search_setup with F = 137).
+ * The PCL algorithms are restated (PCL is not part of the reference tree); radius-search
+ * ties are broken by point index. */
+typedef struct {
+  int32_t subdiv;     /* subdivision_size (0 = one histogram) */
+  int32_t offset[3];
+  float rsd_radius;   /* rsd_radius_search (0.01 in the reference) */
+  int32_t normalize;  /* is_normalize (default false) */
+} c3h_grsd_params;
+int c3h_compute_normals(c3h_ctx* ctx, float radius, const float viewpoint[3]);
+int c3h_get_normals(c3h_ctx* ctx, float* out, int on_device);
+int c3h_extract_grsd(c3h_ctx* ctx, const c3h_grsd_params* p, int32_t subdiv_out[3], int64_t* hist_num);
+int c3h_get_rsd(c3h_ctx* ctx, float* radii, int32_t* types, int on_device);
+int c3h_extract_vosch(c3h_ctx* ctx, const c3h_grsd_params* p, const int32_t thr[3], int32_t lut_double,
+                      int32_t subdiv_out[3], int64_t* hist_num);
 /* SearchObj::setData(subdiv_b, feature) (search.cpp:539-658) with features computed
  * elsewhere (VOSCH / ConVOSCH / GRSD extractors, search_new.h:34-76, or stored C3-HLAC
  * rows): subdiv_b[0]*[1]*[2] rows of dim floats, row h = x + y*xn + z*xn*yn.  exist =

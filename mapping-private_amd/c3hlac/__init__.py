@@ -154,6 +154,49 @@ class Context:
             self._chk(self.lib.c3h_get_features(self.h, ptr(out), 0), "get_features")
         return out
 
+    def compute_normals(self, radius=0.02, viewpoint=(0.0, 0.0, 0.0)):
+        vp = (C.c_float * 3)(*viewpoint)
+        self._chk(self.lib.c3h_compute_normals(self.h, float(radius), vp), "compute_normals")
+
+    def normals(self, n):
+        out = np.zeros((n, 4), np.float32)
+        self._chk(self.lib.c3h_get_normals(self.h, ptr(out), 0), "get_normals")
+        return out
+
+    @staticmethod
+    def _grsd_params(subdiv, offset, rsd_radius, normalize):
+        p = _capi.GrsdParams()
+        p.subdiv = int(subdiv)
+        p.offset = (C.c_int32 * 3)(*[int(o) for o in offset])
+        p.rsd_radius = float(rsd_radius)
+        p.normalize = int(bool(normalize))
+        return p
+
+    def extract_grsd(self, subdiv=0, offset=(0, 0, 0), rsd_radius=0.01, normalize=False):
+        sb = (C.c_int32 * 3)()
+        hn = C.c_int64()
+        p = self._grsd_params(subdiv, offset, rsd_radius, normalize)
+        self._chk(self.lib.c3h_extract_grsd(self.h, C.byref(p), sb, C.byref(hn)), "extract_grsd")
+        self.hist_num, self.subdiv, self.variant = int(hn.value), tuple(int(x) for x in sb), 20
+        return self.subdiv, self.hist_num
+
+    def rsd(self):
+        n = self._chk(self.lib.c3h_get_rsd(self.h, None, None, 0), "get_rsd")
+        radii = np.zeros((n, 2), np.float32)
+        types = np.zeros(n, np.int32)
+        self._chk(self.lib.c3h_get_rsd(self.h, ptr(radii), ptr(types), 0), "get_rsd")
+        return radii, types
+
+    def extract_vosch(self, thr, subdiv=0, offset=(0, 0, 0), rsd_radius=0.01, normalize=False, lut_double=True):
+        sb = (C.c_int32 * 3)()
+        hn = C.c_int64()
+        p = self._grsd_params(subdiv, offset, rsd_radius, normalize)
+        t = (C.c_int32 * 3)(*[int(x) for x in thr])
+        self._chk(self.lib.c3h_extract_vosch(self.h, C.byref(p), t, int(bool(lut_double)), sb, C.byref(hn)),
+                  "extract_vosch")
+        self.hist_num, self.subdiv, self.variant = int(hn.value), tuple(int(x) for x in sb), 137
+        return self.subdiv, self.hist_num
+
     def set_search_precision(self, fp16):
         """c3h_set_search_precision: fp16 matrix-core compress for large grids."""
         self._chk(self.lib.c3h_set_search_precision(self.h, int(bool(fp16))), "set_search_precision")

@@ -34,6 +34,11 @@ class ExtractParams(C.Structure):
                 ("offset", C.c_int32 * 3), ("lut_double", C.c_int32)]
 
 
+class GrsdParams(C.Structure):
+    _fields_ = [("subdiv", C.c_int32), ("offset", C.c_int32 * 3), ("rsd_radius", C.c_float),
+                ("normalize", C.c_int32)]
+
+
 class Det(C.Structure):
     _fields_ = [("score", C.c_double), ("x", C.c_int32), ("y", C.c_int32), ("z", C.c_int32),
                 ("mode", C.c_int32)]
@@ -88,6 +93,12 @@ _SIGS = {
     "c3h_get_scores": (C.c_int, [_P, _P, C.POINTER(C.c_int64), C.c_int]),
     "c3h_remove_overlap": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(C.c_int32), _P]),
     "c3h_pca_read": (C.c_int, [C.c_char_p, C.c_int32, _P, _P, _P, C.POINTER(C.c_int32), C.c_int32]),
+    "c3h_compute_normals": (C.c_int, [_P, C.c_float, _P]),
+    "c3h_get_normals": (C.c_int, [_P, _P, C.c_int]),
+    "c3h_extract_grsd": (C.c_int, [_P, C.POINTER(GrsdParams), C.POINTER(C.c_int32), C.POINTER(C.c_int64)]),
+    "c3h_get_rsd": (C.c_int, [_P, _P, _P, C.c_int]),
+    "c3h_extract_vosch": (C.c_int, [_P, C.POINTER(GrsdParams), C.POINTER(C.c_int32), C.c_int32,
+                                    C.POINTER(C.c_int32), C.POINTER(C.c_int64)]),
     "c3h_set_search_precision": (C.c_int, [_P, C.c_int32]),
     "c3h_set_features": (C.c_int, [_P, _P, C.POINTER(C.c_int32), C.c_int32, _P, C.c_int32, C.c_int]),
     "c3h_pca_write": (C.c_int, [C.c_char_p, C.c_int32, C.c_int32, _P, _P, _P]),

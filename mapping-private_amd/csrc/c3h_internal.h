@@ -179,6 +179,37 @@ hipError_t launch_offcell_delta(const int32_t* rec, int nrec, const C3Launch& l,
                                 const int sb[3], float inv_s, hipStream_t s);
 hipError_t launch_c3_finalize(const unsigned long long* acc64, int64_t hist_num, int variant,
                               float* feat, int32_t* exist, int nframes, hipStream_t s);
+// radius-search grid over a point cloud (rsd.hip): cells of `cell` metres from origin,
+// the points sorted by cell, per cell its [cstart, cend) range in `sorted`
+struct NbrGrid {
+  const float4* pts;
+  int64_t n;
+  float origin[3];
+  float cell, inv_cell;
+  int dim[3];
+  const uint32_t* sorted;
+  const uint32_t* cstart;
+  const uint32_t* cend;
+};
+struct GrsdArgs {
+  const float4* cent;     // downsampled centroids, leaf-layout order
+  int64_t nc;
+  const int32_t* layout;  // leaf layout (-1 empty)
+  const int32_t* types;   // per centroid
+  int32_t* trans;         // hist_num x 6 x 6
+  int div_b[3], min_b[3], off[3], sb[3];
+  float leaf, inv_leaf, inv_s;
+  int hist1;              // one histogram for the whole cloud
+};
+hipError_t nbr_build(NbrGrid& g, uint32_t* keys, uint32_t* keys2, uint32_t* idx, uint32_t* idx2, void* tmp,
+                     size_t* tmp_bytes, hipStream_t s);
+hipError_t launch_normals(const NbrGrid& g, float radius, const float vp[3], float4* out, hipStream_t s);
+hipError_t launch_rsd(const NbrGrid& g, const float4* nrm, const float4* cent, int64_t nc, float max_dist,
+                      float2* radii, int32_t* types, hipStream_t s);
+hipError_t launch_grsd(const GrsdArgs& a, hipStream_t s);
+hipError_t launch_grsd_feat(const int32_t* trans, int64_t H, float norm, float* out, int stride, hipStream_t s);
+hipError_t launch_vosch_concat(const float* grsd, const float* c3, const int32_t* exist, int64_t H, float* out,
+                               hipStream_t s);
 // sensor_msgs/PointCloud2 bytes -> n x float4 (x, y, z, rgb bits) (ingest.hip)
 hipError_t launch_pc2_convert(const void* data, uint32_t height, uint32_t width, uint32_t point_step,
                               uint32_t row_step, const int32_t off[4], int big, float* out, hipStream_t s);
@@ -319,6 +350,18 @@ struct c3h_ctx {
   const uint32_t* grid_ptr = nullptr;  // the grid in use (owned or bound)
   c3h::DevBuf<float> pts;           // staging copy of host points
   c3h::DevBuf<uint32_t> raw;        // staging copy of host PointCloud2 bytes
+  c3h::DevBuf<float> dsbuf;         // host readback staging of the downsampled cloud
+  // normals / RSD / GRSD (rsd.hip): radius-search grid of the last voxelize's points
+  c3h::DevBuf<float4> normals;
+  bool normals_valid = false;
+  c3h::NbrGrid nbr{};
+  c3h::DevBuf<uint32_t> nkeys, nkeys2, nidx, nidx2, ncstart, ncend;
+  c3h::DevBuf<uint8_t> ntmp;
+  c3h::DevBuf<float4> dsamp;        // downsampled centroids (leaf-layout order)
+  c3h::DevBuf<float2> rsd_radii;
+  c3h::DevBuf<int32_t> rsd_types, grsd_trans;
+  c3h::DevBuf<float> grsd_feat, vosch_feat;
+  int64_t rsd_n = 0;                // centroids with valid radii / types
   // voxeliser state (voxelize.hip): global hash table, slot / grid-word lists by epoch
   // parity, counters; what the previous frame listed is cleared by the next frame
   c3h::DevBuf<c3h::VoxSlot> vtab[2];

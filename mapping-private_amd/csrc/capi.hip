@@ -625,6 +625,21 @@ void c3h_destroy(c3h_ctx* ctx) {
   release(ctx->grid);
   release(ctx->pts);
   release(ctx->raw);
+  release(ctx->dsbuf);
+  release(ctx->normals);
+  release(ctx->nkeys);
+  release(ctx->nkeys2);
+  release(ctx->nidx);
+  release(ctx->nidx2);
+  release(ctx->ncstart);
+  release(ctx->ncend);
+  release(ctx->ntmp);
+  release(ctx->dsamp);
+  release(ctx->rsd_radii);
+  release(ctx->rsd_types);
+  release(ctx->grsd_trans);
+  release(ctx->grsd_feat);
+  release(ctx->vosch_feat);
   release(ctx->vtab[0]);
   release(ctx->vtab[1]);
   release(ctx->vlists);
@@ -701,6 +716,8 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
   ctx->g_valid = false;
   ctx->table_valid = false;
   ctx->vcent_valid = false;
+  ctx->normals_valid = false;
+  ctx->rsd_n = 0;
   ctx->n_offcell = 0;
   c3h_grid_info gi{};
   gi.leaf = leaf;
@@ -958,9 +975,9 @@ int c3h_get_downsampled(c3h_ctx* ctx, float* out, int on_device) {
   rc = compute_leaf_layout(ctx, ctx->tmp_i32.p);
   if (rc != C3H_OK) return rc;
   float* dst = out;
-  if (!on_device) {
-    ENSURE(ctx->pts, (size_t)ctx->info.n_occ * 4);
-    dst = ctx->pts.p;
+  if (!on_device) {  // not ctx->pts: it may hold the voxelize input the normals read
+    ENSURE(ctx->dsbuf, (size_t)ctx->info.n_occ * 4);
+    dst = ctx->dsbuf.p;
   }
   HIPCHK(c3h::launch_vox_downsampled(ctx->vargs, ctx->vcent.p, ctx->vcounts.p, ctx->tmp_i32.p, dst, ctx->stream));
   if (!on_device)
@@ -1260,6 +1277,208 @@ int c3h_voxelize_pointcloud2(c3h_ctx* ctx, const void* data, uint32_t height, ui
   HIPCHK(c3h::launch_pc2_convert(src, height, width, point_step, height > 1 ? row_step : width * point_step, offsets,
                                  is_bigendian ? 1 : 0, ctx->pts.p, ctx->stream));
   return c3h_voxelize(ctx, ctx->pts.p, n, 1, leaf, z_limit, info);
+}
+
+// ---- normals, RSD, GRSD, VOSCH (rsd.hip; grsd_colorCHLAC_tools.hpp) -----------------
+// radius-search grid over the points of the last c3h_voxelize (those it kept)
+static int nbr_grid(c3h_ctx* ctx, float cell) {
+  const c3h::VoxArgs& a = ctx->vargs;
+  c3h::NbrGrid g{};
+  g.pts = a.pts;
+  g.n = a.n;
+  g.cell = cell;
+  g.inv_cell = 1.0f / cell;
+  for (int ax = 0; ax < 3; ++ax) {
+    const double lo = (double)ctx->info.min_b[ax] * ctx->info.leaf, hi = (double)(ctx->info.max_b[ax] + 1) * ctx->info.leaf;
+    g.origin[ax] = (float)(lo - cell);
+    g.dim[ax] = (int)std::ceil((hi - lo) / cell) + 3;
+  }
+  const int64_t ncell = (int64_t)g.dim[0] * g.dim[1] * g.dim[2];
+  if (ncell > ((int64_t)1 << 27)) return fail(ctx, C3H_ERR_RANGE, "normals: more than 2^27 search cells");
+  const size_t n = (size_t)std::max<int64_t>(g.n, 1);
+  ENSURE(ctx->nkeys, n);
+  ENSURE(ctx->nkeys2, n);
+  ENSURE(ctx->nidx, n);
+  ENSURE(ctx->nidx2, n);
+  ENSURE(ctx->ncstart, (size_t)ncell);
+  ENSURE(ctx->ncend, (size_t)ncell);
+  g.cstart = ctx->ncstart.p;
+  g.cend = ctx->ncend.p;
+  size_t tb = 0;
+  HIPCHK(c3h::nbr_build(g, ctx->nkeys.p, ctx->nkeys2.p, ctx->nidx.p, ctx->nidx2.p, nullptr, &tb, ctx->stream));
+  ENSURE(ctx->ntmp, std::max<size_t>(tb, 1));
+  tb = ctx->ntmp.n;
+  HIPCHK(c3h::nbr_build(g, ctx->nkeys.p, ctx->nkeys2.p, ctx->nidx.p, ctx->nidx2.p, ctx->ntmp.p, &tb, ctx->stream));
+  ctx->nbr = g;
+  return C3H_OK;
+}
+
+int c3h_compute_normals(c3h_ctx* ctx, float radius, const float viewpoint[3]) {
+  if (!ctx || !(radius > 0)) return C3H_ERR_ARG;
+  QUIESCE(ctx);
+  if (!ctx->have_grid || !ctx->table_valid)
+    return fail(ctx, C3H_ERR_STATE, "compute_normals: needs the points of a c3h_voxelize");
+  HIPCHK(hipSetDevice(ctx->device));
+  ctx->normals_valid = false;
+  int rc = nbr_grid(ctx, radius);
+  if (rc != C3H_OK) return rc;
+  ENSURE(ctx->normals, (size_t)std::max<int64_t>(ctx->vargs.n, 1));
+  const float vp0[3] = {0.0f, 0.0f, 0.0f};
+  HIPCHK(c3h::launch_normals(ctx->nbr, radius, viewpoint ? viewpoint : vp0, ctx->normals.p, ctx->stream));
+  ctx->normals_valid = true;
+  return C3H_OK;
+}
+
+int c3h_get_normals(c3h_ctx* ctx, float* out, int on_device) {
+  if (!ctx || !out) return C3H_ERR_ARG;
+  QUIESCE(ctx);
+  if (!ctx->normals_valid) return fail(ctx, C3H_ERR_STATE, "get_normals: c3h_compute_normals first");
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipMemcpyAsync(out, ctx->normals.p, (size_t)ctx->vargs.n * 16,
+                        on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return C3H_OK;
+}
+
+// extractGRSDSignature21 (grsd_colorCHLAC_tools.hpp:131-296) into grsd_feat (H x 20)
+static int grsd_frames(c3h_ctx* ctx, const c3h_grsd_params* p, int32_t sb[3], int64_t* Hout) {
+  if (!ctx->normals_valid) return fail(ctx, C3H_ERR_STATE, "extract_grsd: c3h_compute_normals first");
+  const int* div = ctx->info.div_b;
+  int64_t H = 1;
+  float inv_s = 0.0f;
+  sb[0] = sb[1] = sb[2] = 0;
+  *Hout = 0;
+  if (p->subdiv > 0) {
+    inv_s = 1.0 / p->subdiv;
+    if (div[0] <= p->offset[0] || div[1] <= p->offset[1] || div[2] <= p->offset[2]) return C3H_OK;  // :150-153
+    for (int a = 0; a < 3; ++a) sb[a] = (int)ceilf((div[a] - p->offset[a]) * inv_s);
+    H = (int64_t)sb[0] * sb[1] * sb[2];
+  } else if (p->subdiv < 0) {
+    return C3H_OK;  // :159-162: invalid subdivision size -> empty
+  } else {
+    sb[0] = sb[1] = sb[2] = 1;
+  }
+  const int64_t nc = ctx->info.n_occ;
+  const int64_t nvox = grid_voxels(ctx);
+  int rc = exact_centroids(ctx);
+  if (rc != C3H_OK) return rc;
+  ENSURE(ctx->tmp_i32, (size_t)std::max<int64_t>(nvox, 1));
+  rc = compute_leaf_layout(ctx, ctx->tmp_i32.p);
+  if (rc != C3H_OK) return rc;
+  ENSURE(ctx->dsamp, (size_t)std::max<int64_t>(nc, 1));
+  HIPCHK(c3h::launch_vox_downsampled(ctx->vargs, ctx->vcent.p, ctx->vcounts.p, ctx->tmp_i32.p,
+                                     reinterpret_cast<float*>(ctx->dsamp.p), ctx->stream));
+  // RSD radius: max(rsd_radius_search, voxel_size / 2 * sqrt(3)) (:172)
+  const float max_dist = (float)std::max((double)p->rsd_radius, (double)ctx->info.leaf / 2 * std::sqrt(3.0));
+  if (max_dist > 4 * ctx->nbr.cell) return fail(ctx, C3H_ERR_ARG, "extract_grsd: RSD radius > 4 x normal radius");
+  ENSURE(ctx->rsd_radii, (size_t)std::max<int64_t>(nc, 1));
+  ENSURE(ctx->rsd_types, (size_t)std::max<int64_t>(nc, 1));
+  HIPCHK(c3h::launch_rsd(ctx->nbr, ctx->normals.p, ctx->dsamp.p, nc, max_dist, ctx->rsd_radii.p, ctx->rsd_types.p,
+                         ctx->stream));
+  ctx->rsd_n = nc;
+  ENSURE(ctx->grsd_trans, (size_t)H * 36);
+  HIPCHK(hipMemsetAsync(ctx->grsd_trans.p, 0, (size_t)H * 36 * 4, ctx->stream));
+  c3h::GrsdArgs ga{};
+  ga.cent = ctx->dsamp.p;
+  ga.nc = nc;
+  ga.layout = ctx->tmp_i32.p;
+  ga.types = ctx->rsd_types.p;
+  ga.trans = ctx->grsd_trans.p;
+  for (int a = 0; a < 3; ++a) {
+    ga.div_b[a] = div[a];
+    ga.min_b[a] = ctx->info.min_b[a];
+    ga.off[a] = p->subdiv > 0 ? p->offset[a] : 0;
+    ga.sb[a] = sb[a];
+  }
+  ga.leaf = ctx->info.leaf;
+  ga.inv_leaf = 1.0f / ctx->info.leaf;
+  ga.inv_s = inv_s;
+  ga.hist1 = H == 1 ? 1 : 0;
+  HIPCHK(c3h::launch_grsd(ga, ctx->stream));
+  ENSURE(ctx->grsd_feat, (size_t)H * 20);
+  // NORMALIZE_GRSD = 20 / 26 (grsd_colorCHLAC_tools.h:32) when is_normalize
+  HIPCHK(c3h::launch_grsd_feat(ctx->grsd_trans.p, H, p->normalize ? (float)(20.0 / 26) : 1.0f, ctx->grsd_feat.p, 20,
+                               ctx->stream));
+  *Hout = H;
+  return C3H_OK;
+}
+
+int c3h_extract_grsd(c3h_ctx* ctx, const c3h_grsd_params* p, int32_t subdiv_out[3], int64_t* hist_num) {
+  if (!ctx || !p) return C3H_ERR_ARG;
+  QUIESCE(ctx);
+  if (!ctx->have_grid || !ctx->table_valid) return fail(ctx, C3H_ERR_STATE, "extract_grsd: no c3h_voxelize grid");
+  HIPCHK(hipSetDevice(ctx->device));
+  ctx->have_feat = false;
+  ctx->g_valid = false;
+  ctx->rows_valid = false;
+  int32_t sb[3];
+  int64_t H = 0;
+  int rc = grsd_frames(ctx, p, sb, &H);
+  if (rc != C3H_OK) return rc;
+  ENSURE(ctx->feat, (size_t)std::max<int64_t>(H, 1) * 20);
+  ENSURE(ctx->exist, (size_t)std::max<int64_t>(H, 1));
+  if (H > 0) {
+    HIPCHK(hipMemcpyAsync(ctx->feat.p, ctx->grsd_feat.p, (size_t)H * 20 * 4, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(c3h::launch_exist_rule(ctx->feat.p, H, 20, C3H_EXIST_GRSD, ctx->exist.p, ctx->stream));
+  }
+  ctx->hist_num = H;
+  ctx->feat_dim = 20;
+  for (int a = 0; a < 3; ++a) ctx->subdiv_b[a] = sb[a];
+  ctx->nframes_feat = 1;
+  ctx->feat_sparse = false;
+  ctx->have_feat = true;
+  if (subdiv_out) memcpy(subdiv_out, sb, sizeof(sb));
+  if (hist_num) *hist_num = H;
+  return C3H_OK;
+}
+
+int c3h_get_rsd(c3h_ctx* ctx, float* radii, int32_t* types, int on_device) {
+  if (!ctx) return C3H_ERR_ARG;
+  QUIESCE(ctx);
+  if (ctx->rsd_n == 0 && !ctx->normals_valid) return fail(ctx, C3H_ERR_STATE, "get_rsd: no RSD computed");
+  HIPCHK(hipSetDevice(ctx->device));
+  const hipMemcpyKind k = on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+  if (radii && ctx->rsd_n) HIPCHK(hipMemcpyAsync(radii, ctx->rsd_radii.p, (size_t)ctx->rsd_n * 8, k, ctx->stream));
+  if (types && ctx->rsd_n) HIPCHK(hipMemcpyAsync(types, ctx->rsd_types.p, (size_t)ctx->rsd_n * 4, k, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return (int)std::min<int64_t>(ctx->rsd_n, INT_MAX);
+}
+
+// extractVOSCH (grsd_colorCHLAC_tools.hpp:832-843): [GRSD-20 | C3-HLAC-117] per subdivision
+int c3h_extract_vosch(c3h_ctx* ctx, const c3h_grsd_params* p, const int32_t thr[3], int32_t lut_double,
+                      int32_t subdiv_out[3], int64_t* hist_num) {
+  if (!ctx || !p || !thr) return C3H_ERR_ARG;
+  QUIESCE(ctx);
+  if (!ctx->have_grid || !ctx->table_valid) return fail(ctx, C3H_ERR_STATE, "extract_vosch: no c3h_voxelize grid");
+  HIPCHK(hipSetDevice(ctx->device));
+  int32_t sb[3];
+  int64_t H = 0;
+  int rc = grsd_frames(ctx, p, sb, &H);
+  if (rc != C3H_OK) return rc;
+  c3h_extract_params e{};
+  e.variant = 117;
+  for (int a = 0; a < 3; ++a) {
+    e.thr[a] = thr[a];
+    e.offset[a] = p->offset[a];
+  }
+  e.subdiv = p->subdiv;
+  e.lut_double = lut_double;
+  const uint32_t* g = ctx->grid_ptr;
+  int32_t sb2[3];
+  int64_t H2 = 0;
+  rc = extract_frames(ctx, &g, 1, &e, sb2, &H2);
+  if (rc != C3H_OK) return rc;
+  if (H2 != H) return fail(ctx, C3H_ERR_STATE, "extract_vosch: GRSD / C3 subdivisions differ");
+  ENSURE(ctx->vosch_feat, (size_t)std::max<int64_t>(H, 1) * 137);
+  HIPCHK(c3h::launch_vosch_concat(ctx->grsd_feat.p, ctx->feat.p, ctx->exist.p, H, ctx->vosch_feat.p, ctx->stream));
+  std::swap(ctx->feat, ctx->vosch_feat);
+  ctx->feat_dim = 137;
+  ctx->feat_sparse = false;
+  ctx->g_valid = false;
+  ctx->rows_valid = false;
+  if (subdiv_out) memcpy(subdiv_out, sb, sizeof(sb));
+  if (hist_num) *hist_num = H;
+  return C3H_OK;
 }
 
 // SearchObj::setData (search.cpp:539-658) with caller-computed features (VOSCH, GRSD,

@@ -1,0 +1,111 @@
+"""VOSCH / GRSD on the GPU (csrc/rsd.hip) against oracle/grsd_oracle.py,
+the restatement of the reference's extractGRSDSignature21 / extractVOSCH
+(color_chlac/include/color_chlac/grsd_colorCHLAC_tools.hpp:63-296, 832-843) and of the PCL
+normal / RSD estimation they call (PCL is not part of the reference tree: "parity
+unpinned" beyond this restatement; the reference's *_GRSD_CCHLAC.pcd files were written by
+an older GRSD -- no EMPTY class -- and do not match its current source either).
+
+On the reference's own shape clouds (tests/golden/ref_fixtures/pcd), leaf 0.01 as
+example_GRSD_CCHLAC.cpp:
+- normals (radius 0.02): unit vectors within 1e-5 of the float64 oracle, flipped the same
+  way towards the viewpoint, curvature within 1e-5;
+- RSD radii from the device normals within 1e-5 relative of the oracle's computeRSD, types
+  equal except where a radius sits within 1e-4 of a get_type threshold;
+- GRSD transition counts bit-exact given equal types (whole cloud and subdivisions);
+- VOSCH = [GRSD-20 | C3-HLAC-117] rows, exist by the setVOSCH rule, searchable at F=137."""
+import numpy as np
+import pytest
+
+import c3hlac
+import grsd_oracle as go
+import pyoracle as po
+from c3hlac import synth
+from conftest import GOLDEN, THR
+
+pytestmark = pytest.mark.gpu
+PCD = GOLDEN / "ref_fixtures" / "pcd"
+CLOUDS = ["noiseless_cone_red", "noisy_sphere_green", "noisy_torus_blue", "noisy_plane_purple"]
+THRESH = (0.100, 0.175, 0.015, 0.050)
+
+
+def _setup(ctx, name, leaf=0.01):
+    pts = c3hlac.read_pcd(PCD / (name + ".pcd"))
+    ctx.voxelize(pts, leaf)
+    ctx.compute_normals(0.02)
+    return pts
+
+
+@pytest.mark.parametrize("name", CLOUDS)
+def test_normals_rsd_grsd_whole_cloud(ctx, name):
+    pts = _setup(ctx, name)
+    n = len(pts)
+    nrm = ctx.normals(n).astype(np.float64)
+    ref = go.normals(pts, 0.02)
+    ok = np.isfinite(ref[:, 0])
+    assert np.array_equal(ok, np.isfinite(nrm[:, 0])), name
+    np.testing.assert_allclose(nrm[ok, :3], ref[ok, :3], atol=1e-5)
+    np.testing.assert_allclose(nrm[ok, 3], ref[ok, 3], atol=1e-5)
+    sb, H = ctx.extract_grsd(0)
+    assert sb == (1, 1, 1) and H == 1
+    radii, types = ctx.rsd()
+    g, layout, cloud = po.voxelize(pts, 0.01)
+    assert len(radii) == len(cloud)
+    dn = ctx.normals(n).astype(np.float64)  # the oracle RSD on the device normals
+    feat_ref, _, radii_ref, types_ref = go.grsd(pts, dn, g, layout, cloud, 0.01)
+    np.testing.assert_allclose(radii, radii_ref, rtol=1e-5, atol=1e-7)
+    near = np.zeros(len(types), bool)
+    for t in THRESH:
+        near |= (np.abs(radii_ref - t) < 1e-4).any(1)
+    near |= np.abs(radii_ref[:, 1] - radii_ref[:, 0] - 0.050) < 1e-4
+    assert np.array_equal(types[~near], types_ref[~near]), name
+    assert (types != types_ref).sum() <= near.sum()
+    if np.array_equal(types, types_ref):  # equal types: the transition counts are exact
+        assert np.array_equal(ctx.features()[0], feat_ref[0].astype(np.float32)), name
+    print(name, "voxels", len(types), "type mismatches", int((types != types_ref).sum()),
+          "types", np.bincount(types, minlength=5).tolist())
+    # every voxel sees 26 neighbours; bins (i, j > i) and bin 20 (5, 5) hold the rest
+    assert ctx.features()[0].sum() <= 26 * len(cloud)
+
+
+def test_grsd_subdivisions_and_normalize(ctx):
+    name = "noisy_torus_blue"
+    pts = _setup(ctx, name, leaf=0.005)
+    sb, H = ctx.extract_grsd(4, offset=(1, 0, 2), normalize=True)
+    g, layout, cloud = po.voxelize(pts, 0.005)
+    dn = ctx.normals(len(pts)).astype(np.float64)
+    feat_ref, sb_ref, _, types_ref = go.grsd(pts, dn, g, layout, cloud, 0.005, subdiv=4, offset=(1, 0, 2))
+    assert list(sb) == list(sb_ref) and H == len(feat_ref)
+    _, types = ctx.rsd()
+    print("subdiv: type mismatches", int((types != types_ref).sum()), "of", len(types))
+    if np.array_equal(types, types_ref):
+        np.testing.assert_array_equal(ctx.features(), (feat_ref * np.float32(20.0 / 26)).astype(np.float32))
+    assert ctx.exist().shape == (H,)
+
+
+def test_vosch_rows_and_search(ctx):
+    pts = synth.kinect_scene(150_000, grid=48, leaf=0.02, seed=77)
+    ctx.voxelize(pts, 0.02)
+    ctx.compute_normals(0.04)
+    ctx.extract_grsd(6)
+    grsd = ctx.features().copy()
+    sb, H = ctx.extract(117, THR, 6)
+    c3, ex = ctx.features().copy(), ctx.exist().copy()
+    sbv, Hv = ctx.extract_vosch(THR, 6)
+    assert sbv == sb and Hv == H
+    v = ctx.features()
+    assert v.shape == (H, 137)
+    np.testing.assert_array_equal(v[:, :20], grsd)
+    np.testing.assert_array_equal(v[:, 20:][ex > 0], c3[ex > 0])
+    assert (v[:, 20:][ex == 0] == 0).all()
+    np.testing.assert_array_equal(ctx.exist(), ex)  # setVOSCH rule on f20, f21 = the C3 rule
+    axis_t, var, axis_q = synth.random_bases(137, 30, 2, 5, seed=78)
+    fmax = v.max(0) * np.float32(0.9)
+    ctx.search_setup(axis_t, var, axis_q, feature_max=fmax)
+    ctx.set_rank(1)
+    ctx.search((2, 2, 2), 20, rotate=False)
+    _, _, scd = po.search(sb, v, ex, synth.whiten(axis_t, var), axis_q, (2, 2, 2), 1, 20, rotate=False,
+                          dbl=True, fmax=fmax, want_scores=True)
+    sc = ctx.scores()
+    ok = scd > 0
+    assert ok.any()
+    np.testing.assert_allclose(sc[ok], scd[ok], rtol=1e-5)
