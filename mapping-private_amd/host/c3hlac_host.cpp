@@ -238,6 +238,66 @@ void extractC3HLACSignature117(VoxelGrid& grid, std::vector<float>& feature, int
   feature = tmp.empty() ? std::vector<float>() : tmp[0];
 }
 
+// ------------------------------------------------------------------------- VOSCH / GRSD
+void computeNormal(VoxelGrid& grid, double radius) {
+  const Context& ctx = grid.context();
+  ctx.check(c3h_compute_normals(ctx.get(), (float)radius, nullptr), "c3h_compute_normals");
+}
+
+std::vector<float> getNormals(const VoxelGrid& grid) {
+  const Context& ctx = grid.context();
+  c3h_grid_info gi;
+  grid_info(ctx, &gi);
+  std::vector<float> out((size_t)gi.n_valid * 4);
+  ctx.check(c3h_get_normals(ctx.get(), out.data(), 0), "c3h_get_normals");
+  return out;
+}
+
+static Vector3i grsd_like(VoxelGrid& grid, std::vector<std::vector<float> >& feature, float voxel_size, int subdiv,
+                          int ox, int oy, int oz, bool normalize, const int* thr) {
+  feature.resize(0);
+  if (grid.leaf() != 0.0f && voxel_size != grid.leaf())
+    throw Error(C3H_ERR_ARG, "extractGRSDSignature21: voxel_size differs from the grid's leaf size");
+  const Context& ctx = grid.context();
+  c3h_grsd_params p;
+  p.subdiv = subdiv;
+  p.offset[0] = ox;
+  p.offset[1] = oy;
+  p.offset[2] = oz;
+  p.rsd_radius = (float)rsd_radius_search;
+  p.normalize = normalize ? 1 : 0;
+  int32_t sb[3] = {0, 0, 0};
+  int64_t H = 0;
+  auto run = [&] {
+    return thr ? c3h_extract_vosch(ctx.get(), &p, thr, 1, sb, &H) : c3h_extract_grsd(ctx.get(), &p, sb, &H);
+  };
+  int rc = run();
+  if (rc == C3H_ERR_STATE) {  // no normals yet: computeNormal with the reference's radius
+    computeNormal(grid);
+    rc = run();
+  }
+  ctx.check(rc, thr ? "c3h_extract_vosch" : "c3h_extract_grsd");
+  const int F = thr ? 137 : 20;
+  if (H > 0) {
+    std::vector<float> flat((size_t)H * F);
+    ctx.check(c3h_get_features(ctx.get(), flat.data(), 0), "c3h_get_features");
+    feature.resize((size_t)H);
+    for (int64_t h = 0; h < H; ++h) feature[h].assign(flat.begin() + h * F, flat.begin() + (h + 1) * F);
+  }
+  return v3(sb);
+}
+
+Vector3i extractGRSDSignature21(VoxelGrid& grid, std::vector<std::vector<float> >& feature, float voxel_size,
+                                int subdiv, int ox, int oy, int oz, bool is_normalize) {
+  return grsd_like(grid, feature, voxel_size, subdiv, ox, oy, oz, is_normalize, nullptr);
+}
+
+Vector3i extractVOSCH(VoxelGrid& grid, std::vector<std::vector<float> >& feature, int thR, int thG, int thB,
+                      float voxel_size, int subdiv, int ox, int oy, int oz, bool is_normalize) {
+  const int thr[3] = {thR, thG, thB};
+  return grsd_like(grid, feature, voxel_size, subdiv, ox, oy, oz, is_normalize, thr);
+}
+
 // ------------------------------------------------------------------------- PCA
 void PCA::read(const char* filename, bool ascii) {
   // c3h_pca_read returns the axis column-major (eigenvector i contiguous), as the file
@@ -610,6 +670,43 @@ void SearchC3HLACMulti::setC3HLAC(int dim, int r, int g, int b, const VoxelGrid&
   (void)dim;
   ensureSetup(C3H_VARIANT_981);
   set_c3hlac(*this, C3H_VARIANT_981, r, g, b, grid, voxel_size, subdiv);
+}
+
+// setVOSCH / setGRSD (search_new.h:34-76): features on the grid's context, handed to the
+// search context with their exist rule (setData)
+static void set_external(SearchObj& so, VoxelGrid& grid, double voxel_size, int subdiv, const int* thr) {
+  std::vector<std::vector<float> > f;
+  const Vector3i sb = grsd_like(grid, f, (float)voxel_size, subdiv, 0, 0, 0, false, thr);
+  const int F = thr ? 137 : 20;
+  std::vector<float> flat;
+  flat.reserve(f.size() * F);
+  for (const auto& row : f) flat.insert(flat.end(), row.begin(), row.end());
+  const int32_t sbv[3] = {sb[0], sb[1], sb[2]};
+  const Context& ctx = so.context();
+  ctx.check(c3h_set_features(ctx.get(), flat.empty() ? nullptr : flat.data(), sbv, F, nullptr,
+                             thr ? C3H_EXIST_VOSCH : C3H_EXIST_GRSD, 0),
+            "c3h_set_features");
+  so.setDataFromContext(sb);
+}
+
+void SearchVOSCH::setVOSCH(int dim, int r, int g, int b, VoxelGrid& grid, double voxel_size, int subdiv) {
+  (void)dim;
+  ensureSetup(137);
+  const int thr[3] = {r, g, b};
+  set_external(*this, grid, voxel_size, subdiv, thr);
+}
+
+void SearchVOSCHMulti::setVOSCH(int dim, int r, int g, int b, VoxelGrid& grid, double voxel_size, int subdiv) {
+  (void)dim;
+  ensureSetup(137);
+  const int thr[3] = {r, g, b};
+  set_external(*this, grid, voxel_size, subdiv, thr);
+}
+
+void SearchGRSD::setGRSD(int dim, VoxelGrid& grid, double voxel_size, int subdiv) {
+  (void)dim;
+  ensureSetup(20);
+  set_external(*this, grid, voxel_size, subdiv, nullptr);
 }
 
 }  // namespace c3hlac

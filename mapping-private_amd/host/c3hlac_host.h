@@ -120,6 +120,21 @@ void extractC3HLACSignature117(VoxelGrid& grid, std::vector<float>& feature, int
                                int color_threshold_g, int color_threshold_b, float voxel_size,
                                bool lut_double = true);
 
+// VOSCH / GRSD (color_chlac/include/color_chlac/grsd_colorCHLAC_tools.h:27-32, .hpp:63-296,
+// 832-843) on the grid's cloud: computeNormal (radius normals_radius_search) runs on the
+// points the grid was built from (PCL's normals are not a field of PointXYZRGB here: they
+// stay on the device); extractGRSDSignature21 computes them first when needed.
+const double rsd_radius_search = 0.01;
+const double normals_radius_search = 0.02;
+void computeNormal(VoxelGrid& grid, double radius = normals_radius_search);
+std::vector<float> getNormals(const VoxelGrid& grid);  // n x 4: nx, ny, nz, curvature
+Vector3i extractGRSDSignature21(VoxelGrid& grid, std::vector<std::vector<float> >& feature, float voxel_size,
+                                int subdivision_size = 0, int offset_x = 0, int offset_y = 0, int offset_z = 0,
+                                bool is_normalize = false);
+Vector3i extractVOSCH(VoxelGrid& grid, std::vector<std::vector<float> >& feature, int thR, int thG, int thB,
+                      float voxel_size, int subdivision_size = 0, int offset_x = 0, int offset_y = 0,
+                      int offset_z = 0, bool is_normalize = false);
+
 // pcl::io::loadPCDFile for x y z rgb clouds (c3h_pcd_read_xyzrgb): 0 on success, -1 when
 // the file cannot be opened or parsed, as PCL returns.
 int loadPCDFile(const std::string& file_name, std::vector<PointXYZRGB>& cloud);
@@ -289,6 +304,27 @@ class SearchC3HLACMulti : public SearchObjMulti {
   using SearchObjMulti::SearchObjMulti;
   void setC3HLAC(int dim, int color_threshold_r, int color_threshold_g, int color_threshold_b,
                  const VoxelGrid& grid, double voxel_size, int subdivision_size);
+};
+// SearchVOSCH{,Multi}::setVOSCH and SearchGRSD::setGRSD
+// (color_voxel_recognition_2/include/color_voxel_recognition_2/search_new.h:34-76, 106-126):
+// the features of extractVOSCH / extractGRSDSignature21 on the device, their exist rule,
+// setData.  The grid must come from getVoxelGrid (it holds the cloud).
+class SearchVOSCH : public SearchObj {
+ public:
+  using SearchObj::SearchObj;
+  void setVOSCH(int dim, int color_threshold_r, int color_threshold_g, int color_threshold_b, VoxelGrid& grid,
+                double voxel_size, int subdivision_size);
+};
+class SearchVOSCHMulti : public SearchObjMulti {
+ public:
+  using SearchObjMulti::SearchObjMulti;
+  void setVOSCH(int dim, int color_threshold_r, int color_threshold_g, int color_threshold_b, VoxelGrid& grid,
+                double voxel_size, int subdivision_size);
+};
+class SearchGRSD : public SearchObj {
+ public:
+  using SearchObj::SearchObj;
+  void setGRSD(int dim, VoxelGrid& grid, double voxel_size, int subdivision_size);
 };
 
 }  // namespace c3hlac

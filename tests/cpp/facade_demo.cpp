@@ -8,6 +8,7 @@
 //   facade_demo thr <cloud.pcd> <leaf>                  (GPU: calc_scene_auto_threshold flow)
 //   facade_demo rot <dim> <mode>                        (host only: rotateFeature90 of 0..dim-1)
 //   facade_demo train <rows.bin> <out_dir> <D> <n_model> (GPU: pca_scene.cpp + pca_models.cpp)
+//   facade_demo vosch <cloud.pcd> <leaf>                (GPU: example_GRSD_CCHLAC / setVOSCH flow)
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -183,6 +184,25 @@ static int train(const char* rows_path, const std::string& out, int D, int n_mod
   return 0;
 }
 
+// example_GRSD_CCHLAC.cpp's flow: loadPCDFile -> computeNormal -> getVoxelGrid ->
+// extractGRSDSignature21 + extractVOSCH (whole cloud)
+static int vosch(const char* path, float leaf) {
+  std::vector<PointXYZRGB> cloud, down;
+  loadPCDFile(path, cloud);
+  VoxelGrid grid;
+  getVoxelGrid(grid, cloud, down, leaf);
+  computeNormal(grid, normals_radius_search);
+  std::vector<std::vector<float> > grsd, vosch_f;
+  extractGRSDSignature21(grid, grsd, leaf);
+  extractVOSCH(grid, vosch_f, 127, 127, 127, leaf);
+  printf("{\"grsd\": [");
+  for (size_t i = 0; i < grsd[0].size(); ++i) printf(i ? ", %.9g" : "%.9g", grsd[0][i]);
+  printf("], \"vosch_dim\": %d, \"vosch_head\": [", (int)vosch_f[0].size());
+  for (int i = 0; i < 22; ++i) printf(i ? ", %.9g" : "%.9g", vosch_f[0][i]);
+  printf("]}\n");
+  return 0;
+}
+
 int main(int argc, char** argv) {
   try {
     if (argc == 4 && !strcmp(argv[1], "params")) return params(argv[2], argv[3]);
@@ -191,6 +211,7 @@ int main(int argc, char** argv) {
     if (argc == 4 && !strcmp(argv[1], "thr")) return thr(argv[2], (float)atof(argv[3]));
     if (argc == 4 && !strcmp(argv[1], "rot")) return rot(atoi(argv[2]), atoi(argv[3]));
     if (argc == 6 && !strcmp(argv[1], "train")) return train(argv[2], argv[3], atoi(argv[4]), atoi(argv[5]));
+    if (argc == 4 && !strcmp(argv[1], "vosch")) return vosch(argv[2], (float)atof(argv[3]));
   } catch (const Error& e) {
     fprintf(stderr, "c3hlac::Error %d: %s\n", e.code, e.what());
     return 2;

@@ -172,3 +172,24 @@ def test_facade_pca_training(ctx, demo, tmp_path):
     # leading model subspace (r = 10 as in the demos) equals the oracle's
     P1, P2 = ma[:, :10].astype(np.float64), ref_m[0][:, :10]
     assert np.abs(P1 @ P1.T - P2 @ P2.T).max() < 1e-4
+
+
+@pytest.mark.gpu
+def test_facade_vosch_flow(ctx, demo):
+    """example_GRSD_CCHLAC.cpp through the facade: GRSD equals the binding's, VOSCH is
+    [GRSD-20 | C3-117] with the C3 part equal to extractC3HLACSignature117."""
+    path = FIX / "pcd" / "noisy_torus_blue.pcd"
+    out = subprocess.run([str(demo), "vosch", str(path), "0.01"], check=True, capture_output=True,
+                         text=True).stdout
+    j = json.loads(out)
+    pts = c3hlac.read_pcd(path)
+    ctx.voxelize(pts, 0.01)
+    ctx.compute_normals(0.02)
+    ctx.extract_grsd(0)
+    g = ctx.features()[0]
+    assert np.array_equal(np.float32(j["grsd"]), g)
+    assert j["vosch_dim"] == 137
+    ctx.extract(117, (127, 127, 127), 0)
+    c3 = ctx.features()[0]
+    assert np.array_equal(np.float32(j["vosch_head"][:20]), g)
+    assert np.array_equal(np.float32(j["vosch_head"][20:22]), c3[:2])
