@@ -342,6 +342,15 @@ int c3h_rotate_feature90(const float* in, float* out, int64_t n, int64_t ld, int
 /* the same rotation as a gather map: map_out[o] = input index of output o (host). */
 int c3h_rotate_map(int32_t dim, int32_t mode, int32_t* map_out);
 
+/* Multi-GPU: one process per GPU, frames sharded across them with no
+ * data-path collective; the one exchange is this gather of every rank's detection records
+ * (rank-major into d_all = world x n_local records) with RCCL ncclAllGather on the
+ * context's stream, after the context's queued work (an open c3h_stream_frames stream is
+ * flushed first).  nccl_comm = the caller's ncclComm_t (ncclCommInitRank); asynchronous:
+ * d_all is complete after c3h_synchronize.  librccl is loaded at the first call. */
+int c3h_allgather_detections(c3h_ctx* ctx, void* nccl_comm, const c3h_det* d_local, int64_t n_local,
+                             c3h_det* d_all);
+
 /* per-kernel device time (ms) accumulated since the last reset with HIP events on the
  * context stream; slots: 0 voxelize, 1 C3-HLAC, 2 compress, 3 score, 4 rank replay,
  * 5 pipeline tick (c3h_run_frames' fused launches: every stage of four batches).

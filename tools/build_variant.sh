@@ -5,7 +5,7 @@ set -e
 cd "$(dirname "$0")/../mapping-private_amd"
 NAME=$1; shift
 B=build/variants/$NAME; mkdir -p $B lib/variants
-for f in capi voxelize c3hlac search pipeline colour pcdio pca ingest rsd; do
+for f in capi voxelize c3hlac search pipeline colour pcdio pca ingest rsd dist; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function $* -c csrc/$f.hip -o $B/$f.o &
 done
 wait
