@@ -273,6 +273,8 @@ struct SparseSearch {
   c3h_det* lists;          // rank 1 fused replay: M lists (nullable = no fused replay)
   int clean;               // apply a pending cleanMax first
   long long* prof;         // diagnostics (C3H_PROF): [blocks][8]
+  float* gbox = nullptr;   // large grids: box-summed G rows of every position (pstart order)
+  int64_t s_gbox = 0;
 };
 // sparse compress fused into the gate launch (nullable in launch_sparse_search)
 struct SparseCompress {
@@ -289,6 +291,7 @@ struct SparseCompress {
   int Fp16 = 0;
 };
 bool compress_rows_ok(int F, int Dpad);
+constexpr int64_t kBoxsumRows = 65536;  // subdivisions from which the search precomputes box sums
 hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc, hipStream_t s);
 int64_t sparse_score_blocks(const SparseSearch& a);
 
@@ -409,6 +412,7 @@ struct c3h_ctx {
   bool g_sparse = false;            // G holds only the listed rows (others stale)
   bool feat_sparse = false;         // feature rows of empty subdivisions are stale (exist == 0)
   c3h::DevBuf<long long> glist;     // sparse search: gate list
+  c3h::DevBuf<float> gbox;          // large grids: box sums of G per position (P_total x D)
   c3h::DevBuf<uint32_t> gcnt;       // [2] gate-list counters by search epoch parity
   uint32_t search_epoch = 0;
   int gcnt_frames = 0;

@@ -404,6 +404,10 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
     if (rc != C3H_OK) return rc;
   }
   if (clean == 1 || (clean == 0 && ctx->pending_clean)) clean = 1;
+  // rank 1: the replay runs in the score launch's last workgroup; on large grids its serial
+  // reduction over every score chunk's partials would be the critical path, so there a
+  // parallel argmax over the written scores feeds the same finalize (search.cpp:464-474)
+  const bool large = !ctx->capture && nf == 1 && H >= c3h::kBoxsumRows;
   const bool use_argmax = fast && ctx->rank == 1;
   std::vector<c3h::ScoreLaunch> launches;
   for (int i = 0; i < rm.n; ++i) {
@@ -476,10 +480,17 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
     q.s_cnt = 4;
     q.s_lists = (int64_t)per_lists;
     for (int f = 0; f < c3h::kMaxBatch; ++f) q.outs[f] = (d_outs && f < nf) ? d_outs[f] : nullptr;
+    // large grids (config 5): the box sums of every position in one streaming pass
+    // before the score launch (the same (dz, dy, dx) order, so the same scores)
+    if (large) {
+      ENSURE(ctx->gbox, (size_t)std::max<int64_t>(ptot, 1) * ctx->D);
+      q.gbox = ctx->gbox.p;
+      q.s_gbox = ptot * ctx->D;
+    }
     const int64_t nparts = c3h::sparse_score_blocks(q);
     q.s_partials = std::max<int64_t>(nparts, 1) * ctx->M;
     if (use_argmax) {  // rank 1: the replay runs in the score launch's last workgroup
-      ENSURE(ctx->partials, (size_t)nf * q.s_partials);
+      ENSURE(ctx->partials, std::max<size_t>((size_t)nf * q.s_partials, (size_t)256 * ctx->M));
       q.partials = ctx->partials.p;
       q.lists = ctx->d_lists.p;
       q.clean = clean;
@@ -663,6 +674,7 @@ void c3h_destroy(c3h_ctx* ctx) {
   release(ctx->rows);
   release(ctx->work);
   release(ctx->glist);
+  release(ctx->gbox);
   release(ctx->gcnt);
   release(ctx->lut);
   release(ctx->axis_pt);

@@ -205,6 +205,62 @@ __global__ __launch_bounds__(kBlock) void compress_f16_kernel(CompressRows cr, c
   compress_f16_body(cr, PT16, Fp16, blockIdx.x, gridDim.x, blockIdx.y);
 }
 
+__global__ __launch_bounds__(kBlock) void boxsum_kernel(SparseSearch a) {
+  const int64_t n = a.pstart[a.nmodes] * (a.D >> 2);
+  for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < n; e += (int64_t)gridDim.x * kBlock)
+    boxsum_body(a, e, blockIdx.y);
+}
+
+// rank 1 on large grids: block (b, m) reduces model m's scores of global positions
+// g = b, b + grid, ... (every mode, scan order) to a (score desc, scan order asc) partial
+constexpr int kArgmaxBlocks = 256;
+__global__ __launch_bounds__(kBlock) void scores_argmax_kernel(SparseSearch a) {
+  const int m = blockIdx.y;
+  const int64_t ptot = a.pstart[a.nmodes];
+  double best = -2.0;
+  long long bo = -1;
+  for (int64_t g = blockIdx.x * (int64_t)kBlock + threadIdx.x; g < ptot; g += (int64_t)gridDim.x * kBlock) {
+    const int mi = find_mode(a, g);
+    const ModeGeom& md = a.md[mi];
+    const int64_t p = g - a.pstart[mi];
+    const double sc = a.scores[md.offset + (int64_t)m * md.P + p];
+    const long long o = a.order_base[mi] + p;
+    if (sc >= 0 && (sc > best || (sc == best && o < bo))) {
+      best = sc;
+      bo = o;
+    }
+  }
+  __shared__ double s_sc[kBlock / 64];
+  __shared__ long long s_o[kBlock / 64];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double os = __shfl_xor(best, o, 64);
+    const long long oo = __shfl_xor(bo, o, 64);
+    if (oo >= 0 && (os > best || (os == best && (bo < 0 || oo < bo)))) {
+      best = os;
+      bo = oo;
+    }
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    s_sc[w] = best;
+    s_o[w] = bo;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < kBlock / 64; ++i)
+      if (s_o[i] >= 0 && (s_sc[i] > best || (s_sc[i] == best && (bo < 0 || s_o[i] < bo)))) {
+        best = s_sc[i];
+        bo = s_o[i];
+      }
+    a.partials[(int64_t)blockIdx.x * a.M + m] = ScorePartial{best, bo};
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void argmax_finalize_kernel(SparseSearch a, int nparts) {
+  argmax_finalize(a, a.partials, a.lists, a.outs[0], nparts);
+}
+
 __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch b) {
   extern __shared__ __attribute__((aligned(16))) float sl_smem[];
   score_list_body(b, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y, sl_smem);
@@ -444,11 +500,25 @@ hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc,
     gate_kernel<<<dim3(ngate, nf), kBlock, 0, s>>>(a);
   }
 score:
+  if (a.gbox) {
+    const int64_t n = ptot * (a.D >> 2);
+    boxsum_kernel<<<dim3((unsigned)std::min<int64_t>((n + kBlock - 1) / kBlock, 16384), nf), kBlock, 0, s>>>(a);
+  }
   const size_t lds = score_list_lds_bytes(a.D, a.mpg);
   const unsigned groups = (unsigned)((a.M + a.mpg - 1) / a.mpg);
   // workgroups per (group, frame): list chunks beyond the cap loop (dense scenes only);
   // surface frames pass ~1k positions (~30 chunks), so few workgroups exit unused
-  const unsigned gx = (unsigned)std::min<int64_t>(sparse_score_blocks(a), kScoreGridCap);
+  // (large grids with precomputed box sums: enough workgroups to fill the chip)
+  const unsigned gx = (unsigned)std::min<int64_t>(sparse_score_blocks(a), a.gbox ? 2048 : kScoreGridCap);
+  if (a.gbox && a.lists) {  // large grid, rank 1: scores, then a parallel argmax + finalize
+    SparseSearch b = a;
+    b.partials = nullptr;
+    b.lists = nullptr;
+    score_list_kernel<<<dim3(gx, groups, nf), kBlock, lds, s>>>(b);
+    scores_argmax_kernel<<<dim3(kArgmaxBlocks, a.M), kBlock, 0, s>>>(a);
+    argmax_finalize_kernel<<<1, kBlock, 0, s>>>(a, kArgmaxBlocks);
+    return hipGetLastError();
+  }
   score_list_kernel<<<dim3(gx, groups, nf), kBlock, lds, s>>>(a);
   return hipGetLastError();
 }

@@ -484,6 +484,39 @@ __device__ __forceinline__ void gate_body(const SparseSearch& a, int bid, int64_
   }
 }
 
+// box sums of G for every position of every mode (large grids): thread = (position, d4);
+// the cells in the score body's (dz, dy, dx) order, rows of empty subdivisions skipped,
+// so each sum is the one the score body would form
+__device__ __forceinline__ void boxsum_body(const SparseSearch& a, int64_t e, int64_t f) {
+  const int D4 = a.D >> 2;
+  const int64_t g = e / D4;
+  const int d4 = (int)(e - g * D4);
+  if (g >= a.pstart[a.nmodes]) return;
+  const int mi = find_mode(a, g);
+  const ModeGeom& md = a.md[mi];
+  const int64_t p = g - a.pstart[mi];
+  const int64_t xye = (int64_t)md.xe * md.ye;
+  const int x = (int)(p % md.xe), y = (int)((p / md.xe) % md.ye), z = (int)(p / xye);
+  const int xyn = a.xn * a.yn;
+  const int h = z * xyn + y * a.xn + x;
+  const int32_t* __restrict__ fexist = a.exist + f * a.s_exist;
+  const float4* G4 = reinterpret_cast<const float4*>(a.G + f * a.s_G);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int dz = 0; dz < md.zr; ++dz)
+    for (int dy = 0; dy < md.yr; ++dy)
+      for (int dx = 0; dx < md.xr; ++dx) {
+        const int hh = h + dz * xyn + dy * a.xn + dx;
+        if (fexist[hh] != 0) {
+          const float4 v = G4[(int64_t)hh * D4 + d4];
+          s.x += v.x;
+          s.y += v.y;
+          s.z += v.z;
+          s.w += v.w;
+        }
+      }
+  reinterpret_cast<float4*>(a.gbox + f * a.s_gbox)[g * D4 + d4] = s;
+}
+
 // Rank-1 replay fused into the score launch (search.cpp:464-474 with rank_num == 1:
 // checkOverlap returns slot 0, so the update is "first strictly greater maximum in scan
 // order").  One wave per model reduces the partials with (score desc, scan order asc);
@@ -634,7 +667,21 @@ __device__ __forceinline__ void score_list_body(const SparseSearch& b, int bx, i
     }
     lds_barrier();
     C3H_SPROF(1);
-    {  // box sums in the fixed (dz, dy, dx) order over non-empty rows; lane = position.
+    if (b.gbox) {  // precomputed box sums (boxsum_kernel): one row per position
+      const float4* B4 = reinterpret_cast<const float4*>(b.gbox + fz * b.s_gbox);
+      for (int e = tid; e < kFP * D4; e += kBlock) {
+        const int pp = e & (kFP - 1), d4 = e / kFP;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gate[pp]) {
+          const long long en = ent[pp];
+          v = B4[(a.pstart[(int)(en >> 40)] + (en & ((1ll << 40) - 1))) * D4 + d4];
+        }
+        fT[(4 * d4 + 0) * kFP + pp] = v.x;
+        fT[(4 * d4 + 1) * kFP + pp] = v.y;
+        fT[(4 * d4 + 2) * kFP + pp] = v.z;
+        fT[(4 * d4 + 3) * kFP + pp] = v.w;
+      }
+    } else {  // box sums in the fixed (dz, dy, dx) order over non-empty rows; lane = position.
        // Cells go in batches of 4 x (this thread's d4 slots): every load of a batch is in
        // flight together.  Rows of empty subdivisions read as 0 (their G rows may be stale;
        // +0 added to a sum that starts at +0 changes nothing).
