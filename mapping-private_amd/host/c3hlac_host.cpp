@@ -576,6 +576,71 @@ void SearchObj::ensureSetup(int F) {
   setup_dirty_ = false;
 }
 
+void SearchObj::readData(const char* filenameF, const char* filenameN, int dim, bool ascii) {
+  if (dim < 1) throw Error(C3H_ERR_ARG, "readData: dim");
+  FILE* fp = fopen(filenameF, ascii ? "r" : "rb");
+  FILE* fp2 = fopen(filenameN, ascii ? "r" : "rb");
+  if (!fp || !fp2) {
+    if (fp) fclose(fp);
+    if (fp2) fclose(fp2);
+    throw Error(C3H_ERR_NOTFOUND, "readData: cannot open the integral tables");
+  }
+  int n3[3] = {0, 0, 0};
+  bool ok = ascii ? fscanf(fp, "%d %d %d\n", &n3[0], &n3[1], &n3[2]) == 3 : fread(n3, sizeof(int), 3, fp) == 3;
+  ok = ok && n3[0] > 0 && n3[1] > 0 && n3[2] > 0;
+  const int64_t H = ok ? (int64_t)n3[0] * n3[1] * n3[2] : 0;
+  std::vector<double> I((size_t)H * dim);
+  std::vector<int64_t> E((size_t)H);
+  for (int64_t n = 0; n < H && ok; ++n) {
+    for (int j = 0; j < dim && ok; ++j) {
+      double v;
+      if (ascii) {
+        int idx;
+        ok = fscanf(fp, "%d:%lf ", &idx, &v) == 2;
+      } else {
+        ok = fread(&v, sizeof(double), 1, fp) == 1;
+      }
+      I[(size_t)n * dim + j] = (double)(float)v;  // integral_features is VectorXf
+    }
+    int e = 0;
+    ok = ok && (ascii ? fscanf(fp2, "%d\n", &e) == 1 : fread(&e, sizeof(int), 1, fp2) == 1);
+    E[(size_t)n] = e;
+  }
+  fclose(fp);
+  fclose(fp2);
+  if (!ok) throw Error(C3H_ERR_FORMAT, "readData: malformed integral tables");
+  // per-subdivision values: 3-D differences of the summed-volume tables (search.cpp:579-653)
+  const int X = n3[0], Y = n3[1];
+  auto at = [&](int x, int y, int z) -> int64_t { return x < 0 || y < 0 || z < 0 ? -1 : x + (int64_t)X * (y + (int64_t)Y * z); };
+  std::vector<float> cell((size_t)H * dim);
+  std::vector<int32_t> ex((size_t)H);
+  for (int z = 0; z < n3[2]; ++z)
+    for (int y = 0; y < Y; ++y)
+      for (int x = 0; x < X; ++x) {
+        const int64_t id[8] = {at(x, y, z), at(x - 1, y, z), at(x, y - 1, z), at(x - 1, y - 1, z),
+                               at(x, y, z - 1), at(x - 1, y, z - 1), at(x, y - 1, z - 1), at(x - 1, y - 1, z - 1)};
+        const int sg[8] = {1, -1, -1, 1, -1, 1, 1, -1};
+        const int64_t h = id[0];
+        int64_t e = 0;
+        for (int k = 0; k < 8; ++k)
+          if (id[k] >= 0) e += sg[k] * E[(size_t)id[k]];
+        ex[(size_t)h] = (int32_t)e;
+        for (int j = 0; j < dim; ++j) {
+          double v = 0;
+          for (int k = 0; k < 8; ++k)
+            if (id[k] >= 0) v += sg[k] * I[(size_t)id[k] * dim + j];
+          cell[(size_t)h * dim + j] = (float)v;
+        }
+      }
+  compress_ = false;  // the tables hold compressed features already
+  axis_p_ = MatrixXf();
+  setup_dirty_ = true;
+  ensureSetup(dim);
+  const int32_t sb[3] = {n3[0], n3[1], n3[2]};
+  ctx_.check(c3h_set_features(ctx_.get(), cell.data(), sb, dim, ex.data(), 0, 0), "c3h_set_features");
+  setDataFromContext(Vector3i{n3[0], n3[1], n3[2]});
+}
+
 void SearchObj::setDataFromContext(const Vector3i& subdiv_b) {
   xn_ = subdiv_b[0];
   yn_ = subdiv_b[1];

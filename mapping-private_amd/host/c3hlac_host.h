@@ -245,6 +245,11 @@ class SearchObj {
   virtual int maxYrange(int num) const { return yRange(maxMode(num)); }
   virtual int maxZrange(int num) const { return zRange(maxMode(num)); }
   void setNormalizeVal(const char* filename);
+  // readData (search.cpp:169-210): the legacy integral tables of an already compressed scene
+  // (dim values per subdivision, and the exist counts).  They are differenced back to
+  // per-subdivision values (double) and searched without a scene axis (D = dim), the box
+  // sums formed directly instead of clipValue's inclusion-exclusion.
+  void readData(const char* filenameF, const char* filenameN, int dim, bool ascii);
 
   // setData (search.cpp:539-658) on features already extracted into this context
   void setDataFromContext(const Vector3i& subdiv_b);

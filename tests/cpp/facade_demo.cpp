@@ -9,6 +9,7 @@
 //   facade_demo rot <dim> <mode>                        (host only: rotateFeature90 of 0..dim-1)
 //   facade_demo train <rows.bin> <out_dir> <D> <n_model> (GPU: pca_scene.cpp + pca_models.cpp)
 //   facade_demo vosch <cloud.pcd> <leaf>                (GPU: example_GRSD_CCHLAC / setVOSCH flow)
+//   facade_demo readdata <F.bin> <N.bin> <dir> <dim>     (GPU: SearchObj::readData + search)
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -203,6 +204,29 @@ static int vosch(const char* path, float leaf) {
   return 0;
 }
 
+// SearchObj::readData (search.cpp:169-210) of binary integral tables, 2 synthetic models
+static int readdata(const char* fF, const char* fN, const std::string& dir, int dim) {
+  const std::string m0 = dir + "/m0", m1 = dir + "/m1";
+  write_pca(m0.c_str(), dim, 11);
+  write_pca(m1.c_str(), dim, 12);
+  char* files[2] = {const_cast<char*>(m0.c_str()), const_cast<char*>(m1.c_str())};
+  SearchObjMulti so;
+  so.setModelNum(2);
+  so.readAxis(files, dim, 4, false, true);
+  so.setRank(1);
+  so.setRange(2, 2, 2);
+  so.setThreshold(5);
+  so.readData(fF, fN, dim, false);
+  so.search();
+  printf("{\"dets\": [");
+  for (int m = 0; m < 2; ++m) {
+    const c3h_det& d = so.detections()[m];
+    printf(m ? ", [%.17g, %d, %d, %d, %d]" : "[%.17g, %d, %d, %d, %d]", d.score, d.x, d.y, d.z, d.mode);
+  }
+  printf("]}\n");
+  return 0;
+}
+
 int main(int argc, char** argv) {
   try {
     if (argc == 4 && !strcmp(argv[1], "params")) return params(argv[2], argv[3]);
@@ -212,6 +236,7 @@ int main(int argc, char** argv) {
     if (argc == 4 && !strcmp(argv[1], "rot")) return rot(atoi(argv[2]), atoi(argv[3]));
     if (argc == 6 && !strcmp(argv[1], "train")) return train(argv[2], argv[3], atoi(argv[4]), atoi(argv[5]));
     if (argc == 4 && !strcmp(argv[1], "vosch")) return vosch(argv[2], (float)atof(argv[3]));
+    if (argc == 6 && !strcmp(argv[1], "readdata")) return readdata(argv[2], argv[3], argv[4], atoi(argv[5]));
   } catch (const Error& e) {
     fprintf(stderr, "c3hlac::Error %d: %s\n", e.code, e.what());
     return 2;

@@ -193,3 +193,38 @@ def test_facade_vosch_flow(ctx, demo):
     c3 = ctx.features()[0]
     assert np.array_equal(np.float32(j["vosch_head"][:20]), g)
     assert np.array_equal(np.float32(j["vosch_head"][20:22]), c3[:2])
+
+
+@pytest.mark.gpu
+def test_facade_read_data_integral_tables(ctx, demo, tmp_path):
+    """SearchObj::readData (search.cpp:169-210): binary integral tables of compressed
+    features and exist counts -> search; the same lists as the binding's search on the
+    per-subdivision values the tables difference to (readAxis of the same model files)."""
+    rng = np.random.default_rng(5)
+    X, Y, Z, D = 9, 8, 7, 16
+    cells = rng.standard_normal((Z, Y, X, D))
+    ex = rng.integers(0, 6, (Z, Y, X)).astype(np.int64)
+    I = cells.cumsum(0).cumsum(1).cumsum(2)
+    E = ex.cumsum(0).cumsum(1).cumsum(2)
+    fF, fN = tmp_path / "F.bin", tmp_path / "N.bin"
+    fF.write_bytes(np.array([X, Y, Z], np.int32).tobytes() + I.astype(np.float64).tobytes())
+    fN.write_bytes(E.astype(np.int32).tobytes())
+    out = subprocess.run([str(demo), "readdata", str(fF), str(fN), str(tmp_path), str(D)], check=True,
+                         capture_output=True, text=True).stdout
+    dets = json.loads(out)["dets"]
+    # the facade's cells: 3-D differences (double) of the float-stored integral table
+    If = I.astype(np.float32).astype(np.float64)
+    P = np.pad(If, ((1, 0), (1, 0), (1, 0), (0, 0)))
+    c = (P[1:, 1:, 1:] - P[1:, 1:, :-1] - P[1:, :-1, 1:] + P[1:, :-1, :-1]
+         - P[:-1, 1:, 1:] + P[:-1, 1:, :-1] + P[:-1, :-1, 1:] - P[:-1, :-1, :-1]).astype(np.float32)
+    qs = []
+    for m in (0, 1):
+        a, v, _ = c3hlac.pca_read(tmp_path / ("m%d" % m))
+        qs.append(c3hlac.read_axis(a, v, D, 4))
+    ctx.set_features(c.reshape(-1, D), (X, Y, Z), ex.reshape(-1).astype(np.int32))
+    ctx.search_setup(None, None, np.stack(qs))
+    ctx.set_rank(1)
+    lists, _ = ctx.search((2, 2, 2), 5)
+    for m in (0, 1):
+        e = lists[m, 0]
+        assert [float(e["score"]), int(e["x"]), int(e["y"]), int(e["z"]), int(e["mode"])] == dets[m]
