@@ -264,7 +264,7 @@ def main():
 
 def pmc_traffic(frames_per_tick):
     """HBM bytes per tick launch from the committed rocprofv3 --pmc summary of this build
-    (tools/scripts_pmc.sh -> tools/pmc_summary.py): FETCH_SIZE x2 (gfx950 correction) +
+    (tools/pmc.sh -> tools/pmc_summary.py): FETCH_SIZE x2 (gfx950 correction) +
     WRITE_SIZE of c3h_tick_kernel per frame through the pipeline, times the frames per tick.
     PMC needs its own profiler pass, so it cannot be collected inside the timed run; None
     when no summary is committed."""
