@@ -158,7 +158,10 @@ __global__ __launch_bounds__(kBlock) void c3_occupancy_kernel(OccArgs oa) {
 }
 
 // dense frames: one tile per wave on the i8 matrix cores (c3hlac_mfma.h)
-__global__ __launch_bounds__(kBlock, 2) void c3hlac_mfma_kernel(KArgs a) {
+#ifndef C3H_MF_MINB
+#define C3H_MF_MINB 3
+#endif
+__global__ __launch_bounds__(kBlock, C3H_MF_MINB) void c3hlac_mfma_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t mf_smem[];
   c3hlac_mfma_body(a, blockIdx.x * kMfWaves + (threadIdx.x >> 6), gridDim.x * kMfWaves, blockIdx.y, mf_smem);
 }
@@ -424,7 +427,7 @@ C3Args build_c3_args(const C3Launch& l) {
   a.debug = l.debug;
   a.prof = l.prof;
   a.wave117 = wave117_ok(l) ? 1 : 0;
-  a.mf_ty = l.lmax[1] + 2;
+  a.mf_pb = mf_plane_bytes(l.lmax[0], l.lmax[1]);
   a.mfma = 0;  // set by launch_c3hlac (the stand-alone path), never in the tick
   if (a.wave117) a.tw_max = w117_halo_words(l.lmax[0], l.lmax[1], l.lmax[2]);
   c.tile_lds = a.wave117 ? w117_lds_bytes(a.tw_max, a.list_max) : c3hlac_lds_bytes(a.tw_max, a.list_max);
@@ -479,7 +482,7 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
     c3_occupancy_kernel<false, false><<<g1d, kBlock, 0, s>>>(c.oa);
   c3hlac_tile_kernel<<<dim3((unsigned)c.tgrid, (unsigned)l.nframes), kBlock, c.tile_lds, s>>>(c.ka);
   if (mf) {  // both kernels read the frame's work count; each takes the frames of its kind
-    const size_t lds = mf_lds_bytes(c.ka.mf_ty);
+    const size_t lds = mf_lds_bytes(c.ka.mf_pb);
     c3hlac_mfma_kernel<<<dim3((unsigned)mfma_grid(l, lds), (unsigned)l.nframes), kBlock, lds, s>>>(c.ka);
   }
   return hipGetLastError();

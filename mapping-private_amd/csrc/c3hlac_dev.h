@@ -440,7 +440,7 @@ struct KArgs {
   int wave117;      // C3-HLAC-117 per-wave tiles (c3hlac_wave117_body), else the block body
   int mfma;         // the dense-tile MFMA kernel runs beside (c3hlac_mfma.h): frames with
                     // >= half of their tiles non-empty are left to it
-  int mf_ty;        // its largest tile row count (ly + 2)
+  int mf_pb;        // its largest channel-plane size (mf_plane_bytes of the largest tile)
   int debug;  // diagnostics only (C3H_C3_DEBUG): 1 stop after the loads, 2 after compaction,
              // 3 skip the tile kernel
 };

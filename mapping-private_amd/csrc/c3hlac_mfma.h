@@ -10,20 +10,27 @@
 // 16 x 16 x K integer GEMM per k with K = centre voxels:
 //   A = X (row c = channel, 12 of 16 rows), B_k = Y shifted by r_k (column n = channel).
 // u8 channel values are stored offset by -128 (byte ^ 0x80), which i8 holds exactly, and
-// the exact sums are recovered with the tile's own row / column sums, which the padding
-// rows / columns compute for free: row 15 of A and column 15 of B are constant 1, so
+// the exact sums are recovered with the padding rows / columns: row 15 of A and column 15
+// of B are constant 1, so
 //   sum a b = C[c][n] + 128 (C[c][15] + C[15][n]) + 128^2 C[15][15]
-// (an empty or masked position carries a = 0, i.e. -128, and the identity holds
-// elementwise).  i32 accumulation is exact (|a' b'| <= 2^14, K <= 16 * 16 * 16 * 2).
+// elementwise over the K positions: a position that is no centre carries a = 0 (A' = -128,
+// whatever B holds there), so the K positions need not all be centres.  C[c][15] is the
+// same for every k (A does not move), C[15][15] is the position count.  u32 arithmetic is
+// exact (every true sum is < 2^32; |a' b'| <= 2^14 per position).
 //
-// Mapping: one wave per tile (<= 16 x 16 centres per layer), walking the tile's layers
-// in z.  Layer L (z = z0 - 1 + L) is built in LDS as 12 channel planes of (ly + 2) rows x
-// 32 B (x = -1 at byte 0); a K step covers 4 rows x 16 x (lane group h = lane >> 4 takes
-// row y = 4 ks + h, byte j = centre x j), so every A / B fragment of a lane is 16
-// consecutive bytes of one plane row: two aligned ds_read_b128 and a byte shift
-// (v_alignbyte) give the dx = -1, 0, +1 fragments of a row.  Per K step: 10 LDS reads, 14
-// MFMAs.  The next layer's grid words are loaded into registers before the current
-// layer's MFMAs and stored after them (three layer slots in a ring).
+// Mapping: one wave per tile (<= 16 x 16 centres per layer), walking the tile's layers in
+// z.  Layer L (z = z0 - 1 + L) is held in LDS as 12 channel planes, each the layer's
+// (ly + 2) rows of (lx + 2) bytes (halo included) at a row pitch PW = lx + 2 rounded up to
+// 4, packed one after another: a voxel's neighbour at (dx, dy) is dy * PW + dx bytes away.
+// A K step is 64 consecutive plane positions (lane group h = lane >> 4 takes 16 of them)
+// starting at row 1, so a K step spans row boundaries and only the positions that are
+// centres count (a per-tile byte mask plane); S = 10 tiles take 2 K steps per layer where a
+// 16-byte row per lane group took 3.  The K origin is 16-byte aligned; PW mod 16 (0, 4, 8,
+// 12) is a template parameter, so every fragment is read as aligned dwords (ds_read_b128 /
+// b64 / b32 by its alignment) and the dx = +-1 shifts are one v_alignbyte per dword.  Per K
+// step: 5 plane rows + the mask, 14 MFMAs.  The next layer's grid words are loaded into
+// registers two layers ahead (three layer slots in a ring).  The epilogue corrects and
+// scatters the accumulator tiles from registers (the padding lanes' sums by ds_bpermute).
 #pragma once
 #include "c3hlac_dev.h"
 
@@ -31,79 +38,131 @@ namespace c3h {
 
 typedef int mf_v4i __attribute__((ext_vector_type(4)));
 constexpr int kMfWaves = kBlock / 64;
-constexpr int kMfRowB = 32;  // bytes per plane row
 constexpr int kMfCh = 12;
-constexpr int kMfK = 14;     // 13 offsets + the centre's own channels
-constexpr int kMfLoad = 2;  // (row, dword) pairs per lane of a layer (<= 18 rows x 5 dwords)
-constexpr int kMfTyMax = 18;
+constexpr int kMfK = 14;    // 13 offsets + the centre's own channels
+constexpr int kMfLoad = 2;  // (row, dword) items per lane of a layer (<= 18 rows x 5 dwords)
 #ifndef C3H_MF_EXP
 #define C3H_MF_EXP 0  // diagnostics variants: 1 no K steps, 2 no conversion
 #endif
 
-__host__ __device__ inline int mf_slot_bytes(int ty) { return kMfCh * ty * kMfRowB; }
-// per wave: 2 constant planes (rows 12..15 of A / columns 12..15 of B: zeros, and ones
-// in 15), then 3 plane slots or (aliasing them) the epilogue's accumulator tiles
-constexpr int kMfConstBytes = 2 * kMfTyMax * kMfRowB;
-__host__ __device__ inline int mf_wave_bytes(int ty) {
-  const int work = 3 * mf_slot_bytes(ty), epi = kMfK * 256 * 4;
-  return kMfConstBytes + (((work > epi ? work : epi) + 15) & ~15);
+__host__ __device__ inline int mf_pitch(int lx) { return (lx + 2 + 3) & ~3; }
+// byte of position 0 in a plane: (off0 + PW) % 16 == 0 (the K origin), >= 16 bytes of
+// headroom for the dy = -1 reads of the first K step
+__host__ __device__ inline int mf_off0(int pw) { return 16 + ((16 - (pw & 15)) & 15); }
+__host__ __device__ inline int mf_nks(int lx, int ly, int pw) { return ((ly - 1) * pw + lx + 1 + 63) / 64; }
+// LDS banks: a ds_read_b128 serves 16 lanes per cycle, lane (h, n) reading 16 bytes of
+// plane n at chunk h.  With the plane stride = 32 mod 256 bytes, the layer slots and the
+// wave regions 256-byte aligned and the constant planes (read by lanes n >= 12) at 128 mod
+// 256, every lane group's 16 reads hit 16 distinct 4-bank blocks (no conflicts; a stride of
+// 192 bytes was 2-way).
+__host__ __device__ inline int mf_plane_bytes(int lx, int ly) {
+  const int pw = mf_pitch(lx), o = mf_off0(pw), n = mf_nks(lx, ly, pw);
+  const int a = o + (ly + 2) * pw, b = o + 2 * pw + 64 * n + 16;
+  const int m = a > b ? a : b;
+  return ((m - 32 + 255) & ~255) + 32;
 }
-// 3 x 256 channel-byte tables | 984 epilogue bin codes | per-wave regions
-__host__ __device__ inline size_t mf_lds_bytes(int ty) { return 3072 + 3936 + (size_t)kMfWaves * mf_wave_bytes(ty); }
-
-// 16 bytes starting at byte s (0..2) of a 32-byte plane row held as two uint4
-__device__ __forceinline__ mf_v4i mf_frag(const uint4& lo, const uint4& hi, int s) {
-  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-  mf_v4i f;
-  f[0] = (int)__builtin_amdgcn_alignbyte(w[1], w[0], s);
-  f[1] = (int)__builtin_amdgcn_alignbyte(w[2], w[1], s);
-  f[2] = (int)__builtin_amdgcn_alignbyte(w[3], w[2], s);
-  f[3] = (int)__builtin_amdgcn_alignbyte(w[4], w[3], s);
-  return f;
+__host__ __device__ inline int mf_r256(int x) { return (x + 255) & ~255; }
+__host__ __device__ inline int mf_slot_stride(int pb) { return mf_r256(kMfCh * pb); }
+__host__ __device__ inline int mf_wave_stride(int pb) { return 3 * mf_slot_stride(pb) + mf_r256(pb); }
+__host__ __device__ inline int mf_const_bytes(int pb) { return mf_r256(128 + 3 * pb); }
+// 3 x 256 channel-byte tables | 128 B | 3 constant planes (0x00, 0x01, 0xff) | per-wave
+// regions: 3 layer slots of 12 planes, the centre mask
+__host__ __device__ inline size_t mf_lds_bytes(int pb) {
+  return 3072 + (size_t)mf_const_bytes(pb) + (size_t)kMfWaves * mf_wave_stride(pb);
 }
-
-__device__ __forceinline__ void wave_lds_sync() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // channel plane of (type t: 0 colour LUT / 1 binary, reference channel c in 0..5): the
 // planes hold per colour col the bytes {sin, cos, beta, 1 - beta} (4 col + s)
 __host__ __device__ inline int mf_plane(int t, int c) { return 4 * (c >> 1) + 2 * t + (c & 1); }
 
-// epilogue code of bin e (0..980): bin | kind << 10 | k << 12 | c << 16 | n << 20, kind 0 =
-// product bin (offset k's tile at plane c, plane n), 1 = zero order (plane c's row sum)
-__device__ inline uint32_t mf_bin_code(int e) {
-  int bin, kind = 0, k = 13, c, nn;
-  if (e < 936) {  // first order: k, type (colour / binary), c, n
-    k = e / 72;
-    const int rem = e - 72 * k, ty = rem / 36, cc = (rem % 36) / 6, n6 = rem % 6;
-    bin = 495 * ty + bin981(k, cc, n6);
-    c = mf_plane(ty, cc);
-    nn = mf_plane(ty, n6);
-  } else if (e < 957) {  // centre auto products (c <= n)
-    const int q = e - 936;
-    int cc = 0;
-    while (q >= tri6(cc + 1, cc + 1)) ++cc;
-    bin = 474 + q;
-    c = mf_plane(0, cc);
-    nn = mf_plane(0, cc + (q - tri6(cc, cc)));
-  } else if (e < 969) {  // centre bin-pair counts
-    const int q = e - 957;
-    const int cc = q < 8 ? q / 4 : 2 + (q - 8) / 2, n6 = q < 8 ? 2 + q % 4 : 4 + (q - 8) % 2;
-    bin = 969 + q;
-    c = mf_plane(1, cc);
-    nn = mf_plane(1, n6);
-  } else {  // zero order: colour channels, then binary counts
-    const int q = e - 969;
-    bin = q < 6 ? q : 495 + (q - 6);
-    kind = 1;
-    c = mf_plane(q < 6 ? 0 : 1, q < 6 ? q : q - 6);
-    nn = 15;
+__device__ __forceinline__ void mf_compiler_fence() { __asm__ volatile("" ::: "memory"); }
+
+typedef uint32_t mf_u4 __attribute__((ext_vector_type(4)));
+constexpr int mf_fdiv16(int x) { return x >= 0 ? x / 16 : -((15 - x) / 16); }
+
+// The 16-byte blocks of a plane row holding the bytes at DYR + dx .. + 15 for dx in
+// [DXLO, DXHI] (DYR = dy * (PW mod 16), compile time), read from the row's 16-byte aligned
+// base as whole ds_read_b128 blocks, and its dx fragments (v_alignbyte for dx = +-1)
+template <int DYR, int DXLO, int DXHI>
+struct MfRow {
+  static constexpr int B0 = mf_fdiv16(DYR + DXLO), NB = mf_fdiv16(DYR + DXHI + 15) - B0 + 1;
+  uint32_t w[4 * NB];
+  __device__ __forceinline__ void load(const uint8_t* row) {
+    const uint8_t* p = static_cast<const uint8_t*>(__builtin_assume_aligned(row, 16));
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      mf_u4 v = *reinterpret_cast<const mf_u4*>(p + 16 * (B0 + b));
+      __asm__("" : "+v"(v));  // keep the whole block: a narrowed ds_read_b32 bank-conflicts
+      w[4 * b] = v.x; w[4 * b + 1] = v.y; w[4 * b + 2] = v.z; w[4 * b + 3] = v.w;
+    }
   }
-  return (uint32_t)bin | ((uint32_t)kind << 10) | ((uint32_t)k << 12) | ((uint32_t)c << 16) | ((uint32_t)nn << 20);
+  template <int DX>
+  __device__ __forceinline__ mf_v4i frag() const {
+    constexpr int e = DYR + DX - 16 * B0, d = e >> 2, sh = e & 3;
+    mf_v4i f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      f[i] = sh ? (int)__builtin_amdgcn_alignbyte(w[d + i + 1], w[d + i], sh) : (int)w[d + i];
+    return f;
+  }
+};
+
+// The K steps of one layer.  pp / pc / pm: this lane's dz = -1 plane, dz = 0 plane and mask
+// plane at the K origin (byte off0 + PW, 16-byte aligned); pw16 = PW - R.
+template <int R>
+__device__ __forceinline__ void mf_layer_ksteps(const uint8_t* pp, const uint8_t* pc, const uint8_t* pm, int pw16,
+                                                int nks, int h4, mf_v4i (&acc)[kMfK]) {
+#pragma unroll 1
+  for (int ks = 0; ks < nks; ++ks) {
+    const int o = 64 * ks + 16 * h4;
+    // dz = 0: row 0 (the centres and dx = -1), row -1
+    MfRow<0, -1, 0> c0;
+    MfRow<-R, -1, 1> cm;
+    c0.load(pc + o);
+    cm.load(pc + o - pw16);
+    const mf_u4 m = *reinterpret_cast<const mf_u4*>(__builtin_assume_aligned(pm + o, 16));
+    const mf_v4i a0 = c0.frag<0>();
+    mf_v4i A;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) A[i] = (int)(((uint32_t)a0[i] & m[i]) | (0x80808080u & ~m[i]));
+    acc[13] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, A, acc[13], 0, 0, 0);                  // own channels
+    acc[12] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, c0.frag<-1>(), acc[12], 0, 0, 0);  // (-1, 0, 0)
+    acc[9] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, cm.template frag<-1>(), acc[9], 0, 0, 0);    // (dx, -1, 0)
+    acc[10] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, cm.template frag<0>(), acc[10], 0, 0, 0);
+    acc[11] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, cm.template frag<1>(), acc[11], 0, 0, 0);
+    // dz = -1, rows dy = -1, 0, +1: k = 3 (dx + 1) + (dy + 1)
+    {
+      MfRow<-R, -1, 1> r;
+      r.load(pp + o - pw16);
+      acc[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, r.template frag<-1>(), acc[0], 0, 0, 0);
+      acc[3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, r.template frag<0>(), acc[3], 0, 0, 0);
+      acc[6] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, r.template frag<1>(), acc[6], 0, 0, 0);
+    }
+    {
+      MfRow<0, -1, 1> r;
+      r.load(pp + o);
+      acc[1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, r.template frag<-1>(), acc[1], 0, 0, 0);
+      acc[4] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, r.template frag<0>(), acc[4], 0, 0, 0);
+      acc[7] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, r.template frag<1>(), acc[7], 0, 0, 0);
+    }
+    {
+      MfRow<R, -1, 1> r;
+      r.load(pp + o + pw16);
+      acc[2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, r.template frag<-1>(), acc[2], 0, 0, 0);
+      acc[5] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, r.template frag<0>(), acc[5], 0, 0, 0);
+      acc[8] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, r.template frag<1>(), acc[8], 0, 0, 0);
+    }
+  }
 }
 
-// wave wid of nw (all waves of this launch for frame fy); smem = mf_lds_bytes(TYmax)
-__device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw, int fy_, uint32_t* smem) {
+// plane p -> (type, reference channel); p >= 12 is padding
+__device__ __forceinline__ int mf_type(int p) { return (p >> 1) & 1; }
+__device__ __forceinline__ int mf_chan(int p) { return 2 * (p >> 2) + (p & 1); }
+
+// wave wid of nw (all waves of this launch for frame fy); smem = mf_lds_bytes(a.mf_pb)
+__device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int nw, int fy_, uint32_t* smem) {
   const int64_t fy = fy_;
+  const int wid = wid_;
   const uint32_t* __restrict__ fgrid = a.grids[fy];
   float* __restrict__ ffeat = a.feat + fy * a.s_feat;
   int32_t* __restrict__ fexist = a.exist + fy * a.s_h;
@@ -112,9 +171,9 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
   const int32_t* __restrict__ fwork = a.work + fy * a.s_work;
   int32_t* frows = a.rows ? a.rows + fy * a.s_h : nullptr;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int PBM = a.mf_pb;
   // channel-byte tables: T_col[v] = {sin, cos, beta, 1 - beta} ^ 0x80 (setColor LUT, thresholds)
   uint32_t* s_tab = smem;
-  uint32_t* s_bins = smem + 768;
   for (int i = threadIdx.x; i < 768; i += kBlock) {
     const int col = i >> 8, v = i & 255;
     const uint32_t l = a.lut[v];
@@ -122,18 +181,18 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
     const uint32_t be = v > thr ? 1u : 0u;
     s_tab[i] = ((l & 0xffu) | (l & 0xff00u) | (be << 16) | ((be ^ 1u) << 24)) ^ 0x80808080u;
   }
-  for (int e = threadIdx.x; e < 981; e += kBlock) s_bins[e] = mf_bin_code(e);
-  uint8_t* cplanes = reinterpret_cast<uint8_t*>(smem + 768 + 984) + (size_t)wave * mf_wave_bytes(a.mf_ty);
-  uint8_t* wl = cplanes + kMfConstBytes;  // 3 layer slots, or the epilogue
-  uint8_t* planes = wl;
-  for (int i = lane; i < 2 * kMfTyMax * kMfRowB / 4; i += 64)
-    reinterpret_cast<uint32_t*>(cplanes)[i] = i >= kMfTyMax * kMfRowB / 4 ? 0x01010101u : 0u;
+  if (threadIdx.x == 0) s_tab[768] = 0x80808080u;  // an empty voxel (in the 128-byte gap)
+  uint8_t* cplanes = reinterpret_cast<uint8_t*>(smem + 768) + 128;  // zeros | ones | 0xff
+  for (int i = threadIdx.x; i < 3 * PBM / 4; i += kBlock)
+    reinterpret_cast<uint32_t*>(cplanes)[i] = i < PBM / 4 ? 0u : (i < 2 * PBM / 4 ? 0x01010101u : 0xffffffffu);
+  uint8_t* wl = reinterpret_cast<uint8_t*>(smem + 768) + mf_const_bytes(PBM) + (size_t)wave * mf_wave_stride(PBM);
   __syncthreads();
   const int nwork = (int)ftf[2 + (a.epoch & 1)];
   if (2 * nwork < a.ntiles) return;  // sparse frame: the dot4 tile body takes it
   const int F = a.variant;
-  const int h4 = lane >> 4, n = lane & 15;
-  const bool real = n < kMfCh;
+  // this lane holds C_k[c = 4 (lane >> 4) + r][lane & 15]
+  const int h4k = lane >> 4, nk = lane & 15;
+  const bool realk = nk < kMfCh;
 
   for (int wi = wid; wi < nwork; wi += nw) {
     const int tile = fwork[wi];
@@ -143,24 +202,46 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
     const int32_t* sz = a.segs + 3 * (2 * a.seg_stride + iz);
     const int x0 = sx[0], lx = sx[1], y0 = sy[0], ly = sy[1], z0 = sz[0], lz = sz[1];
     const int64_t h = sx[2] + (int64_t)sy[2] * a.sbx + (int64_t)sz[2] * a.sbx * a.sby;
-    const int TY = ly + 2, nks = (ly + 3) >> 2, npair = TY * 5;
-    const int sb = mf_slot_bytes(TY);
-    // layer words in registers: (row, dword q) pairs e = lane + 64 i, x = x0 - 1 + 4 q + j;
-    // two layers in flight
+    const int TW = lx + 2, TY = ly + 2, PW = mf_pitch(lx), off0 = mf_off0(PW), nks = mf_nks(lx, ly, PW);
+    const int PB = mf_plane_bytes(lx, ly);
+    const int ipr = PW >> 2, nitem = TY * ipr;
+    const int SS = mf_slot_stride(PB);
+    uint8_t* mask = wl + 3 * SS;
+    // centre mask of the K positions PW + 4 j + b: rows 1..ly, columns 1..lx
+    for (int j = lane; j < 16 * nks; j += 64) {
+      uint32_t m = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int p = PW + 4 * j + b, row = p / PW, col = p - row * PW;
+        m |= (row <= ly && col >= 1 && col <= lx ? 0xffu : 0u) << (8 * b);
+      }
+      *reinterpret_cast<uint32_t*>(mask + off0 + PW + 4 * j) = m;
+    }
+    // layer items (row, dword q) of lane + 64 i: x = x0 - 1 + 4 q + j, valid x bits, the
+    // row (-1 when out of the tile or the grid) and the item's byte in a plane
+    int it_gy[kMfLoad], it_x[kMfLoad], it_dst[kMfLoad];
+    uint32_t it_xm[kMfLoad];
+#pragma unroll
+    for (int i = 0; i < kMfLoad; ++i) {
+      const int e = lane + 64 * i, row = e / ipr, q = e - row * ipr, gy = y0 - 1 + row;
+      it_gy[i] = e < nitem && (unsigned)gy < (unsigned)a.gy ? gy : -1;
+      it_x[i] = x0 - 1 + 4 * q;
+      it_dst[i] = e < nitem ? off0 + row * PW + 4 * q : -1;
+      uint32_t xm = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xm |= (4 * q + j < TW && (unsigned)(it_x[i] + j) < (unsigned)a.gx ? 1u : 0u) << j;
+      it_xm[i] = xm;
+    }
     uint32_t wv[2][kMfLoad][4];
     auto load_layer = [&](int L, uint32_t (&w)[kMfLoad][4]) {
       const int gz = z0 - 1 + L;
+      const bool zin = (unsigned)gz < (unsigned)a.gz;
 #pragma unroll
       for (int i = 0; i < kMfLoad; ++i) {
-        const int e = lane + 64 * i, row = e / 5, q = e - row * 5;
-        const int gy = y0 - 1 + row;
-        const bool rowin = e < npair && (unsigned)gy < (unsigned)a.gy && (unsigned)gz < (unsigned)a.gz;
-        const uint32_t* src = fgrid + ((int64_t)gz * a.gy + gy) * a.gx;
+        const bool rowin = zin && it_gy[i] >= 0;
+        const uint32_t* src = fgrid + (((int64_t)gz * a.gy + it_gy[i]) * a.gx + it_x[i]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int gxx = x0 - 1 + 4 * q + j;
-          w[i][j] = rowin && (unsigned)gxx < (unsigned)a.gx ? src[gxx] : 0u;
-        }
+        for (int j = 0; j < 4; ++j) w[i][j] = rowin && ((it_xm[i] >> j) & 1u) ? src[j] : 0u;
       }
     };
     // 12 channel planes of layer L: per voxel and colour one table read gives the 4 channel
@@ -169,17 +250,18 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
 #if C3H_MF_EXP & 2
       return;
 #endif
-      uint8_t* slot = planes + (size_t)(L % 3) * sb;
+      uint8_t* slot = wl + (L % 3) * SS;
 #pragma unroll
       for (int i = 0; i < kMfLoad; ++i) {
-        const int e = lane + 64 * i, row = e / 5, q = e - row * 5;
-        if (e >= npair) continue;
+        if (it_dst[i] < 0) continue;
+        // empty voxels read entry 768 (all channels 0, i.e. 0x80 each)
         uint32_t t[3][4];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
           for (int col = 0; col < 3; ++col)
-            t[col][j] = w[i][j] ? s_tab[col * 256 + ((w[i][j] >> (16 - 8 * col)) & 0xffu)] : 0x80808080u;
+            t[col][j] = s_tab[w[i][j] ? col * 256 + ((w[i][j] >> (16 - 8 * col)) & 0xffu) : 768u];
+        uint8_t* dst = slot + it_dst[i];
 #pragma unroll
         for (int col = 0; col < 3; ++col) {
           const uint32_t u0 = __builtin_amdgcn_perm(t[col][1], t[col][0], 0x05010400u);
@@ -189,20 +271,10 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
           const uint32_t o[4] = {__builtin_amdgcn_perm(u2, u0, 0x05040100u), __builtin_amdgcn_perm(u2, u0, 0x07060302u),
                                  __builtin_amdgcn_perm(u3, u1, 0x05040100u), __builtin_amdgcn_perm(u3, u1, 0x07060302u)};
 #pragma unroll
-          for (int s2 = 0; s2 < 4; ++s2)
-            *reinterpret_cast<uint32_t*>(slot + ((size_t)(4 * col + s2) * TY + row) * kMfRowB + 4 * q) = o[s2];
+          for (int s2 = 0; s2 < 4; ++s2) *reinterpret_cast<uint32_t*>(dst + (4 * col + s2) * PB) = o[s2];
         }
       }
     };
-    // centre mask of A: bytes j >= lx are no centre (a = 0 -> 0x80); the constant lanes keep all
-    uint32_t keep[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      uint32_t m = 0;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) m |= (4 * d + b < lx ? 0xffu : 0u) << (8 * b);
-      keep[d] = real ? m : 0xffffffffu;
-    }
     mf_v4i acc[kMfK];
 #pragma unroll
     for (int k = 0; k < kMfK; ++k) acc[k] = mf_v4i{0, 0, 0, 0};
@@ -212,45 +284,25 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
     store_layer(1, wv[1]);
     if (2 <= lz) load_layer(2, wv[0]);
     if (3 <= lz) load_layer(3, wv[1]);
+    // this lane's planes at the K origin: real channels from the layer slots, padding rows /
+    // columns from the constant planes (12..14 zeros, 15 ones; their mask keeps everything)
+    const int korg = off0 + PW;
+    const uint8_t* cpad = cplanes + (nk == 15 ? PBM : 0) + korg;
+    const uint8_t* pmask = realk ? mask + korg : cplanes + 2 * PBM + korg;
+    const int pw16 = PW & ~15;
     for (int z = 0; z < lz; ++z) {
-      wave_lds_sync();
-      const uint8_t* sp = planes + (size_t)(z % 3) * sb;        // dz = -1
-      const uint8_t* sc = planes + (size_t)((z + 1) % 3) * sb;  // dz = 0
-      // padding lanes read the constant planes (their rows are the same for every layer)
-      const uint8_t* pc = real ? sc + (size_t)n * TY * kMfRowB : cplanes + (n == 15 ? kMfTyMax * kMfRowB : 0);
-      const uint8_t* pp = real ? sp + (size_t)n * TY * kMfRowB : pc;
-      for (int ks = 0; ks < ((C3H_MF_EXP & 1) ? 0 : nks); ++ks) {
-        const int y = 4 * ks + h4;
-        const bool ym = y < ly;
-        const int rm = min(y, TY - 1), rc = min(y + 1, TY - 1), rp = min(y + 2, TY - 1);
-        auto row = [&](const uint8_t* plane, int r, uint4& lo, uint4& hi) {
-          lo = *reinterpret_cast<const uint4*>(plane + r * kMfRowB);
-          hi = *reinterpret_cast<const uint4*>(plane + r * kMfRowB + 16);
-        };
-        uint4 lo, hi;
-        row(pc, rc, lo, hi);
-        mf_v4i A = mf_frag(lo, hi, 1);
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          const uint32_t m = (ym || !real) ? keep[d] : 0u;
-          A[d] = (int)(((uint32_t)A[d] & m) | (0x80808080u & ~m));
-        }
-        acc[13] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, A, acc[13], 0, 0, 0);  // own channels
-        acc[12] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, mf_frag(lo, hi, 0), acc[12], 0, 0, 0);  // (-1, 0, 0)
-        row(pc, rm, lo, hi);  // (dx, -1, 0): k = 9 + dx + 1
-#pragma unroll
-        for (int dxi = 0; dxi < 3; ++dxi)
-          acc[9 + dxi] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, mf_frag(lo, hi, dxi), acc[9 + dxi], 0, 0, 0);
-        // (dx, dy, -1): k = 3 (dx + 1) + (dy + 1)
-#pragma unroll
-        for (int dyi = 0; dyi < 3; ++dyi) {
-          row(pp, dyi == 0 ? rm : (dyi == 1 ? rc : rp), lo, hi);
-#pragma unroll
-          for (int dxi = 0; dxi < 3; ++dxi)
-            acc[3 * dxi + dyi] =
-                __builtin_amdgcn_mfma_i32_16x16x64_i8(A, mf_frag(lo, hi, dxi), acc[3 * dxi + dyi], 0, 0, 0);
-        }
+      mf_compiler_fence();  // same-wave LDS accesses complete in order; keep the compiler's too
+      const uint8_t* pp = realk ? wl + ((z % 3) * SS + nk * PB + korg) : cpad;        // dz = -1
+      const uint8_t* pc = realk ? wl + (((z + 1) % 3) * SS + nk * PB + korg) : cpad;  // dz = 0
+#if !(C3H_MF_EXP & 1)
+      switch (PW & 15) {
+        case 0: mf_layer_ksteps<0>(pp, pc, pmask, pw16, nks, h4k, acc); break;
+        case 4: mf_layer_ksteps<4>(pp, pc, pmask, pw16, nks, h4k, acc); break;
+        case 8: mf_layer_ksteps<8>(pp, pc, pmask, pw16, nks, h4k, acc); break;
+        default: mf_layer_ksteps<12>(pp, pc, pmask, pw16, nks, h4k, acc); break;
       }
+#endif
+      mf_compiler_fence();
       // layer z + 2 into the plane slot of layer z - 1 (loaded two layers ago), then the
       // loads of layer z + 4 into its registers
       if (z + 2 <= lz) {
@@ -263,63 +315,93 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid, int nw
         }
       }
     }
-    wave_lds_sync();
-    // epilogue: accumulator tiles -> LDS (C/D map: row 4 (lane >> 4) + r, column lane & 15);
-    // the bins are formed from them directly (exact corrected sums, then the reference's
-    // normalisation / the 117 fold)
-    int32_t* T = reinterpret_cast<int32_t*>(wl);
+    mf_compiler_fence();
+    // (the lane's coordinates made opaque per tile, so the bin arithmetic below is not
+    // hoisted out of the tile loop and held in registers across it)
+    int le = lane;
+    __asm__ volatile("" : "+v"(le));
+    const int h4 = le >> 4, n = le & 15, tn = mf_type(n), nn = mf_chan(n);
+    const bool real = n < kMfCh;
+    // epilogue from registers.  pos = C[15][15] (positions), rs[r] = C[4 h4 + r][15] = sum of
+    // A'_c (the same for every k), cs_k = C_k[15][n]; value = C + 128 (rs + cs) + 128^2 pos
+    const uint32_t pos = (uint32_t)__shfl(acc[13][3], 63, 64);
+    uint32_t rs[4];
 #pragma unroll
-    for (int k = 0; k < kMfK; ++k)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) T[k * 256 + (4 * h4 + r) * 16 + n] = acc[k][r];
-    wave_lds_sync();
-    const long long K = T[13 * 256 + 255];
-    auto corr = [&](int k, int c, int nn) -> long long {
-      const int32_t* Tk = T + k * 256;
-      return (long long)Tk[c * 16 + nn] + 128ll * ((long long)Tk[c * 16 + 15] + Tk[15 * 16 + nn]) + 16384ll * K;
-    };
-    auto code_value = [&](uint32_t code) -> uint32_t {
-      const int kind = (code >> 10) & 3, k = (code >> 12) & 15, c = (code >> 16) & 15, nn = (code >> 20) & 15;
-      return (uint32_t)(kind ? (long long)T[k * 256 + c * 16 + 15] + 128ll * K : corr(k, c, nn));
-    };
-    if (a.atomic) {
-      for (int e = lane; e < 981; e += 64) {
-        const uint32_t code = s_bins[e], v = code_value(code);
-        if (v) atomicAdd(&facc[h * 981 + (code & 1023)], (unsigned long long)v);
-      }
-    } else {
+    for (int r = 0; r < 4; ++r) rs[r] = (uint32_t)__shfl(acc[13][r], 16 * h4 + 15, 64);
+    const uint32_t k2 = 16384u * pos;
+    if (a.atomic || F == 981) {
       float* out = ffeat + h * F;
-      if (F == 981) {
-        for (int e = lane; e < 981; e += 64) {
-          const uint32_t code = s_bins[e];
-          const int bin = code & 1023;
-          out[bin] = (float)code_value(code) * norm981(bin);
+      unsigned long long* hacc = a.atomic ? facc + h * 981 : nullptr;
+      auto emit = [&](int bin, uint32_t v) {
+        if (hacc) {
+          if (v) atomicAdd(&hacc[bin], (unsigned long long)v);
+        } else {
+          out[bin] = (float)v * norm981(bin);
         }
-      } else {  // color_chlac.hpp:1647-1743: first-order bins summed over the 13 offsets
-        for (int i = lane; i < 117; i += 64) {
-          uint32_t v;
-          if (i < 6 || (i >= 63 && i < 69)) {  // zero order
-            const int t = i < 6 ? 0 : 1, c = i < 6 ? i : i - 63;
-            v = (uint32_t)((long long)T[13 * 256 + mf_plane(t, c) * 16 + 15] + 128ll * K);
-          } else if (i < 42 || (i >= 69 && i < 105)) {  // first order, all offsets
-            const int t = i < 42 ? 0 : 1, q = i < 42 ? i - 6 : i - 69, c = q / 6, nn = q % 6;
-            long long sum = 0;
-            for (int k = 0; k < 13; ++k) sum += corr(k, mf_plane(t, c), mf_plane(t, nn));
-            v = (uint32_t)sum;
-          } else {  // centre auto products / bin-pair counts: codes 936.. / 957..
-            v = code_value(s_bins[i < 63 ? 936 + (i - 42) : 957 + (i - 105)]);
+      };
+#pragma unroll
+      for (int k = 0; k < kMfK; ++k) {
+        const uint32_t cs = (uint32_t)__shfl(acc[k][3], 48 + n, 64);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = 4 * h4 + r;
+          if (c >= kMfCh) continue;
+          const int tc = mf_type(c), cc = mf_chan(c);
+          const uint32_t v = (uint32_t)acc[k][r] + 128u * (rs[r] + cs) + k2;
+          if (k < 13) {
+            if (real && tc == tn) emit(495 * tc + bin981(k, cc, nn), v);
+          } else if (real) {
+            if (tc == 0 && tn == 0) {
+              if (cc <= nn) emit(474 + tri6(cc, nn), v);
+            } else if (tc == 1 && tn == 1) {
+              if (cc <= 1 && nn >= 2) emit(969 + 4 * cc + (nn - 2), v);
+              else if ((cc == 2 || cc == 3) && nn >= 4) emit(977 + 2 * (cc - 2) + (nn - 4), v);
+            }
+          } else if (n == 15) {  // zero order: sum of the channel
+            emit(tc ? 495 + cc : cc, rs[r] + 128u * pos);
           }
-          out[i] = (float)v * norm117(i);
         }
       }
-      if (lane == 0) {  // exist_voxel_num from the zero-order r sums (search_c3_hlac.h:60-61)
-        const uint32_t s0 = (uint32_t)((long long)T[13 * 256 + mf_plane(0, 0) * 16 + 15] + 128ll * K);
-        const uint32_t s1 = (uint32_t)((long long)T[13 * 256 + mf_plane(0, 1) * 16 + 15] + 128ll * K);
-        fexist[h] = exist_from((float)s0, (float)s1);
+    } else {  // 117: first-order bins summed over the 13 offsets (color_chlac.hpp:1647-1743)
+      float* out = ffeat + h * F;
+      uint32_t s1[4] = {0, 0, 0, 0};
+      int csum = 0;
+#pragma unroll
+      for (int k = 0; k < 13; ++k) {
+        csum += acc[k][3];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s1[r] += (uint32_t)acc[k][r];
+      }
+      const uint32_t cs1 = (uint32_t)__shfl(csum, 48 + n, 64);
+      const uint32_t cs0 = (uint32_t)__shfl(acc[13][3], 48 + n, 64);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = 4 * h4 + r;
+        if (c >= kMfCh) continue;
+        const int tc = mf_type(c), cc = mf_chan(c);
+        if (real) {
+          if (tc == tn) {
+            const int i = (tc ? 69 : 6) + 6 * cc + nn;
+            out[i] = (float)(s1[r] + 128u * (13u * rs[r] + cs1) + 13u * k2) * norm117(i);
+          }
+          const uint32_t v0 = (uint32_t)acc[13][r] + 128u * (rs[r] + cs0) + k2;
+          int i = -1;
+          if (tc == 0 && tn == 0) {
+            if (cc <= nn) i = 42 + tri6(cc, nn);
+          } else if (tc == 1 && tn == 1) {
+            if (cc <= 1 && nn >= 2) i = 105 + 4 * cc + (nn - 2);
+            else if ((cc == 2 || cc == 3) && nn >= 4) i = 113 + 2 * (cc - 2) + (nn - 4);
+          }
+          if (i >= 0) out[i] = (float)v0 * norm117(i);
+        } else if (n == 15) {
+          const int i = tc ? 63 + cc : cc;
+          out[i] = (float)(rs[r] + 128u * pos) * norm117(i);
+        }
       }
     }
+    if (!a.atomic && lane == 15)  // exist_voxel_num from the zero-order r sums (search_c3_hlac.h:60-61)
+      fexist[h] = exist_from((float)(rs[0] + 128u * pos), (float)(rs[1] + 128u * pos));
     if (frows && lane == 0) frows[wi] = (int32_t)h;
-    wave_lds_sync();  // the tile's LDS is rebuilt by the next tile
   }
 }
 

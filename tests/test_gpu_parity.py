@@ -329,6 +329,19 @@ def test_dense_grid_512_style_small(ctx):
         assert np.array_equal(ctx.exist(), ex)
 
 
+@pytest.mark.parametrize("G,S", [(36, 3), (37, 6), (39, 13), (34, 16), (33, 7)])
+def test_dense_grid_tile_pitches(ctx, G, S):
+    """The dense matrix-core tile body at every plane pitch it specialises (row pitch
+    lx + 2 rounded up to 4 = 4, 8, 12, 16, 20 bytes; ragged edge tiles): exact vs numpy."""
+    words = synth.dense_words(G, seed=8 + S)
+    ctx.set_grid(words.reshape(-1), (G, G, G))
+    for variant in (981, 117):
+        ctx.extract(variant, THR, S)
+        fn, ex, _ = npr.c3hlac(words, variant, THR, S)
+        assert np.array_equal(ctx.features(), fn)
+        assert np.array_equal(ctx.exist(), ex)
+
+
 def test_dense_256_bin_block_linearity(ctx):
     """Size-independent property at full size: the binary-count bins (normalised by 1)
     are exact integers, and summing them over subdivisions must give the whole-grid
