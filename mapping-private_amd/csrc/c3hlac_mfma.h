@@ -107,20 +107,32 @@ struct MfRow {
   }
 };
 
+constexpr int kMfMaxKs = 5;  // K steps per layer of a 16 x 16 tile (PW = 20)
+
 // The K steps of one layer.  pp / pc / pm: this lane's dz = -1 plane, dz = 0 plane and mask
-// plane at the K origin (byte off0 + PW, 16-byte aligned); pw16 = PW - R.
+// plane at the K origin (byte off0 + PW, 16-byte aligned); pw16 = PW - R.  The six row
+// pointers are formed once per layer; the K steps are unrolled, so their offsets (64 ks) are
+// instruction immediates.
 template <int R>
 __device__ __forceinline__ void mf_layer_ksteps(const uint8_t* pp, const uint8_t* pc, const uint8_t* pm, int pw16,
                                                 int nks, int h4, mf_v4i (&acc)[kMfK]) {
-#pragma unroll 1
-  for (int ks = 0; ks < nks; ++ks) {
-    const int o = 64 * ks + 16 * h4;
+  const int o = 16 * h4;
+  const uint8_t* r_c0 = pc + o;          // dz = 0, dy = 0
+  const uint8_t* r_cm = pc + o - pw16;   // dz = 0, dy = -1
+  const uint8_t* r_pm = pp + o - pw16;   // dz = -1, dy = -1
+  const uint8_t* r_p0 = pp + o;          // dz = -1, dy = 0
+  const uint8_t* r_pp = pp + o + pw16;   // dz = -1, dy = +1
+  const uint8_t* r_m = pm + o;
+#pragma unroll
+  for (int ks = 0; ks < kMfMaxKs; ++ks) {
+    if (ks >= nks) break;
+    const int ko = 64 * ks;
     // dz = 0: row 0 (the centres and dx = -1), row -1
     MfRow<0, -1, 0> c0;
     MfRow<-R, -1, 1> cm;
-    c0.load(pc + o);
-    cm.load(pc + o - pw16);
-    const mf_u4 m = *reinterpret_cast<const mf_u4*>(__builtin_assume_aligned(pm + o, 16));
+    c0.load(r_c0 + ko);
+    cm.load(r_cm + ko);
+    const mf_u4 m = *reinterpret_cast<const mf_u4*>(__builtin_assume_aligned(r_m + ko, 16));
     const mf_v4i a0 = c0.frag<0>();
     mf_v4i A;
 #pragma unroll
@@ -133,21 +145,21 @@ __device__ __forceinline__ void mf_layer_ksteps(const uint8_t* pp, const uint8_t
     // dz = -1, rows dy = -1, 0, +1: k = 3 (dx + 1) + (dy + 1)
     {
       MfRow<-R, -1, 1> r;
-      r.load(pp + o - pw16);
+      r.load(r_pm + ko);
       acc[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, r.template frag<-1>(), acc[0], 0, 0, 0);
       acc[3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, r.template frag<0>(), acc[3], 0, 0, 0);
       acc[6] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, r.template frag<1>(), acc[6], 0, 0, 0);
     }
     {
       MfRow<0, -1, 1> r;
-      r.load(pp + o);
+      r.load(r_p0 + ko);
       acc[1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, r.template frag<-1>(), acc[1], 0, 0, 0);
       acc[4] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, r.template frag<0>(), acc[4], 0, 0, 0);
       acc[7] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, r.template frag<1>(), acc[7], 0, 0, 0);
     }
     {
       MfRow<R, -1, 1> r;
-      r.load(pp + o + pw16);
+      r.load(r_pp + ko);
       acc[2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, r.template frag<-1>(), acc[2], 0, 0, 0);
       acc[5] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, r.template frag<0>(), acc[5], 0, 0, 0);
       acc[8] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, r.template frag<1>(), acc[8], 0, 0, 0);
