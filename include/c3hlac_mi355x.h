@@ -230,6 +230,14 @@ int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_
  * the float64 oracle within 2e-3 relative (fp16 = 0, the default: fp32, 1e-5).  Smaller
  * grids and the pipelined c3h_run_frames path always compress in fp32. */
 int c3h_set_search_precision(c3h_ctx* ctx, int32_t fp16);
+/* Engine of the single-frame search's projection step (SearchObjMulti::searchPart's
+ * M x r x D products, search.cpp:915-968): 0 = automatic (default: the matrix cores for
+ * grids of >= 65,536 subdivisions and for models with r > 64, the VALU list kernel
+ * otherwise), 1 = VALU (score_list_kernel for r <= 64; the generic kernel beyond),
+ * 2 = matrix cores (score_mfma_kernel, v_mfma_f32_32x32x2_f32; D <= 160, D % 4 == 0).
+ * Both engines form every product as the same k-ordered fp32 fma chain, so the scores are
+ * bit-identical.  Batched / pipelined searches (c3h_run_frames) always use the VALU kernel. */
+int c3h_set_score_engine(c3h_ctx* ctx, int32_t engine);
 /* SearchObj::setRank / SearchObjMulti::setRank (search.cpp:130-143, 778-815):
  * (re)allocates the per-model lists; modes start at S_MODE_1. */
 int c3h_set_rank(c3h_ctx* ctx, int32_t rank);

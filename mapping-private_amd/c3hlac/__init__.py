@@ -197,6 +197,10 @@ class Context:
         self.hist_num, self.subdiv, self.variant = int(hn.value), tuple(int(x) for x in sb), 137
         return self.subdiv, self.hist_num
 
+    def set_score_engine(self, engine):
+        """c3h_set_score_engine: 0 automatic, 1 VALU, 2 matrix cores (single-frame search)."""
+        self._chk(self.lib.c3h_set_score_engine(self.h, int(engine)), "set_score_engine")
+
     def set_search_precision(self, fp16):
         """c3h_set_search_precision: fp16 matrix-core compress for large grids."""
         self._chk(self.lib.c3h_set_search_precision(self.h, int(bool(fp16))), "set_search_precision")

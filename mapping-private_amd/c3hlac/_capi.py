@@ -101,6 +101,7 @@ _SIGS = {
     "c3h_extract_vosch": (C.c_int, [_P, C.POINTER(GrsdParams), C.POINTER(C.c_int32), C.c_int32,
                                     C.POINTER(C.c_int32), C.POINTER(C.c_int64)]),
     "c3h_set_search_precision": (C.c_int, [_P, C.c_int32]),
+    "c3h_set_score_engine": (C.c_int, [_P, C.c_int32]),
     "c3h_set_features": (C.c_int, [_P, _P, C.POINTER(C.c_int32), C.c_int32, _P, C.c_int32, C.c_int]),
     "c3h_pca_write": (C.c_int, [C.c_char_p, C.c_int32, C.c_int32, _P, _P, _P]),
     "c3h_pca_create": (C.c_int, [C.c_int, C.c_int32, C.POINTER(_P)]),

@@ -275,7 +275,9 @@ struct SparseSearch {
   long long* prof;         // diagnostics (C3H_PROF): [blocks][8]
   float* gbox = nullptr;   // large grids: box-summed G rows of every position (pstart order)
   int64_t s_gbox = 0;
+  int score_mfma = 0;      // project on the matrix cores (score_mfma_kernel; needs gbox, nframes 1)
 };
+bool score_mfma_ok(int D);  // D fits score_mfma_kernel
 // sparse compress fused into the gate launch (nullable in launch_sparse_search)
 struct SparseCompress {
   const float* feat;
@@ -431,6 +433,7 @@ struct c3h_ctx {
   c3h::DevBuf<_Float16> axis_pt16;  // 128 x Fp16 f16 copy (column-major) for the fp16 compress
   int Fp16 = 0;
   bool prec16 = false;              // c3h_set_search_precision: fp16 matrix-core compress
+  int score_engine = 0;             // c3h_set_score_engine: 0 auto, 1 VALU, 2 matrix cores
   c3h::DevBuf<float> axis_q;        // M x r x D
   c3h::DevBuf<float> fmax;
   int fmax_len = 0;

@@ -357,7 +357,13 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
   const int64_t H = (int64_t)xn * yn * zn;
   if (ctx->lists.M != std::max(ctx->M, 1) || ctx->lists.rank != ctx->rank) init_lists(ctx);
   if (H < 1 || H != ctx->hist_num) return 0;  // setData returns early; search is skipped
-  const bool fast = c3h::score_fast_ok(ctx->D, ctx->r);
+  // projection engine (c3h_set_score_engine): the VALU list kernel (r <= 64), the matrix
+  // cores over precomputed box sums (single frames), or the generic kernel (r > 64, VALU)
+  const bool valu_fast = c3h::score_fast_ok(ctx->D, ctx->r);
+  const bool mf = nf == 1 && !ctx->capture && c3h::score_mfma_ok(ctx->D) &&
+                  (ctx->score_engine == 2 ||
+                   (ctx->score_engine == 0 && (!valu_fast || H >= c3h::kBoxsumRows)));
+  const bool fast = valu_fast || mf;  // the sparse (gate list) search
   if (nf > 1 && !fast) return fail(ctx, C3H_ERR_STATE, "search: batched frames need the fast path");
   int modes[6];
   const int nm = mode_schedule(range[0], range[1], range[2], rotate, modes);
@@ -452,6 +458,7 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
     q.mpg = std::max(1, 64 / ctx->r);
     q.scores = ctx->scores.p;
     q.nmodes = rm.n;
+    q.score_mfma = mf ? 1 : 0;
     q.pstart[0] = 0;
     for (int i = 0; i < rm.n; ++i) {
       const auto& a = launches[i];
@@ -482,7 +489,7 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
     for (int f = 0; f < c3h::kMaxBatch; ++f) q.outs[f] = (d_outs && f < nf) ? d_outs[f] : nullptr;
     // large grids (config 5): the box sums of every position in one streaming pass
     // before the score launch (the same (dz, dy, dx) order, so the same scores)
-    if (large) {
+    if (large || mf) {
       ENSURE(ctx->gbox, (size_t)std::max<int64_t>(ptot, 1) * ctx->D);
       q.gbox = ctx->gbox.p;
       q.s_gbox = ptot * ctx->D;
@@ -1587,6 +1594,14 @@ int c3h_set_search_precision(c3h_ctx* ctx, int32_t fp16) {
   QUIESCE(ctx);
   ctx->prec16 = fp16 != 0;
   ctx->g_valid = false;
+  return C3H_OK;
+}
+
+int c3h_set_score_engine(c3h_ctx* ctx, int32_t engine) {
+  if (!ctx) return C3H_ERR_ARG;
+  if (engine < 0 || engine > 2) return fail(ctx, C3H_ERR_ARG, "c3h_set_score_engine: engine must be 0, 1 or 2");
+  QUIESCE(ctx);
+  ctx->score_engine = engine;
   return C3H_OK;
 }
 

@@ -211,6 +211,147 @@ __global__ __launch_bounds__(kBlock) void boxsum_kernel(SparseSearch a) {
     boxsum_body(a, e, blockIdx.y);
 }
 
+// ---------------------------------------------------------------- score on the matrix cores
+// SearchObjMulti::searchPart's projections (search.cpp:915-968) for the listed positions
+// of one frame as a GEMM: Q = B * qt, B = the box-summed G rows (boxsum_kernel, P x D),
+// qt = the models' basis rows (D x M*r).  Workgroup = 128 listed positions (32 per wave:
+// the wave's A fragment, D/2 k-pairs, lives in registers for the whole column sweep) x the
+// columns of one model group [m0*r, m1*r), swept in chunks of 32 columns staged in LDS
+// (double-buffered, prefetched one chunk ahead in registers); one
+// v_mfma_f32_32x32x2_f32 per k-pair.  The MFMA is bit-for-bit the k-ordered fmaf chain
+// (compress_mfma_body), so every q is the VALU kernels' q.  Epilogue per chunk: the 32x32
+// tile goes to a per-wave LDS scratch and lane p (< 32) folds its position's row in
+// column order into |Q_m f|^2 (the fmaf chain over i = 0..r-1 of score_list_body),
+// finishing model m at its last column: sqrt(q2)/sqrt(f.f) in double, as the reference.
+constexpr int kSMP = 128;  // listed positions per workgroup
+constexpr int kSMC = 32;   // basis columns per chunk
+constexpr int kSMES = 33;  // epilogue scratch row stride (conflict-free row reads)
+
+__host__ __device__ constexpr size_t score_mfma_lds_bytes(int KP) {
+  return sizeof(float) * (2 * (size_t)(2 * KP) * kSMC + (size_t)(kBlock / 64) * 32 * kSMES);
+}
+
+template <int KP>  // k-pairs (D <= 2 KP), KP % 4 == 0
+__global__ __launch_bounds__(kBlock) void score_mfma_kernel(SparseSearch a, int ngroups) {
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  constexpr int K2 = 2 * KP;
+  constexpr int kBE = K2 * kSMC / kBlock;  // B-chunk elements per thread
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hk = lane >> 5, l32 = lane & 31;
+  float* se = smf + 2 * K2 * kSMC + wave * 32 * kSMES;
+  const int D = a.D, r = a.r, Qs = a.Opad;
+  const int n = (int)a.cnt[a.epoch & 1];
+  const int g = blockIdx.y;
+  const int m0 = (int)((int64_t)g * a.M / ngroups), m1 = (int)((int64_t)(g + 1) * a.M / ngroups);
+  const int cb = m0 * r, ce = m1 * r;
+  const int nch = (ce - cb + kSMC - 1) / kSMC;
+  for (int pb = blockIdx.x; pb * kSMP < n; pb += gridDim.x) {
+    const int e = pb * kSMP + wave * 32 + l32;
+    const bool valid = e < n;
+    const long long en = valid ? a.list[e] : 0;
+    const int mi = (int)(en >> 40);
+    const int64_t p = en & ((1ll << 40) - 1);
+    const float* __restrict__ row = a.gbox + (a.pstart[mi] + p) * D;
+    float av[KP];
+#pragma unroll
+    for (int j = 0; j < KP; ++j) {
+      const int k = 2 * j + hk;
+      av[j] = (valid && k < D) ? row[k] : 0.0f;
+    }
+    // f.f in ascending d (lane p holds the even k of its row, lane p + 32 the odd one)
+    float ff = 0.0f;
+#pragma unroll
+    for (int j = 0; j < KP; ++j) {
+      const float odd = __shfl(av[j], l32 + 32, 64);
+      if (2 * j < D) ff = __builtin_fmaf(av[j], av[j], ff);
+      if (2 * j + 1 < D) ff = __builtin_fmaf(odd, odd, ff);
+    }
+    const int64_t sbase = a.md[mi].offset + p, sP = a.md[mi].P;
+    float bl[kBE];
+    auto load_b = [&](int c) {
+      const int col0 = cb + c * kSMC;
+#pragma unroll
+      for (int i = 0; i < kBE; ++i) {
+        const int el = tid + i * kBlock, k = el / kSMC, col = col0 + (el % kSMC);
+        bl[i] = (k < D && col < ce) ? a.qt[(int64_t)k * Qs + col] : 0.0f;
+      }
+    };
+    load_b(0);
+    float q2 = 0.0f;
+    int m = m0, ir = 0;  // model and basis row of the next folded column (wave-uniform)
+    for (int c = 0; c < nch; ++c) {
+      float* sb = smf + (c & 1) * K2 * kSMC;
+#pragma unroll
+      for (int i = 0; i < kBE; ++i) sb[tid + i * kBlock] = bl[i];
+      if (c + 1 < nch) load_b(c + 1);
+      __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      mf_f32x16 acc;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+      const float* bcol = sb + hk * kSMC + l32;
+#pragma unroll
+      for (int j = 0; j < KP; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], bcol[2 * j * kSMC], acc, 0, 0, 0);
+      // C/D map: column l32, row (q & 3) + 8 (q >> 2) + 4 hk
+#pragma unroll
+      for (int q = 0; q < 16; ++q) se[((q & 3) + 8 * (q >> 2) + 4 * hk) * kSMES + l32] = acc[q];
+      __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const int ncol = min(kSMC, ce - (cb + c * kSMC));
+      if (hk == 0) {
+        const float* qrow = se + l32 * kSMES;
+        for (int j = 0; j < ncol; ++j) {
+          const float v = qrow[j];
+          q2 = __builtin_fmaf(v, v, q2);
+          if (++ir == r) {  // model m complete
+            if (valid) a.scores[sbase + (int64_t)m * sP] = sqrt((double)q2) / sqrt((double)ff);
+            q2 = 0.0f;
+            ir = 0;
+            ++m;
+          }
+        }
+      }
+      __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // scratch reads before the next tile's writes
+    }
+    __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // B buffers reused by the next block
+  }
+}
+
+template <int KP>
+hipError_t launch_score_mfma_kp(const SparseSearch& a, hipStream_t s) {
+  static thread_local int slots = 0, dev_c = -1;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const size_t lds = score_mfma_lds_bytes(KP);
+  if (dev != dev_c) {
+    int n_cu = 256, per_cu = 0;
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, score_mfma_kernel<KP>, kBlock, lds) != hipSuccess ||
+        per_cu < 1)
+      per_cu = 1;
+    slots = per_cu * n_cu;
+    dev_c = dev;
+  }
+  // the list count is on the device: size for every position passing (dense grids), the
+  // workgroups past the count exit at once; model groups fill the chip when positions
+  // alone would not (whole models per group: |Q_m f|^2 never spans workgroups)
+  const int64_t pblocks = (a.pstart[a.nmodes] + kSMP - 1) / kSMP;
+  const int ng = (int)std::max<int64_t>(1, std::min<int64_t>(a.M, (2 * (int64_t)slots + pblocks - 1) / pblocks));
+  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(pblocks, 65535));
+  score_mfma_kernel<KP><<<dim3(gx, (unsigned)ng), kBlock, lds, s>>>(a, ng);
+  return hipGetLastError();
+}
+
+hipError_t launch_score_mfma(const SparseSearch& a, hipStream_t s) {
+  const int kp = (a.D + 1) / 2;
+  if (kp <= 16) return launch_score_mfma_kp<16>(a, s);
+  if (kp <= 24) return launch_score_mfma_kp<24>(a, s);
+  if (kp <= 32) return launch_score_mfma_kp<32>(a, s);
+  if (kp <= 40) return launch_score_mfma_kp<40>(a, s);
+  if (kp <= 52) return launch_score_mfma_kp<52>(a, s);
+  if (kp <= 64) return launch_score_mfma_kp<64>(a, s);
+  if (kp <= 72) return launch_score_mfma_kp<72>(a, s);
+  if (kp <= 80) return launch_score_mfma_kp<80>(a, s);
+  return hipErrorInvalidValue;
+}
+
 // rank 1 on large grids: block (b, m) reduces model m's scores of global positions
 // g = b, b + grid, ... (every mode, scan order) to a (score desc, scan order asc) partial
 constexpr int kArgmaxBlocks = 256;
@@ -421,6 +562,7 @@ size_t score_lds_bytes(int D, int r, int SP) {
 }
 
 bool score_fast_ok(int D, int r) { return D <= 160 && (D & 3) == 0 && r <= kOC; }
+bool score_mfma_ok(int D) { return D >= 4 && D <= 160 && (D & 3) == 0; }
 
 int64_t score_blocks(const ScoreLaunch& a) {
   const int64_t P = (int64_t)a.xe * a.ye * a.ze;
@@ -503,6 +645,16 @@ score:
   if (a.gbox) {
     const int64_t n = ptot * (a.D >> 2);
     boxsum_kernel<<<dim3((unsigned)std::min<int64_t>((n + kBlock - 1) / kBlock, 16384), nf), kBlock, 0, s>>>(a);
+  }
+  if (a.score_mfma) {  // single frame, box sums above: the matrix-core projection
+    if (!a.gbox || nf != 1 || !score_mfma_ok(a.D)) return hipErrorInvalidValue;
+    const hipError_t e = launch_score_mfma(a, s);
+    if (e != hipSuccess) return e;
+    if (a.lists) {  // rank 1: parallel argmax over the written scores + finalize
+      scores_argmax_kernel<<<dim3(kArgmaxBlocks, a.M), kBlock, 0, s>>>(a);
+      argmax_finalize_kernel<<<1, kBlock, 0, s>>>(a, kArgmaxBlocks);
+    }
+    return hipGetLastError();
   }
   const size_t lds = score_list_lds_bytes(a.D, a.mpg);
   const unsigned groups = (unsigned)((a.M + a.mpg - 1) / a.mpg);

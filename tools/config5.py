@@ -14,6 +14,14 @@ from c3hlac import synth  # noqa: E402
 
 G, S, THR = 512, 10, (147, 146, 148)
 M, D, R = 10, 100, 20
+
+
+def _arg(name, dflt):
+    return int(sys.argv[sys.argv.index(name) + 1]) if name in sys.argv else dflt
+
+
+M, R = _arg("--models", M), _arg("--r", R)  # the stress case: --models 63 --r 70
+ENGINE = _arg("--engine", 0)  # c3h_set_score_engine: 0 auto, 1 VALU, 2 matrix cores
 t0 = time.time()
 words = synth.dense_words(G, seed=synth.BASE_SEED + 5).reshape(-1)
 print("grid generated in %.1f s" % (time.time() - t0), flush=True)
@@ -25,6 +33,8 @@ with c3hlac.Context(0) as ctx:
     ctx.set_rank(1)
     if "--fp16" in sys.argv:
         ctx.set_search_precision(True)
+    ctx.set_score_engine(ENGINE)
+    print("models %d x r=%d, D=%d, score engine %d" % (M, R, D, ENGINE), flush=True)
     res = []
     for rep in range(4):
         ctx.timing(True)
@@ -49,4 +59,7 @@ with c3hlac.Context(0) as ctx:
     s_ms = kt["compress"][0] + kt["score"][0] + kt["replay"][0]
     print("config5: search (compress + score + replay) %.3f ms = %.3g detections/s (%d positions x %d models)"
           % (s_ms, P * M / s_ms * 1e3, P, M))
+    pf = 2.0 * P * M * R * D
+    print("config5: projection GEMM %.1f GFLOP; score stage (box sums + projection + argmax) %.3f ms = %.1f TFLOP/s"
+          % (pf / 1e9, kt["score"][0], pf / kt["score"][0] / 1e9))
     print("config5: end to end (extract + search, host wall) %.2f ms = %.0f Mvoxels/s" % (wall * 1e3, nvox / wall / 1e6))
