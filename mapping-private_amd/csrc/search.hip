@@ -228,16 +228,27 @@ constexpr int kSMC = 32;   // basis columns per chunk
 constexpr int kSMES = 33;  // epilogue scratch row stride (conflict-free row reads)
 
 __host__ __device__ constexpr size_t score_mfma_lds_bytes(int KP) {
-  return sizeof(float) * (2 * (size_t)(2 * KP) * kSMC + (size_t)(kBlock / 64) * 32 * kSMES);
+  return sizeof(float) * (2 * (size_t)(2 * KP) * kSMC + (size_t)(kBlock / 64) * 32 * kSMES) + 3 * 6 * sizeof(int64_t);
 }
 
+#ifndef C3H_SMF_WAVES
+#define C3H_SMF_WAVES 2  // waves per SIMD the registers must allow (3 spills: the B fragments of a chunk are hoisted)
+#endif
 template <int KP>  // k-pairs (D <= 2 KP), KP % 4 == 0
-__global__ __launch_bounds__(kBlock) void score_mfma_kernel(SparseSearch a, int ngroups) {
+__global__ __launch_bounds__(kBlock, C3H_SMF_WAVES) void score_mfma_kernel(SparseSearch a, int ngroups) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
   constexpr int K2 = 2 * KP;
   constexpr int kBE = K2 * kSMC / kBlock;  // B-chunk elements per thread
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hk = lane >> 5, l32 = lane & 31;
   float* se = smf + 2 * K2 * kSMC + wave * 32 * kSMES;
+  // the mode table (pstart, score offset, P) in LDS: indexed per lane by the entry's mode
+  int64_t* s_mode = reinterpret_cast<int64_t*>(smf + 2 * K2 * kSMC + (kBlock / 64) * 32 * kSMES);
+  if (tid < a.nmodes) {
+    s_mode[3 * tid] = a.pstart[tid];
+    s_mode[3 * tid + 1] = a.md[tid].offset;
+    s_mode[3 * tid + 2] = a.md[tid].P;
+  }
+  __syncthreads();
   const int D = a.D, r = a.r, Qs = a.Opad;
   const int n = (int)a.cnt[a.epoch & 1];
   const int g = blockIdx.y;
@@ -250,13 +261,12 @@ __global__ __launch_bounds__(kBlock) void score_mfma_kernel(SparseSearch a, int 
     const long long en = valid ? a.list[e] : 0;
     const int mi = (int)(en >> 40);
     const int64_t p = en & ((1ll << 40) - 1);
-    const float* __restrict__ row = a.gbox + (a.pstart[mi] + p) * D;
+    // no per-lane masks (they would live in SGPR pairs): entries past the count read row 0
+    // and are never stored; k-pairs past D (D even: a wave-uniform test) are zero
+    const float* __restrict__ row = a.gbox + (valid ? (s_mode[3 * mi] + p) * D : 0);
     float av[KP];
 #pragma unroll
-    for (int j = 0; j < KP; ++j) {
-      const int k = 2 * j + hk;
-      av[j] = (valid && k < D) ? row[k] : 0.0f;
-    }
+    for (int j = 0; j < KP; ++j) av[j] = 2 * j < D ? row[2 * j + hk] : 0.0f;
     // f.f in ascending d (lane p holds the even k of its row, lane p + 32 the odd one)
     float ff = 0.0f;
 #pragma unroll
@@ -265,14 +275,16 @@ __global__ __launch_bounds__(kBlock) void score_mfma_kernel(SparseSearch a, int 
       if (2 * j < D) ff = __builtin_fmaf(av[j], av[j], ff);
       if (2 * j + 1 < D) ff = __builtin_fmaf(odd, odd, ff);
     }
-    const int64_t sbase = a.md[mi].offset + p, sP = a.md[mi].P;
+    const int64_t sbase = s_mode[3 * mi + 1] + p, sP = s_mode[3 * mi + 2];
     float bl[kBE];
     auto load_b = [&](int c) {
       const int col0 = cb + c * kSMC;
 #pragma unroll
       for (int i = 0; i < kBE; ++i) {
-        const int el = tid + i * kBlock, k = el / kSMC, col = col0 + (el % kSMC);
-        bl[i] = (k < D && col < ce) ? a.qt[(int64_t)k * Qs + col] : 0.0f;
+        // clamped, not masked: rows past D meet A = 0, columns past the group are never
+        // folded (qt is finite everywhere)
+        const int el = tid + i * kBlock, k = min(el / kSMC, D - 1), col = min(col0 + (el % kSMC), Qs - 1);
+        bl[i] = a.qt[(int64_t)k * Qs + col];
       }
     };
     load_b(0);
@@ -332,8 +344,21 @@ hipError_t launch_score_mfma_kp(const SparseSearch& a, hipStream_t s) {
   // the list count is on the device: size for every position passing (dense grids), the
   // workgroups past the count exit at once; model groups fill the chip when positions
   // alone would not (whole models per group: |Q_m f|^2 never spans workgroups)
+  // Model groups: the launch takes ~ rounds of resident workgroups x a workgroup's time,
+  // which is a fixed part (its positions' box rows into registers, f.f: ~3 column chunks of
+  // matrix work, measured) plus one unit per 32-column chunk of its group's models
   const int64_t pblocks = (a.pstart[a.nmodes] + kSMP - 1) / kSMP;
-  const int ng = (int)std::max<int64_t>(1, std::min<int64_t>(a.M, (2 * (int64_t)slots + pblocks - 1) / pblocks));
+  int ng = 1;
+  double best = 1e300;
+  for (int g = 1; g <= a.M; ++g) {
+    const int64_t rounds = (pblocks * g + slots - 1) / slots;
+    const int64_t cols = (int64_t)((a.M + g - 1) / g) * a.r;
+    const double t = (double)rounds * (3.0 + (double)((cols + kSMC - 1) / kSMC));
+    if (t < best) {
+      best = t;
+      ng = g;
+    }
+  }
   const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(pblocks, 65535));
   score_mfma_kernel<KP><<<dim3(gx, (unsigned)ng), kBlock, lds, s>>>(a, ng);
   return hipGetLastError();

@@ -80,3 +80,80 @@ def test_gloo_two_ranks_gather_matches_single_process():
         np.testing.assert_array_equal(out, ref)  # every rank holds all frames in order
     assert sorted(shards[0] + shards[1]) == list(range(N_FRAMES))
     assert any(np.frombuffer(ref[:, 0].tobytes(), np.float64) > 0)
+
+
+# ---------------------------------------------------------------- one scene in z-slabs
+SLAB_G, SLAB_S = 40, 8
+
+
+def _oracle_records(words, ranges, offset=(0, 0, 0), z0=0):
+    """Rank-1 records of the float64 oracle on words[z, y, x] (c3h_det layout, global z)."""
+    import np_ref as npr
+    import pyoracle as po
+    from c3hlac import synth
+    from c3hlac._capi import DET_DTYPE
+    feat, ex, sb = npr.c3hlac(words, 117, THR, SLAB_S, offset)
+    axis_t, var, axis_q = synth.random_bases(117, 12, 3, 4, seed=7)
+    L, _, _ = po.search(sb, feat, ex, synth.whiten(axis_t, var), axis_q, ranges, 1, 10, dbl=True)
+    rec = np.zeros(3, DET_DTYPE)
+    for m in range(3):
+        rec[m] = (L.score[m], L.x[m], L.y[m], L.z[m] + (z0 if L.score[m] > 0 else 0), L.mode[m])
+    return rec
+
+
+def _sparse_words():
+    rng = np.random.default_rng(33)
+    w = rng.integers(0, 1 << 24, size=(SLAB_G,) * 3, dtype=np.uint32) | np.uint32(1 << 24)
+    w[rng.random(w.shape) > 0.08] = 0
+    return w
+
+
+def _slab_worker(rank, world, port, ranges, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from c3hlac.dist import gather_slab_lists, mode_ranges, mode_schedule, slab_extent
+    words = _sparse_words()
+    zr_max = max(mode_ranges(md, ranges)[2] for md in mode_schedule(ranges))
+    ext = slab_extent(SLAB_G, SLAB_S, zr_max, rank, world)
+    local = None
+    if ext is not None:
+        p0, p1, vz0, vz1, zoff = ext
+        local = _oracle_records(words[vz0:vz1], ranges, (0, 0, zoff), p0)
+    out = gather_slab_lists(local, 3, mode_schedule(ranges), dist)
+    q.put((rank, out.tobytes()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ranges", [(2, 2, 2), (1, 2, 3)])
+def test_gloo_two_ranks_scene_slabs_match_whole_scene(ranges):
+    from c3hlac._capi import DET_DTYPE
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_slab_worker, args=(r, 2, port, ranges, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = _oracle_records(_sparse_words(), ranges)
+    assert (ref["score"] > 0).all()
+    for rank, raw in res:
+        got = np.frombuffer(raw, DET_DTYPE)
+        for f in ("x", "y", "z", "mode"):
+            np.testing.assert_array_equal(got[f], ref[f])
+        np.testing.assert_allclose(got["score"], ref["score"], rtol=1e-12)
+
+
+def test_slab_partition():
+    from c3hlac.dist import slab_extent, slab_planes
+    assert [b - a for a, b in slab_planes(52, 8)] == [7, 7, 7, 7, 6, 6, 6, 6]
+    for n in (1, 5, 52):
+        for w in (1, 2, 3, 8):
+            sp = slab_planes(n, w)
+            assert sp[0][0] == 0 and sp[-1][1] == n and all(sp[i][1] == sp[i + 1][0] for i in range(w - 1))
+    # halo plane below every slab but the first, zr_max - 1 planes after, clipped to the grid
+    assert slab_extent(512, 10, 2, 0, 8) == (0, 7, 0, 80, 0)
+    assert slab_extent(512, 10, 2, 1, 8) == (7, 14, 69, 150, 1)
+    assert slab_extent(512, 10, 2, 7, 8) == (46, 52, 459, 512, 1)

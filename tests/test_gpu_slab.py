@@ -1,0 +1,55 @@
+"""One scene split into z-slabs of subdivision planes over ranks (BASELINE
+config 5 across GPUs; c3hlac.dist.slab_search): every rank's slab runs through the C-ABI
+on its own sub-grid (one halo voxel plane below, zr_max - 1 planes after), and the merged
+rank-1 records must equal the whole-scene search bit-for-bit (score, x, y, z, mode).  The
+ranks run one after another on this process's context (the GPU box has one GPU); the
+gather itself is covered with gloo in test_dist.py."""
+import numpy as np
+import pytest
+
+from c3hlac import synth
+from c3hlac.dist import merge_slab_lists, mode_schedule, slab_search
+from conftest import THR
+
+pytestmark = pytest.mark.gpu
+
+
+def _whole(ctx, words, variant, S, ranges, thr):
+    gz, gy, gx = words.shape
+    ctx.set_grid(np.ascontiguousarray(words).reshape(-1), (gx, gy, gz))
+    ctx.extract(variant, THR, S)
+    ctx.set_rank(1)
+    lists, _ = ctx.search(ranges, thr)
+    return np.ascontiguousarray(lists[:, 0])
+
+
+def _split(ctx, words, variant, S, ranges, thr, world):
+    parts = [slab_search(ctx, words, variant, THR, S, ranges, thr, r, world) for r in range(world)]
+    return merge_slab_lists([p for p in parts if p is not None], mode_schedule(ranges))
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("ranges", [(2, 2, 2), (1, 2, 3), (3, 1, 1)])
+def test_slabs_kinect_256(ctx, world, ranges):
+    pts = synth.kinect_scene(1_000_000, grid=256, leaf=0.01, seed=synth.BASE_SEED + 11)
+    gi = ctx.voxelize(pts, 0.01)
+    d = gi.div_b
+    words = ctx.grid().reshape(d[2], d[1], d[0])
+    axis_t, var, axis_q = synth.random_bases(117, 100, 10, 20, seed=4)
+    ctx.search_setup(axis_t, var, axis_q)
+    whole = _whole(ctx, words, 117, 10, ranges, 100)
+    assert (whole["score"] > 0).all()
+    got = _split(ctx, words, 117, 10, ranges, 100, world)
+    assert np.array_equal(got, whole)
+
+
+def test_slabs_config5_dense_512_eight_ranks(ctx):
+    """512^3 dense, C3-HLAC-981, 52 planes over 8 ranks (7,7,7,7,6,6,6,6): every interior
+    position ties, so the merge's scan-order tie-break decides the records."""
+    G, S, n = 512, 10, 52
+    words = np.tile(synth.dense_words(S, seed=51), (n, n, n))[:G, :G, :G]
+    axis_t, var, axis_q = synth.random_bases(981, 100, 10, 20, seed=52)
+    ctx.search_setup(axis_t, var, axis_q)
+    whole = _whole(ctx, words, 981, S, (2, 2, 2), 100)
+    got = _split(ctx, words, 981, S, (2, 2, 2), 100, 8)
+    assert np.array_equal(got, whole)

@@ -6,7 +6,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${1:-smf}
 mkdir -p $O
 export C3H_REQUIRE_GPU=1
-timeout -k 10 600 python -u -m pytest tests/test_gpu_score_mfma.py -x -v --timeout 300 --timeout-method thread \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_score_mfma.py tests/test_gpu_slab.py -x -v --timeout 300 --timeout-method thread \
   -p no:cacheprovider > $O/tests.log 2>&1 || exit 3
 for e in 1 2; do
   timeout -k 10 300 python -u tools/config5.py --engine $e > $O/config5_e$e.log 2>&1 || exit 4
