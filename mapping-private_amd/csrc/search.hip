@@ -232,8 +232,12 @@ __host__ __device__ constexpr size_t score_mfma_lds_bytes(int KP) {
 }
 
 #ifndef C3H_SMF_WAVES
-#define C3H_SMF_WAVES 2  // waves per SIMD the registers must allow (3 spills: the B fragments of a chunk are hoisted)
+#define C3H_SMF_WAVES 3  // waves per SIMD the registers must allow (LDS: 3 workgroups per CU)
 #endif
+#ifndef C3H_SMF_GROUP
+#define C3H_SMF_GROUP 16
+#endif
+constexpr int kSMG = C3H_SMF_GROUP;  // k-pairs whose B fragments are in registers together
 template <int KP>  // k-pairs (D <= 2 KP), KP % 4 == 0
 __global__ __launch_bounds__(kBlock, C3H_SMF_WAVES) void score_mfma_kernel(SparseSearch a, int ngroups) {
   extern __shared__ __attribute__((aligned(16))) float smf[];
@@ -300,23 +304,39 @@ __global__ __launch_bounds__(kBlock, C3H_SMF_WAVES) void score_mfma_kernel(Spars
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
       const float* bcol = sb + hk * kSMC + l32;
+      // k-pairs in groups of kSMG: the group's B fragments are read (LDS) while the previous
+      // group's MFMAs run, and no more than a group's are held in registers
 #pragma unroll
-      for (int j = 0; j < KP; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], bcol[2 * j * kSMC], acc, 0, 0, 0);
+      for (int j0 = 0; j0 < KP; j0 += kSMG) {
+#pragma unroll
+        for (int j = j0; j < j0 + kSMG && j < KP; ++j)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], bcol[2 * j * kSMC], acc, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       // C/D map: column l32, row (q & 3) + 8 (q >> 2) + 4 hk
 #pragma unroll
       for (int q = 0; q < 16; ++q) se[((q & 3) + 8 * (q >> 2) + 4 * hk) * kSMES + l32] = acc[q];
       __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const int ncol = min(kSMC, ce - (cb + c * kSMC));
       if (hk == 0) {
+        // the row's 32 reads issued together (one LDS round trip, not 32 dependent ones),
+        // then the fold over registers
         const float* qrow = se + l32 * kSMES;
-        for (int j = 0; j < ncol; ++j) {
-          const float v = qrow[j];
-          q2 = __builtin_fmaf(v, v, q2);
-          if (++ir == r) {  // model m complete
-            if (valid) a.scores[sbase + (int64_t)m * sP] = sqrt((double)q2) / sqrt((double)ff);
-            q2 = 0.0f;
-            ir = 0;
-            ++m;
+#pragma unroll
+        for (int h0 = 0; h0 < kSMC; h0 += 16) {
+          float qv[16];
+#pragma unroll
+          for (int j = 0; j < 16; ++j) qv[j] = qrow[h0 + j];
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            if (h0 + j >= ncol) break;  // uniform
+            q2 = __builtin_fmaf(qv[j], qv[j], q2);
+            if (++ir == r) {  // model m complete
+              if (valid) a.scores[sbase + (int64_t)m * sP] = sqrt((double)q2) / sqrt((double)ff);
+              q2 = 0.0f;
+              ir = 0;
+              ++m;
+            }
           }
         }
       }

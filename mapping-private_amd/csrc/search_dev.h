@@ -784,6 +784,7 @@ __device__ __forceinline__ void score_list_body(const SparseSearch& b, int bx, i
       if (gate[pp]) {
         float q2 = 0.0f;
         const float* q = qv + pp * (kOC + 1) + mm * a.r;
+#pragma unroll 4  // reads issued four at a time (a dependent LDS round trip per element otherwise)
         for (int i = 0; i < a.r; ++i) q2 = __builtin_fmaf(q[i], q[i], q2);
         sc = sqrt((double)q2) / sqrt((double)ffv[pp]);
         const long long en = ent[pp];

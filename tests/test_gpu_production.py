@@ -150,6 +150,39 @@ def test_stream_frames_at_bench_shape_vs_oracle(ctx, prod):
         _check_det(got[i], prod["ref"][_frame_grid(i)][2].reshape(M, -1), (P1, P1, P1), "drain %d" % i)
 
 
+def test_bases_swapped_between_unsynchronised_runs(ctx, prod):
+    """c3h_search_setup while a streamed run is still queued (no host sync): the queued
+    frames must finish on the old bases, the next run must use the new ones."""
+    import torch
+    B, nfr = 8, 19
+    ptrs = np.array([prod["d_grids"][_frame_grid(i)].data_ptr() for i in range(nfr)], np.uint64)
+    d_old = torch.zeros((nfr, M * 3), dtype=torch.int64, device="cuda:0")
+    d_new = torch.zeros((nfr, M * 3), dtype=torch.int64, device="cuda:0")
+    torch.cuda.synchronize()
+    ctx.set_batch(B)
+    ctx.set_pipeline(True)
+    ctx.run_frames(ptrs, (G,) * 3, (0, 0, 0), LEAF, F, THR, S, BOX, EXIST, True, d_old.data_ptr(), stream=True)
+    axis_t2, var2, axis_q2 = synth.random_bases(F, D, M, R, seed=synth.BASE_SEED + 77)
+    try:
+        ctx.search_setup(axis_t2, var2, axis_q2)  # same sizes: the buffers are overwritten in place
+        ctx.set_rank(1)
+        ctx.run_frames(ptrs, (G,) * 3, (0, 0, 0), LEAF, F, THR, S, BOX, EXIST, True, d_new.data_ptr())
+        ctx.synchronize()
+        old = d_old.cpu().numpy().reshape(nfr, M, 3)
+        new = d_new.cpu().numpy().reshape(nfr, M, 3)
+        ap2 = synth.whiten(axis_t2, var2)
+        for i in range(nfr):
+            fe, ex, sc = prod["ref"][_frame_grid(i)]
+            _check_det(old[i], sc.reshape(M, -1), (P1, P1, P1), "old bases, frame %d" % i)
+            if i % 6 == 0:
+                _, _, sc2 = po.search((P1 + 1,) * 3, fe, ex, ap2, axis_q2, BOX, 1, EXIST, dbl=True, want_scores=True)
+                _check_det(new[i], sc2.reshape(M, -1), (P1, P1, P1), "new bases, frame %d" % i)
+    finally:
+        axis_t, var, axis_q = synth.random_bases(F, D, M, R, seed=synth.BASE_SEED)
+        ctx.search_setup(axis_t, var, axis_q)
+        ctx.set_rank(1)
+
+
 def test_config4_shape_voxelise_and_run_frames(ctx):
     """BASELINE configs[3] on one GPU: 64 independent 1M-point frames (8 ray-cast scenes,
     each under 8 colour masks and x translations by whole cells) voxelised on the GPU at
