@@ -73,8 +73,9 @@ def make_grids(ctx, dev, nf, rank, synth, c3hlac, torch):
         pts = synth.kinect_scene(N_RAYS, grid=GRID, leaf=LEAF, seed=synth.BASE_SEED + 1000 * rank + s)
         d_pts = torch.from_numpy(pts).to(dev)
         torch.cuda.current_stream(dev).synchronize()
-        if s == 0:  # untimed first call: sizes the voxeliser's tables (hipMalloc) on this context
-            ctx.voxelize(d_pts, LEAF)
+        # untimed first call per scene: a scene with more points than any before it grows the
+        # voxeliser's buffers (hipMalloc); the timed call is the steady-state per-frame cost
+        ctx.voxelize(d_pts, LEAF)
         ctx.timing(True)
         gi = ctx.voxelize(d_pts, LEAF)
         t_vox_ms.append(ctx.kernel_times(reset=True)["voxelize"][0])
@@ -237,8 +238,8 @@ def main():
                               "are per frame); c3hlac = occupancy pass + tile kernel; score = compress(non-empty "
                               "rows)+gate launch + score launch with the fused rank-1 replay" % (n_sep, LANES, B),
         "voxelize_mpoints_per_s": n_points / (sum(t_vox_ms) / 1e3) / 1e6 if sum(t_vox_ms) else None,
-        "voxelize_note": "c3h_voxelize of each 1M-ray scene, HIP events around all of its kernels (one untimed "
-                         "call first sizes the context's tables)",
+        "voxelize_note": "c3h_voxelize of each 1M-ray scene, HIP events around all of its kernels (an untimed "
+                         "call on the scene first sizes the context's buffers for its point count)",
         "roofline": {
             "kernel": "c3h_tick_kernel (pipeline tick: occupancy stream of one batch + C3 tile pass, compress+gate "
                       "and scoring of the three previous batches)",
