@@ -224,11 +224,13 @@ int c3h_get_exist(c3h_ctx* ctx, int32_t* out, int on_device);
 int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_t D,
                      int32_t F, const float* axis_q, int32_t M, int32_t r,
                      const float* feature_max, int32_t feature_max_len);
-/* Search precision of the matrix-core compress (grids of >= 65,536 subdivisions, e.g.
- * BASELINE config 5; D <= 128): fp16 = 1 rounds the normalised features and the whitened
- * axis to f16 and accumulates in f32 on v_mfma_f32_32x32x16_f16; scores then agree with
- * the float64 oracle within 2e-3 relative (fp16 = 0, the default: fp32, 1e-5).  Smaller
- * grids and the pipelined c3h_run_frames path always compress in fp32. */
+/* Search precision of the matrix-core stages.  fp16 = 1: the compress of grids of >= 65,536
+ * subdivisions (e.g. BASELINE config 5; D <= 128) rounds the normalised features and the
+ * whitened axis to f16, and the matrix-core projection (c3h_set_score_engine) rounds each
+ * position's box row -- scaled by a power of two, |Q f|/|f| is scale-free -- and the model
+ * basis to f16; both accumulate in f32 on v_mfma_f32_32x32x16_f16.  Scores then agree with
+ * the float64 oracle within 2e-3 relative (fp16 = 0, the default: fp32, 1e-5).  The VALU
+ * kernels and the pipelined c3h_run_frames path always run in fp32. */
 int c3h_set_search_precision(c3h_ctx* ctx, int32_t fp16);
 /* Engine of the single-frame search's projection step (SearchObjMulti::searchPart's
  * M x r x D products, search.cpp:915-968): 0 = automatic (default: the matrix cores for

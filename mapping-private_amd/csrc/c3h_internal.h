@@ -276,6 +276,8 @@ struct SparseSearch {
   float* gbox = nullptr;   // large grids: box-summed G rows of every position (pstart order)
   int64_t s_gbox = 0;
   int score_mfma = 0;      // project on the matrix cores (score_mfma_kernel; needs gbox, nframes 1)
+  const _Float16* qt16 = nullptr;  // fp16 search precision: the basis as f16, [Opad][16 * Kq16]
+  int Kq16 = 0;                    // 16-wide k steps (D rounded up to 16, / 16)
 };
 bool score_mfma_ok(int D);  // D fits score_mfma_kernel
 // sparse compress fused into the gate launch (nullable in launch_sparse_search)
@@ -434,6 +436,8 @@ struct c3h_ctx {
   int Fp16 = 0;
   bool prec16 = false;              // c3h_set_search_precision: fp16 matrix-core compress
   int score_engine = 0;             // c3h_set_score_engine: 0 auto, 1 VALU, 2 matrix cores
+  c3h::DevBuf<_Float16> qt16;       // f16 basis for the fp16 matrix-core projection
+  int Kq16 = 0;
   c3h::DevBuf<float> axis_q;        // M x r x D
   c3h::DevBuf<float> fmax;
   int fmax_len = 0;

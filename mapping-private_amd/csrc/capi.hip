@@ -459,6 +459,10 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
     q.scores = ctx->scores.p;
     q.nmodes = rm.n;
     q.score_mfma = mf ? 1 : 0;
+    if (mf && ctx->prec16 && ctx->Kq16 > 0) {  // fp16 search precision: f16 operands
+      q.qt16 = ctx->qt16.p;
+      q.Kq16 = ctx->Kq16;
+    }
     q.pstart[0] = 0;
     for (int i = 0; i < rm.n; ++i) {
       const auto& a = launches[i];
@@ -695,6 +699,7 @@ void c3h_destroy(c3h_ctx* ctx) {
   release(ctx->d_lists);
   release(ctx->prof);
   release(ctx->chist);
+  release(ctx->qt16);
   for (int s = 0; s < C3H_NTIMERS; ++s)
     for (auto& e : ctx->timer.pending[s]) ctx->timer.pool.push_back({e.a, e.b});
   for (auto& e : ctx->timer.pool) {
@@ -1657,6 +1662,18 @@ int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_
   ENSURE(ctx->qt, qt.size());
   HIPCHK(hipMemcpy(ctx->qt.p, qt.data(), qt.size() * 4, hipMemcpyHostToDevice));
   ctx->Opad = Opad;
+  // f16 basis for the fp16 matrix-core projection: column-major [Opad][16 * Kq16] (a lane's
+  // 8 consecutive k are one 16-B load), zero past D and past M * r
+  ctx->Kq16 = 0;
+  if (c3h::score_mfma_ok(D)) {
+    const int Kq = (D + 15) / 16, KH = 16 * Kq;
+    std::vector<_Float16> q16((size_t)Opad * KH, (_Float16)0.0f);
+    for (int c = 0; c < M * r; ++c)
+      for (int d = 0; d < D; ++d) q16[(size_t)c * KH + d] = (_Float16)axis_q[(size_t)c * D + d];
+    ENSURE(ctx->qt16, q16.size());
+    HIPCHK(hipMemcpy(ctx->qt16.p, q16.data(), q16.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    ctx->Kq16 = Kq;
+  }
   ctx->fmax_len = feature_max_len;
   if (feature_max_len > 0) {
     ENSURE(ctx->fmax, (size_t)feature_max_len);

@@ -329,13 +329,14 @@ __global__ __launch_bounds__(kBlock, C3H_SMF_WAVES) void score_mfma_kernel(Spars
           for (int j = 0; j < 16; ++j) qv[j] = qrow[h0 + j];
 #pragma unroll
           for (int j = 0; j < 16; ++j) {
-            if (h0 + j >= ncol) break;  // uniform
-            q2 = __builtin_fmaf(qv[j], qv[j], q2);
-            if (++ir == r) {  // model m complete
-              if (valid) a.scores[sbase + (int64_t)m * sP] = sqrt((double)q2) / sqrt((double)ff);
-              q2 = 0.0f;
-              ir = 0;
-              ++m;
+            if (h0 + j < ncol) {  // uniform (no break: the loop must unroll, qv stays in registers)
+              q2 = __builtin_fmaf(qv[j], qv[j], q2);
+              if (++ir == r) {  // model m complete
+                if (valid) a.scores[sbase + (int64_t)m * sP] = sqrt((double)q2) / sqrt((double)ff);
+                q2 = 0.0f;
+                ir = 0;
+                ++m;
+              }
             }
           }
         }
@@ -395,6 +396,166 @@ hipError_t launch_score_mfma(const SparseSearch& a, hipStream_t s) {
   if (kp <= 72) return launch_score_mfma_kp<72>(a, s);
   if (kp <= 80) return launch_score_mfma_kp<80>(a, s);
   return hipErrorInvalidValue;
+}
+
+// fp16 search precision (c3h_set_search_precision(ctx, 1)): the same projection with f16
+// operands on v_mfma_f32_32x32x16_f16 (f32 accumulation, 16x the f32 matrix rate).  The
+// score |Q f| / |f| is invariant to scaling f, so each position's box row is scaled by a
+// power of two that puts its largest element in [0.5, 1) before rounding to f16 (exact
+// scaling: no overflow, full f16 precision), and f.f is taken over the same rounded values.
+// The basis is f16 too (qt16, [column][16 * Kq16]); each wave reads its B fragments straight
+// from L2 (16 B per lane per k step, one tile ahead) -- no LDS staging, no barriers.  Stated
+// tolerance with the fp16 compress: 2e-3 relative of the float64 oracle.
+template <int KQ>  // 16-wide k steps
+__global__ __launch_bounds__(kBlock, 3) void score_mfma_f16_kernel(SparseSearch a, int ngroups) {
+  extern __shared__ __attribute__((aligned(16))) float smh[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hk = lane >> 5, l32 = lane & 31;
+  float* se = smh + wave * 32 * kSMES;
+  int64_t* s_mode = reinterpret_cast<int64_t*>(smh + (kBlock / 64) * 32 * kSMES);
+  if (tid < a.nmodes) {
+    s_mode[3 * tid] = a.pstart[tid];
+    s_mode[3 * tid + 1] = a.md[tid].offset;
+    s_mode[3 * tid + 2] = a.md[tid].P;
+  }
+  __syncthreads();
+  constexpr int KH = 16 * KQ;
+  const int D = a.D, r = a.r, Qs = a.Opad;
+  const int n = (int)a.cnt[a.epoch & 1];
+  const int g = blockIdx.y;
+  const int m0 = (int)((int64_t)g * a.M / ngroups), m1 = (int)((int64_t)(g + 1) * a.M / ngroups);
+  const int cb = m0 * r, ce = m1 * r;
+  const int ntile = (ce - cb + 31) / 32;
+  for (int pb = blockIdx.x; pb * kSMP < n; pb += gridDim.x) {
+    const int e = pb * kSMP + wave * 32 + l32;
+    const bool valid = e < n;
+    const long long en = valid ? a.list[e] : 0;
+    const int mi = (int)(en >> 40);
+    const int64_t p = en & ((1ll << 40) - 1);
+    const float* __restrict__ row = a.gbox + (valid ? (s_mode[3 * mi] + p) * D : 0);
+    float v[KQ][8];
+    float mx = 0.0f;
+#pragma unroll
+    for (int s = 0; s < KQ; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 16 * s + 8 * hk + j;
+        const float x = row[min(k, D - 1)];
+        v[s][j] = k < D ? x : 0.0f;
+        mx = fmaxf(mx, fabsf(v[s][j]));
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    int ex = 0;
+    (void)frexpf(mx, &ex);  // mx = m * 2^ex, m in [0.5, 1) (ex = 0 for a zero row)
+    mf_f16x8 av[KQ];
+    float ff = 0.0f;
+#pragma unroll
+    for (int s = 0; s < KQ; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const _Float16 h = (_Float16)ldexpf(v[s][j], -ex);
+        av[s][j] = h;
+        ff = __builtin_fmaf((float)h, (float)h, ff);
+      }
+    ff += __shfl_xor(ff, 32, 64);  // this lane's k and its partner's (a + b == b + a)
+    const int64_t sbase = s_mode[3 * mi + 1] + p, sP = s_mode[3 * mi + 2];
+    auto load_b = [&](int t, mf_f16x8 (&dst)[KQ]) {
+      const int col = min(cb + 32 * t + l32, Qs - 1);  // clamped: columns past the group are never folded
+#pragma unroll
+      for (int s = 0; s < KQ; ++s)
+        dst[s] = *reinterpret_cast<const mf_f16x8*>(a.qt16 + (int64_t)col * KH + 16 * s + 8 * hk);
+    };
+    mf_f16x8 bcur[KQ];
+    load_b(0, bcur);
+    float q2 = 0.0f;
+    int m = m0, ir = 0;
+    for (int t = 0; t < ntile; ++t) {
+      mf_f16x8 bnxt[KQ];
+      if (t + 1 < ntile) load_b(t + 1, bnxt);
+      mf_f32x16 acc;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+#pragma unroll
+      for (int s = 0; s < KQ; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s], bcur[s], acc, 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) se[((q & 3) + 8 * (q >> 2) + 4 * hk) * kSMES + l32] = acc[q];
+      __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const int ncol = min(32, ce - (cb + 32 * t));
+      if (hk == 0) {
+        const float* qrow = se + l32 * kSMES;
+#pragma unroll
+        for (int h0 = 0; h0 < 32; h0 += 16) {
+          float qv[16];
+#pragma unroll
+          for (int j = 0; j < 16; ++j) qv[j] = qrow[h0 + j];
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            if (h0 + j < ncol) {  // uniform
+              q2 = __builtin_fmaf(qv[j], qv[j], q2);
+              if (++ir == r) {
+                if (valid) a.scores[sbase + (int64_t)m * sP] = sqrt((double)q2) / sqrt((double)ff);
+                q2 = 0.0f;
+                ir = 0;
+                ++m;
+              }
+            }
+          }
+        }
+      }
+      __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (t + 1 < ntile) {
+#pragma unroll
+        for (int s = 0; s < KQ; ++s) bcur[s] = bnxt[s];
+      }
+    }
+  }
+}
+
+template <int KQ>
+hipError_t launch_score_mfma_f16_kq(const SparseSearch& a, hipStream_t s) {
+  static thread_local int slots = 0, dev_c = -1;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const size_t lds = sizeof(float) * (kBlock / 64) * 32 * kSMES + 3 * 6 * sizeof(int64_t);
+  if (dev != dev_c) {
+    int n_cu = 256, per_cu = 0;
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, score_mfma_f16_kernel<KQ>, kBlock, lds) !=
+            hipSuccess || per_cu < 1)
+      per_cu = 1;
+    slots = per_cu * n_cu;
+    dev_c = dev;
+  }
+  const int64_t pblocks = (a.pstart[a.nmodes] + kSMP - 1) / kSMP;
+  int ng = 1;
+  double best = 1e300;
+  for (int g = 1; g <= a.M; ++g) {  // the f32 kernel's cost model, in 32-column tiles
+    const int64_t rounds = (pblocks * g + slots - 1) / slots;
+    const int64_t cols = (int64_t)((a.M + g - 1) / g) * a.r;
+    const double t = (double)rounds * (3.0 + (double)((cols + 31) / 32));
+    if (t < best) {
+      best = t;
+      ng = g;
+    }
+  }
+  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(pblocks, 65535));
+  score_mfma_f16_kernel<KQ><<<dim3(gx, (unsigned)ng), kBlock, lds, s>>>(a, ng);
+  return hipGetLastError();
+}
+
+hipError_t launch_score_mfma_f16(const SparseSearch& a, hipStream_t s) {
+  switch (a.Kq16) {
+    case 1: return launch_score_mfma_f16_kq<1>(a, s);
+    case 2: return launch_score_mfma_f16_kq<2>(a, s);
+    case 3: return launch_score_mfma_f16_kq<3>(a, s);
+    case 4: return launch_score_mfma_f16_kq<4>(a, s);
+    case 5: return launch_score_mfma_f16_kq<5>(a, s);
+    case 6: return launch_score_mfma_f16_kq<6>(a, s);
+    case 7: return launch_score_mfma_f16_kq<7>(a, s);
+    case 8: return launch_score_mfma_f16_kq<8>(a, s);
+    case 9: return launch_score_mfma_f16_kq<9>(a, s);
+    case 10: return launch_score_mfma_f16_kq<10>(a, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 // rank 1 on large grids: block (b, m) reduces model m's scores of global positions
@@ -693,7 +854,7 @@ score:
   }
   if (a.score_mfma) {  // single frame, box sums above: the matrix-core projection
     if (!a.gbox || nf != 1 || !score_mfma_ok(a.D)) return hipErrorInvalidValue;
-    const hipError_t e = launch_score_mfma(a, s);
+    const hipError_t e = a.qt16 ? launch_score_mfma_f16(a, s) : launch_score_mfma(a, s);
     if (e != hipSuccess) return e;
     if (a.lists) {  // rank 1: parallel argmax over the written scores + finalize
       scores_argmax_kernel<<<dim3(kArgmaxBlocks, a.M), kBlock, 0, s>>>(a);

@@ -50,9 +50,13 @@ constexpr uint32_t kNoMargin = 0xffffffffu;  // above every float's bits: "no po
 #ifndef C3H_VOX_CHUNK
 #define C3H_VOX_CHUNK 4096
 #endif
+#ifndef C3H_VOX_THREADS
+#define C3H_VOX_THREADS 1024  // accumulate workgroup: 16 waves (4 per SIMD) over one LDS table
+#endif
+constexpr int kVB = C3H_VOX_THREADS;
 constexpr int kVoxChunk = C3H_VOX_CHUNK;      // points per workgroup (16 per thread; 4096 / 2048 slots measured
                                               // 40.9 us per 1M-point frame vs 41.9 at 2048 / 1024, 51 at 1024)
-constexpr int kVoxPer = kVoxChunk / kBlock;
+constexpr int kVoxPer = kVoxChunk / kVB;
 constexpr int kVoxRound = kVoxPer;             // loads in flight per thread (one round)
 #ifndef C3H_VOX_SLOTS
 #define C3H_VOX_SLOTS 2048
@@ -158,7 +162,7 @@ __device__ __forceinline__ void vox_clear_prev(const VoxArgs& a) {
     const int nn = part_of(a, pp)[(size_t)b * kPartW + kPNew];
     const uint32_t* sl = a.lists + (size_t)pp * a.lcap + (size_t)b * kVoxChunk;
     const uint32_t* tl = a.lists + (size_t)(2 + pp) * a.lcap + (size_t)b * kVoxChunk;
-    for (int i = threadIdx.x; i < nn; i += kBlock) {
+    for (int i = threadIdx.x; i < nn; i += kVB) {
       if (a.clear_tables) {
         VoxSlot& t = a.tab_prev[sl[i]];
         *reinterpret_cast<ulonglong2*>(&t.key) = make_ulonglong2(kNoKey, 0ull);
@@ -169,15 +173,15 @@ __device__ __forceinline__ void vox_clear_prev(const VoxArgs& a) {
   }
 }
 
-__global__ __launch_bounds__(kBlock) void vox_accum_kernel(VoxArgs a) {
+__global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
   __shared__ unsigned long long s_key[kLSlots];
   __shared__ unsigned long long s_gb[kLSlots];  // b << 32 | g
   __shared__ unsigned long long s_cr[kLSlots];  // count << 32 | r
   __shared__ uint32_t s_m[kLSlots];
   __shared__ uint32_t s_nnew;                   // global slots this workgroup inserted (its list segment)
-  __shared__ int s_red[kBlock / 64][8];
+  __shared__ int s_red[kVB / 64][8];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int s = tid; s < kLSlots; s += kBlock) {
+  for (int s = tid; s < kLSlots; s += kVB) {
     s_key[s] = kNoKey;
     s_gb[s] = 0;
     s_cr[s] = 0;
@@ -216,7 +220,7 @@ __global__ __launch_bounds__(kBlock) void vox_accum_kernel(VoxArgs a) {
   float4 p[kVoxRound];
 #pragma unroll
   for (int j = 0; j < kVoxRound; ++j) {  // a round of loads in flight together
-    const int64_t i = base + (j0 + j) * kBlock + tid;
+    const int64_t i = base + (j0 + j) * kVB + tid;
     if (i < a.n) {  // streamed once: non-temporal
       const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.pts) + i);
       p[j] = make_float4(v.x, v.y, v.z, v.w);
@@ -261,7 +265,7 @@ __global__ __launch_bounds__(kBlock) void vox_accum_kernel(VoxArgs a) {
   }
   // flush: one global insert + two (three near a cell boundary) atomics per (workgroup, voxel)
   __syncthreads();  // every point's LDS update is in
-  for (int s = tid; s < kLSlots; s += kBlock) {
+  for (int s = tid; s < kLSlots; s += kVB) {
     const unsigned long long key = s_key[s];
     if (key == kNoKey) continue;
     const unsigned long long cr = s_cr[s];
@@ -288,7 +292,7 @@ __global__ __launch_bounds__(kBlock) void vox_accum_kernel(VoxArgs a) {
   int32_t* pr = a.part + ((size_t)a.par * a.nblk_cap + blockIdx.x) * kPartW;
   if (tid < 8) {
     int v = s_red[0][tid];
-    for (int i = 1; i < kBlock / 64; ++i) {
+    for (int i = 1; i < kVB / 64; ++i) {
       const int u = s_red[i][tid];
       v = tid < 3 ? min(v, u) : (tid < 6 ? max(v, u) : (tid == 6 ? v + u : (v | u)));
     }
@@ -623,7 +627,7 @@ int64_t leaf_layout_blocks(int64_t nvox) { return scan_blocks(nvox); }
 
 hipError_t launch_voxelize(const VoxArgs& a, hipStream_t s) {
   // at least one accum block: it also clears the previous frame and resets the totals
-  vox_accum_kernel<<<(unsigned)std::max(a.nblk, 1), kBlock, 0, s>>>(a);
+  vox_accum_kernel<<<(unsigned)std::max(a.nblk, 1), kVB, 0, s>>>(a);
   if (a.nblk > 0) vox_scatter_kernel<<<(unsigned)a.nblk, kBlock, 0, s>>>(a);
   return hipGetLastError();
 }

@@ -69,6 +69,15 @@ def test_r70_models_matrix_cores_vs_generic(ctx, M):
     assert np.array_equal(sa > 0, ok)
     np.testing.assert_allclose(sa[ok], scd[ok], rtol=SCORE_RTOL_F64)
     _assert_replay_matches(ctx, (2, 2, 2), M, la)
+    # fp16 search precision: f16 operands on v_mfma_f32_32x32x16_f16, stated tolerance 2e-3
+    ctx.set_search_precision(True)
+    try:
+        lh, _, sh = _search(ctx, 2, (2, 2, 2), M, 100)
+    finally:
+        ctx.set_search_precision(False)
+    assert np.array_equal(sh > 0, ok)
+    np.testing.assert_allclose(sh[ok], scd[ok], rtol=2e-3)
+    assert not np.array_equal(sh, sa)  # the f16 path really ran
 
 
 def test_config5_stress_63_models_r70(ctx):
@@ -105,3 +114,19 @@ def test_config5_stress_63_models_r70(ctx):
         assert float(lists[m, 0]["score"]) == flat[m, p]
         assert (int(lists[m, 0]["z"]), int(lists[m, 0]["y"]), int(lists[m, 0]["x"])) == \
             np.unravel_index(p, (n - 1,) * 3)
+    # fp16 search precision (f16 compress + f16 projection): stated tolerance 2e-3
+    ctx.set_search_precision(True)
+    try:
+        ctx.set_rank(1)
+        lists16, _ = ctx.search((2, 2, 2), 100)
+        sc16 = ctx.scores().reshape(M, n - 1, n - 1, n - 1)
+    finally:
+        ctx.set_search_precision(False)
+    assert (sc16 > 0).all()
+    inner16 = sc16[:, 1:n - 2, 1:n - 2, 1:n - 2].reshape(M, -1)
+    assert (inner16 == inner16[:, :1]).all()
+    npt.assert_allclose(inner16[:, 0], s64, rtol=2e-3)
+    assert not np.array_equal(inner16[:, 0], inner[:, 0])
+    flat16 = sc16.reshape(M, -1)
+    for m in range(M):
+        assert float(lists16[m, 0]["score"]) == flat16[m].max()
