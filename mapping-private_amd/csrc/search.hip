@@ -604,9 +604,11 @@ __global__ __launch_bounds__(kBlock) void scores_argmax_kernel(SparseSearch a) {
   }
 }
 
+// one wave per model (a model's reduction is a chain of dependent round trips: spread them)
 __global__ __launch_bounds__(kBlock) void argmax_finalize_kernel(SparseSearch a, int nparts) {
-  argmax_finalize(a, a.partials, a.lists, a.outs[0], nparts);
+  argmax_finalize(a, a.partials, a.lists, a.outs[0], nparts, blockIdx.x * (kBlock / 64), gridDim.x * (kBlock / 64));
 }
+unsigned finalize_blocks(int M) { return (unsigned)std::max(1, (M + kBlock / 64 - 1) / (kBlock / 64)); }
 
 __global__ __launch_bounds__(kBlock) void score_list_kernel(SparseSearch b) {
   extern __shared__ __attribute__((aligned(16))) float sl_smem[];
@@ -858,7 +860,7 @@ score:
     if (e != hipSuccess) return e;
     if (a.lists) {  // rank 1: parallel argmax over the written scores + finalize
       scores_argmax_kernel<<<dim3(kArgmaxBlocks, a.M), kBlock, 0, s>>>(a);
-      argmax_finalize_kernel<<<1, kBlock, 0, s>>>(a, kArgmaxBlocks);
+      argmax_finalize_kernel<<<finalize_blocks(a.M), kBlock, 0, s>>>(a, kArgmaxBlocks);
     }
     return hipGetLastError();
   }
@@ -874,7 +876,7 @@ score:
     b.lists = nullptr;
     score_list_kernel<<<dim3(gx, groups, nf), kBlock, lds, s>>>(b);
     scores_argmax_kernel<<<dim3(kArgmaxBlocks, a.M), kBlock, 0, s>>>(a);
-    argmax_finalize_kernel<<<1, kBlock, 0, s>>>(a, kArgmaxBlocks);
+    argmax_finalize_kernel<<<finalize_blocks(a.M), kBlock, 0, s>>>(a, kArgmaxBlocks);
     return hipGetLastError();
   }
   score_list_kernel<<<dim3(gx, groups, nf), kBlock, lds, s>>>(a);

@@ -521,10 +521,12 @@ __device__ __forceinline__ void boxsum_body(const SparseSearch& a, int64_t e, in
 // checkOverlap returns slot 0, so the update is "first strictly greater maximum in scan
 // order").  One wave per model reduces the partials with (score desc, scan order asc);
 // partials of other workgroups are read with device-scope atomic loads.
+// Models w, w + stride, ... of wave w (the standalone kernel spreads the models over
+// workgroups: model_base = blockIdx.x * 4, stride = gridDim.x * 4).
 __device__ void argmax_finalize(const SparseSearch& a, const ScorePartial* partials, c3h_det* lists,
-                                c3h_det* out, int nparts) {
+                                c3h_det* out, int nparts, int model_base = 0, int model_stride = kBlock / 64) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int m = w; m < a.M; m += kBlock / 64) {
+  for (int m = model_base + w; m < a.M; m += model_stride) {
     double best = -2.0;
     long long bo = -1;
     for (int i = lane; i < nparts; i += 64) {
