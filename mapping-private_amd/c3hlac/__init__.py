@@ -57,12 +57,17 @@ class Context:
         return check(rc, self.h, what)
 
     def set_stream(self, stream_handle):
-        """Bind the context to a HIP stream handle (torch.cuda.Stream.cuda_stream).  The
-        legacy default stream (handle 0) cannot be named through the C-ABI, where NULL
-        means the context's own non-blocking stream: run under a non-default torch
-        stream instead, or synchronize() before torch reads the results."""
-        if not stream_handle:
-            raise ValueError("set_stream: handle 0 is the legacy default stream; use a torch.cuda.Stream()")
+        """Bind the context to a HIP stream handle (torch.cuda.Stream.cuda_stream); None
+        returns to the context's own non-blocking stream (NULL in the C-ABI).  Work queued
+        on the previous stream is ordered before the new stream's.  The legacy default
+        stream (integer handle 0) cannot be named through the C-ABI: run under a
+        non-default torch stream instead, or synchronize() before torch reads results."""
+        if stream_handle is None:
+            self._chk(self.lib.c3h_set_stream(self.h, None), "set_stream")
+            return
+        if stream_handle == 0:
+            raise ValueError("set_stream: handle 0 is the legacy default stream; use a torch.cuda.Stream() "
+                             "or None for the context's own stream")
         self._chk(self.lib.c3h_set_stream(self.h, C.c_void_p(stream_handle)), "set_stream")
 
     def synchronize(self):

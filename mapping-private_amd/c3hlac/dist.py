@@ -112,13 +112,26 @@ def merge_slab_lists(parts, schedule):
     return np.ascontiguousarray(out)
 
 
-def slab_search(ctx, words_zyx, variant, thr, subdiv, ranges, exist_threshold, rank, world, rotate=True):
+def slab_search(ctx, words_zyx, variant, thr, subdiv, ranges, exist_threshold, rank, world, rotate=True,
+                search_rank=1):
     """Extract + rank-1 search of rank `rank`'s slab of the packed grid words_zyx[z, y, x]
     (only the slab's planes are read) on this rank's context, whose search bases (and
     engine settings) are already set.  Returns (M,) c3h_det records with global z, or None
-    when the slab owns no plane."""
+    when the slab owns no plane.
+
+    search_rank (SearchObj::setRank) must be 1: the rank > 1 update with checkOverlap
+    (search.cpp:327-356, 464-474) is sequential over the whole scene's scan order, so
+    per-slab lists cannot be merged into it; C3HError(C3H_ERR_ARG) otherwise.
+
+    The slab is loaded from packed grid words (c3h_set_grid), so voxels are placed by their
+    cell index.  A scene voxelised from points whose centroids round across a cell boundary
+    (c3h_voxelize's off-cell records, c3_hlac.cpp:349-377) is matched only by a whole-scene
+    extract of the same words, not of the points."""
     import numpy as np
-    from ._capi import DET_DTYPE
+    from ._capi import C3HError, DET_DTYPE, ERRORS
+    if int(search_rank) != 1:
+        raise C3HError("slab_search: search_rank %d: %s (only rank 1 merges across slabs)"
+                       % (search_rank, ERRORS.get(-1, -1)))
     gz, gy, gx = words_zyx.shape
     zr_max = max(mode_ranges(md, ranges)[2] for md in mode_schedule(ranges, rotate))
     ext = slab_extent(gz, subdiv, zr_max, rank, world)

@@ -713,7 +713,16 @@ void c3h_destroy(c3h_ctx* ctx) {
 
 int c3h_set_stream(c3h_ctx* ctx, void* hip_stream) {
   if (!ctx) return C3H_ERR_ARG;
-  ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own_stream;
+  hipStream_t next = hip_stream ? (hipStream_t)hip_stream : ctx->own_stream;
+  if (next == ctx->stream) return C3H_OK;
+  HIPCHK(hipSetDevice(ctx->device));
+  // an open frame stream runs its remaining ticks on the old stream, and everything queued
+  // there (ticks, lanes' joins, async searches) is ordered before the new stream's work
+  QUIESCE(ctx);
+  if (!ctx->fork_ev) HIPCHK(hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(ctx->fork_ev, ctx->stream));
+  HIPCHK(hipStreamWaitEvent(next, ctx->fork_ev, 0));
+  ctx->stream = next;
   return C3H_OK;
 }
 
@@ -1394,7 +1403,13 @@ static int grsd_frames(c3h_ctx* ctx, const c3h_grsd_params* p, int32_t sb[3], in
                                      reinterpret_cast<float*>(ctx->dsamp.p), ctx->stream));
   // RSD radius: max(rsd_radius_search, voxel_size / 2 * sqrt(3)) (:172)
   const float max_dist = (float)std::max((double)p->rsd_radius, (double)ctx->info.leaf / 2 * std::sqrt(3.0));
-  if (max_dist > 4 * ctx->nbr.cell) return fail(ctx, C3H_ERR_ARG, "extract_grsd: RSD radius > 4 x normal radius");
+  if (max_dist > 4 * ctx->nbr.cell) {
+    // a wide RSD radius (large leaves: leaf sqrt(3)/2 > 4 x the normal radius) gets a search
+    // grid of its own radius; the normals are already computed, and the RSD's per-bin
+    // min/max angles do not depend on the neighbour visiting order
+    rc = nbr_grid(ctx, max_dist);
+    if (rc != C3H_OK) return rc;
+  }
   ENSURE(ctx->rsd_radii, (size_t)std::max<int64_t>(nc, 1));
   ENSURE(ctx->rsd_types, (size_t)std::max<int64_t>(nc, 1));
   HIPCHK(c3h::launch_rsd(ctx->nbr, ctx->normals.p, ctx->dsamp.p, nc, max_dist, ctx->rsd_radii.p, ctx->rsd_types.p,

@@ -157,3 +157,13 @@ def test_slab_partition():
     assert slab_extent(512, 10, 2, 0, 8) == (0, 7, 0, 80, 0)
     assert slab_extent(512, 10, 2, 1, 8) == (7, 14, 69, 150, 1)
     assert slab_extent(512, 10, 2, 7, 8) == (46, 52, 459, 512, 1)
+
+
+def test_slab_search_rejects_rank_above_one():
+    """rank > 1 lists cannot be merged across slabs (the checkOverlap update is sequential
+    over the whole scene): slab_search fails with C3H_ERR_ARG before touching a context."""
+    from c3hlac import dist as cdist
+    from c3hlac._capi import C3HError
+    words = np.zeros((20, 20, 20), np.uint32)
+    with pytest.raises(C3HError, match="C3H_ERR_ARG"):
+        cdist.slab_search(None, words, 117, THR, 10, (2, 2, 2), 0, 0, 2, search_rank=3)

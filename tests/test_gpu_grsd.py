@@ -109,3 +109,21 @@ def test_vosch_rows_and_search(ctx):
     ok = scd > 0
     assert ok.any()
     np.testing.assert_allclose(sc[ok], scd[ok], rtol=1e-5)
+
+
+def test_grsd_leaf_wider_than_four_normal_radii(ctx):
+    """A leaf of 0.1 with the reference's default radii (normals 0.02, RSD 0.01): the RSD
+    radius leaf*sqrt(3)/2 = 0.087 exceeds 4 x the normal radius, which
+    extractGRSDSignature21 accepts (grsd_colorCHLAC_tools.hpp:172); the library builds a
+    search grid of that radius instead of failing."""
+    name = "noisy_sphere_green"
+    pts = _setup(ctx, name, leaf=0.1)
+    sb, H = ctx.extract_grsd(0)
+    assert H == 1
+    g, layout, cloud = po.voxelize(pts, 0.1)
+    dn = ctx.normals(len(pts)).astype(np.float64)
+    feat_ref, _, radii_ref, types_ref = go.grsd(pts, dn, g, layout, cloud, 0.1)
+    radii, types = ctx.rsd()
+    np.testing.assert_allclose(radii, radii_ref, rtol=1e-5, atol=1e-7)
+    if np.array_equal(types, types_ref):
+        assert np.array_equal(ctx.features()[0], feat_ref[0].astype(np.float32))

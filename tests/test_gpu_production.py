@@ -150,6 +150,40 @@ def test_stream_frames_at_bench_shape_vs_oracle(ctx, prod):
         _check_det(got[i], prod["ref"][_frame_grid(i)][2].reshape(M, -1), (P1, P1, P1), "drain %d" % i)
 
 
+def test_stream_switched_mid_stream(ctx, prod):
+    """c3h_set_stream while a frame stream is open (no host sync): the open batches finish
+    on the old stream before anything the new stream runs, and the detections of both
+    pushes equal c3h_run_frames' (set_stream drains and joins the streams)."""
+    import torch
+    B, n1, n2 = 8, 27, 21
+    nfr = n1 + n2
+    ptrs = np.array([prod["d_grids"][_frame_grid(i)].data_ptr() for i in range(nfr)], np.uint64)
+    d_out = torch.zeros((nfr, M * 3), dtype=torch.int64, device="cuda:0")
+    d_ref = torch.zeros((nfr, M * 3), dtype=torch.int64, device="cuda:0")
+    torch.cuda.synchronize()
+    ctx.set_batch(B)
+    ctx.set_pipeline(True)
+    side = torch.cuda.Stream()
+    rec = M * 3 * 8
+    try:
+        ctx.run_frames(ptrs[:n1], (G,) * 3, (0, 0, 0), LEAF, F, THR, S, BOX, EXIST, True, d_out.data_ptr(),
+                       stream=True)
+        ctx.set_stream(side.cuda_stream)
+        ctx.run_frames(ptrs[n1:], (G,) * 3, (0, 0, 0), LEAF, F, THR, S, BOX, EXIST, True,
+                       d_out.data_ptr() + n1 * rec, stream=True)
+        ctx.stream_flush()
+        ctx.synchronize()
+    finally:
+        ctx.set_stream(None)
+    ctx.run_frames(ptrs, (G,) * 3, (0, 0, 0), LEAF, F, THR, S, BOX, EXIST, True, d_ref.data_ptr())
+    ctx.synchronize()
+    got, ref = d_out.cpu().numpy(), d_ref.cpu().numpy()
+    assert np.array_equal(got, ref)
+    got = got.reshape(nfr, M, 3)
+    for i in range(0, nfr, 5):
+        _check_det(got[i], prod["ref"][_frame_grid(i)][2].reshape(M, -1), (P1, P1, P1), "switch %d" % i)
+
+
 def test_bases_swapped_between_unsynchronised_runs(ctx, prod):
     """c3h_search_setup while a streamed run is still queued (no host sync): the queued
     frames must finish on the old bases, the next run must use the new ones."""

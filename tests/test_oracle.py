@@ -267,3 +267,22 @@ def test_exist_gate_formula():
     f[0, :2] = [np.float32(1020 * np.float32(1 / 255.0)), np.float32(1275 * np.float32(1 / 255.0))]
     f[1, :2] = [np.float32(254 / 255.0), 0]
     assert list(po.exist(f)) == [int(np.float64((f[0, 0] + f[0, 1]) * np.float32(2)) + 0.001), 1, 0]
+
+
+@pytest.mark.parametrize("G,S", [(22, 10), (37, 6)])
+def test_crop_oracle_matches_whole_grid(G, S):
+    """The per-subdivision crop oracle of test_gpu_config5_nonperiodic (a subdivision's
+    centres plus its half neighbourhood, x padded to two subdivisions) equals the
+    whole-grid oracle at every subdivision, ragged edges and corners included."""
+    from test_gpu_config5_nonperiodic import _crop_row
+    rng = np.random.default_rng(G)
+    w = (rng.integers(0, 1 << 24, size=G ** 3, dtype=np.uint32) | np.uint32(1 << 24)).reshape(G, G, G)
+    for variant in (981, 117):
+        g, layout, cloud = po.grid_inputs(w.reshape(-1), (G,) * 3, 0.01)
+        fe, sb, _ = po.c3hlac(g, layout, cloud, variant, THR, 0.01, S, exact=True)
+        n = sb[0]
+        fe = fe.reshape(n, n, n, variant)
+        for z in range(n):
+            for y in range(n):
+                for x in range(n):
+                    assert np.array_equal(_crop_row(w, (x, y, z), S, variant), fe[z, y, x]), (x, y, z)
