@@ -57,6 +57,10 @@ def parse():
                     help="resident grids (0: batch + 8; every frame of a tick reads its own grid)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--point-frames", type=int, default=512,
+                    help="configs[3] points-in pass: frames over all ranks (0: skip)")
+    ap.add_argument("--host-point-frames", type=int, default=128,
+                    help="frames of the H2D-inclusive points-in pass per rank (pinned host memory)")
     return ap.parse_args()
 
 
@@ -256,6 +260,9 @@ def main():
             "avg_launch_ms": tick_avg_s * 1e3,
         },
     }
+    if args.point_frames > 0:
+        result["points_in"] = points_pass(ctx, dev, rank, world, dist, torch, synth, c3hlac, args.point_frames,
+                                          args.host_point_frames)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         f0 = args.warmup * B  # the first timed frame: the oracle re-computes it as it is timed
         rec0 = d[f0]
@@ -265,6 +272,86 @@ def main():
     ctx.close()
     if dist:
         dist.destroy_process_group()
+
+
+P_GRID, P_LEAF, P_VARIANT, P_M = 128, 0.02, 981, 1  # BASELINE configs[3] (= configs[1] per frame)
+
+
+def points_pass(ctx, dev, rank, world, dist, torch, synth, c3hlac, n_total, n_host):
+    """BASELINE configs[3]: n_total independent 1M-point frames (128^3, C3-HLAC-981 S=10,
+    compress 981->100, 1 model x r=20, box 2x2x2, rank 1) sharded round-robin over the ranks,
+    each rank's shard through c3h_run_point_frames (voxelised on the GPU, no per-frame host
+    round trip, the software-pipelined tick), then one RCCL all_gather of the detections.
+    Timed twice: points already in HBM, and points in pinned host memory (H2D included,
+    n_host frames per rank).  Frames: 16 ray-cast scenes, each under colour masks and x
+    shifts by whole cells (distinct clouds, distinct grids and min_b)."""
+    nb = 16
+    base = [torch.from_numpy(synth.kinect_scene(N_RAYS, grid=P_GRID, leaf=P_LEAF,
+                                                seed=synth.BASE_SEED + 7000 + s)).to(dev) for s in range(nb)]
+
+    def frame(i):
+        t = base[i % nb].clone()
+        k = i // nb
+        t[:, 3] = (t[:, 3].view(torch.int32) ^ ((k * 0x2F1D37) & 0xFFFFFF)).view(torch.float32)
+        t[:, 0] = (t[:, 0].double() + k * P_LEAF).float()
+        return t
+
+    mine = list(range(rank, n_total, world))
+    frames = [frame(i) for i in mine]
+    axis_t, var, axis_q = synth.random_bases(P_VARIANT, D, P_M, R, seed=synth.BASE_SEED + 31)
+    ctx.search_setup(axis_t, var, axis_q)
+    ctx.set_rank(1)
+    out = torch.zeros((max(len(mine), 1), 3 * P_M), dtype=torch.int64, device=dev)
+    canvas = (P_GRID,) * 3
+    args = (P_LEAF, canvas, P_VARIANT, THR, SUBDIV, BOX, EXIST_THR, True)
+    ctx.run_point_frames(frames[:4 * BATCH], *args[:7], True, out)  # untimed: sizes the buffers
+    torch.cuda.synchronize(dev)
+
+    def timed(fr, d_out, gather):
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        _, info = ctx.run_point_frames(fr, *args[:7], True, d_out)
+        if gather and dist:
+            from c3hlac.dist import gather_records
+            gather_records(d_out[:len(fr)], n_total, rank, world, dist)
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, info
+
+    ctx.timing(c3hlac.timing_mask("voxelize", "pipeline"))
+    ctx.kernel_times(reset=True)
+    el_dev, info = timed(frames, out, True)
+    kt = ctx.kernel_times(reset=True)
+    ctx.timing(False)
+    batched = int((info["status"] == 0).sum())
+    ok = bool((out[:len(mine)].cpu().numpy()[:, 0].view(np.float64) > 0).all())
+    res = {
+        "frames": n_total,
+        "frames_per_s_from_points": n_total / el_dev,
+        "note": "configs[3]: %d independent 1M-point frames (128^3, C3-HLAC-981 S=10, 981->100, 1 model x r=20, "
+                "box 2x2x2, rank 1) sharded over %d GPU(s), c3h_run_point_frames per rank (GPU voxeliser + "
+                "pipelined tick, one host sync per call) + RCCL all_gather; points resident in HBM" % (n_total, world),
+        "ms_per_call": el_dev * 1e3,
+        "frames_batched": batched * world,
+        "all_frames_detected": ok,
+        "voxelize_batched_us_per_frame": (kt["voxelize"][0] / kt["voxelize"][1] * 1e3) if kt["voxelize"][1] else None,
+        "voxelize_batched_gpoints_per_s": (N_RAYS * kt["voxelize"][1] / (kt["voxelize"][0] / 1e3) / 1e9)
+        if kt["voxelize"][0] else None,
+    }
+    if n_host > 0:  # H2D included: the frames start in pinned host memory
+        hf = [f.cpu().pin_memory() for f in frames[:n_host]]
+        hout = torch.zeros((len(hf), 3 * P_M), dtype=torch.int64, device=dev)
+        el_h, _ = timed([h.numpy() for h in hf], hout, False)
+        res["frames_per_s_from_points_h2d"] = len(hf) * world / el_h
+        res["h2d_note"] = "%d frames per GPU from pinned host memory (16 MB each), H2D inside the timed call" % len(hf)
+        res["h2d_equals_device"] = bool(torch.equal(hout, out[:len(hf)]))
+    return res
 
 
 def pmc_traffic(frames_per_tick):

@@ -287,6 +287,36 @@ int c3h_stream_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nfra
                       int32_t rotate, c3h_det* d_out);
 /* Runs the remaining ticks of an open stream (no host synchronisation). */
 int c3h_stream_flush(c3h_ctx* ctx);
+
+/* Points-in batch driver (BASELINE configs[3]: independent RGB-D frames): the per-callback
+ * work of color_voxel_recognition/test/detect_object.cpp:139-186 -- limitPoint + getVoxelGrid
+ * (c3h_voxelize), extractC3HLACSignature981/117 (c3h_extract) and SearchObj(Multi)::search
+ * from fresh lists (setRank state) -- for nframes point clouds, frame i = pts[i] (n[i] x 4
+ * floats as c3h_voxelize takes them; device pointers with on_device = 1, else host memory,
+ * copied by the library: pin it for full PCIe rate).  Frames are voxelised on the device in
+ * batches (c3h_set_batch) with no per-frame host round trip, each into a canvas grid of
+ * canvas[0] x canvas[1] x canvas[2] voxels placed at the frame's own min_b, and go through
+ * the software-pipelined tick of c3h_run_frames; a box position passes only inside the
+ * frame's own subdivisions, so every frame's results are those of its own grid.  Frame i's
+ * M x rank detections land in d_out + i * M * rank (device).  Frames the canvas path cannot
+ * reproduce exactly -- extent beyond the canvas, a voxel centroid that may round across its
+ * cell boundary (c3h_voxelize's exact pass), one subdivision where the canvas has several
+ * (computeC3HLAC's hist_num == 1 rule), no valid point -- are recomputed on the
+ * single-frame path after the batches (status 1).  info (host, nframes records, may be
+ * NULL): the frame's VoxelGrid geometry, getSubdivNum, point and voxel counts and status
+ * (0 batched, 1 single-frame path, < 0 the C3H_ERR_* that frame failed with; its lists are
+ * the fresh setRank state).  One host synchronisation per call (the frames' records).
+ * Rank 1 on the fast search path (else every frame takes the single-frame path).
+ * Returns the number of searched modes or an error. */
+typedef struct {
+  int32_t div_b[3], min_b[3], subdiv_b[3];
+  int32_t status;
+  int64_t n_valid, n_occ;
+} c3h_frame_info;
+int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n, int32_t nframes,
+                         int on_device, float leaf, float z_limit, const int32_t canvas[3],
+                         const c3h_extract_params* p, const int32_t range[3], int32_t exist_threshold,
+                         int32_t rotate, c3h_det* d_out, c3h_frame_info* info);
 /* Frames per pipeline batch / launch in c3h_run_frames and c3h_stream_frames
  * (1..64, default 32; the fast search path only). */
 int c3h_set_batch(c3h_ctx* ctx, int32_t frames);

@@ -12,6 +12,8 @@ import numpy as np
 from . import _capi
 from ._capi import DET_DTYPE, TIMER_NAMES, check, i32x3, ptr
 
+FRAME_INFO_DTYPE = np.dtype([("div_b", "<i4", 3), ("min_b", "<i4", 3), ("subdiv_b", "<i4", 3), ("status", "<i4"),
+                             ("n_valid", "<i8"), ("n_occ", "<i8")])
 S_MODE = {"S_MODE_%d" % (i + 1): i for i in range(6)}
 DIM_C3HLAC_981_1_3_ALL = 981
 DIM_C3HLAC_117_1_3_ALL = 117
@@ -294,6 +296,43 @@ class Context:
         if not stream:  # the context holds the last frame's grid, features and search
             self._refresh()
         return nm
+
+    def run_point_frames(self, frames, leaf, canvas, variant, thr, subdiv, ranges, exist_threshold, rotate=True,
+                         d_out=None, z_limit=float("inf"), offset=(0, 0, 0), lut_double=True):
+        """c3h_run_point_frames: frames = list of (n, 4) float32 point clouds, all numpy host
+        arrays (pinned or not) or all torch device tensors; d_out = device pointer (int) or
+        tensor of len(frames) * M * rank records.  Returns (modes, info) with info a numpy
+        structured array (div_b, min_b, subdiv_b, status, n_valid, n_occ) per frame."""
+        on_dev = hasattr(frames[0], "data_ptr") if len(frames) else False
+        keep = []
+        ptrs = np.zeros(len(frames), np.uint64)
+        ns = np.zeros(len(frames), np.int64)
+        for i, fr in enumerate(frames):
+            if on_dev:
+                assert fr.is_contiguous() and fr.shape[-1] == 4
+                ptrs[i] = fr.data_ptr()
+            else:
+                fr = np.ascontiguousarray(fr, dtype=np.float32)
+                assert fr.ndim == 2 and fr.shape[1] == 4
+                keep.append(fr)
+                ptrs[i] = fr.ctypes.data
+            ns[i] = fr.shape[0]
+        p = _capi.ExtractParams()
+        p.variant = int(variant)
+        p.thr = (C.c_int32 * 3)(*[int(t) for t in thr])
+        p.subdiv = int(subdiv)
+        p.offset = (C.c_int32 * 3)(*[int(o) for o in offset])
+        p.lut_double = int(bool(lut_double))
+        info = (_capi.FrameInfo * max(len(frames), 1))()
+        nm = self._chk(self.lib.c3h_run_point_frames(self.h, ptr(ptrs), ptr(ns), len(frames), int(on_dev),
+                                                     float(leaf), float(z_limit), i32x3(canvas), C.byref(p),
+                                                     i32x3(ranges), int(exist_threshold), int(bool(rotate)),
+                                                     ptr(d_out), info), "run_point_frames")
+        out = np.zeros(len(frames), FRAME_INFO_DTYPE)
+        for i in range(len(frames)):
+            r = info[i]
+            out[i] = (tuple(r.div_b), tuple(r.min_b), tuple(r.subdiv_b), r.status, r.n_valid, r.n_occ)
+        return nm, out
 
     def _refresh(self):
         """Re-read the grid / feature state the library holds (after run_frames)."""

@@ -44,6 +44,11 @@ class Det(C.Structure):
                 ("mode", C.c_int32)]
 
 
+class FrameInfo(C.Structure):
+    _fields_ = [("div_b", C.c_int32 * 3), ("min_b", C.c_int32 * 3), ("subdiv_b", C.c_int32 * 3),
+                ("status", C.c_int32), ("n_valid", C.c_int64), ("n_occ", C.c_int64)]
+
+
 DET_DTYPE = np.dtype([("score", "<f8"), ("x", "<i4"), ("y", "<i4"), ("z", "<i4"), ("mode", "<i4")])
 assert DET_DTYPE.itemsize == C.sizeof(Det)
 
@@ -86,6 +91,9 @@ _SIGS = {
     "c3h_stream_frames": (C.c_int, [_P, _P, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_float,
                                     C.POINTER(ExtractParams), C.POINTER(C.c_int32), C.c_int32, C.c_int32, _P]),
     "c3h_stream_flush": (C.c_int, [_P]),
+    "c3h_run_point_frames": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int, C.c_float, C.c_float, C.POINTER(C.c_int32),
+                                       C.POINTER(ExtractParams), C.POINTER(C.c_int32), C.c_int32, C.c_int32, _P,
+                                       _P]),
     "c3h_set_lanes": (C.c_int, [_P, C.c_int32]),
     "c3h_set_batch": (C.c_int, [_P, C.c_int32]),
     "c3h_set_pipeline": (C.c_int, [_P, C.c_int32]),

@@ -140,6 +140,45 @@ hipError_t launch_leaf_layout(const uint32_t* grid, int64_t nvox, int32_t* leaf,
 #endif
 constexpr int kMaxBatch = C3H_MAX_BATCH;  // frames per launch (blockIdx.y) in c3h_run_frames
 
+// ---- batched voxeliser (c3h_run_point_frames, voxelize.hip) --------------------------
+// Frames of one batch are voxelised together, each into a fixed "canvas" grid of C^3 words
+// placed at the frame's own min_b (canvas index = cell - min_b, so subdivisions, neighbours
+// and box positions are the frame's own).  Per frame a toroidal accumulator of C^3 entries
+// (cell coordinates mod C) replaces the hash table: cells of a frame whose extent fits the
+// canvas never collide.  Per-frame results the host reads back once per call:
+struct VoxFrameRec {
+  int32_t min_b[3], max_b[3];
+  int32_t sb[3];        // the frame's own getSubdivNum (the gate's position limits)
+  uint32_t n_valid, n_occ;
+  uint32_t flagged;     // voxels whose centroid may round across their cell boundary
+  uint32_t err;         // bit 0: cell coordinates beyond +-2^20; bit 1: extent beyond the canvas
+  uint32_t pad;
+};
+struct VoxBatchArgs {
+  int nf, total;                      // frames, accumulate blocks of this batch
+  int prev_nf, prev_total;            // the previous batch on this buffer set (its words to clear)
+  const float4* pts[kMaxBatch];
+  int64_t n[kMaxBatch];
+  int blk0[kMaxBatch + 1];            // accumulate blocks of frame f: [blk0[f], blk0[f+1])
+  int prev_blk0[kMaxBatch + 1];
+  float inv, leaf, z_limit;
+  int C[3];
+  int subdiv, off[3];
+  float inv_s;
+  unsigned long long* accA;           // [frame][C^3] count << 40 | sum r
+  unsigned long long* accB;           //                sum b << 32 | sum g
+  uint32_t* accM;                     //                min boundary margin (float bits), ~0 = none
+  int64_t s_acc;
+  uint32_t* vlist;                    // [block][chunk] accumulator entries first touched by the block
+  uint32_t* wlist;                    // [block][chunk] canvas words the scatter wrote (this set)
+  int32_t* part;                      // [block][kPartW] partial records (this set)
+  uint32_t* grid[kMaxBatch];          // canvas grids of this set's frame slots (all slots)
+  VoxFrameRec* info;                  // [nf]
+  int32_t* lim;                       // [nf][4]: the frame's subdivisions per axis (0 = none)
+};
+int vb_chunk();  // points per accumulate block
+hipError_t launch_vox_batch(const VoxBatchArgs& a, hipStream_t s);
+
 struct C3Launch {
   const uint32_t* grid[kMaxBatch];  // one grid per frame of the batch
   int nframes;
@@ -278,6 +317,10 @@ struct SparseSearch {
   int score_mfma = 0;      // project on the matrix cores (score_mfma_kernel; needs gbox, nframes 1)
   const _Float16* qt16 = nullptr;  // fp16 search precision: the basis as f16, [Opad][16 * Kq16]
   int Kq16 = 0;                    // 16-wide k steps (D rounded up to 16, / 16)
+  // canvas frames (c3h_run_point_frames): per frame its own subdivision counts; a box
+  // position passes only when it lies inside them (search.cpp:218-317 over the frame's
+  // subdiv_b), so the canvas' extra empty subdivisions add no position
+  const int32_t* lim = nullptr;    // [frame][4] (nullable)
 };
 bool score_mfma_ok(int D);  // D fits score_mfma_kernel
 // sparse compress fused into the gate launch (nullable in launch_sparse_search)
@@ -485,6 +528,23 @@ struct c3h_ctx {
     int32_t range[3], thr, rotate, batch, rank;
     uint64_t setup_version;
   };
+  // points-in batches (c3h_run_point_frames).  Per buffer set: the canvas grids of its frame
+  // slots, the words its last batch wrote (cleared by the next batch on the set), the
+  // partial records and the gate limits.  Shared (the calling context): the toroidal
+  // accumulators, the voxel lists, host-point staging, the frames' records.
+  c3h::DevBuf<uint32_t> pb_grid, pb_wlist;
+  c3h::DevBuf<int32_t> pb_part, pb_lim;
+  int64_t pb_cvox = 0;             // canvas voxels per slot the set's buffers hold
+  int pb_slots = 0;
+  int pb_prev_nf = 0, pb_prev_total = 0;
+  std::vector<int> pb_prev_blk0;
+  c3h::DevBuf<unsigned long long> pb_accA, pb_accB;
+  c3h::DevBuf<uint32_t> pb_accM, pb_vlist;
+  int64_t pb_acc_vox = 0;
+  int pb_acc_slots = 0;
+  c3h::DevBuf<float> pb_stage;
+  c3h::DevBuf<c3h::VoxFrameRec> pb_info;
+
   std::vector<PipeBatch> pipe;   // in flight, oldest first
   uint64_t pipe_seq = 0;
   PipeKey pipe_key{};

@@ -700,6 +700,16 @@ void c3h_destroy(c3h_ctx* ctx) {
   release(ctx->prof);
   release(ctx->chist);
   release(ctx->qt16);
+  release(ctx->pb_grid);
+  release(ctx->pb_wlist);
+  release(ctx->pb_part);
+  release(ctx->pb_lim);
+  release(ctx->pb_accA);
+  release(ctx->pb_accB);
+  release(ctx->pb_accM);
+  release(ctx->pb_vlist);
+  release(ctx->pb_stage);
+  release(ctx->pb_info);
   for (int s = 0; s < C3H_NTIMERS; ++s)
     for (auto& e : ctx->timer.pending[s]) ctx->timer.pool.push_back({e.a, e.b});
   for (auto& e : ctx->timer.pool) {
@@ -1934,7 +1944,7 @@ int pipe_quiesce(c3h_ctx* ctx) {
 // Returns > 0 (modes searched), 0 when the configuration does not fit the tick (only
 // possible for the first batch of a stream: the caller then runs the lanes), < 0 on error.
 int pipe_push(c3h_ctx* ctx, const uint32_t* const* grids, c3h_det* const* outs, int nb,
-              const c3h_ctx::PipeKey& k) {
+              const c3h_ctx::PipeKey& k, const int32_t* lim = nullptr) {
   c3h_ctx* c = pipe_set(ctx, ctx->pipe_seq);
   c->capture = true;
   c->cap_c3_valid = c->cap_search_valid = false;
@@ -1942,6 +1952,7 @@ int pipe_push(c3h_ctx* ctx, const uint32_t* const* grids, c3h_det* const* outs, 
   if (rc == C3H_OK) rc = extract_frames(c, grids, nb, &k.p, nullptr, nullptr);
   if (rc == C3H_OK) rc = search_frames(c, nb, k.range, k.thr, k.rotate, outs, 2);
   c->capture = false;
+  c->cap_q.lim = lim;  // canvas frames: each frame's own subdivisions bound its positions
   if (rc < 0) {
     if (c != ctx) ctx->err = c->err;
     return rc;
@@ -2123,6 +2134,231 @@ int c3h_stream_flush(c3h_ctx* ctx) {
   if (!ctx) return C3H_ERR_ARG;
   HIPCHK(hipSetDevice(ctx->device));
   return pipe_flush(ctx);
+}
+
+}  // extern "C"
+
+namespace {
+
+// One frame on the single-frame path (c3h_voxelize + c3h_extract + search from the setRank
+// state) into d_out_f: the frames c3h_run_point_frames' canvas cannot reproduce exactly.
+int point_frame_single(c3h_ctx* ctx, const float* pts, int64_t n, int on_device, float leaf, float z_limit,
+                       const c3h_extract_params* p, const int32_t range[3], int32_t thr, int32_t rotate,
+                       c3h_det* d_out_f, c3h_frame_info* fi) {
+  const size_t per_frame = (size_t)std::max(ctx->M, 1) * ctx->rank;
+  HIPCHK(hipMemsetAsync(d_out_f, 0, per_frame * sizeof(c3h_det), ctx->stream));  // fresh lists
+  c3h_grid_info gi{};
+  int rc = c3h_voxelize(ctx, pts, n, on_device, leaf, z_limit, &gi);
+  int32_t sb[3] = {0, 0, 0};
+  if (rc == C3H_OK) rc = extract_frames(ctx, &ctx->grid_ptr, 1, p, sb, nullptr);
+  if (rc == C3H_OK) rc = search_frames(ctx, 1, range, thr, rotate, &d_out_f, 2);
+  if (fi) {
+    memset(fi, 0, sizeof(*fi));
+    if (rc >= 0) {
+      for (int a = 0; a < 3; ++a) {
+        fi->div_b[a] = gi.div_b[a];
+        fi->min_b[a] = gi.min_b[a];
+        fi->subdiv_b[a] = sb[a];
+      }
+      fi->n_valid = gi.n_valid;
+      fi->n_occ = gi.n_occ;
+    }
+    fi->status = rc >= 0 ? 1 : rc;
+  }
+  return rc < 0 ? rc : C3H_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n, int32_t nframes, int on_device,
+                         float leaf, float z_limit, const int32_t canvas[3], const c3h_extract_params* p,
+                         const int32_t range[3], int32_t exist_threshold, int32_t rotate, c3h_det* d_out,
+                         c3h_frame_info* info) {
+  if (!ctx || !pts || !n || nframes < 0 || !canvas || !p || !range || !d_out || !(leaf > 0)) return C3H_ERR_ARG;
+  if (!ctx->have_setup) return fail(ctx, C3H_ERR_STATE, "c3h_run_point_frames: no axes (call c3h_search_setup)");
+  for (int i = 0; i < nframes; ++i)
+    if (n[i] < 0 || (n[i] > 0 && !pts[i]) || n[i] >= ((int64_t)1 << 24))
+      return fail(ctx, C3H_ERR_ARG, "c3h_run_point_frames: frame point counts must be in [0, 16,777,215]");
+  if (p->variant != 981 && p->variant != 117) return fail(ctx, C3H_ERR_ARG, "c3h_run_point_frames: variant");
+  int64_t cvox = 1;
+  for (int a = 0; a < 3; ++a) {
+    if (canvas[a] < 1) return fail(ctx, C3H_ERR_ARG, "c3h_run_point_frames: canvas dims must be >= 1");
+    cvox *= canvas[a];
+  }
+  if (cvox > 2147483647LL) return fail(ctx, C3H_ERR_RANGE, "c3h_run_point_frames: canvas beyond int32 voxel indices");
+  HIPCHK(hipSetDevice(ctx->device));
+  {
+    int rc = pipe_flush(ctx);  // an open frame stream completes first
+    if (rc != C3H_OK) return rc;
+  }
+  if (nframes == 0) return 0;
+  const size_t per_frame = (size_t)std::max(ctx->M, 1) * ctx->rank;
+  std::vector<c3h_frame_info> fi((size_t)nframes);
+  std::vector<char> redo((size_t)nframes, 1);
+  int nm = 0;
+  // canvas subdivisions: a frame with one subdivision where the canvas has several takes the
+  // single-frame path (computeC3HLAC's hist_num == 1 rule puts every voxel in histogram 0)
+  bool canvas_multi = false;
+  if (p->subdiv > 0) {
+    const float inv_s = 1.0 / p->subdiv;
+    int64_t hn = 1;
+    for (int a = 0; a < 3; ++a) hn *= canvas[a] > p->offset[a] ? (int64_t)ceilf((canvas[a] - p->offset[a]) * inv_s) : 0;
+    canvas_multi = hn > 1;
+  }
+  const bool batched = pipelinable(ctx) && p->subdiv >= 0 && p->thr[0] >= 0 && p->thr[1] >= 0 && p->thr[2] >= 0;
+  if (batched) {
+    const int B = std::max(1, std::min(ctx->nbatch, c3h::kMaxBatch));
+    const int nchunks = (nframes + B - 1) / B;
+    const int chunk = c3h::vb_chunk();
+    int rc = ensure_lanes(ctx, kPipeDepth - 1);
+    if (rc != C3H_OK) return rc;
+    const int32_t zero[3] = {0, 0, 0};
+    const c3h_ctx::PipeKey k = pipe_key(ctx, canvas, zero, leaf, p, range, exist_threshold, rotate, B);
+    // shared: toroidal accumulators (one per frame slot; the scatter returns them to zero),
+    // voxel lists, the frames' records, host staging
+    if (ctx->pb_acc_vox != cvox || ctx->pb_acc_slots < B) {
+      ENSURE(ctx->pb_accA, (size_t)B * cvox);
+      ENSURE(ctx->pb_accB, (size_t)B * cvox);
+      ENSURE(ctx->pb_accM, (size_t)B * cvox);
+      HIPCHK(hipMemsetAsync(ctx->pb_accA.p, 0, (size_t)B * cvox * 8, ctx->stream));
+      HIPCHK(hipMemsetAsync(ctx->pb_accB.p, 0, (size_t)B * cvox * 8, ctx->stream));
+      HIPCHK(hipMemsetAsync(ctx->pb_accM.p, 0xff, (size_t)B * cvox * 4, ctx->stream));
+      ctx->pb_acc_vox = cvox;
+      ctx->pb_acc_slots = B;
+    }
+    ENSURE(ctx->pb_info, (size_t)nframes);
+    PipeScope scope(ctx);
+    for (int ch = 0; ch < nchunks && rc >= 0; ++ch) {
+      const int f0 = ch * B, nb = std::min(B, nframes - f0);
+      c3h_ctx* c = pipe_set(ctx, ctx->pipe_seq);
+      c3h::VoxBatchArgs va{};
+      va.nf = nb;
+      int64_t npts_batch = 0;
+      va.blk0[0] = 0;
+      for (int j = 0; j < nb; ++j) {  // every frame at least one block: it publishes the record
+        va.n[j] = n[f0 + j];
+        va.blk0[j + 1] = va.blk0[j] + (int)std::max<int64_t>(1, (n[f0 + j] + chunk - 1) / chunk);
+        npts_batch += n[f0 + j];
+      }
+      va.total = va.blk0[nb];
+      // this set's buffers; a reallocation loses the previous batch's word lists, so the
+      // canvas grids are then zeroed whole
+      const int blk_cap = (int)std::min<int64_t>(c->pb_part.n / c3h::vox_part_words(), INT_MAX);
+      if (c->pb_cvox != cvox || c->pb_slots < B || blk_cap < va.total) {
+        const int bc = std::max(va.total, blk_cap);
+        ENSURE(c->pb_grid, (size_t)B * cvox);
+        ENSURE(c->pb_lim, (size_t)B * 4);
+        ENSURE(c->pb_part, (size_t)bc * c3h::vox_part_words());
+        ENSURE(c->pb_wlist, (size_t)bc * chunk);
+        HIPCHK(hipMemsetAsync(c->pb_grid.p, 0, (size_t)B * cvox * 4, ctx->stream));
+        c->pb_cvox = cvox;
+        c->pb_slots = B;
+        c->pb_prev_total = 0;
+        c->pb_prev_nf = 0;
+      }
+      ENSURE(ctx->pb_vlist, (size_t)va.total * chunk);
+      va.prev_nf = c->pb_prev_nf;
+      va.prev_total = c->pb_prev_total;
+      for (int j = 0; j <= c3h::kMaxBatch; ++j)
+        va.prev_blk0[j] = j < (int)c->pb_prev_blk0.size() ? c->pb_prev_blk0[j] : va.prev_total;
+      if (on_device) {
+        for (int j = 0; j < nb; ++j) va.pts[j] = reinterpret_cast<const float4*>(pts[f0 + j]);
+      } else {  // host frames: one staging copy per batch, ordered on the stream
+        ENSURE(ctx->pb_stage, (size_t)std::max<int64_t>(npts_batch, 1) * 4);
+        int64_t o = 0;
+        for (int j = 0; j < nb; ++j) {
+          va.pts[j] = reinterpret_cast<const float4*>(ctx->pb_stage.p + 4 * o);
+          if (n[f0 + j] > 0)
+            HIPCHK(hipMemcpyAsync(ctx->pb_stage.p + 4 * o, pts[f0 + j], (size_t)n[f0 + j] * 16,
+                                  hipMemcpyHostToDevice, ctx->stream));
+          o += n[f0 + j];
+        }
+      }
+      va.inv = 1.0f / leaf;
+      va.leaf = leaf;
+      va.z_limit = z_limit;
+      for (int a = 0; a < 3; ++a) {
+        va.C[a] = canvas[a];
+        va.off[a] = p->subdiv > 0 ? p->offset[a] : 0;
+      }
+      va.subdiv = p->subdiv;
+      va.inv_s = p->subdiv > 0 ? (float)(1.0 / p->subdiv) : 0.0f;
+      va.accA = ctx->pb_accA.p;
+      va.accB = ctx->pb_accB.p;
+      va.accM = ctx->pb_accM.p;
+      va.s_acc = cvox;
+      va.vlist = ctx->pb_vlist.p;
+      va.wlist = c->pb_wlist.p;
+      va.part = c->pb_part.p;
+      // every slot of the set: the previous batch on it may have had more frames than this one
+      for (int j = 0; j < c3h::kMaxBatch; ++j)
+        va.grid[j] = j < c->pb_slots ? c->pb_grid.p + (size_t)j * cvox : nullptr;
+      if (va.prev_nf > c->pb_slots || va.nf > c->pb_slots)
+        return fail(ctx, C3H_ERR_STATE, "c3h_run_point_frames: internal: frame slots");
+      va.info = ctx->pb_info.p + f0;
+      va.lim = c->pb_lim.p;
+      {
+        Timed t(ctx, 0, nb);
+        HIPCHK(c3h::launch_vox_batch(va, ctx->stream));
+      }
+      c->pb_prev_nf = nb;
+      c->pb_prev_total = va.total;
+      c->pb_prev_blk0.assign(va.blk0, va.blk0 + nb + 1);
+      const uint32_t* grids[c3h::kMaxBatch];
+      c3h_det* outs[c3h::kMaxBatch];
+      for (int j = 0; j < nb; ++j) {
+        grids[j] = c->pb_grid.p + (size_t)j * cvox;
+        outs[j] = d_out + (size_t)(f0 + j) * per_frame;
+      }
+      rc = pipe_push(ctx, grids, outs, nb, k, c->pb_lim.p);
+      if (rc == 0) rc = fail(ctx, C3H_ERR_STATE, "c3h_run_point_frames: the canvas does not fit the pipeline");
+      if (rc > 0) nm = rc;
+    }
+    while (rc >= 0 && !ctx->pipe.empty()) {
+      const int trc = pipe_tick(ctx, nullptr);
+      if (trc != C3H_OK) rc = trc;
+    }
+    if (rc < 0) {
+      ctx->pipe.clear();
+      return rc;
+    }
+    std::vector<c3h::VoxFrameRec> recs((size_t)nframes);
+    HIPCHK(hipMemcpyAsync(recs.data(), ctx->pb_info.p, recs.size() * sizeof(c3h::VoxFrameRec), hipMemcpyDeviceToHost,
+                          ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    for (int i = 0; i < nframes; ++i) {
+      const c3h::VoxFrameRec& r = recs[i];
+      c3h_frame_info& o = fi[i];
+      bool one = true;
+      for (int a = 0; a < 3; ++a) {
+        o.min_b[a] = r.min_b[a];
+        o.div_b[a] = r.max_b[a] - r.min_b[a] + 1;
+        o.subdiv_b[a] = r.sb[a];
+        one = one && r.sb[a] == 1;
+      }
+      o.n_valid = r.n_valid;
+      o.n_occ = r.n_occ;
+      o.status = 0;
+      const bool hist1_mismatch = p->subdiv > 0 && canvas_multi && one;
+      const bool empty_sub = p->subdiv > 0 && (r.sb[0] == 0 || r.sb[1] == 0 || r.sb[2] == 0);
+      redo[i] = (r.err || r.flagged || r.n_valid == 0 || hist1_mismatch || empty_sub) ? 1 : 0;
+    }
+  }
+  for (int i = 0; i < nframes; ++i) {
+    if (!redo[i]) continue;
+    int rc = point_frame_single(ctx, pts[i], n[i], on_device, leaf, z_limit, p, range, exist_threshold, rotate,
+                                d_out + (size_t)i * per_frame, &fi[i]);
+    if (rc == C3H_ERR_HIP || rc == C3H_ERR_NOMEM) return rc;  // device trouble ends the call
+  }
+  if (!batched) {  // the modes the search schedules (search.cpp:384-417)
+    int modes[6];
+    nm = mode_schedule(range[0], range[1], range[2], rotate, modes);
+  }
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (info) memcpy(info, fi.data(), fi.size() * sizeof(c3h_frame_info));
+  return nm;
 }
 
 int c3h_set_pipeline(c3h_ctx* ctx, int32_t enable) {

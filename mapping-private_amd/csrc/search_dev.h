@@ -471,6 +471,10 @@ __device__ __forceinline__ void gate_body(const SparseSearch& a, int bid, int64_
       for (int dy = 0; dy < md.yr; ++dy)
         for (int dx = 0; dx < md.xr; ++dx) e += fexist[h + dz * xyn + dy * a.xn + dx];
     pass = e > a.thr;
+    if (a.lim) {  // a canvas frame: the position must lie inside the frame's own subdivisions
+      const int32_t* L = a.lim + 4 * f;
+      pass = pass && x + md.xr <= L[0] && y + md.yr <= L[1] && z + md.zr <= L[2];
+    }
     entry = ((int64_t)mi << 40) | p;
     if (!pass)
       for (int m = 0; m < a.M; ++m) fscores[md.offset + (int64_t)m * md.P + p] = -1.0;

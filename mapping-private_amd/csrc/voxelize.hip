@@ -620,7 +620,301 @@ int grid_for(int64_t n, int cap = 4096) {
   return (int)(g > cap ? cap : g);
 }
 
+// ---- batched voxeliser (c3h_run_point_frames) ----------------------------------------
+// Two launches per batch of frames, no host round trip:
+//   voxb_accum   block b = (frame f, chunk of kBChunk consecutive points): first it clears
+//                the canvas words the previous batch on this buffer set wrote through its
+//                own segment b (read before this block rewrites the segment's record);
+//                then per point (limitPoint + VoxelGrid quantisation as vox_accum) an LDS
+//                hash insert keyed by the cell's toroidal index (x mod C, y mod C, z mod C);
+//                the flush adds each (block, voxel) total into the frame's toroidal
+//                accumulator with one returning atomic (count 0 before = first touch: the
+//                entry goes to the block's segment of the voxel list) and one plain one.
+//   voxb_scatter block b reduces its frame's partial records (bounds, counts), then turns
+//                its segment's entries into canvas words -- canvas index = cell - min_b,
+//                with cell = min_b + ((t - min_b) mod C) per axis, exact whenever the
+//                frame's extent fits the canvas -- clears the accumulator entries and
+//                records the words for the next batch's clear.  Block 0 of a frame
+//                publishes its VoxelGrid geometry and getSubdivNum (the gate's limits).
+#ifndef C3H_VB_CHUNK
+#define C3H_VB_CHUNK 4096
+#endif
+#ifndef C3H_VB_THREADS
+#define C3H_VB_THREADS 1024
+#endif
+#ifndef C3H_VB_SLOTS
+#define C3H_VB_SLOTS 2048
+#endif
+constexpr int kBChunk = C3H_VB_CHUNK;
+constexpr int kBT = C3H_VB_THREADS;
+constexpr int kBPer = kBChunk / kBT;
+constexpr int kBSlots = C3H_VB_SLOTS;
+static_assert(kBChunk % kBT == 0 && (kBSlots & (kBSlots - 1)) == 0, "batch voxeliser shape");
+constexpr uint32_t kNoT = 0xffffffffu;
+
+__device__ __forceinline__ int vb_frame(const int* blk0, int nf, int b) {
+  int lo = 0, hi = nf;  // blk0[lo] <= b < blk0[hi]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (blk0[mid] <= b) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ int vb_mod(int v, int c) {
+  const int m = v % c;
+  return m < 0 ? m + c : m;
+}
+
+__global__ __launch_bounds__(kBT) void voxb_accum_kernel(VoxBatchArgs a) {
+  __shared__ uint32_t s_key[kBSlots];
+  __shared__ unsigned long long s_A[kBSlots];  // count << 40 | sum r
+  __shared__ unsigned long long s_B[kBSlots];  // sum b << 32 | sum g
+  __shared__ uint32_t s_m[kBSlots];
+  __shared__ uint32_t s_nnew;
+  __shared__ int s_red[kBT / 64][8];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x;
+  int32_t* pr = a.part + (size_t)b * kPartW;
+  if (b < a.prev_total) {  // the previous batch's canvas words of segment b
+    const int fp = vb_frame(a.prev_blk0, a.prev_nf, b);
+    const int nn = pr[kPNew];
+    uint32_t* g = a.grid[fp];
+    const uint32_t* wl = a.wlist + (size_t)b * kBChunk;
+    for (int i = tid; i < nn; i += kBT) g[wl[i]] = 0u;
+  }
+  if (b >= a.total) return;  // clearing only
+  const int f = vb_frame(a.blk0, a.nf, b);
+  const int64_t base = (int64_t)(b - a.blk0[f]) * kBChunk;
+  const float4* __restrict__ pts = a.pts[f];
+  const int64_t n = a.n[f];
+  const int Cx = a.C[0], Cy = a.C[1], Cz = a.C[2];
+  unsigned long long* __restrict__ A = a.accA + f * a.s_acc;
+  unsigned long long* __restrict__ B = a.accB + f * a.s_acc;
+  uint32_t* __restrict__ Mg = a.accM + f * a.s_acc;
+  uint32_t* __restrict__ vl = a.vlist + (size_t)b * kBChunk;
+  for (int s = tid; s < kBSlots; s += kBT) {
+    s_key[s] = kNoT;
+    s_A[s] = 0;
+    s_B[s] = 0;
+    s_m[s] = kNoMargin;
+  }
+  if (tid == 0) s_nnew = 0;
+  if (base == 0 && tid == 0) a.info[f].flagged = 0;  // the scatter adds its flags
+  __syncthreads();
+  int mn[3] = {INT_MAX, INT_MAX, INT_MAX}, mx[3] = {INT_MIN, INT_MIN, INT_MIN};
+  int nv = 0;
+  bool err = false;
+  auto add_global = [&](uint32_t t, unsigned long long va, unsigned long long vb, uint32_t m) {
+    const unsigned long long old = atomicAdd(A + t, va);
+    if ((old >> 40) == 0) vl[atomicAdd(&s_nnew, 1u)] = t;
+    atomicAdd(B + t, vb);
+    if (m < kMarginFlush) atomicMin(Mg + t, m);
+  };
+  float4 p[kBPer];
+#pragma unroll
+  for (int j = 0; j < kBPer; ++j) {  // every load of the chunk in flight together
+    const int64_t i = base + j * kBT + tid;
+    if (i < n) {
+      const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(pts) + i);
+      p[j] = make_float4(v.x, v.y, v.z, v.w);
+    } else {
+      p[j] = make_float4(NAN, NAN, NAN, 0.0f);
+    }
+  }
+  VoxArgs q{};  // point_cell's quantisation parameters
+  q.inv = a.inv;
+#pragma unroll
+  for (int j = 0; j < kBPer; ++j) {
+    if (!point_valid(p[j], a.z_limit)) continue;
+    int c[3];
+    float margin;
+    if (!point_cell(q, p[j], c, &margin)) {
+      err = true;
+      continue;
+    }
+    ++nv;
+#pragma unroll
+    for (int ax = 0; ax < 3; ++ax) {
+      mn[ax] = min(mn[ax], c[ax]);
+      mx[ax] = max(mx[ax], c[ax]);
+    }
+    const uint32_t t = (uint32_t)vb_mod(c[0], Cx) +
+                       (uint32_t)Cx * ((uint32_t)vb_mod(c[1], Cy) + (uint32_t)Cy * (uint32_t)vb_mod(c[2], Cz));
+    const uint32_t rgb = __float_as_uint(p[j].w);
+    const uint32_t r = (rgb >> 16) & 0xffu, g = (rgb >> 8) & 0xffu, bl = rgb & 0xffu;
+    const uint32_t mb = __float_as_uint(margin);
+    uint32_t h = (t * 0x9E3779B1u) >> (32 - __builtin_ctz(kBSlots));
+    bool done = false;
+    for (int probe = 0; probe < kLProbe; ++probe) {
+      const uint32_t prev = atomicCAS(&s_key[h], kNoT, t);
+      if (prev == kNoT || prev == t) {
+        atomicAdd(&s_A[h], (1ull << 40) | r);
+        atomicAdd(&s_B[h], ((unsigned long long)bl << 32) | g);
+        if (mb < kMarginFlush) atomicMin(&s_m[h], mb);
+        done = true;
+        break;
+      }
+      h = (h + 1) & (kBSlots - 1);
+    }
+    if (!done) add_global(t, (1ull << 40) | r, ((unsigned long long)bl << 32) | g, mb);  // LDS table full
+  }
+  __syncthreads();
+  for (int s = tid; s < kBSlots; s += kBT) {
+    const uint32_t t = s_key[s];
+    if (t != kNoT) add_global(t, s_A[s], s_B[s], s_m[s]);
+  }
+#pragma unroll
+  for (int ax = 0; ax < 3; ++ax) {
+    mn[ax] = wave_reduce(mn[ax], [](int x, int y) { return min(x, y); });
+    mx[ax] = wave_reduce(mx[ax], [](int x, int y) { return max(x, y); });
+  }
+  nv = wave_reduce(nv, [](int x, int y) { return x + y; });
+  const int e = wave_reduce(err ? 1 : 0, [](int x, int y) { return x | y; });
+  if (lane == 0) {
+    for (int ax = 0; ax < 3; ++ax) {
+      s_red[w][ax] = mn[ax];
+      s_red[w][3 + ax] = mx[ax];
+    }
+    s_red[w][6] = nv;
+    s_red[w][7] = e;
+  }
+  __syncthreads();
+  if (tid < 8) {
+    int v = s_red[0][tid];
+    for (int i = 1; i < kBT / 64; ++i) {
+      const int u = s_red[i][tid];
+      v = tid < 3 ? min(v, u) : (tid < 6 ? max(v, u) : (tid == 6 ? v + u : (v | u)));
+    }
+    pr[tid < 7 ? tid : kPErr] = v;
+  }
+  if (tid == 8) pr[kPNew] = (int)s_nnew;
+}
+
+__global__ __launch_bounds__(kBlock) void voxb_scatter_kernel(VoxBatchArgs a) {
+  __shared__ int s_r[kBlock / 64][10];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int f = vb_frame(a.blk0, a.nf, b);
+  // the frame's bounds and totals from its blocks' partial records (a few KB, from L2)
+  int mn[3] = {INT_MAX, INT_MAX, INT_MAX}, mx[3] = {INT_MIN, INT_MIN, INT_MIN};
+  int nv = 0, nn = 0, er = 0;
+  for (int q = a.blk0[f] + tid; q < a.blk0[f + 1]; q += kBlock) {
+    const int32_t* r = a.part + (size_t)q * kPartW;
+    if (r[kPValid]) {
+      for (int ax = 0; ax < 3; ++ax) {
+        mn[ax] = min(mn[ax], r[kPMin + ax]);
+        mx[ax] = max(mx[ax], r[kPMax + ax]);
+      }
+    }
+    nv += r[kPValid];
+    nn += r[kPNew];
+    er |= r[kPErr];
+  }
+  for (int ax = 0; ax < 3; ++ax) {
+    mn[ax] = wave_reduce(mn[ax], [](int x, int y) { return min(x, y); });
+    mx[ax] = wave_reduce(mx[ax], [](int x, int y) { return max(x, y); });
+  }
+  nv = wave_reduce(nv, [](int x, int y) { return x + y; });
+  nn = wave_reduce(nn, [](int x, int y) { return x + y; });
+  er = wave_reduce(er, [](int x, int y) { return x | y; });
+  const int w = tid >> 6;
+  if ((tid & 63) == 0) {
+    for (int ax = 0; ax < 3; ++ax) {
+      s_r[w][ax] = mn[ax];
+      s_r[w][3 + ax] = mx[ax];
+    }
+    s_r[w][6] = nv;
+    s_r[w][7] = nn;
+    s_r[w][8] = er;
+  }
+  __syncthreads();
+  int lo[3], dv[3], tv = 0, tn = 0, te = 0;
+  for (int ax = 0; ax < 3; ++ax) {
+    int l = s_r[0][ax], h = s_r[0][3 + ax];
+    for (int i = 1; i < kBlock / 64; ++i) {
+      l = min(l, s_r[i][ax]);
+      h = max(h, s_r[i][3 + ax]);
+    }
+    lo[ax] = l;
+    dv[ax] = h - l + 1;
+  }
+  for (int i = 0; i < kBlock / 64; ++i) {
+    tv += s_r[i][6];
+    tn += s_r[i][7];
+    te |= s_r[i][8];
+  }
+  const int Cx = a.C[0], Cy = a.C[1], Cz = a.C[2];
+  const bool over = tv > 0 && (dv[0] > Cx || dv[1] > Cy || dv[2] > Cz);
+  if (b == a.blk0[f] && tid == 0) {
+    VoxFrameRec& rec = a.info[f];
+    int sb[3] = {0, 0, 0};
+    if (tv > 0) {
+      if (a.subdiv > 0) {  // setVoxelFilter (c3_hlac.cpp:204-231), float arithmetic as there
+        if (dv[0] > a.off[0] && dv[1] > a.off[1] && dv[2] > a.off[2])
+          for (int ax = 0; ax < 3; ++ax) sb[ax] = (int)ceilf((float)(dv[ax] - a.off[ax]) * a.inv_s);
+      } else {
+        sb[0] = sb[1] = sb[2] = 1;
+      }
+    }
+    for (int ax = 0; ax < 3; ++ax) {
+      rec.min_b[ax] = tv > 0 ? lo[ax] : 0;
+      rec.max_b[ax] = tv > 0 ? lo[ax] + dv[ax] - 1 : -1;
+      rec.sb[ax] = sb[ax];
+      a.lim[4 * f + ax] = (over || te) ? 0 : sb[ax];
+    }
+    a.lim[4 * f + 3] = 0;
+    rec.n_valid = (uint32_t)tv;
+    rec.n_occ = (uint32_t)tn;
+    rec.err = (te ? 1u : 0u) | (over ? 2u : 0u);
+  }
+  if (tv == 0) return;
+  const int nseg = a.part[(size_t)b * kPartW + kPNew];
+  const uint32_t* vl = a.vlist + (size_t)b * kBChunk;
+  uint32_t* wl = a.wlist + (size_t)b * kBChunk;
+  unsigned long long* __restrict__ A = a.accA + f * a.s_acc;
+  unsigned long long* __restrict__ B = a.accB + f * a.s_acc;
+  uint32_t* __restrict__ Mg = a.accM + f * a.s_acc;
+  uint32_t* __restrict__ grid = a.grid[f];
+  uint32_t flagged = 0;
+  for (int i = tid; i < nseg; i += kBlock) {
+    const uint32_t t = vl[i];
+    const unsigned long long va = A[t], vb = B[t];
+    const uint32_t m = Mg[t];
+    A[t] = 0ull;
+    B[t] = 0ull;
+    Mg[t] = kNoMargin;
+    const int tx = (int)(t % (uint32_t)Cx), ty = (int)((t / (uint32_t)Cx) % (uint32_t)Cy),
+              tz = (int)(t / ((uint32_t)Cx * (uint32_t)Cy));
+    const int cx = vb_mod(tx - lo[0], Cx), cy = vb_mod(ty - lo[1], Cy), cz = vb_mod(tz - lo[2], Cz);
+    const uint32_t idx = (uint32_t)cx + (uint32_t)Cx * ((uint32_t)cy + (uint32_t)Cy * (uint32_t)cz);
+    const uint32_t count = (uint32_t)(va >> 40);
+    const float c = (float)count;
+    const uint32_t r = (uint32_t)(int)__fdiv_rn((float)(va & 0xffffffffffull), c);
+    const uint32_t g = (uint32_t)(int)__fdiv_rn((float)(vb & 0xffffffffull), c);
+    const uint32_t bl = (uint32_t)(int)__fdiv_rn((float)(vb >> 32), c);
+    grid[idx] = kOcc | (r << 16) | (g << 8) | bl;
+    wl[i] = idx;
+    // the exact centroid test of vox_scatter_kernel on the absolute cell
+    const int ax_ = lo[0] + cx, ay_ = lo[1] + cy, az_ = lo[2] + cz;
+    const int cmag = max(max(abs(ax_), abs(ay_)), abs(az_)) + 1;
+    const float eps = (float)(count + 4) * (float)cmag * 0x1p-22f;
+    if (__uint_as_float(m) < eps || eps >= __uint_as_float(kMarginFlush)) ++flagged;
+  }
+  flagged = wave_reduce(flagged, [](uint32_t u, uint32_t v) { return u + v; });
+  if ((tid & 63) == 0 && flagged) atomicAdd(&a.info[f].flagged, flagged);
+}
+
 }  // namespace
+
+int vb_chunk() { return kBChunk; }
+
+hipError_t launch_vox_batch(const VoxBatchArgs& a, hipStream_t s) {
+  const int g = std::max(a.total, a.prev_total);
+  if (g > 0) voxb_accum_kernel<<<(unsigned)g, kBT, 0, s>>>(a);
+  if (a.total > 0) voxb_scatter_kernel<<<(unsigned)a.total, kBlock, 0, s>>>(a);
+  return hipGetLastError();
+}
 
 int64_t scan_blocks(int64_t n) { return (n + kScanBlock - 1) / kScanBlock; }
 int64_t leaf_layout_blocks(int64_t nvox) { return scan_blocks(nvox); }

@@ -215,6 +215,91 @@ void ColorThreshold::compute(int threshold[3], double total_average[3]) const {
   for (int i = 0; i < 3; ++i) threshold[i] = t[i];
 }
 
+void getVoxelGrid(VoxelGrid& grid, const std::vector<PointXYZRGBNormal>& input,
+                  std::vector<PointXYZRGBNormal>& output, float voxel_size, float z_limit) {
+  static_assert(sizeof(PointXYZRGBNormal) == 32, "xyzrgb + normal record must be 8 floats");
+  std::vector<PointXYZRGB> xyz(input.size()), cent;
+  for (size_t i = 0; i < input.size(); ++i) xyz[i] = PointXYZRGB{input[i].x, input[i].y, input[i].z, input[i].rgb};
+  getVoxelGrid(grid, xyz, cent, voxel_size, z_limit);
+  output.assign(cent.size(), PointXYZRGBNormal());
+  if (cent.empty()) return;
+  // VoxelGrid::filter averages every float field of the voxel's points: the normal and the
+  // curvature in fp32, input order (the centroid's xyz and colour come from the device)
+  const std::vector<int> layout = grid.getLeafLayout();
+  const Vector3i mn = grid.getMinBoxCoordinates(), dv = grid.getNrDivisions();
+  const float inv = 1.0f / voxel_size;
+  std::vector<float> acc(cent.size() * 4, 0.0f);
+  std::vector<int> cnt(cent.size(), 0);
+  for (const PointXYZRGBNormal& p : input) {
+    if (!std::isfinite(p.x) || !std::isfinite(p.y) || !std::isfinite(p.z) || !(p.z < z_limit)) continue;
+    const int cx = (int)std::floor(p.x * inv) - mn[0], cy = (int)std::floor(p.y * inv) - mn[1],
+              cz = (int)std::floor(p.z * inv) - mn[2];
+    const int o = layout[(size_t)cx + (size_t)dv[0] * ((size_t)cy + (size_t)dv[1] * cz)];
+    float* a = &acc[(size_t)o * 4];
+    a[0] += p.normal_x;
+    a[1] += p.normal_y;
+    a[2] += p.normal_z;
+    a[3] += p.curvature;
+    ++cnt[o];
+  }
+  for (size_t o = 0; o < cent.size(); ++o) {
+    const float c = (float)cnt[o];
+    output[o] = PointXYZRGBNormal{cent[o].x, cent[o].y, cent[o].z, cent[o].rgb, acc[4 * o] / c, acc[4 * o + 1] / c,
+                                  acc[4 * o + 2] / c, acc[4 * o + 3] / c};
+  }
+}
+
+namespace detail {
+
+bool voxel_filter(const VoxelGrid& grid, int subdiv, const int off[3], Vector3i& subdiv_b) {
+  if (subdiv > 0) {
+    const Vector3i div = grid.getNrDivisions();
+    if (div[0] <= off[0] || div[1] <= off[1] || div[2] <= off[2]) {
+      std::cerr << "(In setVoxelFilter) offset values (" << off[0] << "," << off[1] << "," << off[2]
+                << ") exceed voxel grid size (" << div[0] << "," << div[1] << "," << div[2] << ")." << std::endl;
+      return false;
+    }
+    const float inv = 1.0 / subdiv;  // inverse_subdivision_size, float as there
+    for (int a = 0; a < 3; ++a) subdiv_b[a] = (int)std::ceil((div[a] - off[a]) * inv);
+  } else if (subdiv < 0) {
+    std::cerr << "(In setVoxelFilter) Invalid subdivision size: " << subdiv << std::endl;
+    return false;
+  }
+  return true;
+}
+
+int64_t compute_feature(VoxelGrid& grid, int dim, const int thr[3], int subdiv, const int off[3], bool lut_double,
+                        std::vector<float>& flat) {
+  if (thr[0] < 0 || thr[1] < 0 || thr[2] < 0) {  // computeFeature's silent return (c3_hlac.cpp:306-309)
+    std::cerr << "Invalid color_threshold: " << thr[0] << " " << thr[1] << " " << thr[2] << std::endl;
+    flat.clear();
+    return 0;
+  }
+  std::vector<std::vector<float> > rows;
+  extract(grid, dim, rows, thr[0], thr[1], thr[2], grid.leaf(), subdiv, off[0], off[1], off[2], lut_double);
+  flat.resize(rows.size() * (size_t)dim);
+  for (size_t h = 0; h < rows.size(); ++h) std::copy(rows[h].begin(), rows[h].end(), flat.begin() + h * dim);
+  return (int64_t)rows.size();
+}
+
+int64_t grid_occupied(const VoxelGrid& grid) {
+  c3h_grid_info i;
+  grid_info(grid.context(), &i);
+  return i.n_occ;
+}
+
+}  // namespace detail
+
+// the explicit instantiations of c3_hlac.cpp:418-426
+template class C3HLAC117Estimation<PointXYZRGB, C3HLACSignature117>;
+template class C3HLAC117Estimation<PointXYZRGB, C3HLACSignature981>;
+template class C3HLAC981Estimation<PointXYZRGB, C3HLACSignature117>;
+template class C3HLAC981Estimation<PointXYZRGB, C3HLACSignature981>;
+template class C3HLAC117Estimation<PointXYZRGBNormal, C3HLACSignature117>;
+template class C3HLAC117Estimation<PointXYZRGBNormal, C3HLACSignature981>;
+template class C3HLAC981Estimation<PointXYZRGBNormal, C3HLACSignature117>;
+template class C3HLAC981Estimation<PointXYZRGBNormal, C3HLACSignature981>;
+
 Vector3i extractC3HLACSignature981(VoxelGrid& grid, std::vector<std::vector<float> >& feature, int r,
                                    int g, int b, float voxel_size, int subdiv, int ox, int oy, int oz,
                                    bool lut_double) {

@@ -16,6 +16,7 @@
 #ifndef C3HLAC_HOST_H_
 #define C3HLAC_HOST_H_
 
+#include <algorithm>
 #include <cmath>
 #include <limits>
 #include <memory>
@@ -119,6 +120,129 @@ Vector3i extractC3HLACSignature117(VoxelGrid& grid, std::vector<std::vector<floa
 void extractC3HLACSignature117(VoxelGrid& grid, std::vector<float>& feature, int color_threshold_r,
                                int color_threshold_g, int color_threshold_b, float voxel_size,
                                bool lut_double = true);
+
+// ---- the pcl::Feature-style estimators (c3_hlac/include/c3_hlac/c3_hlac.h:42-220) -----
+const int DIM_C3HLAC_981_1_3 = 495;
+const int DIM_C3HLAC_981_BIN_1_3 = 486;
+const int DIM_C3HLAC_981_1_3_ALL = 981;
+const int DIM_C3HLAC_117_1_3 = 63;
+const int DIM_C3HLAC_117_BIN_1_3 = 54;
+const int DIM_C3HLAC_117_1_3_ALL = 117;
+struct C3HLACSignature117 {  // c3_hlac.h:50-53
+  float histogram[117];
+};
+struct C3HLACSignature981 {  // c3_hlac.h:61-64
+  float histogram[981];
+};
+
+// pcl::PointXYZRGBNormal (the estimators' second point type, c3_hlac.cpp:423-426): 8 floats
+// here (x, y, z, rgb bits, normal, curvature; no SSE padding)
+struct PointXYZRGBNormal {
+  float x, y, z, rgb;
+  float normal_x, normal_y, normal_z, curvature;
+};
+// getVoxelGrid for PointXYZRGBNormal clouds: the grid and the centroids' xyz and colour are
+// those of the xyzrgb part (c3h_voxelize); normals and curvature are averaged per voxel in
+// fp32 in input order, as VoxelGrid::filter averages every float field.
+void getVoxelGrid(VoxelGrid& grid, const std::vector<PointXYZRGBNormal>& input,
+                  std::vector<PointXYZRGBNormal>& output, float voxel_size,
+                  float z_limit = std::numeric_limits<float>::infinity());
+
+namespace detail {
+// setVoxelFilter (c3_hlac.cpp:204-231): the offset check and getSubdivNum arithmetic
+bool voxel_filter(const VoxelGrid& grid, int subdiv, const int off[3], Vector3i& subdiv_b);
+// computeFeature (c3_hlac.cpp:303-324, 395-416) on the grid's device context: hist_num rows
+// of `dim` floats (0 rows for the silent-empty cases)
+int64_t compute_feature(VoxelGrid& grid, int dim, const int thr[3], int subdiv, const int off[3],
+                        bool lut_double, std::vector<float>& flat);
+int64_t grid_occupied(const VoxelGrid& grid);  // n_occ of the grid (-1: not from getVoxelGrid)
+}  // namespace detail
+
+// C3HLAC117Estimation<PointT, PointOutT> (c3_hlac.h:79-155): rotation-invariant C3-HLAC of
+// the subdivisions of a voxel grid.  The input cloud is the grid's downsampled cloud (as
+// extractC3HLACSignature117 passes it, c3_hlac_tools.hpp:169-195); the grid on the device
+// already holds its voxels' colours and centroids, so compute() checks the cloud's size
+// against the grid and reads nothing else from it.  Deviations: setVoxelFilter keeps a copy
+// of the VoxelGrid handle, which shares the device grid (re-voxelising into the same
+// VoxelGrid changes what compute() sees); compute() without a successful setVoxelFilter
+// throws; the silent-empty cases (a negative threshold) leave `output` empty where PCL's
+// Feature::compute leaves indices_->size() uninitialised points.
+template <typename PointT, typename PointOutT>
+class C3HLAC117Estimation {
+ public:
+  C3HLAC117Estimation() : feature_name_("C3HLAC117Estimation") {}
+  virtual ~C3HLAC117Estimation() = default;
+  // setColorThreshold (c3_hlac.h:92)
+  void setColorThreshold(int threshold_r, int threshold_g, int threshold_b) {
+    thr_[0] = threshold_r;
+    thr_[1] = threshold_g;
+    thr_[2] = threshold_b;
+  }
+  // setVoxelFilter (c3_hlac.h:102, c3_hlac.cpp:204-231): false when an offset reaches the
+  // grid size or the subdivision size is negative
+  bool setVoxelFilter(const VoxelGrid& grid, int subdivision_size = 0, int offset_x = 0, int offset_y = 0,
+                      int offset_z = 0, float voxel_size = 0.01f) {
+    grid_ = std::make_shared<VoxelGrid>(grid);
+    subdiv_ = subdivision_size;
+    off_[0] = offset_x;
+    off_[1] = offset_y;
+    off_[2] = offset_z;
+    voxel_size_ = voxel_size;
+    filter_ok_ = detail::voxel_filter(grid, subdivision_size, off_, subdiv_b_);
+    return filter_ok_;
+  }
+  Vector3i getSubdivNum() const { return subdiv_b_; }  // c3_hlac.h:105
+  void setInputCloud(const std::vector<PointT>& cloud) { cloud_ = &cloud; }
+  // the radius search extractC3HLACSignature* sets is "not used actually" (c3_hlac_tools.hpp:140-141)
+  void setRadiusSearch(double) {}
+  template <class Tree>
+  void setSearchMethod(const Tree&) {}
+  // setColor's sin/cos evaluation (double = the reference build's, see c3h_extract_params)
+  void setLUTDouble(bool lut_double) { lut_double_ = lut_double; }
+  const std::string& getFeatureName() const { return feature_name_; }
+  // Feature::compute -> computeFeature: one PointOutT per subdivision (hist_num of them)
+  void compute(std::vector<PointOutT>& output) {
+    if (!grid_ || !filter_ok_) throw Error(C3H_ERR_STATE, feature_name_ + "::compute: no valid setVoxelFilter");
+    if (grid_->leaf() != 0.0f && voxel_size_ != grid_->leaf())
+      throw Error(C3H_ERR_ARG, feature_name_ + "::compute: voxel_size differs from the grid's leaf size");
+    const int64_t nocc = detail::grid_occupied(*grid_);
+    if (cloud_ && nocc >= 0 && (int64_t)cloud_->size() != nocc)
+      throw Error(C3H_ERR_ARG, feature_name_ + "::compute: the input cloud is not the grid's downsampled cloud");
+    const int d = dim();
+    if ((size_t)d * sizeof(float) > sizeof(PointOutT))  // c3_hlac.cpp:422 instantiates 981 -> Signature117
+      throw Error(C3H_ERR_ARG, feature_name_ + "::compute: the output type holds fewer than " + std::to_string(d) +
+                                   " floats");
+    std::vector<float> flat;
+    const int64_t hn = detail::compute_feature(*grid_, d, thr_, subdiv_, off_, lut_double_, flat);
+    output.assign((size_t)hn, PointOutT());
+    for (int64_t h = 0; h < hn; ++h) {
+      float* dst = reinterpret_cast<float*>(&output[h]);
+      std::fill(dst, dst + sizeof(PointOutT) / sizeof(float), 0.0f);
+      std::copy(flat.begin() + h * d, flat.begin() + (h + 1) * d, dst);
+    }
+  }
+
+ protected:
+  virtual int dim() const { return DIM_C3HLAC_117_1_3_ALL; }
+  std::string feature_name_;
+  std::shared_ptr<VoxelGrid> grid_;
+  const std::vector<PointT>* cloud_ = nullptr;
+  int thr_[3] = {-1, -1, -1};  // the constructor's -1 (c3_hlac.cpp:178): compute() then returns empty
+  int subdiv_ = 0, off_[3] = {0, 0, 0};
+  float voxel_size_ = 0.0f;
+  bool filter_ok_ = false, lut_double_ = true;
+  Vector3i subdiv_b_;
+};
+
+// C3HLAC981Estimation<PointT, PointOutT> (c3_hlac.h:158-220): rotation-variant, 981 bins
+template <typename PointT, typename PointOutT>
+class C3HLAC981Estimation : public C3HLAC117Estimation<PointT, PointOutT> {
+ public:
+  C3HLAC981Estimation() { this->feature_name_ = "C3HLAC981Estimation"; }
+
+ protected:
+  int dim() const override { return DIM_C3HLAC_981_1_3_ALL; }
+};
 
 // VOSCH / GRSD (color_chlac/include/color_chlac/grsd_colorCHLAC_tools.h:27-32, .hpp:63-296,
 // 832-843) on the grid's cloud: computeNormal (radius normals_radius_search) runs on the

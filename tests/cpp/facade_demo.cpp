@@ -10,6 +10,9 @@
 //   facade_demo train <rows.bin> <out_dir> <D> <n_model> (GPU: pca_scene.cpp + pca_models.cpp)
 //   facade_demo vosch <cloud.pcd> <leaf>                (GPU: example_GRSD_CCHLAC / setVOSCH flow)
 //   facade_demo readdata <F.bin> <N.bin> <dir> <dim>     (GPU: SearchObj::readData + search)
+//   facade_demo estim <param_dir> <cloud.pcd> <out_prefix> (GPU: extract_c3_hlac_scene.cpp's flow
+//                                                        through C3HLAC{981,117}Estimation)
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -227,6 +230,124 @@ static int readdata(const char* fF, const char* fN, const std::string& dir, int 
   return 0;
 }
 
+// color_voxel_recognition/test/extract_c3_hlac_scene.cpp:48-86 with the estimator classes
+// the tool's extractC3HLACSignature981 wraps (c3_hlac_tools.hpp:134-160), for both point
+// types of c3_hlac.cpp:418-426; every path must give the free function's rows.
+template <class PointT>
+static bool same_rows(const std::vector<std::vector<float> >& ref, const std::vector<C3HLACSignature981>& out, int d) {
+  if (ref.size() != out.size()) return false;
+  for (size_t h = 0; h < ref.size(); ++h)
+    for (int i = 0; i < d; ++i)
+      if (ref[h][i] != out[h].histogram[i]) return false;
+  return true;
+}
+
+static int estim(const std::string& pdir, const std::string& pcd, const std::string& prefix) {
+  const std::string pf = pdir + "/parameters.txt", cf = pdir + "/color_threshold.txt";
+  const int subdivision_size = Param::readBoxSizeScene(pf.c_str());
+  const float voxel_size = Param::readVoxelSize(pf.c_str());
+  int thr_r, thr_g, thr_b;
+  Param::readColorThreshold(thr_r, thr_g, thr_b, cf.c_str());
+  VoxelGrid grid(0);
+  grid.setLeafSize(voxel_size, voxel_size, voxel_size);
+  grid.setSaveLeafLayout(true);
+  std::vector<PointXYZRGB> input_cloud, cloud_downsampled;
+  if (loadPCDFile(pcd, input_cloud) != 0) return 2;
+  getVoxelGrid(grid, input_cloud, cloud_downsampled, voxel_size);
+  // the free function (the tool's call)
+  std::vector<std::vector<float> > c3_hlac;
+  const Vector3i sb_free = extractC3HLACSignature981(grid, c3_hlac, thr_r, thr_g, thr_b, voxel_size, subdivision_size);
+  writeFeature((prefix + "_free.pcd").c_str(), c3_hlac);
+  // the estimator, as extractC3HLACSignature981's body constructs it
+  C3HLAC981Estimation<PointXYZRGB, C3HLACSignature981> est;
+  est.setRadiusSearch(0.000000001);  // not used actually
+  est.setColorThreshold(thr_r, thr_g, thr_b);
+  const bool ok = est.setVoxelFilter(grid, subdivision_size, 0, 0, 0, voxel_size);
+  est.setInputCloud(cloud_downsampled);
+  std::vector<C3HLACSignature981> sig;
+  est.compute(sig);
+  std::vector<std::vector<float> > rows(sig.size());
+  for (size_t h = 0; h < sig.size(); ++h) rows[h].assign(sig[h].histogram, sig[h].histogram + DIM_C3HLAC_981_1_3_ALL);
+  writeFeature((prefix + "_estim.pcd").c_str(), rows);
+  const Vector3i sb = est.getSubdivNum();
+  // rotation-invariant 117 into both output types
+  std::vector<std::vector<float> > f117;
+  extractC3HLACSignature117(grid, f117, thr_r, thr_g, thr_b, voxel_size, subdivision_size, 1, 2, 0);
+  C3HLAC117Estimation<PointXYZRGB, C3HLACSignature117> e117;
+  e117.setColorThreshold(thr_r, thr_g, thr_b);
+  e117.setVoxelFilter(grid, subdivision_size, 1, 2, 0, voxel_size);
+  e117.setInputCloud(cloud_downsampled);
+  std::vector<C3HLACSignature117> s117;
+  e117.compute(s117);
+  bool same117 = s117.size() == f117.size();
+  for (size_t h = 0; same117 && h < s117.size(); ++h)
+    same117 = std::equal(f117[h].begin(), f117[h].end(), s117[h].histogram);
+  C3HLAC117Estimation<PointXYZRGB, C3HLACSignature981> e117w;  // wider output: the tail stays zero
+  e117w.setColorThreshold(thr_r, thr_g, thr_b);
+  e117w.setVoxelFilter(grid, subdivision_size, 1, 2, 0, voxel_size);
+  std::vector<C3HLACSignature981> s117w;
+  e117w.compute(s117w);
+  bool wide_ok = s117w.size() == f117.size();
+  for (size_t h = 0; wide_ok && h < s117w.size(); ++h)
+    wide_ok = std::equal(f117[h].begin(), f117[h].end(), s117w[h].histogram) &&
+              std::all_of(s117w[h].histogram + 117, s117w[h].histogram + 981, [](float v) { return v == 0.0f; });
+  bool narrow_throws = false;  // 981 bins do not fit C3HLACSignature117
+  try {
+    C3HLAC981Estimation<PointXYZRGB, C3HLACSignature117> bad;
+    bad.setColorThreshold(thr_r, thr_g, thr_b);
+    bad.setVoxelFilter(grid, subdivision_size);
+    std::vector<C3HLACSignature117> o;
+    bad.compute(o);
+  } catch (const Error& e) {
+    narrow_throws = e.code == C3H_ERR_ARG;
+  }
+  // PointXYZRGBNormal: the same grid and rows; normals averaged per voxel
+  std::vector<PointXYZRGBNormal> in_n(input_cloud.size()), down_n;
+  for (size_t i = 0; i < input_cloud.size(); ++i) {
+    const PointXYZRGB& q = input_cloud[i];
+    in_n[i] = PointXYZRGBNormal{q.x, q.y, q.z, q.rgb, 0.0f, 0.0f, 1.0f, 0.25f};
+  }
+  VoxelGrid grid_n(0);
+  getVoxelGrid(grid_n, in_n, down_n, voxel_size);
+  bool down_same = down_n.size() == cloud_downsampled.size();
+  for (size_t i = 0; down_same && i < down_n.size(); ++i)
+    down_same = down_n[i].x == cloud_downsampled[i].x && down_n[i].y == cloud_downsampled[i].y &&
+                down_n[i].z == cloud_downsampled[i].z && down_n[i].rgb == cloud_downsampled[i].rgb &&
+                down_n[i].normal_z == 1.0f && down_n[i].curvature == 0.25f;
+  C3HLAC981Estimation<PointXYZRGBNormal, C3HLACSignature981> en;
+  en.setColorThreshold(thr_r, thr_g, thr_b);
+  en.setVoxelFilter(grid_n, subdivision_size, 0, 0, 0, voxel_size);
+  en.setInputCloud(down_n);
+  std::vector<C3HLACSignature981> sn;
+  en.compute(sn);
+  // the reference's failure modes: offsets >= the grid -> false; negative threshold -> empty
+  C3HLAC981Estimation<PointXYZRGB, C3HLACSignature981> e2;
+  const Vector3i div = grid.getNrDivisions();
+  const bool off_false = !e2.setVoxelFilter(grid, subdivision_size, div[0], 0, 0, voxel_size);
+  const bool neg_sub_false = !e2.setVoxelFilter(grid, -1);
+  e2.setColorThreshold(-1, 0, 0);
+  e2.setVoxelFilter(grid, subdivision_size, 0, 0, 0, voxel_size);
+  std::vector<C3HLACSignature981> empty;
+  e2.compute(empty);
+  bool unset_throws = false;
+  try {
+    C3HLAC117Estimation<PointXYZRGB, C3HLACSignature117> e3;
+    std::vector<C3HLACSignature117> o;
+    e3.compute(o);
+  } catch (const Error& e) {
+    unset_throws = e.code == C3H_ERR_STATE;
+  }
+  printf("{\"filter_ok\": %d, \"rows\": %zu, \"free_rows\": %zu, \"same981\": %d, \"subdiv\": [%d, %d, %d], "
+         "\"subdiv_free\": [%d, %d, %d], \"same117\": %d, \"rows117\": %zu, \"wide117\": %d, \"narrow_throws\": %d, "
+         "\"normal_down_same\": %d, \"normal_same981\": %d, \"offset_false\": %d, \"negative_subdiv_false\": %d, "
+         "\"negative_thr_empty\": %d, \"unset_throws\": %d, \"name\": \"%s\"}\n",
+         ok, sig.size(), c3_hlac.size(), same_rows<PointXYZRGB>(c3_hlac, sig, DIM_C3HLAC_981_1_3_ALL), sb[0], sb[1], sb[2],
+         sb_free[0], sb_free[1], sb_free[2], same117, s117.size(), wide_ok, narrow_throws, down_same,
+         same_rows<PointXYZRGBNormal>(c3_hlac, sn, DIM_C3HLAC_981_1_3_ALL), off_false, neg_sub_false, empty.empty(),
+         unset_throws, est.getFeatureName().c_str());
+  return 0;
+}
+
 int main(int argc, char** argv) {
   try {
     if (argc == 4 && !strcmp(argv[1], "params")) return params(argv[2], argv[3]);
@@ -236,6 +357,7 @@ int main(int argc, char** argv) {
     if (argc == 4 && !strcmp(argv[1], "rot")) return rot(atoi(argv[2]), atoi(argv[3]));
     if (argc == 6 && !strcmp(argv[1], "train")) return train(argv[2], argv[3], atoi(argv[4]), atoi(argv[5]));
     if (argc == 4 && !strcmp(argv[1], "vosch")) return vosch(argv[2], (float)atof(argv[3]));
+    if (argc == 5 && !strcmp(argv[1], "estim")) return estim(argv[2], argv[3], argv[4]);
     if (argc == 6 && !strcmp(argv[1], "readdata")) return readdata(argv[2], argv[3], argv[4], atoi(argv[5]));
   } catch (const Error& e) {
     fprintf(stderr, "c3hlac::Error %d: %s\n", e.code, e.what());

@@ -228,3 +228,42 @@ def test_facade_read_data_integral_tables(ctx, demo, tmp_path):
     for m in (0, 1):
         e = lists[m, 0]
         assert [float(e["score"]), int(e["x"]), int(e["y"]), int(e["z"]), int(e["mode"])] == dets[m]
+
+
+def _write_pcd(path, pts):
+    hdr = ("# .PCD v0.7 - Point Cloud Data file format\nVERSION 0.7\nFIELDS x y z rgb\nSIZE 4 4 4 4\n"
+           "TYPE F F F F\nCOUNT 1 1 1 1\nWIDTH %d\nHEIGHT 1\nVIEWPOINT 0 0 0 1 0 0 0\nPOINTS %d\nDATA binary\n"
+           % (len(pts), len(pts)))
+    with open(path, "wb") as f:
+        f.write(hdr.encode())
+        f.write(np.ascontiguousarray(pts, np.float32).tobytes())
+
+
+@pytest.mark.gpu
+def test_facade_estimation_classes(demo, tmp_path):
+    """extract_c3_hlac_scene.cpp's flow (Param -> loadPCDFile -> VoxelGrid -> features ->
+    writeFeature) through C3HLAC981Estimation / C3HLAC117Estimation (c3_hlac.h:79-220) for
+    PointXYZRGB and PointXYZRGBNormal: rows equal to extractC3HLACSignature981/117's,
+    getSubdivNum, setVoxelFilter's false returns, the silent-empty threshold case; the
+    written feature file against the oracle."""
+    pts = synth.kinect_scene(200_000, grid=64, leaf=0.02, seed=synth.BASE_SEED + 77)
+    pcd = tmp_path / "scene.pcd"
+    _write_pcd(pcd, pts)
+    r = subprocess.run([str(demo), "estim", str(FIX / "param_v1"), str(pcd), str(tmp_path / "f")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    j = json.loads(r.stdout)
+    assert j["filter_ok"] == 1 and j["rows"] == j["free_rows"] == 7 ** 3
+    assert j["same981"] == 1 and j["subdiv"] == j["subdiv_free"] == [7, 7, 7]
+    assert j["same117"] == 1 and j["rows117"] > 0 and j["wide117"] == 1 and j["narrow_throws"] == 1
+    assert j["normal_down_same"] == 1 and j["normal_same981"] == 1
+    assert j["offset_false"] == 1 and j["negative_subdiv_false"] == 1 and j["negative_thr_empty"] == 1
+    assert j["unset_throws"] == 1 and j["name"] == "C3HLAC981Estimation"
+    est = c3hlac.read_feature(tmp_path / "f_estim.pcd")
+    free = c3hlac.read_feature(tmp_path / "f_free.pcd")
+    assert np.array_equal(est, free)
+    g, layout, cloud = po.voxelize(pts, 0.02)
+    fe, _, _ = po.c3hlac(g, layout, cloud, 981, (147, 146, 148), 0.02, 10, exact=True)
+    fe = fe[(fe != 0).any(1)]  # writeFeature drops all-zero rows (c3_hlac_tools.hpp:89-115)
+    assert est.shape == fe.shape
+    np.testing.assert_allclose(est, fe, atol=5e-7)  # "%f" text

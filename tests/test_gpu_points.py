@@ -1,0 +1,181 @@
+"""Points-in frame pipeline (c3h_run_point_frames): BASELINE configs[3]'s unit of work --
+a point cloud per callback, limitPoint + getVoxelGrid + extractC3HLACSignature981 + search
+(color_voxel_recognition/test/detect_object.cpp:139-186) -- for batches of frames with no
+per-frame host round trip.
+
+- configs[3] at its stated size on one GPU: 512 independent 1M-point frames at 128^3
+  (C3-HLAC-981, S = 10, compress 981 -> 100, 1 model x r = 20, box 2x2x2, rank 1), frames
+  on the device; every 32nd frame re-computed by the oracle from its points (grid
+  geometry and counts exact, detection within 1e-5 of the float64 oracle); the whole
+  batch bit-identical to the single-frame path.
+- host-resident frames (the H2D-inclusive path) give the same records as device frames.
+- mixed geometries in one batch: frames of different extents and min_b inside the canvas,
+  a frame beyond the canvas, an empty frame, a frame whose centroids may round across a
+  cell boundary -- records equal the single-frame path's, statuses as documented."""
+import concurrent.futures as cf
+
+import numpy as np
+import pytest
+
+import c3hlac
+import pyoracle as po
+from c3hlac import synth
+from conftest import THR
+
+pytestmark = pytest.mark.gpu
+
+G, LEAF, S, D, R, BOX, EXIST = 128, 0.02, 10, 100, 20, (2, 2, 2), 100
+RTOL = 1e-5
+
+
+def _single(ctx, pts, variant=981, subdiv=S, z_limit=float("inf")):
+    """The single-frame path (c3h_voxelize + c3h_extract + search from fresh lists)."""
+    ctx.voxelize(pts, LEAF, z_limit)
+    ctx.extract(variant, THR, subdiv)
+    ctx.set_rank(1)
+    lists, _ = ctx.search(BOX, EXIST)
+    return lists.copy()
+
+
+@pytest.fixture(scope="module")
+def bases():
+    return [synth.kinect_scene(1_000_000, grid=G, leaf=LEAF, seed=synth.BASE_SEED + 1300 + s) for s in range(8)]
+
+
+def _variant(torch, base_dev, k):
+    """Frame k of a base scene: colours XOR-masked, x shifted by k whole cells (float64 add,
+    rounded to float32 -- the same arithmetic numpy does for the oracle's copy)."""
+    t = base_dev.clone()
+    bits = t[:, 3].view(torch.int32)
+    t[:, 3] = (bits ^ ((k * 0x2F1D37) & 0xFFFFFF)).view(torch.float32)
+    t[:, 0] = (t[:, 0].double() + k * LEAF).float()
+    return t
+
+
+def _variant_host(base, k):
+    pts = base.copy()
+    pts[:, 3] = (pts[:, 3].view(np.uint32) ^ np.uint32((k * 0x2F1D37) & 0xFFFFFF)).view(np.float32)
+    pts[:, 0] = (pts[:, 0].astype(np.float64) + k * LEAF).astype(np.float32)
+    return pts
+
+
+def test_config4_512_frames_points_in(ctx, bases):
+    import torch
+    dev = torch.device("cuda", 0)
+    bdev = [torch.from_numpy(b).to(dev) for b in bases]
+    nfr = 512
+    frames = [_variant(torch, bdev[i % 8], i // 8) for i in range(nfr)]
+    torch.cuda.synchronize()
+    axis_t, var, axis_q = synth.random_bases(981, D, 1, R, seed=synth.BASE_SEED + 31)
+    ap = synth.whiten(axis_t, var)
+    ctx.search_setup(axis_t, var, axis_q)
+    ctx.set_rank(1)
+    ctx.set_batch(32)
+    ctx.set_pipeline(True)
+    d_out = torch.zeros((nfr, 3), dtype=torch.int64, device=dev)
+    nm, info = ctx.run_point_frames(frames, LEAF, (G,) * 3, 981, THR, S, BOX, EXIST, True, d_out)
+    assert nm == 1
+    got = d_out.cpu().numpy().view(c3hlac.DET_DTYPE).reshape(nfr, 1)
+    assert (info["status"] == 0).all(), np.flatnonzero(info["status"])
+    assert (info["div_b"] == G).all()
+    assert np.array_equal(info["min_b"][:, 0], np.arange(nfr) // 8)  # the x shift moves min_b
+    assert (info["subdiv_b"] == 13).all()
+    assert (got["score"] > 0).all()
+    # the oracle from the points, every 32nd frame
+    P = (-(-G // S) - BOX[0] + 1,) * 3
+
+    def oracle(i):
+        pts = _variant_host(bases[i % 8], i // 8)
+        g, layout, cloud = po.voxelize(pts, LEAF)
+        fe, sb, _ = po.c3hlac(g, layout, cloud, 981, THR, LEAF, S, exact=True)
+        ex = po.exist(fe)
+        L, _, sc = po.search(sb, fe, ex, ap, axis_q, BOX, 1, EXIST, dbl=True, want_scores=True)
+        return i, g, cloud, sc
+
+    with cf.ThreadPoolExecutor(8) as pool:  # the C oracle releases the GIL
+        for i, g, cloud, sc in pool.map(oracle, range(5, nfr, 32)):
+            assert list(info["div_b"][i]) == list(g.div_b) and list(info["min_b"][i]) == list(g.min_b), i
+            assert info["n_valid"][i] == g.n_valid and info["n_occ"][i] == g.n_occ == len(cloud), i
+            e = got[i, 0]
+            p = (int(e["z"]) * P[1] + int(e["y"])) * P[0] + int(e["x"])
+            best = int(np.argmax(sc))
+            assert int(e["mode"]) == 0
+            assert abs(float(e["score"]) - sc[p]) <= RTOL * sc[p], (i, float(e["score"]), sc[p])
+            if p != best:
+                assert sc[p] >= sc[best] * (1 - 2 * RTOL), (i, p, best)
+    # the single-frame path gives the same records (bit-identical)
+    for i in range(0, nfr, 37):
+        ref = _single(ctx, frames[i])
+        assert np.array_equal(got[i], ref[:, 0]), i
+
+
+def test_host_frames_equal_device_frames(ctx, bases):
+    import torch
+    dev = torch.device("cuda", 0)
+    nfr = 40
+    host = [_variant_host(bases[i % 8], 3 + i // 8) for i in range(nfr)]
+    devf = [torch.from_numpy(h).to(dev) for h in host]
+    torch.cuda.synchronize()
+    axis_t, var, axis_q = synth.random_bases(981, D, 2, R, seed=synth.BASE_SEED + 32)
+    ctx.search_setup(axis_t, var, axis_q)
+    ctx.set_rank(1)
+    ctx.set_batch(16)
+    a = torch.zeros((nfr, 6), dtype=torch.int64, device=dev)
+    b = torch.zeros((nfr, 6), dtype=torch.int64, device=dev)
+    _, ia = ctx.run_point_frames(host, LEAF, (G,) * 3, 981, THR, S, BOX, EXIST, True, a)
+    _, ib = ctx.run_point_frames(devf, LEAF, (G,) * 3, 981, THR, S, BOX, EXIST, True, b)
+    assert np.array_equal(a.cpu().numpy(), b.cpu().numpy())
+    assert np.array_equal(ia, ib)
+    ctx.set_batch(32)
+
+
+def test_mixed_geometries_in_one_batch(ctx, bases):
+    """Frames of different extents / origins share one canvas; each frame's positions are
+    bounded by its own subdivisions.  Statuses: 0 batched, 1 recomputed on the
+    single-frame path (beyond the canvas, empty, centroid near a cell boundary)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    axis_t, var, axis_q = synth.random_bases(117, D, 3, R, seed=synth.BASE_SEED + 33)
+    ctx.search_setup(axis_t, var, axis_q)
+    ctx.set_rank(1)
+    ctx.set_batch(8)
+    frames, expect_status = [], []
+    for i in range(20):
+        pts = _variant_host(bases[i % 8], i)[2:]  # no sentinels: the extent is the scene's own
+        kind = i % 5
+        if kind == 1:  # only near points: a smaller grid, another min_b
+            pts = pts[np.isfinite(pts[:, 2]) & (pts[:, 2] < np.float32(0.55 * G * LEAF))]
+        elif kind == 2:  # a slab of x
+            pts = pts[np.isfinite(pts[:, 0]) & (pts[:, 0] > np.float32((i + 20) * LEAF))]
+        frames.append(np.ascontiguousarray(pts))
+        expect_status.append(0)
+    far = frames[0].copy()
+    fin = np.flatnonzero(np.isfinite(far[:, 0]))
+    far[fin[0], :3] = far[fin[1], :3] + np.float32(140 * LEAF)  # extent beyond the 128 canvas
+    frames.append(far)
+    expect_status.append(1)
+    frames.append(np.full((1000, 4), np.nan, np.float32))  # no valid point
+    expect_status.append(1)
+    edge = frames[3].copy()  # a point right on a cell face: its voxel's centroid is flagged
+    k = np.flatnonzero(np.isfinite(edge[:, 0]))[7]
+    edge[k, 0] = np.float32(np.floor(edge[k, 0] / np.float32(LEAF)) * np.float32(LEAF))
+    frames.append(edge)
+    expect_status.append(1)
+    nfr = len(frames)
+    devf = [torch.from_numpy(f).to(dev) for f in frames]
+    torch.cuda.synchronize()
+    d_out = torch.zeros((nfr, 9), dtype=torch.int64, device=dev)
+    _, info = ctx.run_point_frames(devf, LEAF, (G,) * 3, 117, THR, S, BOX, EXIST, True, d_out)
+    got = d_out.cpu().numpy().view(c3hlac.DET_DTYPE).reshape(nfr, 3)
+    assert list(info["status"]) == expect_status, info["status"]
+    assert len(set(map(tuple, info["div_b"][:20]))) > 2  # the geometries differ
+    for i in range(nfr):
+        if i == nfr - 2:  # empty frame: fresh setRank lists
+            assert (got[i]["score"] == 0).all()
+            continue
+        ref = _single(ctx, devf[i], variant=117)
+        assert np.array_equal(got[i], ref[:, 0]), (i, got[i], ref[:, 0])
+        gi = ctx.info
+        assert list(info["div_b"][i]) == list(gi.div_b) and list(info["min_b"][i]) == list(gi.min_b), i
+        assert info["n_occ"][i] == gi.n_occ
+    ctx.set_batch(32)
