@@ -162,13 +162,14 @@ struct VoxBatchArgs {
   int blk0[kMaxBatch + 1];            // accumulate blocks of frame f: [blk0[f], blk0[f+1])
   int prev_blk0[kMaxBatch + 1];
   float inv, leaf, z_limit;
-  int C[3];
+  int C[3];                           // canvas dims
+  int tb[3];                          // toroidal accumulator: 2^tb[a] >= C[a] cells per axis
   int subdiv, off[3];
   float inv_s;
-  unsigned long long* accA;           // [frame][C^3] count << 40 | sum r
-  unsigned long long* accB;           //                sum b << 32 | sum g
+  ulonglong2* acc;                    // [frame][2^(tb0+tb1+tb2)] {count << 40 | sum r, sum b << 32 | sum g}
   uint32_t* accM;                     //                min boundary margin (float bits), ~0 = none
   int64_t s_acc;
+  uint32_t* fcnt;                     // [kMaxBatch] finished accumulate blocks per frame (self-resetting)
   uint32_t* vlist;                    // [block][chunk] accumulator entries first touched by the block
   uint32_t* wlist;                    // [block][chunk] canvas words the scatter wrote (this set)
   int32_t* part;                      // [block][kPartW] partial records (this set)
@@ -538,8 +539,8 @@ struct c3h_ctx {
   int pb_slots = 0;
   int pb_prev_nf = 0, pb_prev_total = 0;
   std::vector<int> pb_prev_blk0;
-  c3h::DevBuf<unsigned long long> pb_accA, pb_accB;
-  c3h::DevBuf<uint32_t> pb_accM, pb_vlist;
+  c3h::DevBuf<ulonglong2> pb_acc;
+  c3h::DevBuf<uint32_t> pb_accM, pb_vlist, pb_fcnt;
   int64_t pb_acc_vox = 0;
   int pb_acc_slots = 0;
   c3h::DevBuf<float> pb_stage;

@@ -704,9 +704,9 @@ void c3h_destroy(c3h_ctx* ctx) {
   release(ctx->pb_wlist);
   release(ctx->pb_part);
   release(ctx->pb_lim);
-  release(ctx->pb_accA);
-  release(ctx->pb_accB);
+  release(ctx->pb_acc);
   release(ctx->pb_accM);
+  release(ctx->pb_fcnt);
   release(ctx->pb_vlist);
   release(ctx->pb_stage);
   release(ctx->pb_info);
@@ -2218,14 +2218,24 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
     const c3h_ctx::PipeKey k = pipe_key(ctx, canvas, zero, leaf, p, range, exist_threshold, rotate, B);
     // shared: toroidal accumulators (one per frame slot; the scatter returns them to zero),
     // voxel lists, the frames' records, host staging
-    if (ctx->pb_acc_vox != cvox || ctx->pb_acc_slots < B) {
-      ENSURE(ctx->pb_accA, (size_t)B * cvox);
-      ENSURE(ctx->pb_accB, (size_t)B * cvox);
-      ENSURE(ctx->pb_accM, (size_t)B * cvox);
-      HIPCHK(hipMemsetAsync(ctx->pb_accA.p, 0, (size_t)B * cvox * 8, ctx->stream));
-      HIPCHK(hipMemsetAsync(ctx->pb_accB.p, 0, (size_t)B * cvox * 8, ctx->stream));
-      HIPCHK(hipMemsetAsync(ctx->pb_accM.p, 0xff, (size_t)B * cvox * 4, ctx->stream));
-      ctx->pb_acc_vox = cvox;
+    // toroidal accumulator dims: powers of two >= the canvas (a frame whose extent fits the
+    // canvas never wraps onto itself; the index is then three masks and shifts)
+    int tb[3];
+    int64_t tvox = 1;
+    for (int a = 0; a < 3; ++a) {
+      tb[a] = 0;
+      while ((1 << tb[a]) < canvas[a]) ++tb[a];
+      tvox <<= tb[a];
+    }
+    if (tvox > ((int64_t)1 << 31)) return fail(ctx, C3H_ERR_RANGE, "c3h_run_point_frames: canvas too large");
+    if (ctx->pb_acc_vox != tvox || ctx->pb_acc_slots < B) {
+      ENSURE(ctx->pb_acc, (size_t)B * tvox);
+      ENSURE(ctx->pb_accM, (size_t)B * tvox);
+      ENSURE(ctx->pb_fcnt, (size_t)c3h::kMaxBatch);
+      HIPCHK(hipMemsetAsync(ctx->pb_acc.p, 0, (size_t)B * tvox * 16, ctx->stream));
+      HIPCHK(hipMemsetAsync(ctx->pb_accM.p, 0xff, (size_t)B * tvox * 4, ctx->stream));
+      HIPCHK(hipMemsetAsync(ctx->pb_fcnt.p, 0, (size_t)c3h::kMaxBatch * 4, ctx->stream));
+      ctx->pb_acc_vox = tvox;
       ctx->pb_acc_slots = B;
     }
     ENSURE(ctx->pb_info, (size_t)nframes);
@@ -2285,10 +2295,11 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
       }
       va.subdiv = p->subdiv;
       va.inv_s = p->subdiv > 0 ? (float)(1.0 / p->subdiv) : 0.0f;
-      va.accA = ctx->pb_accA.p;
-      va.accB = ctx->pb_accB.p;
+      for (int a = 0; a < 3; ++a) va.tb[a] = tb[a];
+      va.acc = ctx->pb_acc.p;
       va.accM = ctx->pb_accM.p;
-      va.s_acc = cvox;
+      va.s_acc = tvox;
+      va.fcnt = ctx->pb_fcnt.p;
       va.vlist = ctx->pb_vlist.p;
       va.wlist = c->pb_wlist.p;
       va.part = c->pb_part.p;

@@ -624,23 +624,28 @@ int grid_for(int64_t n, int cap = 4096) {
 // Two launches per batch of frames, no host round trip:
 //   voxb_accum   block b = (frame f, chunk of kBChunk consecutive points): first it clears
 //                the canvas words the previous batch on this buffer set wrote through its
-//                own segment b (read before this block rewrites the segment's record);
-//                then per point (limitPoint + VoxelGrid quantisation as vox_accum) an LDS
-//                hash insert keyed by the cell's toroidal index (x mod C, y mod C, z mod C);
-//                the flush adds each (block, voxel) total into the frame's toroidal
-//                accumulator with one returning atomic (count 0 before = first touch: the
-//                entry goes to the block's segment of the voxel list) and one plain one.
-//   voxb_scatter block b reduces its frame's partial records (bounds, counts), then turns
-//                its segment's entries into canvas words -- canvas index = cell - min_b,
-//                with cell = min_b + ((t - min_b) mod C) per axis, exact whenever the
-//                frame's extent fits the canvas -- clears the accumulator entries and
-//                records the words for the next batch's clear.  Block 0 of a frame
-//                publishes its VoxelGrid geometry and getSubdivNum (the gate's limits).
+//                own segment b (read before this block rewrites the segment's record).
+//                Points (limitPoint + VoxelGrid quantisation, as vox_accum) are keyed by
+//                the cell's toroidal index (x, y, z mod powers of two >= the canvas).  A
+//                depth camera's consecutive pixels hit the same voxel in runs: within each
+//                16-lane row of a wave the runs are summed by a segmented DPP scan and only
+//                a run's last lane inserts into the LDS hash (one CAS + two adds for ~5
+//                points).  The flush adds each (block, voxel) total into the frame's
+//                toroidal accumulator (one 16-B record) with one returning atomic (count 0
+//                before = first touch: the entry goes to the block's segment of the voxel
+//                list) and one plain one.
+//   voxb_reduce  one block per frame: its blocks' partial records -> its VoxelGrid
+//                geometry, getSubdivNum and the gate's position limits.
+//   voxb_scatter block b turns its segment's entries into canvas words -- canvas index =
+//                cell - min_b, with cell - min_b = (t - min_b) mod 2^tb per axis, exact
+//                whenever the frame's extent fits the canvas -- clears the accumulator
+//                records and lists the words for the next batch's clear.
 #ifndef C3H_VB_CHUNK
-#define C3H_VB_CHUNK 4096
+#define C3H_VB_CHUNK 16384  // a depth camera's rows: 16k pixels per block, each voxel flushed by 1.16 blocks
+                            // at 256^3 (4k: 1.71), 1.40 at 128^3 (4k: 2.67)
 #endif
 #ifndef C3H_VB_THREADS
-#define C3H_VB_THREADS 1024
+#define C3H_VB_THREADS 512  // 8 waves over a 2,048-slot table (1,024 threads: 8.0 vs 6.5 us per 128^3 frame)
 #endif
 #ifndef C3H_VB_SLOTS
 #define C3H_VB_SLOTS 2048
@@ -648,9 +653,23 @@ int grid_for(int64_t n, int cap = 4096) {
 constexpr int kBChunk = C3H_VB_CHUNK;
 constexpr int kBT = C3H_VB_THREADS;
 constexpr int kBPer = kBChunk / kBT;
+#ifndef C3H_VB_ROUND
+#define C3H_VB_ROUND 8
+#endif
+constexpr int kBRound = kBPer < C3H_VB_ROUND ? kBPer : C3H_VB_ROUND;  // loads in flight per thread
+static_assert(kBPer % kBRound == 0, "rounds");
 constexpr int kBSlots = C3H_VB_SLOTS;
 static_assert(kBChunk % kBT == 0 && (kBSlots & (kBSlots - 1)) == 0, "batch voxeliser shape");
 constexpr uint32_t kNoT = 0xffffffffu;
+#ifndef C3H_VB_DIAG
+#define C3H_VB_DIAG 0  // diagnostics builds only: 1 = no global flush, 2 = no LDS insert either
+#endif
+#ifndef C3H_VB_ATOM_SCOPE
+#define C3H_VB_ATOM_SCOPE __HIP_MEMORY_SCOPE_AGENT  // diagnostics: workgroup scope times L2-local atomics
+#endif
+#ifndef C3H_VB_MERGE
+#define C3H_VB_MERGE 1  // the run merge (0: every point inserts into the LDS hash itself)
+#endif
 
 __device__ __forceinline__ int vb_frame(const int* blk0, int nf, int b) {
   int lo = 0, hi = nf;  // blk0[lo] <= b < blk0[hi]
@@ -662,9 +681,10 @@ __device__ __forceinline__ int vb_frame(const int* blk0, int nf, int b) {
   return lo;
 }
 
-__device__ __forceinline__ int vb_mod(int v, int c) {
-  const int m = v % c;
-  return m < 0 ? m + c : m;
+// DPP row_shr:o (within 16-lane rows); lanes without a source read 0
+template <int O>
+__device__ __forceinline__ uint32_t row_shr(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 | O, 0xf, 0xf, true);
 }
 
 __global__ __launch_bounds__(kBT) void voxb_accum_kernel(VoxBatchArgs a) {
@@ -689,9 +709,9 @@ __global__ __launch_bounds__(kBT) void voxb_accum_kernel(VoxBatchArgs a) {
   const int64_t base = (int64_t)(b - a.blk0[f]) * kBChunk;
   const float4* __restrict__ pts = a.pts[f];
   const int64_t n = a.n[f];
-  const int Cx = a.C[0], Cy = a.C[1], Cz = a.C[2];
-  unsigned long long* __restrict__ A = a.accA + f * a.s_acc;
-  unsigned long long* __restrict__ B = a.accB + f * a.s_acc;
+  const uint32_t mx_ = (1u << a.tb[0]) - 1, my_ = (1u << a.tb[1]) - 1, mz_ = (1u << a.tb[2]) - 1;
+  const int sy = a.tb[0], sz = a.tb[0] + a.tb[1];
+  ulonglong2* __restrict__ acc = a.acc + f * a.s_acc;
   uint32_t* __restrict__ Mg = a.accM + f * a.s_acc;
   uint32_t* __restrict__ vl = a.vlist + (size_t)b * kBChunk;
   for (int s = tid; s < kBSlots; s += kBT) {
@@ -701,21 +721,24 @@ __global__ __launch_bounds__(kBT) void voxb_accum_kernel(VoxBatchArgs a) {
     s_m[s] = kNoMargin;
   }
   if (tid == 0) s_nnew = 0;
-  if (base == 0 && tid == 0) a.info[f].flagged = 0;  // the scatter adds its flags
   __syncthreads();
   int mn[3] = {INT_MAX, INT_MAX, INT_MAX}, mx[3] = {INT_MIN, INT_MIN, INT_MIN};
   int nv = 0;
   bool err = false;
   auto add_global = [&](uint32_t t, unsigned long long va, unsigned long long vb, uint32_t m) {
-    const unsigned long long old = atomicAdd(A + t, va);
+    const unsigned long long old = atomicAdd(&acc[t].x, va);
     if ((old >> 40) == 0) vl[atomicAdd(&s_nnew, 1u)] = t;
-    atomicAdd(B + t, vb);
+    atomicAdd(&acc[t].y, vb);
     if (m < kMarginFlush) atomicMin(Mg + t, m);
   };
-  float4 p[kBPer];
+  VoxArgs q{};  // point_cell's quantisation parameters
+  q.inv = a.inv;
+  const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1);  // lanes <= this one
+  for (int r0 = 0; r0 < kBPer; r0 += kBRound) {
+  float4 p[kBRound];
 #pragma unroll
-  for (int j = 0; j < kBPer; ++j) {  // every load of the chunk in flight together
-    const int64_t i = base + j * kBT + tid;
+  for (int j = 0; j < kBRound; ++j) {  // a round of loads in flight together
+    const int64_t i = base + (int64_t)(r0 + j) * kBT + tid;
     if (i < n) {
       const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(pts) + i);
       p[j] = make_float4(v.x, v.y, v.z, v.w);
@@ -723,47 +746,89 @@ __global__ __launch_bounds__(kBT) void voxb_accum_kernel(VoxBatchArgs a) {
       p[j] = make_float4(NAN, NAN, NAN, 0.0f);
     }
   }
-  VoxArgs q{};  // point_cell's quantisation parameters
-  q.inv = a.inv;
 #pragma unroll
-  for (int j = 0; j < kBPer; ++j) {
-    if (!point_valid(p[j], a.z_limit)) continue;
+  for (int j = 0; j < kBRound; ++j) {
     int c[3];
     float margin;
-    if (!point_cell(q, p[j], c, &margin)) {
+    bool valid = point_valid(p[j], a.z_limit);
+    if (valid && !point_cell(q, p[j], c, &margin)) {
       err = true;
-      continue;
+      valid = false;
     }
-    ++nv;
+    uint32_t t = kNoT, w0 = 0, w1 = 0, mb = kNoMargin;
+    if (valid) {
+      ++nv;
 #pragma unroll
-    for (int ax = 0; ax < 3; ++ax) {
-      mn[ax] = min(mn[ax], c[ax]);
-      mx[ax] = max(mx[ax], c[ax]);
-    }
-    const uint32_t t = (uint32_t)vb_mod(c[0], Cx) +
-                       (uint32_t)Cx * ((uint32_t)vb_mod(c[1], Cy) + (uint32_t)Cy * (uint32_t)vb_mod(c[2], Cz));
-    const uint32_t rgb = __float_as_uint(p[j].w);
-    const uint32_t r = (rgb >> 16) & 0xffu, g = (rgb >> 8) & 0xffu, bl = rgb & 0xffu;
-    const uint32_t mb = __float_as_uint(margin);
-    uint32_t h = (t * 0x9E3779B1u) >> (32 - __builtin_ctz(kBSlots));
-    bool done = false;
-    for (int probe = 0; probe < kLProbe; ++probe) {
-      const uint32_t prev = atomicCAS(&s_key[h], kNoT, t);
-      if (prev == kNoT || prev == t) {
-        atomicAdd(&s_A[h], (1ull << 40) | r);
-        atomicAdd(&s_B[h], ((unsigned long long)bl << 32) | g);
-        if (mb < kMarginFlush) atomicMin(&s_m[h], mb);
-        done = true;
-        break;
+      for (int ax = 0; ax < 3; ++ax) {
+        mn[ax] = min(mn[ax], c[ax]);
+        mx[ax] = max(mx[ax], c[ax]);
       }
-      h = (h + 1) & (kBSlots - 1);
+      t = ((uint32_t)c[0] & mx_) | (((uint32_t)c[1] & my_) << sy) | (((uint32_t)c[2] & mz_) << sz);
+      const uint32_t rgb = __float_as_uint(p[j].w);
+      w0 = ((rgb >> 16) & 0xffu) | (((rgb >> 8) & 0xffu) << 12) | (1u << 24);  // r | g << 12 | count << 24
+      w1 = rgb & 0xffu;                                                         // b
+      const uint32_t mbits = __float_as_uint(margin);
+      mb = mbits < kMarginFlush ? mbits : kNoMargin;
     }
-    if (!done) add_global(t, (1ull << 40) | r, ((unsigned long long)bl << 32) | g, mb);  // LDS table full
+    // runs of equal keys inside each 16-lane row: a lane starts a run when it is invalid,
+    // the row's first lane, or its key differs from the previous lane's
+    const uint32_t tp = row_shr<1>(t);
+    const bool head = !C3H_VB_MERGE || !valid || (lane & 15) == 0 || tp != t;
+    const uint64_t hm = __ballot(head);
+    const int hpos = 63 - __clzll(hm & le);  // this lane's run start
+    const int o0 = lane - hpos;              // lanes before this one in its run
+    uint32_t s0, s1, sm;
+    s0 = row_shr<1>(w0); s1 = row_shr<1>(w1); sm = row_shr<1>(mb);
+    if (o0 >= 1) { w0 += s0; w1 += s1; mb = min(mb, sm); }
+    s0 = row_shr<2>(w0); s1 = row_shr<2>(w1); sm = row_shr<2>(mb);
+    if (o0 >= 2) { w0 += s0; w1 += s1; mb = min(mb, sm); }
+    s0 = row_shr<4>(w0); s1 = row_shr<4>(w1); sm = row_shr<4>(mb);
+    if (o0 >= 4) { w0 += s0; w1 += s1; mb = min(mb, sm); }
+    s0 = row_shr<8>(w0); s1 = row_shr<8>(w1); sm = row_shr<8>(mb);
+    if (o0 >= 8) { w0 += s0; w1 += s1; mb = min(mb, sm); }
+    const bool tail = C3H_VB_DIAG < 2 && valid && ((lane & 15) == 15 || ((hm >> (lane + 1)) & 1));
+    if (tail) {  // the run's totals: count <= 16, channel sums <= 4080
+      const unsigned long long A = ((unsigned long long)(w0 >> 24) << 40) | (w0 & 0xfffu);
+      const unsigned long long Bv = ((unsigned long long)w1 << 32) | ((w0 >> 12) & 0xfffu);
+      uint32_t h = (t * 0x9E3779B1u) >> (32 - __builtin_ctz(kBSlots));
+      bool done = false;
+      for (int probe = 0; probe < kLProbe; ++probe) {
+        const uint32_t prev = atomicCAS(&s_key[h], kNoT, t);
+        if (prev == kNoT || prev == t) {
+          atomicAdd(&s_A[h], A);
+          atomicAdd(&s_B[h], Bv);
+          if (mb != kNoMargin) atomicMin(&s_m[h], mb);
+          done = true;
+          break;
+        }
+        h = (h + 1) & (kBSlots - 1);
+      }
+      if (!done) add_global(t, A, Bv, mb);  // LDS table full
+    }
+  }
   }
   __syncthreads();
-  for (int s = tid; s < kBSlots; s += kBT) {
-    const uint32_t t = s_key[s];
-    if (t != kNoT) add_global(t, s_A[s], s_B[s], s_m[s]);
+  // flush: a thread's slots' returning atomics are all issued before any result is used
+  // (they are round trips to the memory side; one after the other they kept blocks resident)
+  if (C3H_VB_DIAG == 0) {
+    constexpr int kFl = (kBSlots + kBT - 1) / kBT;
+    uint32_t key[kFl];
+    unsigned long long old[kFl];
+#pragma unroll
+    for (int k = 0; k < kFl; ++k) {
+      const int s = tid + k * kBT;
+      key[k] = s < kBSlots ? s_key[s] : kNoT;
+      old[k] = key[k] != kNoT ? __hip_atomic_fetch_add(&acc[key[k]].x, s_A[s], __ATOMIC_RELAXED, C3H_VB_ATOM_SCOPE)
+                              : 1ull << 40;
+    }
+#pragma unroll
+    for (int k = 0; k < kFl; ++k) {
+      const int s = tid + k * kBT;
+      if (key[k] == kNoT) continue;
+      __hip_atomic_fetch_add(&acc[key[k]].y, s_B[s], __ATOMIC_RELAXED, C3H_VB_ATOM_SCOPE);
+      if (s_m[s] < kMarginFlush) __hip_atomic_fetch_min(Mg + key[k], s_m[s], __ATOMIC_RELAXED, C3H_VB_ATOM_SCOPE);
+      if ((old[k] >> 40) == 0) vl[atomicAdd(&s_nnew, 1u)] = key[k];
+    }
   }
 #pragma unroll
   for (int ax = 0; ax < 3; ++ax) {
@@ -792,111 +857,123 @@ __global__ __launch_bounds__(kBT) void voxb_accum_kernel(VoxBatchArgs a) {
   if (tid == 8) pr[kPNew] = (int)s_nnew;
 }
 
-__global__ __launch_bounds__(kBlock) void voxb_scatter_kernel(VoxBatchArgs a) {
-  __shared__ int s_r[kBlock / 64][10];
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const int f = vb_frame(a.blk0, a.nf, b);
-  // the frame's bounds and totals from its blocks' partial records (a few KB, from L2)
-  int mn[3] = {INT_MAX, INT_MAX, INT_MAX}, mx[3] = {INT_MIN, INT_MIN, INT_MIN};
-  int nv = 0, nn = 0, er = 0;
-  for (int q = a.blk0[f] + tid; q < a.blk0[f + 1]; q += kBlock) {
-    const int32_t* r = a.part + (size_t)q * kPartW;
-    if (r[kPValid]) {
+// one block per frame: its accumulate blocks' records -> the frame's VoxelGrid geometry,
+// getSubdivNum and the gate's position limits (a separate launch: a last-block hand-off
+// inside voxb_accum kept every block resident until its flush atomics had drained)
+__global__ __launch_bounds__(kBlock) void voxb_reduce_kernel(VoxBatchArgs a) {
+  __shared__ int s_red[kBlock / 64][8];
+  const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int lo[3] = {INT_MAX, INT_MAX, INT_MAX}, hi[3] = {INT_MIN, INT_MIN, INT_MIN};
+  int tv = 0, tn = 0, te = 0;
+  for (int qb = a.blk0[f] + tid; qb < a.blk0[f + 1]; qb += kBlock) {
+    const int32_t* r = a.part + (size_t)qb * kPartW;
+    const int rv = r[kPValid];
+    if (rv) {
       for (int ax = 0; ax < 3; ++ax) {
-        mn[ax] = min(mn[ax], r[kPMin + ax]);
-        mx[ax] = max(mx[ax], r[kPMax + ax]);
+        lo[ax] = min(lo[ax], r[kPMin + ax]);
+        hi[ax] = max(hi[ax], r[kPMax + ax]);
       }
     }
-    nv += r[kPValid];
-    nn += r[kPNew];
-    er |= r[kPErr];
+    tv += rv;
+    tn += r[kPNew];
+    te |= r[kPErr];
   }
   for (int ax = 0; ax < 3; ++ax) {
-    mn[ax] = wave_reduce(mn[ax], [](int x, int y) { return min(x, y); });
-    mx[ax] = wave_reduce(mx[ax], [](int x, int y) { return max(x, y); });
+    lo[ax] = wave_reduce(lo[ax], [](int x, int y) { return min(x, y); });
+    hi[ax] = wave_reduce(hi[ax], [](int x, int y) { return max(x, y); });
   }
-  nv = wave_reduce(nv, [](int x, int y) { return x + y; });
-  nn = wave_reduce(nn, [](int x, int y) { return x + y; });
-  er = wave_reduce(er, [](int x, int y) { return x | y; });
-  const int w = tid >> 6;
-  if ((tid & 63) == 0) {
+  tv = wave_reduce(tv, [](int x, int y) { return x + y; });
+  tn = wave_reduce(tn, [](int x, int y) { return x + y; });
+  te = wave_reduce(te, [](int x, int y) { return x | y; });
+  if (lane == 0) {
     for (int ax = 0; ax < 3; ++ax) {
-      s_r[w][ax] = mn[ax];
-      s_r[w][3 + ax] = mx[ax];
+      s_red[w][ax] = lo[ax];
+      s_red[w][3 + ax] = hi[ax];
     }
-    s_r[w][6] = nv;
-    s_r[w][7] = nn;
-    s_r[w][8] = er;
+    s_red[w][6] = tv;
+    s_red[w][7] = tn | (te ? INT_MIN : 0);
   }
   __syncthreads();
-  int lo[3], dv[3], tv = 0, tn = 0, te = 0;
+  if (tid != 0) return;
+  int dv[3];
+  bool err = false;
+  tv = tn = 0;
   for (int ax = 0; ax < 3; ++ax) {
-    int l = s_r[0][ax], h = s_r[0][3 + ax];
-    for (int i = 1; i < kBlock / 64; ++i) {
-      l = min(l, s_r[i][ax]);
-      h = max(h, s_r[i][3 + ax]);
+    int l = INT_MAX, h = INT_MIN;
+    for (int i = 0; i < kBlock / 64; ++i) {
+      l = min(l, s_red[i][ax]);
+      h = max(h, s_red[i][3 + ax]);
     }
     lo[ax] = l;
     dv[ax] = h - l + 1;
   }
   for (int i = 0; i < kBlock / 64; ++i) {
-    tv += s_r[i][6];
-    tn += s_r[i][7];
-    te |= s_r[i][8];
+    tv += s_red[i][6];
+    tn += s_red[i][7] & INT_MAX;
+    err = err || s_red[i][7] < 0;
   }
-  const int Cx = a.C[0], Cy = a.C[1], Cz = a.C[2];
-  const bool over = tv > 0 && (dv[0] > Cx || dv[1] > Cy || dv[2] > Cz);
-  if (b == a.blk0[f] && tid == 0) {
-    VoxFrameRec& rec = a.info[f];
-    int sb[3] = {0, 0, 0};
-    if (tv > 0) {
-      if (a.subdiv > 0) {  // setVoxelFilter (c3_hlac.cpp:204-231), float arithmetic as there
-        if (dv[0] > a.off[0] && dv[1] > a.off[1] && dv[2] > a.off[2])
-          for (int ax = 0; ax < 3; ++ax) sb[ax] = (int)ceilf((float)(dv[ax] - a.off[ax]) * a.inv_s);
-      } else {
-        sb[0] = sb[1] = sb[2] = 1;
-      }
+  const bool over = tv > 0 && (dv[0] > a.C[0] || dv[1] > a.C[1] || dv[2] > a.C[2]);
+  int sb[3] = {0, 0, 0};
+  if (tv > 0) {
+    if (a.subdiv > 0) {  // setVoxelFilter (c3_hlac.cpp:204-231), float arithmetic as there
+      if (dv[0] > a.off[0] && dv[1] > a.off[1] && dv[2] > a.off[2])
+        for (int ax = 0; ax < 3; ++ax) sb[ax] = (int)ceilf((float)(dv[ax] - a.off[ax]) * a.inv_s);
+    } else {
+      sb[0] = sb[1] = sb[2] = 1;
     }
-    for (int ax = 0; ax < 3; ++ax) {
-      rec.min_b[ax] = tv > 0 ? lo[ax] : 0;
-      rec.max_b[ax] = tv > 0 ? lo[ax] + dv[ax] - 1 : -1;
-      rec.sb[ax] = sb[ax];
-      a.lim[4 * f + ax] = (over || te) ? 0 : sb[ax];
-    }
-    a.lim[4 * f + 3] = 0;
-    rec.n_valid = (uint32_t)tv;
-    rec.n_occ = (uint32_t)tn;
-    rec.err = (te ? 1u : 0u) | (over ? 2u : 0u);
   }
-  if (tv == 0) return;
+  VoxFrameRec& rec = a.info[f];
+  for (int ax = 0; ax < 3; ++ax) {
+    rec.min_b[ax] = tv > 0 ? lo[ax] : 0;
+    rec.max_b[ax] = tv > 0 ? lo[ax] + dv[ax] - 1 : -1;
+    rec.sb[ax] = sb[ax];
+    a.lim[4 * f + ax] = (over || err) ? 0 : sb[ax];
+  }
+  a.lim[4 * f + 3] = 0;
+  rec.n_valid = (uint32_t)tv;
+  rec.n_occ = (uint32_t)tn;
+  rec.flagged = 0;  // the scatter adds its flags
+  rec.err = (err ? 1u : 0u) | (over ? 2u : 0u);
+}
+
+__global__ __launch_bounds__(kBlock) void voxb_scatter_kernel(VoxBatchArgs a) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int f = vb_frame(a.blk0, a.nf, b);
+  const VoxFrameRec& rec = a.info[f];  // published by the last accumulate block of the frame
+  if (rec.n_valid == 0) return;
+  const int lo[3] = {rec.min_b[0], rec.min_b[1], rec.min_b[2]};
+  const int Cx = a.C[0], Cy = a.C[1];
+  const uint32_t mx_ = (1u << a.tb[0]) - 1, my_ = (1u << a.tb[1]) - 1, mz_ = (1u << a.tb[2]) - 1;
+  const int sy = a.tb[0], sz = a.tb[0] + a.tb[1];
   const int nseg = a.part[(size_t)b * kPartW + kPNew];
   const uint32_t* vl = a.vlist + (size_t)b * kBChunk;
   uint32_t* wl = a.wlist + (size_t)b * kBChunk;
-  unsigned long long* __restrict__ A = a.accA + f * a.s_acc;
-  unsigned long long* __restrict__ B = a.accB + f * a.s_acc;
+  ulonglong2* __restrict__ acc = a.acc + f * a.s_acc;
   uint32_t* __restrict__ Mg = a.accM + f * a.s_acc;
   uint32_t* __restrict__ grid = a.grid[f];
   uint32_t flagged = 0;
   for (int i = tid; i < nseg; i += kBlock) {
     const uint32_t t = vl[i];
-    const unsigned long long va = A[t], vb = B[t];
+    const ulonglong2 v = acc[t];
     const uint32_t m = Mg[t];
-    A[t] = 0ull;
-    B[t] = 0ull;
+    acc[t] = make_ulonglong2(0ull, 0ull);
     Mg[t] = kNoMargin;
-    const int tx = (int)(t % (uint32_t)Cx), ty = (int)((t / (uint32_t)Cx) % (uint32_t)Cy),
-              tz = (int)(t / ((uint32_t)Cx * (uint32_t)Cy));
-    const int cx = vb_mod(tx - lo[0], Cx), cy = vb_mod(ty - lo[1], Cy), cz = vb_mod(tz - lo[2], Cz);
-    const uint32_t idx = (uint32_t)cx + (uint32_t)Cx * ((uint32_t)cy + (uint32_t)Cy * (uint32_t)cz);
-    const uint32_t count = (uint32_t)(va >> 40);
+    // offsets from min_b: the toroidal coordinates minus min_b, modulo 2^tb
+    const uint32_t cx = ((t & mx_) - (uint32_t)lo[0]) & mx_;
+    const uint32_t cy = (((t >> sy) & my_) - (uint32_t)lo[1]) & my_;
+    const uint32_t cz = (((t >> sz) & mz_) - (uint32_t)lo[2]) & mz_;
+    // an extent beyond the canvas (flagged by the reduction) may land past it: clamp
+    const uint32_t idx = min(cx, (uint32_t)Cx - 1) +
+                         (uint32_t)Cx * (min(cy, (uint32_t)Cy - 1) + (uint32_t)Cy * min(cz, (uint32_t)a.C[2] - 1));
+    const uint32_t count = (uint32_t)(v.x >> 40);
     const float c = (float)count;
-    const uint32_t r = (uint32_t)(int)__fdiv_rn((float)(va & 0xffffffffffull), c);
-    const uint32_t g = (uint32_t)(int)__fdiv_rn((float)(vb & 0xffffffffull), c);
-    const uint32_t bl = (uint32_t)(int)__fdiv_rn((float)(vb >> 32), c);
+    const uint32_t r = (uint32_t)(int)__fdiv_rn((float)(v.x & 0xffffffffffull), c);
+    const uint32_t g = (uint32_t)(int)__fdiv_rn((float)(v.y & 0xffffffffull), c);
+    const uint32_t bl = (uint32_t)(int)__fdiv_rn((float)(v.y >> 32), c);
     grid[idx] = kOcc | (r << 16) | (g << 8) | bl;
     wl[i] = idx;
     // the exact centroid test of vox_scatter_kernel on the absolute cell
-    const int ax_ = lo[0] + cx, ay_ = lo[1] + cy, az_ = lo[2] + cz;
+    const int ax_ = lo[0] + (int)cx, ay_ = lo[1] + (int)cy, az_ = lo[2] + (int)cz;
     const int cmag = max(max(abs(ax_), abs(ay_)), abs(az_)) + 1;
     const float eps = (float)(count + 4) * (float)cmag * 0x1p-22f;
     if (__uint_as_float(m) < eps || eps >= __uint_as_float(kMarginFlush)) ++flagged;
@@ -912,7 +989,10 @@ int vb_chunk() { return kBChunk; }
 hipError_t launch_vox_batch(const VoxBatchArgs& a, hipStream_t s) {
   const int g = std::max(a.total, a.prev_total);
   if (g > 0) voxb_accum_kernel<<<(unsigned)g, kBT, 0, s>>>(a);
-  if (a.total > 0) voxb_scatter_kernel<<<(unsigned)a.total, kBlock, 0, s>>>(a);
+  if (a.total > 0) {
+    voxb_reduce_kernel<<<(unsigned)a.nf, kBlock, 0, s>>>(a);
+    voxb_scatter_kernel<<<(unsigned)a.total, kBlock, 0, s>>>(a);
+  }
   return hipGetLastError();
 }
 

@@ -135,6 +135,46 @@ def train(rows, axis=None, var=None, rotate=False, mean_flg=False, reg=None, whi
     return V[:, order], w[order], mean, n, C
 
 
+def train_f32(rows, axis=None, var=None, rotate=False, mean_flg=False, reg=None, whitening=True):
+    """The reference's own float32 numerics (pca.cpp:48-105), as pca_models / pca_scene run it:
+    each vector (and its 23 rotations) compressed by compressFeature in float32, then
+    PCA::addData one vector at a time -- `correlation(idx) += val * feature[j]` on the upper
+    triangle of a float MatrixXf (product rounded to float, then added: no FMA in the x86-64
+    build), `mean(i) += feature[i]` in float --, PCA::solve's `*= inv_nsample` (a double,
+    the float result of float * double), the mirror, `mean *= inv_nsample`,
+    `correlation -= mean * mean^T` (float), the float regularisation, and the eigensolve in
+    float32 (Eigen's SelfAdjointEigenSolver<MatrixXf> is not available here: LAPACK ssyevd,
+    also float32, stands in; both are backward-stable tridiagonal solvers, so only last-ulp
+    eigenvector components and near-degenerate eigenvalues can differ).
+    Returns as train(): (axis, variance, mean or None, nsample, correlation) in float32."""
+    rows = np.asarray(rows, np.float32)
+    vecs = []
+    for f in rows:
+        vecs.extend(rotations24(f) if rotate else [f])
+    if axis is not None:
+        vecs = [compress(g, axis, var, whitening) for g in vecs]
+    X = np.asarray(vecs, np.float32)
+    n, dim = X.shape
+    C = np.zeros((dim, dim), np.float32)
+    mean = np.zeros(dim, np.float32)
+    iu = np.triu_indices(dim)
+    for f in X:  # addData: sequential float accumulation, one vector at a time (the whole
+        if mean_flg:  # square: f_j f_i == f_i f_j, so its upper triangle is addData's)
+            mean += f
+        C += np.outer(f, f)
+    inv = 1.0 / float(n)  # solve: const double inv_nsample
+    C[iu] = (C[iu].astype(np.float64) * inv).astype(np.float32)
+    C = np.triu(C) + np.triu(C, 1).T
+    if mean_flg:
+        mean = (mean.astype(np.float64) * inv).astype(np.float32)
+        C = (C - np.outer(mean, mean).astype(np.float32)).astype(np.float32)
+    if reg is not None:
+        C[np.diag_indices(dim)] += np.float32(reg)
+    w, V = np.linalg.eigh(C)  # float32 in, float32 out
+    order = sort_desc(w)
+    return V[:, order], w[order], (mean if mean_flg else None), n, C
+
+
 def sort_desc(vals):
     """sortVecAndVal's index order: bubble sort swapping only on strict '<' (stable)."""
     idx = list(range(len(vals)))
