@@ -510,8 +510,209 @@ __global__ __launch_bounds__(kBlock, 3) void score_mfma_f16_kernel(SparseSearch 
   }
 }
 
+// fp16 projection for models of r >= 16 (a 32-column tile then meets at most 3 models),
+// basis-stationary: a workgroup of 8 waves holds one model group's whole f16 basis in LDS
+// (loaded once; the host picks the fewest groups whose columns fit, 63 x r = 70 -> 8 groups
+// of <= 8 models, 134 KB) and streams listed positions through it, 32 per wave at a time
+// (their f16 rows in registers, the next set's rows loaded during this set's sweep).  Per
+// 32-column tile: KQ ds_read_b128 of B fragments (column stride 2 KH + 16 bytes: the 16
+// lanes of a read hit distinct banks) and KQ MFMAs formed transposed (rows = basis columns,
+// columns = positions), so lane (l32, hk) holds position l32's products with columns
+// i(q) = (q & 3) + 8 (q >> 2) + 4 hk; their squares are summed per model slot in registers,
+// the two lane halves combined with one exchange, and a model's |Q_m f|^2 completes at its
+// last column.  No global traffic in the sweep, no barrier after the basis load.
+// x + the same variable of lane ^ 32 (one v_permlane32_swap: each lane gets its own value
+// and its partner's, in either order; a + b == b + a, so both halves hold the same sum)
+__device__ __forceinline__ float sum_half_pair(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float max_half_pair(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+constexpr int kSSW = 8;                 // waves per workgroup
+constexpr int kSSP = 32 * kSSW;         // listed positions per workgroup step
+constexpr size_t kSSLds = 152 * 1024;   // LDS bytes for a group's basis
+__host__ __device__ constexpr int ss_rs(int KQ) { return 2 * 16 * KQ + 16; }  // bytes per basis column
+
+template <int KQ>
+__global__ __launch_bounds__(64 * kSSW, 1) void score_mfma_f16s_kernel(SparseSearch a, int ngroups) {
+  constexpr int KH = 16 * KQ;
+  constexpr int RS = ss_rs(KQ);
+  extern __shared__ __attribute__((aligned(16))) uint8_t sss[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hk = lane >> 5, l32 = lane & 31;
+  const int D = a.D, r = a.r, Qs = a.Opad;
+  const int g = blockIdx.y;
+  const int m0 = (int)((int64_t)g * a.M / ngroups), m1 = (int)((int64_t)(g + 1) * a.M / ngroups);
+  const int cb = m0 * r, ce = m1 * r;
+  const int ncols = ce - cb, ntile = (ncols + 31) / 32;
+  int64_t* s_mode = reinterpret_cast<int64_t*>(sss + (size_t)ntile * 32 * RS);
+  if (tid < a.nmodes) {
+    s_mode[3 * tid] = a.pstart[tid];
+    s_mode[3 * tid + 1] = a.md[tid].offset;
+    s_mode[3 * tid + 2] = a.md[tid].P;
+  }
+  // the group's basis, column c (< ntile * 32) at c * RS: 2 KQ 16-byte parts
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  for (int e = tid; e < ntile * 32 * 2 * KQ; e += 64 * kSSW) {
+    const int c = e / (2 * KQ), part = e - c * (2 * KQ);
+    const int gc = min(cb + c, Qs - 1);  // clamped: columns past the group are never folded
+    *reinterpret_cast<u4*>(sss + (size_t)c * RS + 16 * part) =
+        *reinterpret_cast<const u4*>(a.qt16 + (int64_t)gc * KH + 8 * part);
+  }
+  __syncthreads();
+  const int n = (int)a.cnt[a.epoch & 1];
+  // this wave's position sets: e0 = pb * kSSP + 32 * wave, pb = blockIdx.x, + gridDim.x, ...
+  const int step = gridDim.x * kSSP;
+  float v[KQ][8];
+  auto load_rows = [&](int e0) {
+    const int e = e0 + l32;
+    const long long en = e < n ? a.list[e] : 0;
+    const int mi = (int)(en >> 40);
+    const int64_t p = en & ((1ll << 40) - 1);
+    const float4* __restrict__ row = reinterpret_cast<const float4*>(a.gbox + (e < n ? (s_mode[3 * mi] + p) * D : 0));
+#pragma unroll
+    for (int s = 0; s < KQ; ++s)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {  // D % 4 == 0: a 4-float chunk is wholly inside or past the row
+        const int k = 16 * s + 8 * hk + 4 * h;
+        float4 x = row[min(k, D - 4) >> 2];  // unconditional (no branch per load), then masked
+        if (k >= D) x = make_float4(0.f, 0.f, 0.f, 0.f);
+        v[s][4 * h] = x.x;
+        v[s][4 * h + 1] = x.y;
+        v[s][4 * h + 2] = x.z;
+        v[s][4 * h + 3] = x.w;
+      }
+  };
+  int e0 = blockIdx.x * kSSP + 32 * wave;
+  if (e0 < n) load_rows(e0);
+  for (; e0 < n; e0 += step) {
+    // this set: scale (the power of two of score_mfma_f16_kernel) and round to f16
+    const int e = e0 + l32;
+    const bool valid = e < n;
+    float mx = 0.0f;
+#pragma unroll
+    for (int s = 0; s < KQ; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(v[s][j]));
+    mx = max_half_pair(mx);
+    int ex = 0;
+    (void)frexpf(mx, &ex);
+    mf_f16x8 av[KQ];
+    float ff = 0.0f;
+#pragma unroll
+    for (int s = 0; s < KQ; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const _Float16 h = (_Float16)ldexpf(v[s][j], -ex);
+        av[s][j] = h;
+        ff = __builtin_fmaf((float)h, (float)h, ff);
+      }
+    ff = sum_half_pair(ff);
+    int64_t sbase = 0, sP = 0;
+    {
+      const long long en = valid ? a.list[e] : 0;
+      const int mi = (int)(en >> 40);
+      sbase = s_mode[3 * mi + 1] + (en & ((1ll << 40) - 1));
+      sP = s_mode[3 * mi + 2];
+    }
+    if (e0 + step < n) load_rows(e0 + step);  // the next set's rows, in flight during the sweep
+    const uint8_t* bl = sss + (size_t)l32 * RS + 16 * hk;
+    auto tile_mfma = [&](int t, mf_f32x16& acc) {
+      mf_f16x8 bf[KQ];
+#pragma unroll
+      for (int s = 0; s < KQ; ++s) bf[s] = *reinterpret_cast<const mf_f16x8*>(bl + (size_t)t * 32 * RS + 32 * s);
+      // every fragment read is issued before the first MFMA waits on one: one LDS round
+      // trip per tile (interleaved read / MFMA pairs exposed it four times)
+#pragma unroll
+      for (int s = 0; s < KQ; ++s) __asm__ volatile("" : "+v"(bf[s]));
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+#pragma unroll
+      for (int s = 0; s < KQ; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(bf[s], av[s], acc, 0, 0, 0);
+    };
+    const float rf = 1.0f / __fsqrt_rn(ff);  // scores in float: within the fp16 tolerance
+    float q2 = 0.0f;
+    auto epilogue = [&](int t, const mf_f32x16& acc) {
+      const int c0 = cb + 32 * t;
+      const int ncol = min(32, ce - c0);
+      const int mA = c0 / r, b1 = (mA + 1) * r - c0, b2 = b1 + r;
+      float p0 = 0.0f, p1 = 0.0f, p2 = 0.0f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = (q & 3) + 8 * (q >> 2) + 4 * hk;
+        const float x = acc[q] * acc[q];
+        if (i < ncol) {
+          if (i < b1) p0 += x;
+          else if (i < b2) p1 += x;
+          else p2 += x;
+        }
+      }
+      p0 = sum_half_pair(p0);
+      p1 = sum_half_pair(p1);
+      p2 = sum_half_pair(p2);
+      q2 += p0;
+      if (b1 <= ncol) {  // model mA ends in this tile (uniform)
+        if (valid && hk == 0) a.scores[sbase + (int64_t)mA * sP] = (double)(__fsqrt_rn(q2) * rf);
+        q2 = p1;
+        if (b2 <= ncol) {  // r >= 16: model mA + 2 cannot end here too
+          if (valid && hk == 0) a.scores[sbase + (int64_t)(mA + 1) * sP] = (double)(__fsqrt_rn(q2) * rf);
+          q2 = p2;
+        }
+      }
+    };
+    // two accumulators in turn: tile t + 1's fragment reads and MFMAs are issued before tile
+    // t's epilogue reads its accumulator (no register copy waits on an MFMA in flight)
+    mf_f32x16 accA, accB;
+    tile_mfma(0, accA);
+    for (int t = 0; t < ntile; t += 2) {
+      if (t + 1 < ntile) tile_mfma(t + 1, accB);
+      epilogue(t, accA);
+      if (t + 1 < ntile) {
+        if (t + 2 < ntile) tile_mfma(t + 2, accA);
+        epilogue(t + 1, accB);
+      }
+    }
+  }
+}
+
+// fewest model groups whose padded columns fit kSSLds (0: none fits)
+int ss_groups(int M, int r, int KQ) {
+  for (int g = 1; g <= M; ++g) {
+    const int cols = (M + g - 1) / g * r;
+    if ((size_t)((cols + 31) / 32) * 32 * ss_rs(KQ) + 3 * 6 * sizeof(int64_t) <= kSSLds) return g;
+  }
+  return 0;
+}
+
+template <int KQ>
+hipError_t launch_score_mfma_f16s_kq(const SparseSearch& a, int ng, hipStream_t s) {
+  static thread_local int n_cu = 0, dev_c = -1;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev != dev_c) {
+    n_cu = 256;
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&score_mfma_f16s_kernel<KQ>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSSLds);
+    dev_c = dev;
+  }
+  const int cols = (a.M + ng - 1) / ng * a.r;
+  const size_t lds = (size_t)((cols + 31) / 32) * 32 * ss_rs(KQ) + 3 * 6 * sizeof(int64_t);
+  // one workgroup per CU over all groups (LDS holds one), each sweeping its positions
+  const int64_t pblocks = (a.pstart[a.nmodes] + kSSP - 1) / kSSP;
+  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(pblocks, std::max(1, n_cu / ng)));
+  score_mfma_f16s_kernel<KQ><<<dim3(gx, (unsigned)ng), 64 * kSSW, lds, s>>>(a, ng);
+  return hipGetLastError();
+}
+
 template <int KQ>
 hipError_t launch_score_mfma_f16_kq(const SparseSearch& a, hipStream_t s) {
+  if (a.r >= 16) {
+    const int ng = ss_groups(a.M, a.r, KQ);
+    if (ng > 0) return launch_score_mfma_f16s_kq<KQ>(a, ng, s);
+  }
   static thread_local int slots = 0, dev_c = -1;
   int dev = 0;
   (void)hipGetDevice(&dev);
