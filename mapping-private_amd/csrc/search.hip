@@ -201,8 +201,9 @@ __global__ __launch_bounds__(kBlock, 3) void compress_dma_kernel(CompressRows cr
   compress_mfma_dma_body(cr, blockIdx.x, gridDim.x, blockIdx.y, cd_smem, g_zero_word);
 }
 
-__global__ __launch_bounds__(kBlock) void compress_f16_kernel(CompressRows cr, const _Float16* PT16, int Fp16) {
-  compress_f16_body(cr, PT16, Fp16, blockIdx.x, gridDim.x, blockIdx.y);
+__global__ __launch_bounds__(kBlock, 3) void compress_f16_kernel(CompressRows cr, const _Float16* PT16, int Fp16) {
+  __shared__ __attribute__((aligned(16))) _Float16 cf_smem[kCFLds / 2];
+  compress_f16_body(cr, PT16, Fp16, blockIdx.x, gridDim.x, blockIdx.y, cf_smem);
 }
 
 __global__ __launch_bounds__(kBlock) void boxsum_kernel(SparseSearch a) {
@@ -512,15 +513,18 @@ __global__ __launch_bounds__(kBlock, 3) void score_mfma_f16_kernel(SparseSearch 
 
 // fp16 projection for models of r >= 16 (a 32-column tile then meets at most 3 models),
 // basis-stationary: a workgroup of 8 waves holds one model group's whole f16 basis in LDS
-// (loaded once; the host picks the fewest groups whose columns fit, 63 x r = 70 -> 8 groups
-// of <= 8 models, 134 KB) and streams listed positions through it, 32 per wave at a time
-// (their f16 rows in registers, the next set's rows loaded during this set's sweep).  Per
-// 32-column tile: KQ ds_read_b128 of B fragments (column stride 2 KH + 16 bytes: the 16
-// lanes of a read hit distinct banks) and KQ MFMAs formed transposed (rows = basis columns,
-// columns = positions), so lane (l32, hk) holds position l32's products with columns
-// i(q) = (q & 3) + 8 (q >> 2) + 4 hk; their squares are summed per model slot in registers,
-// the two lane halves combined with one exchange, and a model's |Q_m f|^2 completes at its
-// last column.  No global traffic in the sweep, no barrier after the basis load.
+// (loaded once; the host picks the fewest groups whose columns fit, 63 x r = 70 -> 7 groups
+// of 9 models, 145 KB) and streams listed positions through it, 32 per wave at a time
+// (their f16 rows in registers, the next set's rows loaded during this set's sweep).  Each
+// model's columns are padded to rp = r rounded up to 4 with zero basis rows, so the four
+// consecutive columns a lane holds per accumulator quad always belong to one model: the
+// epilogue is branch-free per lane (uniform branch on whether a model ends in the tile).
+// Per 32-column tile: KQ ds_read_b128 of B fragments (column stride 2 KH + 16 bytes: the
+// 16 lanes of a read hit distinct banks) and KQ MFMAs formed transposed (rows = basis
+// columns, columns = positions), so lane (l32, hk) holds position l32's products with
+// columns (q & 3) + 8 (q >> 2) + 4 hk; their squares accumulate per lane and the two lane
+// halves are combined with one exchange when a model completes.  No global traffic in the
+// sweep but the score stores, no barrier after the basis load.
 // x + the same variable of lane ^ 32 (one v_permlane32_swap: each lane gets its own value
 // and its partner's, in either order; a + b == b + a, so both halves hold the same sum)
 __device__ __forceinline__ float sum_half_pair(float x) {
@@ -535,6 +539,7 @@ constexpr int kSSW = 8;                 // waves per workgroup
 constexpr int kSSP = 32 * kSSW;         // listed positions per workgroup step
 constexpr size_t kSSLds = 152 * 1024;   // LDS bytes for a group's basis
 __host__ __device__ constexpr int ss_rs(int KQ) { return 2 * 16 * KQ + 16; }  // bytes per basis column
+__host__ __device__ constexpr int ss_rp(int r) { return (r + 3) & ~3; }       // padded model columns
 
 template <int KQ>
 __global__ __launch_bounds__(64 * kSSW, 1) void score_mfma_f16s_kernel(SparseSearch a, int ngroups) {
@@ -542,24 +547,25 @@ __global__ __launch_bounds__(64 * kSSW, 1) void score_mfma_f16s_kernel(SparseSea
   constexpr int RS = ss_rs(KQ);
   extern __shared__ __attribute__((aligned(16))) uint8_t sss[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hk = lane >> 5, l32 = lane & 31;
-  const int D = a.D, r = a.r, Qs = a.Opad;
+  const int D = a.D, r = a.r, rp = ss_rp(a.r);
   const int g = blockIdx.y;
   const int m0 = (int)((int64_t)g * a.M / ngroups), m1 = (int)((int64_t)(g + 1) * a.M / ngroups);
-  const int cb = m0 * r, ce = m1 * r;
-  const int ncols = ce - cb, ntile = (ncols + 31) / 32;
+  const int ncols = (m1 - m0) * rp, ntile = (ncols + 31) / 32;
   int64_t* s_mode = reinterpret_cast<int64_t*>(sss + (size_t)ntile * 32 * RS);
   if (tid < a.nmodes) {
     s_mode[3 * tid] = a.pstart[tid];
     s_mode[3 * tid + 1] = a.md[tid].offset;
     s_mode[3 * tid + 2] = a.md[tid].P;
   }
-  // the group's basis, column c (< ntile * 32) at c * RS: 2 KQ 16-byte parts
+  // the group's basis, padded column c (< ntile * 32) at c * RS: 2 KQ 16-byte parts; model
+  // m0 + c / rp's basis row c % rp, zero past r and past the group
   typedef unsigned int u4 __attribute__((ext_vector_type(4)));
   for (int e = tid; e < ntile * 32 * 2 * KQ; e += 64 * kSSW) {
     const int c = e / (2 * KQ), part = e - c * (2 * KQ);
-    const int gc = min(cb + c, Qs - 1);  // clamped: columns past the group are never folded
-    *reinterpret_cast<u4*>(sss + (size_t)c * RS + 16 * part) =
-        *reinterpret_cast<const u4*>(a.qt16 + (int64_t)gc * KH + 8 * part);
+    const int mm = c / rp, ii = c - mm * rp;
+    u4 x = {0u, 0u, 0u, 0u};
+    if (ii < r && m0 + mm < m1) x = *reinterpret_cast<const u4*>(a.qt16 + (int64_t)((m0 + mm) * r + ii) * KH + 8 * part);
+    *reinterpret_cast<u4*>(sss + (size_t)c * RS + 16 * part) = x;
   }
   __syncthreads();
   const int n = (int)a.cnt[a.epoch & 1];
@@ -627,39 +633,49 @@ __global__ __launch_bounds__(64 * kSSW, 1) void score_mfma_f16s_kernel(SparseSea
       // trip per tile (interleaved read / MFMA pairs exposed it four times)
 #pragma unroll
       for (int s = 0; s < KQ; ++s) __asm__ volatile("" : "+v"(bf[s]));
+      const mf_f32x16 zero = {};
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(bf[0], av[0], zero, 0, 0, 0);
 #pragma unroll
-      for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
-#pragma unroll
-      for (int s = 0; s < KQ; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(bf[s], av[s], acc, 0, 0, 0);
+      for (int s = 1; s < KQ; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(bf[s], av[s], acc, 0, 0, 0);
     };
     const float rf = 1.0f / __fsqrt_rn(ff);  // scores in float: within the fp16 tolerance
-    float q2 = 0.0f;
+    const bool emit = valid && hk == 0;
+    float q2 = 0.0f;  // this lane's share of the current model's |Q f|^2
+    auto finish = [&](int m, float x) {
+      const float tot = sum_half_pair(x);
+      if (emit) a.scores[sbase + (int64_t)(m0 + m) * sP] = (double)(__fsqrt_rn(tot) * rf);
+    };
     auto epilogue = [&](int t, const mf_f32x16& acc) {
-      const int c0 = cb + 32 * t;
-      const int ncol = min(32, ce - c0);
-      const int mA = c0 / r, b1 = (mA + 1) * r - c0, b2 = b1 + r;
+      float sq[4];  // this lane's quad j: columns 32 t + 8 j + 4 hk + 0..3, one model
+      typedef float f2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {  // packed: register pairs (4j, 4j+1), (4j+2, 4j+3)
+        const f2 x = {acc[4 * j], acc[4 * j + 1]}, y = {acc[4 * j + 2], acc[4 * j + 3]};
+        const f2 s2 = __builtin_elementwise_fma(y, y, x * x);
+        sq[j] = s2.x + s2.y;
+      }
+      const int c0 = 32 * t, mA = c0 / rp, b1 = (mA + 1) * rp - c0;  // uniform
+      if (b1 > 32) {  // no model ends in this tile
+        q2 += (sq[0] + sq[1]) + (sq[2] + sq[3]);
+        return;
+      }
+      // quads before b1 close model mA, quads in [b1, b1 + rp) go to mA + 1, the rest to
+      // mA + 2 (r >= 16: at most two boundaries in 32 columns; a model may end exactly at
+      // the tile's end, the group's last one always ends in the last tile)
+      const int t1 = b1 - 4 * hk, t2 = t1 + rp;
       float p0 = 0.0f, p1 = 0.0f, p2 = 0.0f;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int i = (q & 3) + 8 * (q >> 2) + 4 * hk;
-        const float x = acc[q] * acc[q];
-        if (i < ncol) {
-          if (i < b1) p0 += x;
-          else if (i < b2) p1 += x;
-          else p2 += x;
-        }
+      for (int j = 0; j < 4; ++j) {
+        const bool in0 = 8 * j < t1, in1 = 8 * j < t2;
+        p0 += in0 ? sq[j] : 0.0f;
+        p1 += (!in0 && in1) ? sq[j] : 0.0f;
+        p2 += in1 ? 0.0f : sq[j];
       }
-      p0 = sum_half_pair(p0);
-      p1 = sum_half_pair(p1);
-      p2 = sum_half_pair(p2);
-      q2 += p0;
-      if (b1 <= ncol) {  // model mA ends in this tile (uniform)
-        if (valid && hk == 0) a.scores[sbase + (int64_t)mA * sP] = (double)(__fsqrt_rn(q2) * rf);
-        q2 = p1;
-        if (b2 <= ncol) {  // r >= 16: model mA + 2 cannot end here too
-          if (valid && hk == 0) a.scores[sbase + (int64_t)(mA + 1) * sP] = (double)(__fsqrt_rn(q2) * rf);
-          q2 = p2;
-        }
+      if (m0 + mA < m1) finish(mA, q2 + p0);
+      q2 = p1;
+      if (b1 + rp <= 32) {
+        if (m0 + mA + 1 < m1) finish(mA + 1, q2);
+        q2 = p2;
       }
     };
     // two accumulators in turn: tile t + 1's fragment reads and MFMAs are issued before tile
@@ -680,7 +696,7 @@ __global__ __launch_bounds__(64 * kSSW, 1) void score_mfma_f16s_kernel(SparseSea
 // fewest model groups whose padded columns fit kSSLds (0: none fits)
 int ss_groups(int M, int r, int KQ) {
   for (int g = 1; g <= M; ++g) {
-    const int cols = (M + g - 1) / g * r;
+    const int cols = (M + g - 1) / g * ss_rp(r);
     if ((size_t)((cols + 31) / 32) * 32 * ss_rs(KQ) + 3 * 6 * sizeof(int64_t) <= kSSLds) return g;
   }
   return 0;
@@ -698,7 +714,7 @@ hipError_t launch_score_mfma_f16s_kq(const SparseSearch& a, int ng, hipStream_t 
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSSLds);
     dev_c = dev;
   }
-  const int cols = (a.M + ng - 1) / ng * a.r;
+  const int cols = (a.M + ng - 1) / ng * ss_rp(a.r);
   const size_t lds = (size_t)((cols + 31) / 32) * 32 * ss_rs(KQ) + 3 * 6 * sizeof(int64_t);
   // one workgroup per CU over all groups (LDS holds one), each sweeping its positions
   const int64_t pblocks = (a.pstart[a.nmodes] + kSSP - 1) / kSSP;

@@ -332,16 +332,21 @@ __device__ __forceinline__ void compress_mfma_dma_body(const CompressRows& cr, i
 }
 
 // fp16 variant of the matrix-core compress (c3h_set_search_precision): the normalised
-// features are rounded to f16 on load, the whitened axis is kept as f16 (PT16: 128
-// columns x Fp16 = F rounded up to 16, column-major so a lane's 8 consecutive k are one
-// 16-B load), products accumulate in f32 on v_mfma_f32_32x32x16_f16.  No LDS: each wave
-// reads its 32 rows' features and the (L2-resident) f16 axis straight into its operand
-// registers, one k step ahead.  Stated tolerance: scores within 2e-3 relative of the
-// float64 oracle (tests/test_gpu_parity.py::test_config5_dense_512_periodic).
+// features are rounded to f16, the whitened axis is kept as f16 (PT16: 128 columns x
+// Fp16 = F rounded up to 16, column-major), products accumulate in f32 on
+// v_mfma_f32_32x32x16_f16.  Workgroup = 128 rows; k runs in chunks of 64 staged through
+// LDS: each wave-wide load reads 64 consecutive floats of ONE row (256 coalesced bytes,
+// not 64 rows' scattered dwords), the next chunk's loads are in flight in registers while
+// the matrix cores consume the current one.  Stated tolerance: scores within 2e-3
+// relative of the float64 oracle (tests/test_gpu_parity.py::test_config5_dense_512_periodic).
 typedef _Float16 mf_f16x8 __attribute__((ext_vector_type(8)));
+constexpr int kCFK = 64;             // k per LDS chunk
+constexpr int kCFS = kCFK + 8;       // LDS row stride in halves (144 B: conflict-free b128 reads)
+constexpr int kCFRows = kMR / 4;     // rows of one wave's loads (= the wave's 32 A rows)
+constexpr int kCFLds = 2 * 128 * kCFS * 2;  // A (128 rows) + B (128 columns), bytes
 
 __device__ __forceinline__ void compress_f16_body(const CompressRows& cr, const _Float16* __restrict__ PT16,
-                                                  int Fp16, int bid, int nblk, int64_t f) {
+                                                  int Fp16, int bid, int nblk, int64_t f, _Float16* smem) {
   const float* __restrict__ feat = cr.feat + f * cr.s_feat;
   const float* __restrict__ fmax = cr.fmax;
   float* __restrict__ G = cr.G + f * cr.s_G;
@@ -349,56 +354,68 @@ __device__ __forceinline__ void compress_f16_body(const CompressRows& cr, const 
   const int F = cr.F, D = cr.D, fmax_len = cr.fmax_len;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = (int)cr.nrows[f * cr.s_nrows];
-  const int kh = 8 * (lane >> 5);
+  const int nch = (Fp16 + kCFK - 1) / kCFK;
+  _Float16* As = smem;               // [128 rows][kCFS]
+  _Float16* Bs = smem + 128 * kCFS;  // [128 columns][kCFS]
+  const bool ident = n == cr.H;
   for (int r0 = bid * kMR; r0 < n; r0 += nblk * kMR) {
     // every subdivision listed (dense frame): the list is a permutation of 0..H-1, so row
     // block r0 covers subdivisions r0.. in memory order instead (contiguous feature rows)
-    const bool ident = n == cr.H;
     const int myrow = r0 + wave * 32 + (lane & 31);
-    const int64_t abase = myrow < n ? (int64_t)(ident ? myrow : rows[myrow]) * F : -1;
-    auto load_a = [&](int k0, mf_f16x8& av) {
+    const int hrow = myrow < n ? (ident ? myrow : rows[myrow]) : -1;  // lane j: the wave's row j
+    float areg[kCFRows];
+    uint4 breg[4];
+    auto fetch = [&](int c) {
+      const int k = c * kCFK + lane;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = k0 + kh + j;
-        float v = 0.0f;
-        if (abase >= 0 && k < F) {
-          v = feat[abase + k];
-          if (k < fmax_len) {  // setData max-normalisation (search.cpp:563-570)
-            const float mx = fmax[k];
-            if (mx == 0.0f) v = 0.0f;
-            else if (v == mx) v = 1.0f;
-            else v = __fdiv_rn(v, mx);
-          }
-        }
-        av[j] = (_Float16)v;
+      for (int j = 0; j < kCFRows; ++j) {
+        const int h = __builtin_amdgcn_readlane(hrow, j);
+        areg[j] = (h >= 0 && k < F) ? __builtin_nontemporal_load(feat + (int64_t)h * F + k) : 0.0f;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int pc = tid + kBlock * i, col = pc >> 3, kk = c * kCFK + (pc & 7) * 8;
+        breg[i] = kk < Fp16 ? *reinterpret_cast<const uint4*>(PT16 + (int64_t)col * Fp16 + kk) : make_uint4(0, 0, 0, 0);
       }
     };
-    auto load_b = [&](int k0, mf_f16x8 (&bv)[4]) {
+    auto stage = [&](int c) {
+      const int k = c * kCFK + lane;
+      float mx = 1.0f;
+      const bool norm = k < fmax_len;  // setData max-normalisation (search.cpp:563-570)
+      if (norm) mx = fmax[k];
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-        bv[t] = *reinterpret_cast<const mf_f16x8*>(PT16 + (int64_t)(32 * t + (lane & 31)) * Fp16 + k0 + kh);
+      for (int j = 0; j < kCFRows; ++j) {
+        float v = areg[j];
+        if (norm) v = mx == 0.0f ? 0.0f : (v == mx ? 1.0f : __fdiv_rn(v, mx));
+        As[(wave * 32 + j) * kCFS + lane] = (_Float16)v;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int pc = tid + kBlock * i;
+        *reinterpret_cast<uint4*>(Bs + (pc >> 3) * kCFS + (pc & 7) * 8) = breg[i];
+      }
     };
     mf_f32x16 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[t][q] = 0.0f;
-    mf_f16x8 a_cur, b_cur[4];
-    load_a(0, a_cur);
-    load_b(0, b_cur);
-    for (int k0 = 0; k0 < Fp16; k0 += 16) {
-      mf_f16x8 a_nxt, b_nxt[4];
-      const bool more = k0 + 16 < Fp16;
-      if (more) {
-        load_a(k0 + 16, a_nxt);
-        load_b(k0 + 16, b_nxt);
-      }
+    fetch(0);
+    const _Float16* arow = As + (wave * 32 + (lane & 31)) * kCFS + 8 * (lane >> 5);
+    const _Float16* bcol = Bs + (lane & 31) * kCFS + 8 * (lane >> 5);
+    for (int c = 0; c < nch; ++c) {
+      __syncthreads();  // every wave is done reading chunk c - 1
+      stage(c);
+      __syncthreads();
+      if (c + 1 < nch) fetch(c + 1);  // in flight while the matrix cores run
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_cur, b_cur[t], acc[t], 0, 0, 0);
-      if (more) {
-        a_cur = a_nxt;
+      for (int s = 0; s < kCFK / 16; ++s) {
+        const mf_f16x8 av = *reinterpret_cast<const mf_f16x8*>(arow + 16 * s);
+        mf_f16x8 bv[4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) b_cur[t] = b_nxt[t];
+        for (int t = 0; t < 4; ++t) bv[t] = *reinterpret_cast<const mf_f16x8*>(bcol + 32 * t * kCFS + 16 * s);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bv[t], acc[t], 0, 0, 0);
       }
     }
 #pragma unroll
