@@ -545,6 +545,10 @@ struct c3h_ctx {
   int pb_acc_slots = 0;
   c3h::DevBuf<float> pb_stage;
   c3h::DevBuf<c3h::VoxFrameRec> pb_info;
+  // the batched voxeliser runs on its own stream, one batch ahead of the tick that consumes
+  // it (events: a batch's voxels are done / the tick that last read a buffer set is done)
+  hipStream_t pb_vstream = nullptr;
+  hipEvent_t pb_vox_ev = nullptr, pb_tick_ev[4] = {nullptr, nullptr, nullptr, nullptr};
 
   std::vector<PipeBatch> pipe;   // in flight, oldest first
   uint64_t pipe_seq = 0;

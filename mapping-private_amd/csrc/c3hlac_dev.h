@@ -178,12 +178,13 @@ __device__ __forceinline__ void occ_flush_bits(const uint32_t* s_bits, int nword
     const uint32_t m = wi < nwords ? s_bits[wi] : 0u;
     int total;
     const int base = block_excl_scan(__popc(m), s_wsum, &total);
+    uint32_t mm = m;  // this thread's bits not yet listed (slices take them in order)
+    int idx = base;
     for (int l0 = 0; l0 < total; l0 += kOccSet) {  // list slices of kOccSet tiles
-      uint32_t mm = m;
-      for (int idx = base; mm; ++idx) {
+      for (; mm && idx < l0 + kOccSet; ++idx) {  // each bit visited once over all slices
         const int bit = __ffs(mm) - 1;
         mm &= mm - 1;
-        if (idx >= l0 && idx < l0 + kOccSet) s_list[idx - l0] = wi * 32 + bit;
+        s_list[idx - l0] = wi * 32 + bit;
       }
       __syncthreads();
       const int nl = min(total - l0, kOccSet);

@@ -42,7 +42,7 @@ constexpr int kMfCh = 12;
 constexpr int kMfK = 14;    // 13 offsets + the centre's own channels
 constexpr int kMfLoad = 2;  // (row, dword) items per lane of a layer (<= 18 rows x 5 dwords)
 #ifndef C3H_MF_EXP
-#define C3H_MF_EXP 0  // diagnostics variants: 1 no K steps, 2 no conversion
+#define C3H_MF_EXP 0  // diagnostics variants: 1 no K steps, 2 no conversion, 4 no bin epilogue
 #endif
 
 __host__ __device__ inline int mf_pitch(int lx) { return (lx + 2 + 3) & ~3; }
@@ -341,14 +341,28 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
 #pragma unroll
     for (int r = 0; r < 4; ++r) rs[r] = (uint32_t)__shfl(acc[13][r], 16 * h4 + 15, 64);
     const uint32_t k2 = 16384u * pos;
+#if C3H_MF_EXP & 4
+    {  // diagnostics: no bin epilogue (one word keeps the accumulators live)
+      uint32_t x = k2;
+#pragma unroll
+      for (int k = 0; k < kMfK; ++k) x ^= (uint32_t)(acc[k][0] + acc[k][1] + acc[k][2] + acc[k][3]);
+      ffeat[h * F + lane] = (float)x;
+      continue;
+    }
+#endif
     if (a.atomic || F == 981) {
       float* out = ffeat + h * F;
       unsigned long long* hacc = a.atomic ? facc + h * 981 : nullptr;
+      // 981 rows are staged in the wave's (now idle) plane slots and stored coalesced: a
+      // lane's bins are scattered over the row, 56 scattered dword stores per lane were
+      // ~0.25 ms of a 512^3 frame
+      float* sf = reinterpret_cast<float*>(wl);
+      mf_compiler_fence();
       auto emit = [&](int bin, uint32_t v) {
         if (hacc) {
           if (v) atomicAdd(&hacc[bin], (unsigned long long)v);
         } else {
-          out[bin] = (float)v * norm981(bin);
+          sf[bin] = (float)v * norm981(bin);
         }
       };
 #pragma unroll
@@ -373,6 +387,12 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
             emit(tc ? 495 + cc : cc, rs[r] + 128u * pos);
           }
         }
+      }
+      if (!hacc) {
+        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's bins are in LDS
+        __builtin_amdgcn_wave_barrier();
+        for (int i = lane; i < 981; i += 64) out[i] = sf[i];
+        mf_compiler_fence();  // the next tile's planes overwrite sf after these reads
       }
     } else {  // 117: first-order bins summed over the 13 offsets (color_chlac.hpp:1647-1743)
       float* out = ffeat + h * F;

@@ -81,8 +81,9 @@ struct Timed {
   c3h::Timer* T;
   int slot, weight;
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
-  Timed(c3h_ctx* c, int s, int w = 1)
-      : ctx(c), T(c->parent ? &c->parent->timer : &c->timer), slot(s), weight(w) {
+  hipStream_t st;
+  Timed(c3h_ctx* c, int s, int w = 1, hipStream_t on = nullptr)
+      : ctx(c), T(c->parent ? &c->parent->timer : &c->timer), slot(s), weight(w), st(on ? on : c->stream) {
     if (!(T->mask >> (s + 1) & 1) || c->capture) return;
     std::lock_guard<std::mutex> g(T->mu);
     if (T->pool.empty()) {
@@ -96,11 +97,11 @@ struct Timed {
     }
     ev = T->pool.back();
     T->pool.pop_back();
-    (void)hipEventRecord(ev.first, ctx->stream);  // on the stream the kernels run on
+    (void)hipEventRecord(ev.first, st);  // on the stream the kernels run on
   }
   ~Timed() {
     if (!ev.first) return;
-    (void)hipEventRecord(ev.second, ctx->stream);
+    (void)hipEventRecord(ev.second, st);
     std::lock_guard<std::mutex> g(T->mu);
     T->pending[slot].push_back(c3h::TimedPair{ev.first, ev.second, weight});
   }
@@ -644,6 +645,13 @@ void c3h_destroy(c3h_ctx* ctx) {
   for (hipEvent_t e : ctx->lane_ev) (void)hipEventDestroy(e);
   if (ctx->fork_ev) (void)hipEventDestroy(ctx->fork_ev);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->pb_vstream) {
+    (void)hipStreamSynchronize(ctx->pb_vstream);
+    (void)hipStreamDestroy(ctx->pb_vstream);
+  }
+  if (ctx->pb_vox_ev) (void)hipEventDestroy(ctx->pb_vox_ev);
+  for (hipEvent_t e : ctx->pb_tick_ev)
+    if (e) (void)hipEventDestroy(e);
   release(ctx->grid);
   release(ctx->pts);
   release(ctx->raw);
@@ -2239,6 +2247,35 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
       ctx->pb_acc_slots = B;
     }
     ENSURE(ctx->pb_info, (size_t)nframes);
+    // shared buffers sized for the largest batch up front: the voxeliser stream may still be
+    // reading them while the next batch is prepared
+    {
+      int64_t max_blk = 1, max_pts = 1;
+      for (int ch = 0; ch < nchunks; ++ch) {
+        int64_t b = 0, q = 0;
+        for (int j = ch * B; j < std::min(nframes, (ch + 1) * B); ++j) {
+          b += std::max<int64_t>(1, (n[j] + chunk - 1) / chunk);
+          q += n[j];
+        }
+        max_blk = std::max(max_blk, b);
+        max_pts = std::max(max_pts, q);
+      }
+      if (max_blk > INT_MAX / chunk) return fail(ctx, C3H_ERR_RANGE, "c3h_run_point_frames: batch too large");
+      ENSURE(ctx->pb_vlist, (size_t)max_blk * chunk);
+      if (!on_device) ENSURE(ctx->pb_stage, (size_t)max_pts * 4);
+    }
+    if (!ctx->pb_vstream) HIPCHK(hipStreamCreateWithFlags(&ctx->pb_vstream, hipStreamNonBlocking));
+    if (!ctx->pb_vox_ev) HIPCHK(hipEventCreateWithFlags(&ctx->pb_vox_ev, hipEventDisableTiming));
+    for (hipEvent_t& e : ctx->pb_tick_ev)
+      if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    // overlap pays where the tick is light: 512 x 128^3 frames 51k -> 74k frames/s, while at
+    // 256^3 the tick's 67 MB grid stream and the voxeliser's atomics slow each other down
+    // (33k -> 30k; profiles/r3/points_overlap/), so large canvases stay on one stream
+    const bool overlap = cvox <= ((int64_t)1 << 22);
+    const hipStream_t vs = overlap ? ctx->pb_vstream : ctx->stream;
+    // the voxeliser stream starts after everything enqueued so far (the memsets above)
+    HIPCHK(hipEventRecord(ctx->pb_vox_ev, ctx->stream));
+    HIPCHK(hipStreamWaitEvent(vs, ctx->pb_vox_ev, 0));
     PipeScope scope(ctx);
     for (int ch = 0; ch < nchunks && rc >= 0; ++ch) {
       const int f0 = ch * B, nb = std::min(B, nframes - f0);
@@ -2257,32 +2294,33 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
       // canvas grids are then zeroed whole
       const int blk_cap = (int)std::min<int64_t>(c->pb_part.n / c3h::vox_part_words(), INT_MAX);
       if (c->pb_cvox != cvox || c->pb_slots < B || blk_cap < va.total) {
+        // (re)allocation: nothing in flight may still use the set's old buffers
+        HIPCHK(hipStreamSynchronize(vs));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
         const int bc = std::max(va.total, blk_cap);
         ENSURE(c->pb_grid, (size_t)B * cvox);
         ENSURE(c->pb_lim, (size_t)B * 4);
         ENSURE(c->pb_part, (size_t)bc * c3h::vox_part_words());
         ENSURE(c->pb_wlist, (size_t)bc * chunk);
-        HIPCHK(hipMemsetAsync(c->pb_grid.p, 0, (size_t)B * cvox * 4, ctx->stream));
+        HIPCHK(hipMemsetAsync(c->pb_grid.p, 0, (size_t)B * cvox * 4, vs));
         c->pb_cvox = cvox;
         c->pb_slots = B;
         c->pb_prev_total = 0;
         c->pb_prev_nf = 0;
       }
-      ENSURE(ctx->pb_vlist, (size_t)va.total * chunk);
       va.prev_nf = c->pb_prev_nf;
       va.prev_total = c->pb_prev_total;
       for (int j = 0; j <= c3h::kMaxBatch; ++j)
         va.prev_blk0[j] = j < (int)c->pb_prev_blk0.size() ? c->pb_prev_blk0[j] : va.prev_total;
       if (on_device) {
         for (int j = 0; j < nb; ++j) va.pts[j] = reinterpret_cast<const float4*>(pts[f0 + j]);
-      } else {  // host frames: one staging copy per batch, ordered on the stream
-        ENSURE(ctx->pb_stage, (size_t)std::max<int64_t>(npts_batch, 1) * 4);
+      } else {  // host frames: one staging copy per batch, ordered on the voxeliser stream
         int64_t o = 0;
         for (int j = 0; j < nb; ++j) {
           va.pts[j] = reinterpret_cast<const float4*>(ctx->pb_stage.p + 4 * o);
           if (n[f0 + j] > 0)
             HIPCHK(hipMemcpyAsync(ctx->pb_stage.p + 4 * o, pts[f0 + j], (size_t)n[f0 + j] * 16,
-                                  hipMemcpyHostToDevice, ctx->stream));
+                                  hipMemcpyHostToDevice, vs));
           o += n[f0 + j];
         }
       }
@@ -2310,10 +2348,16 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
         return fail(ctx, C3H_ERR_STATE, "c3h_run_point_frames: internal: frame slots");
       va.info = ctx->pb_info.p + f0;
       va.lim = c->pb_lim.p;
+      // the set's grids and gate limits were last read by the tick pushed two batches ago
+      // (tile role: one tick after the batch's own, gate role: two), so this batch's voxels
+      // overlap the previous batch's tick
+      if (ch >= 2) HIPCHK(hipStreamWaitEvent(vs, ctx->pb_tick_ev[(ch - 2) & 3], 0));
       {
-        Timed t(ctx, 0, nb);
-        HIPCHK(c3h::launch_vox_batch(va, ctx->stream));
+        Timed t(ctx, 0, nb, vs);
+        HIPCHK(c3h::launch_vox_batch(va, vs));
       }
+      HIPCHK(hipEventRecord(ctx->pb_vox_ev, vs));
+      HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->pb_vox_ev, 0));
       c->pb_prev_nf = nb;
       c->pb_prev_total = va.total;
       c->pb_prev_blk0.assign(va.blk0, va.blk0 + nb + 1);
@@ -2326,7 +2370,9 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
       rc = pipe_push(ctx, grids, outs, nb, k, c->pb_lim.p);
       if (rc == 0) rc = fail(ctx, C3H_ERR_STATE, "c3h_run_point_frames: the canvas does not fit the pipeline");
       if (rc > 0) nm = rc;
+      if (rc >= 0) HIPCHK(hipEventRecord(ctx->pb_tick_ev[ch & 3], ctx->stream));
     }
+    if (rc < 0) (void)hipStreamSynchronize(vs);
     while (rc >= 0 && !ctx->pipe.empty()) {
       const int trc = pipe_tick(ctx, nullptr);
       if (trc != C3H_OK) rc = trc;
