@@ -96,18 +96,57 @@ def make_grids(ctx, dev, nf, rank, synth, c3hlac, torch):
     return grids[:nf], t_vox_ms, n_points
 
 
+class _StagedGloo:
+    """Rehearsal of the multi-GPU path on a one-GPU box (C3H_BENCH_REHEARSAL=1): every rank
+    runs on device 0 and the collectives go over gloo, which has no GPU all_gather, so they
+    are staged through host memory.  Not a measurement: the driver's N > 1 runs use RCCL."""
+
+    def __init__(self, dist):
+        self.d = dist
+        self.ReduceOp = dist.ReduceOp
+
+    def all_gather(self, parts, buf):
+        host = [torch_mod().empty_like(buf, device="cpu") for _ in parts]
+        self.d.all_gather(host, buf.cpu())
+        for p, h in zip(parts, host):
+            p.copy_(h)
+
+    def all_reduce(self, t, op=None):
+        h = t.cpu()
+        self.d.all_reduce(h, op=op)
+        t.copy_(h)
+
+    def barrier(self):
+        self.d.barrier()
+
+    def destroy_process_group(self):
+        self.d.destroy_process_group()
+
+
+def torch_mod():
+    import torch
+    return torch
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    rehearsal = os.environ.get("C3H_BENCH_REHEARSAL") == "1" and world > 1
+    if rehearsal:
+        local = 0
     import torch
     dist = None
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearsal:
+            dist.init_process_group("gloo")
+            dist = _StagedGloo(dist)
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     import c3hlac
     from c3hlac import synth
