@@ -384,6 +384,7 @@ C3Args build_c3_args(const C3Launch& l) {
   oa.work = l.work;
   oa.s_tf = l.s_tf;
   oa.s_work = l.s_work;
+  oa.contiguous = 0;  // the tick keeps the rotated order (frames' occupancy varies with y)
   oa.ntiles = (int)l.ntiles;
   KArgs& a = c.ka;
   for (int f = 0; f < kMaxBatch; ++f) a.grids[f] = f < l.nframes ? l.grid[f] : nullptr;
@@ -466,6 +467,10 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
   C3Args c = build_c3_args(l);
   const bool mf = mfma_ok(l);
   c.ka.mfma = mf ? 1 : 0;
+#ifndef C3H_OCC_CONTIG
+#define C3H_OCC_CONTIG 1
+#endif
+  c.oa.contiguous = C3H_OCC_CONTIG && l.ntiles >= 65536 ? 1 : 0;  // large grids (config 5): contiguous chunk ranges
   const dim3 g1d((unsigned)c.g1, (unsigned)l.nframes);
   if (c.bits) {
     if (c.ax)

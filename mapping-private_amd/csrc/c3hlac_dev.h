@@ -124,6 +124,7 @@ struct OccArgs {
   uint32_t* tf;    // per frame: [2] reserved | [2] work counters | [ntiles] stamps
   int32_t* work;   // per frame: [ntiles]
   int64_t s_tf, s_work;
+  int contiguous;  // 1: workgroup b streams one contiguous chunk range (large stand-alone grids)
 };
 
 // Bitmap variant (every tile one bit of LDS, ntiles <= kOccBitsMax): an occupied centre
@@ -176,6 +177,7 @@ __device__ __forceinline__ void occ_flush_bits(const uint32_t* s_bits, int nword
   for (int w0 = 0; w0 < nwords; w0 += kBlock) {  // one bitmap word per thread per round
     const int wi = w0 + tid;
     const uint32_t m = wi < nwords ? s_bits[wi] : 0u;
+    if (!__syncthreads_or(m != 0u)) continue;  // no tile of these words touched (uniform)
     int total;
     const int base = block_excl_scan(__popc(m), s_wsum, &total);
     uint32_t mm = m;  // this thread's bits not yet listed (slices take them in order)
@@ -279,7 +281,12 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
     const int lg = gx == 256 ? 8 : gx == 512 ? 9 : 10;
     const int64_t nch = (n4 + kChunk4 - 1) / kChunk4;
     uint4 w[kOccBitsUnroll];
-    auto chunk_of = [&](int64_t i) { return i * gdx + (bx + i) % gdx; };
+    // large stand-alone grids: contiguous ranges (a tile's 10 planes meet few workgroups,
+    // so the flush stamps each tile ~2.5x fewer times on a dense 512^3 frame)
+    const int64_t per = (nch + gdx - 1) / gdx;
+    auto chunk_of = [&](int64_t i) {
+      return oa.contiguous ? (i < per ? bx * per + i : nch) : i * gdx + (bx + i) % gdx;
+    };
     if (kOccPipe && chunk_of(0) < nch) load_chunk(w, chunk_of(0) * kChunk4);
     for (int64_t i = 0; i * gdx < nch; ++i) {
       const int64_t cidx = chunk_of(i);
@@ -326,7 +333,7 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
             const int t = tx0[k] + tyz;
             if (ws[k] && tx0[k] >= 0 && t != last) {
               last = t;
-              atomicOr(&s_bits[t >> 5], 1u << (t & 31));  // result unused: ds_or_b32, no wait
+              atomicOr(&s_bits[t >> 5], 1u << (t & 31));
             }
           }
         }

@@ -2282,12 +2282,10 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
       c3h_ctx* c = pipe_set(ctx, ctx->pipe_seq);
       c3h::VoxBatchArgs va{};
       va.nf = nb;
-      int64_t npts_batch = 0;
       va.blk0[0] = 0;
       for (int j = 0; j < nb; ++j) {  // every frame at least one block: it publishes the record
         va.n[j] = n[f0 + j];
         va.blk0[j + 1] = va.blk0[j] + (int)std::max<int64_t>(1, (n[f0 + j] + chunk - 1) / chunk);
-        npts_batch += n[f0 + j];
       }
       va.total = va.blk0[nb];
       // this set's buffers; a reallocation loses the previous batch's word lists, so the

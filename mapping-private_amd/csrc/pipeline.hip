@@ -60,15 +60,34 @@ __device__ __forceinline__ int tick_canonical_block(const TickArgs& t) {
   return b;
 }
 
+// wave priorities per role (s_setprio; 0 = the default): the arbiter of a SIMD picks the
+// highest-priority ready wave
+#ifndef C3H_TICK_PRIO_OCC
+#define C3H_TICK_PRIO_OCC 0
+#endif
+#ifndef C3H_TICK_PRIO_TILE
+#define C3H_TICK_PRIO_TILE 0
+#endif
+#ifndef C3H_TICK_PRIO_CG
+#define C3H_TICK_PRIO_CG 0
+#endif
+#ifndef C3H_TICK_PRIO_SCORE
+#define C3H_TICK_PRIO_SCORE 0
+#endif
+#define C3H_SETPRIO(p) \
+  if constexpr ((p) > 0) __builtin_amdgcn_s_setprio(p)
+
 __device__ __forceinline__ void tick_roles(const TickArgs& t, uint32_t* tick_smem) {
   int b = t.order == 0x3210 ? (int)blockIdx.x : tick_canonical_block(t);
   if (b < t.n_occ) {
+    C3H_SETPRIO(C3H_TICK_PRIO_OCC);
     const int f = b / t.o_grid;
     occupancy_bits_body<true>(t.oa, b - f * t.o_grid, f, t.o_grid, tick_smem);
     return;
   }
   b -= t.n_occ;
   if (b < t.n_tile) {
+    C3H_SETPRIO(C3H_TICK_PRIO_TILE);
     const int f = b / t.t_grid;
     if (t.ka.wave117) c3hlac_wave117_body(t.ka, b - f * t.t_grid, f, t.t_grid, tick_smem);
     else c3hlac_tile_body(t.ka, b - f * t.t_grid, f, t.t_grid, tick_smem);
@@ -76,12 +95,14 @@ __device__ __forceinline__ void tick_roles(const TickArgs& t, uint32_t* tick_sme
   }
   b -= t.n_tile;
   if (b < t.n_cg) {
+    C3H_SETPRIO(C3H_TICK_PRIO_CG);
     const int per = t.g_ngate + t.g_ncomp, f = b / per, r = b - f * per;
     if (r < t.g_ngate) gate_body(t.gq, r, f);
     else compress_rows_body(t.cr, r - t.g_ngate, t.g_ncomp, f, reinterpret_cast<float*>(tick_smem));
     return;
   }
   b -= t.n_cg;
+  C3H_SETPRIO(C3H_TICK_PRIO_SCORE);
   const int per = t.s_gx * t.s_groups, f = b / per, r = b - f * per;
   score_list_body(t.sq, r % t.s_gx, r / t.s_gx, f, t.s_gx, t.s_groups, reinterpret_cast<float*>(tick_smem));
 }
