@@ -189,16 +189,9 @@ __global__ __launch_bounds__(kBlock) void compress_gate_kernel(CompressRows cr, 
   else compress_rows_body(cr, blockIdx.x - ngate, gridDim.x - ngate, blockIdx.y, cg_smem);
 }
 
-__global__ __launch_bounds__(kBlock) void compress_mfma_kernel(CompressRows cr) {
-  extern __shared__ __attribute__((aligned(16))) float cm_smem[];
-  compress_mfma_body(cr, blockIdx.x, gridDim.x, blockIdx.y, cm_smem);
-}
-
-__device__ float g_zero_word[4];  // zero-initialised: the DMA source of padding lanes
-
-__global__ __launch_bounds__(kBlock, 3) void compress_dma_kernel(CompressRows cr) {
-  extern __shared__ __attribute__((aligned(16))) float cd_smem[];
-  compress_mfma_dma_body(cr, blockIdx.x, gridDim.x, blockIdx.y, cd_smem, g_zero_word);
+__global__ __launch_bounds__(kBlock, 3) void compress_f32c_kernel(CompressRows cr) {
+  extern __shared__ __attribute__((aligned(16))) float cc_smem[];
+  compress_f32c_body(cr, blockIdx.x, gridDim.x, blockIdx.y, cc_smem);
 }
 
 __global__ __launch_bounds__(kBlock, 3) void compress_f16_kernel(CompressRows cr, const _Float16* PT16, int Fp16) {
@@ -1028,34 +1021,28 @@ hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc,
         gate_kernel<<<dim3(ngate, nf), kBlock, 0, s>>>(a);
         goto score;
       }
-      {
-      const bool dma = sc->fmax_len == 0;  // the DMA ring cannot normalise by feature_max
-      static thread_local int c_slots[2] = {0, 0}, c_dev = -1;
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      if (dev != c_dev) {
-        int n_cu = 256;
-        (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-        for (int v = 0; v < 2; ++v) {
-          int per_cu = 0;
-          const hipError_t e =
-              v ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, compress_dma_kernel, kBlock,
-                                                               compress_dma_lds_bytes())
-                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, compress_mfma_kernel, kBlock,
-                                                               compress_mfma_lds_bytes());
-          c_slots[v] = (e == hipSuccess && per_cu > 0 ? per_cu : 1) * n_cu;
+      {  // f32: row-coalesced LDS staging (3 workgroups per CU at 49 KB)
+        static thread_local int c_slots = 0, c_dev = -1;
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (dev != c_dev) {
+          int n_cu = 256, per_cu = 0;
+          (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&compress_f32c_kernel),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCLds);
+          if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, compress_f32c_kernel, kBlock, kCLds) != hipSuccess ||
+              per_cu < 1)
+            per_cu = 1;
+          c_slots = per_cu * n_cu;
+          c_dev = dev;
         }
-        c_dev = dev;
-      }
-      const int64_t rblocks = (sc->H + kMR - 1) / kMR;
-      const int64_t slots = std::max<int64_t>(1, c_slots[dma] / std::max(1u, nf));
-      const int64_t rounds = (rblocks + slots - 1) / slots;
-      const unsigned ncomp = (unsigned)std::min<int64_t>(rblocks, (rblocks + rounds - 1) / rounds);
-      if (dma)
-        compress_dma_kernel<<<dim3(ncomp, nf), kBlock, compress_dma_lds_bytes(), s>>>(cr);
-      else
-        compress_mfma_kernel<<<dim3(ncomp, nf), kBlock, compress_mfma_lds_bytes(), s>>>(cr);
-      gate_kernel<<<dim3(ngate, nf), kBlock, 0, s>>>(a);
+        // persistent: every workgroup resident (row blocks b, b + grid, ...), balanced rounds
+        const int64_t rblocks = (sc->H + kCR - 1) / kCR;
+        const int64_t slots = std::max<int64_t>(1, c_slots / std::max(1u, nf));
+        const int64_t rounds = (rblocks + slots - 1) / slots;
+        const unsigned ncomp = (unsigned)std::min<int64_t>(rblocks, (rblocks + rounds - 1) / rounds);
+        compress_f32c_kernel<<<dim3(ncomp, nf), kBlock, kCLds, s>>>(cr);
+        gate_kernel<<<dim3(ngate, nf), kBlock, 0, s>>>(a);
       }
     } else {
       const size_t lds = compress_rows_lds_bytes(sc->Dpad);

@@ -135,200 +135,112 @@ __device__ __forceinline__ void compress_rows_body(const CompressRows& cr, int b
   }
 }
 
-// Dense frames (tens of thousands of listed rows): the same G = f' * P on the f32 matrix
-// cores.  v_mfma_f32_32x32x2_f32 is bit-for-bit a k-ordered fmaf chain
-// (D = fma(a_k1, b_k1, fma(a_k0, b_k0, C))), so feeding j in ascending order gives the
-// VALU body's G exactly (one extra fma with a = 0 pads an odd F).  128 listed rows per
-// workgroup (wave = 32 rows x 4 column tiles of 32 = Dpad <= 128); per 32-feature chunk
-// the rows' feature slice and P's slice are staged in LDS (prefetched one chunk ahead in
-// registers), then 16 k-pair steps of 4 MFMAs (one A float, four B floats per lane).
-constexpr int kMR = 128, kMK = 16;
-constexpr int kMAS = kMK + 1;  // A slice row stride (lanes read 32 rows of one column)
-__host__ __device__ inline size_t compress_mfma_lds_bytes() {
-  return sizeof(float) * ((size_t)kMR * kMAS + (size_t)kMK * 128);
-}
+// Dense frames (tens of thousands of listed rows): the same G = f' * P on the matrix cores.
+// v_mfma_f32_32x32x2_f32 is bit-for-bit a k-ordered fmaf chain
+// (D = fma(a_k1, b_k1, fma(a_k0, b_k0, C))), so feeding k in ascending order gives the VALU
+// body's G exactly (zero products pad F to the chunk size: fma(0, 0, x) = x).
+constexpr int kMR = 128;  // rows per workgroup of the fp16 compress
 typedef float mf_f32x16 __attribute__((ext_vector_type(16)));
 
-__device__ __forceinline__ void compress_mfma_body(const CompressRows& cr, int bid, int nblk, int64_t f,
-                                                   float* csm) {
+// f32 matrix-core compress, row-coalesced (round 3; replaced an LDS-DMA ring whose 64-lane
+// loads touched four rows in 64-B pieces: 0.57 -> 0.41 ms at 512^3): ascending k pairs on
+// v_mfma_f32_32x32x2_f32 (G bit-identical to the VALU body), with
+// k in chunks of 64 staged in LDS from registers: every wave-wide feature load reads 64
+// consecutive floats of ONE row (256 B) instead of 16-float pieces of four rows, and the
+// next chunk's loads (the block's 64 rows, a 64 x 128 slice of P) are in flight in
+// registers while this chunk's MFMAs run.  64 rows per workgroup, wave (rw, cw) = 32 rows x
+// 2 column tiles: 32 accumulator registers per lane, so 3 waves per SIMD and 3 workgroups
+// per CU (49 KB of LDS each), and 2,197 row blocks of a 512^3 frame fill 768 slots in 2.9
+// rounds where 128-row blocks took 3 rounds of twice the work (1,099 over 512 slots).
+// Normalises by feature_max on the LDS store.
+constexpr int kCK = 64;                 // k per chunk
+constexpr int kCR = 64;                 // rows per workgroup
+constexpr int kCAS = kCK + 1;           // A row stride in floats (odd: conflict-free column reads)
+constexpr size_t kCLds = sizeof(float) * ((size_t)kCR * kCAS + (size_t)kCK * 128);
+
+__device__ __forceinline__ void compress_f32c_body(const CompressRows& cr, int bid, int nblk, int64_t f,
+                                                   float* smem) {
   const float* __restrict__ feat = cr.feat + f * cr.s_feat;
   const float* __restrict__ fmax = cr.fmax;
   float* __restrict__ G = cr.G + f * cr.s_G;
   const int32_t* __restrict__ rows = cr.rows + f * cr.s_rows;
   const int F = cr.F, D = cr.D, Dpad = cr.Dpad, fmax_len = cr.fmax_len;
-  float* sa = csm;                 // kMR x kMAS feature slice
-  float* sbm = csm + kMR * kMAS;   // kMK x 128 slice of P (columns >= Dpad zero)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rw = wave & 1, cw = wave >> 1;
   const int n = (int)cr.nrows[f * cr.s_nrows];
-  const int nch = (F + kMK - 1) / kMK;
-  constexpr int kFE = kMR * kMK / kBlock;   // feature-slice elements per thread (16)
-  constexpr int kPE = kMK * 128 / kBlock;   // P-slice elements per thread (16)
-  for (int r0 = bid * kMR; r0 < n; r0 += nblk * kMR) {
-    int64_t rbase[kFE / 4];  // 4 consecutive features per thread share a row
+  const int nch = (F + kCK - 1) / kCK;
+  float* As = smem;               // [kCR rows][kCAS]
+  float* Bs = smem + kCR * kCAS;  // [kCK][128]
+  const bool ident = n == cr.H;
+  for (int r0 = bid * kCR; r0 < n; r0 += nblk * kCR) {
+    // every subdivision listed (dense frame): rows in memory order (contiguous feature rows)
+    const int myrow = r0 + wave * 16 + (lane & 15);
+    const int hrow = myrow < n ? (ident ? myrow : rows[myrow]) : -1;  // lane j < 16: this wave's load row j
+    float areg[16];
+    float4 breg[8];
+    auto fetch = [&](int c) {
+      const int k = c * kCK + lane;
 #pragma unroll
-    for (int i = 0; i < kFE / 4; ++i) {
-      const int e = 4 * (tid + i * kBlock), r = e / kMK;
-      rbase[i] = r0 + r < n ? (int64_t)rows[r0 + r] * F : -1;
-    }
-    float fa[kFE], pb[kPE];
-    auto load = [&](int c) {
-#pragma unroll
-      for (int i = 0; i < kFE / 4; ++i) {
-        const int e = 4 * (tid + i * kBlock), jb = c * kMK + (e % kMK);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int j = jb + u;
-          float v = 0.0f;
-          if (rbase[i] >= 0 && j < F) {
-            v = feat[rbase[i] + j];
-            if (j < fmax_len) {  // setData max-normalisation (search.cpp:563-570)
-              const float mx = fmax[j];
-              if (mx == 0.0f) v = 0.0f;
-              else if (v == mx) v = 1.0f;
-              else v = __fdiv_rn(v, mx);
-            }
-          }
-          fa[4 * i + u] = v;
-        }
+      for (int j = 0; j < 16; ++j) {
+        const int h = __builtin_amdgcn_readlane(hrow, j);
+        areg[j] = (h >= 0 && k < F) ? __builtin_nontemporal_load(feat + (int64_t)h * F + k) : 0.0f;
       }
 #pragma unroll
-      for (int i = 0; i < kPE; ++i) {
-        const int e = tid + i * kBlock, j = c * kMK + e / 128, col = e % 128;
-        pb[i] = (j < F && col < Dpad) ? cr.PT[(int64_t)j * Dpad + col] : 0.0f;
+      for (int i = 0; i < 8; ++i) {
+        const int pc = tid + kBlock * i, kk = c * kCK + (pc >> 5), col = 4 * (pc & 31);
+        breg[i] = (kk < F && col < Dpad) ? *reinterpret_cast<const float4*>(cr.PT + (int64_t)kk * Dpad + col)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     };
-    load(0);
-    mf_f32x16 acc[4];
+    auto stage = [&](int c) {
+      const int k = c * kCK + lane;
+      float mx = 1.0f;
+      const bool norm = k < fmax_len;  // setData max-normalisation (search.cpp:563-570)
+      if (norm) mx = fmax[k];
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[t][q] = 0.0f;
-    for (int c = 0; c < nch; ++c) {
-      lds_barrier();
-#pragma unroll
-      for (int i = 0; i < kFE / 4; ++i) {
-        const int e = 4 * (tid + i * kBlock), r = e / kMK, j = e % kMK;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) sa[r * kMAS + j + u] = fa[4 * i + u];
+      for (int j = 0; j < 16; ++j) {
+        float v = areg[j];
+        if (norm) v = mx == 0.0f ? 0.0f : (v == mx ? 1.0f : __fdiv_rn(v, mx));
+        As[(wave * 16 + j) * kCAS + lane] = v;
       }
 #pragma unroll
-      for (int i = 0; i < kPE; ++i) sbm[tid + i * kBlock] = pb[i];
-      if (c + 1 < nch) load(c + 1);
-      lds_barrier();
-      // the slice is zero past F (A and P), so every chunk runs all kMK: the k loop unrolls
-      // and its LDS reads are issued ahead of the MFMAs that use them
-      const float* arow = sa + (wave * 32 + (lane & 31)) * kMAS + (lane >> 5);
-      const float* bcol = sbm + (lane >> 5) * 128 + (lane & 31);
-#pragma unroll
-      for (int k = 0; k < kMK; k += 2) {
-        const float av = arow[k];
-        float bv[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) bv[t] = bcol[k * 128 + 32 * t];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[t], acc[t], 0, 0, 0);
-      }
-    }
-    // C/D map: column lane & 31 (+ 32 t), row (q & 3) + 8 (q >> 2) + 4 (lane >> 5)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int rr = r0 + wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
-      if (rr >= n) continue;
-      const int64_t hh = rows[rr];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int col = 32 * t + (lane & 31);
-        if (col < D) G[hh * D + col] = acc[t][q];
-      }
-    }
-  }
-}
-
-// The same GEMM with the slices moved by LDS DMA (global_load_lds, no VGPR staging) into a
-// ring of three chunk buffers, two chunks ahead of the MFMAs: the row gather's HBM latency
-// is covered by two chunks of matrix work instead of one, and the registers stay with the
-// accumulators.  Without setNormalizeVal only (the DMA cannot divide by feature_max); lanes
-// past F / past the row list / past Dpad read a zero word.  A chunk buffer is the
-// kMR x kMAS feature slice (pad column: a zero) then the kMK x 128 P slice.
-constexpr int kMDA = (kMR * kMAS + kBlock - 1) / kBlock;  // A-slice DMA dwords per lane
-constexpr int kMDP = kMK * 128 / kBlock;                  // P-slice DMA dwords per lane
-constexpr int kMDBuf = kMDA * kBlock + kMK * 128;         // floats per ring buffer
-__host__ __device__ inline size_t compress_dma_lds_bytes() { return sizeof(float) * 3 * (size_t)kMDBuf; }
-
-__device__ __forceinline__ void compress_mfma_dma_body(const CompressRows& cr, int bid, int nblk, int64_t f,
-                                                       float* csm, const float* zero) {
-  const float* __restrict__ feat = cr.feat + f * cr.s_feat;
-  float* __restrict__ G = cr.G + f * cr.s_G;
-  const int32_t* __restrict__ rows = cr.rows + f * cr.s_rows;
-  const int F = cr.F, D = cr.D, Dpad = cr.Dpad;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n = (int)cr.nrows[f * cr.s_nrows];
-  const int nch = (F + kMK - 1) / kMK;
-  for (int r0 = bid * kMR; r0 < n; r0 += nblk * kMR) {
-    // this lane's DMA sources: A dword i = j * kBlock + tid -> (row i / kMAS, k i % kMAS)
-    const bool ident = n == cr.H;  // dense frame: the list is a permutation, read in memory order
-    int32_t arow_h[kMDA];  // subdivision of this lane's A dword j, -1 = padding
-#pragma unroll
-    for (int j = 0; j < kMDA; ++j) {
-      const int i = j * kBlock + tid, r = i / kMAS, k = i - r * kMAS;
-      arow_h[j] = (i < kMR * kMAS && k < kMK && r0 + r < n) ? (ident ? r0 + r : rows[r0 + r]) : -1;
-    }
-    auto issue = [&](int c) {
-      float* buf = csm + (c % 3) * kMDBuf;
-#pragma unroll
-      for (int j = 0; j < kMDA; ++j) {
-        const int i = j * kBlock + tid, col = c * kMK + (i % kMAS);
-        const float* src = (arow_h[j] >= 0 && col < F) ? feat + (int64_t)arow_h[j] * F + col : zero;
-        __builtin_amdgcn_global_load_lds(src, buf + j * kBlock + wave * 64, 4, 0, 0);
-      }
-#pragma unroll
-      for (int j = 0; j < kMDP; ++j) {
-        const int e = j * kBlock + tid, k = c * kMK + e / 128, col = e % 128;
-        const float* src = (k < F && col < Dpad) ? cr.PT + (int64_t)k * Dpad + col : zero;
-        __builtin_amdgcn_global_load_lds(src, buf + kMDA * kBlock + j * kBlock + wave * 64, 4, 0, 0);
+      for (int i = 0; i < 8; ++i) {
+        const int pc = tid + kBlock * i;
+        *reinterpret_cast<float4*>(Bs + (pc >> 5) * 128 + 4 * (pc & 31)) = breg[i];
       }
     };
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // row indices in; no stores in flight
-    issue(0);
-    if (nch > 1) issue(1);
-    mf_f32x16 acc[4];
+    mf_f32x16 acc[2];
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[t][q] = 0.0f;
+    fetch(0);
+    const float* arow = As + (rw * 32 + (lane & 31)) * kCAS + (lane >> 5);
+    const float* bcol = Bs + (lane >> 5) * 128 + 64 * cw + (lane & 31);
     for (int c = 0; c < nch; ++c) {
-      // chunk c landed (the next chunk's kMDA + kMDP DMAs may still be in flight), in every wave
-      if (c + 1 < nch) __asm__ volatile("s_waitcnt vmcnt(%0)" ::"n"(kMDA + kMDP) : "memory");
-      else __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lds_barrier();
-      if (c + 2 < nch) issue(c + 2);  // into the buffer chunk c - 1 used (every wave is past it)
-      const float* buf = csm + (c % 3) * kMDBuf;
-      const float* arow = buf + (wave * 32 + (lane & 31)) * kMAS + (lane >> 5);
-      const float* bcol = buf + kMDA * kBlock + (lane >> 5) * 128 + (lane & 31);
-#pragma unroll 2
-      for (int k = 0; k < kMK; k += 2) {
+      __syncthreads();  // every wave is done reading chunk c - 1
+      stage(c);
+      __syncthreads();
+      if (c + 1 < nch) fetch(c + 1);  // in flight while the matrix cores run
+#pragma unroll 8
+      for (int k = 0; k < kCK; k += 2) {
         const float av = arow[k];
-        float bv[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) bv[t] = bcol[k * 128 + 32 * t];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[t], acc[t], 0, 0, 0);
+        const float b0 = bcol[k * 128], b1 = bcol[k * 128 + 32];
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b0, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b1, acc[1], 0, 0, 0);
       }
     }
-    lds_barrier();  // the ring is refilled by the next row block
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const int rr = r0 + wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
+      const int rr = r0 + rw * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
       if (rr >= n) continue;
       const int64_t hh = ident ? rr : rows[rr];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int col = 32 * t + (lane & 31);
+      for (int t = 0; t < 2; ++t) {
+        const int col = 64 * cw + 32 * t + (lane & 31);
         if (col < D) G[hh * D + col] = acc[t][q];
       }
     }
   }
-  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS DMA outlives the workgroup
 }
 
 // fp16 variant of the matrix-core compress (c3h_set_search_precision): the normalised

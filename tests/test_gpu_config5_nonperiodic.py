@@ -3,7 +3,7 @@ differ (VERDICT r2 "next" item 1).
 
 The engines below switch on at >= 65,536 subdivisions (c3h_internal.h kBoxsumRows,
 search.hip kCompressMfmaRows) -- BASELINE config 5's regime:
-- compress_dma_kernel / compress_mfma_kernel (f32 matrix cores; the same k-ordered fma
+- compress_f32c_kernel (f32 matrix cores; the same k-ordered fma
   chain as the VALU compress_kernel, so G must be bit-identical to it),
 - compress_f16_kernel + score_mfma_f16_kernel (fp16 search precision, 2e-3),
 - boxsum_kernel, score_mfma_kernel (f32 matrix cores; bit-identical to the VALU engine),
@@ -72,8 +72,8 @@ def kinect256(ctx):
 
 @pytest.mark.parametrize("variant,M,r,use_fmax", [(117, 10, 20, True), (981, 10, 20, False), (981, 5, 70, False)])
 def test_kinect256_s6_large_grid_engines(ctx, kinect256, variant, M, r, use_fmax):
-    """use_fmax: setNormalizeVal maxima (search.cpp:563-570) -- compress_mfma_kernel (the
-    DMA ring cannot normalise) instead of compress_dma_kernel."""
+    """use_fmax: setNormalizeVal maxima (search.cpp:563-570), applied on the LDS store of
+    the matrix-core compress."""
     words, g, layout, cloud = kinect256
     S, D, BOX, THRX = 6, 100, (2, 2, 2), 100
     ctx.set_grid(words, (256,) * 3, leaf=0.01)
