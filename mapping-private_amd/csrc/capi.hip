@@ -2273,6 +2273,12 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
     // (33k -> 30k; profiles/r3/points_overlap/), so large canvases stay on one stream
     const bool overlap = cvox <= ((int64_t)1 << 22);
     const hipStream_t vs = overlap ? ctx->pb_vstream : ctx->stream;
+    // every exit (errors included) leaves the voxeliser stream idle: the next call may
+    // reallocate the buffers its work reads
+    struct VsIdle {
+      hipStream_t s;
+      ~VsIdle() { (void)hipStreamSynchronize(s); }
+    } vs_idle{vs};
     // the voxeliser stream starts after everything enqueued so far (the memsets above)
     HIPCHK(hipEventRecord(ctx->pb_vox_ev, ctx->stream));
     HIPCHK(hipStreamWaitEvent(vs, ctx->pb_vox_ev, 0));
@@ -2370,7 +2376,6 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
       if (rc > 0) nm = rc;
       if (rc >= 0) HIPCHK(hipEventRecord(ctx->pb_tick_ev[ch & 3], ctx->stream));
     }
-    if (rc < 0) (void)hipStreamSynchronize(vs);
     while (rc >= 0 && !ctx->pipe.empty()) {
       const int trc = pipe_tick(ctx, nullptr);
       if (trc != C3H_OK) rc = trc;
