@@ -297,6 +297,7 @@ struct SparseSearch {
   const float* qt;        // D x Opad (row stride), zero-padded past M*r
   int M, r, Opad;
   int mpg;                // models per workgroup (whole models, mpg*r <= 64)
+  int group_loop;         // 1: a workgroup runs every model group over one box-sum pass (tick)
   double* scores;
   ModeGeom md[6];
   int nmodes;

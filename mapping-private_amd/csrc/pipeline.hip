@@ -162,6 +162,11 @@ void tick_prof_dump(const TickArgs& t, long long* d_prof, int total, hipStream_t
           wmax = std::max(wmax, (hi - lo) * 0.01);
         }
         fprintf(fp, " occ_frame_end[%.1f..%.1f within<=%.1f]", fmin, fmax, wmax);
+        std::vector<double> ends;  // workgroup end times: the balance of the stream
+        for (int b = b0; b < b0 + n[r]; ++b) ends.push_back((v[2 * b + 1] - t0) * 0.01);
+        std::sort(ends.begin(), ends.end());
+        fprintf(fp, " occ_end_p10/50/90[%.1f %.1f %.1f]", ends[ends.size() / 10], ends[ends.size() / 2],
+                ends[ends.size() * 9 / 10]);
       }
     }
     b0 += n[r];
@@ -199,6 +204,16 @@ hipError_t launch_tick(const TickParts& p, hipStream_t s) {
     t.sq = a;
     t.s_gx = (int)std::max<int64_t>(1, std::min<int64_t>(sparse_score_blocks(a), env_int("C3H_TICK_SCORE", 16)));
     t.s_groups = (a.M + a.mpg - 1) / a.mpg;
+    // one workgroup per list chunk running every model group over one box-sum pass (the
+    // gathers were repeated per group): the projections then alias the basis window, which
+    // must hold them
+#ifndef C3H_TICK_GROUP_LOOP
+#define C3H_TICK_GROUP_LOOP 1
+#endif
+    if (C3H_TICK_GROUP_LOOP && t.s_groups > 1 && a.D * kOC >= kFP * (kOC + 1)) {
+      t.sq.group_loop = 1;
+      t.s_groups = 1;
+    }
     lds = std::max(lds, score_list_lds_bytes(a.D, a.mpg));
     t.n_score = t.s_gx * t.s_groups * a.nframes;
   }

@@ -542,15 +542,18 @@ __device__ __forceinline__ void score_list_body(const SparseSearch& b, int bx, i
   const int64_t ptot = a.pstart[a.nmodes];
   long long en_first = -1;
   if (tid < kFP) en_first = flist[min((int64_t)bx * kFP + tid, ptot - 1)];
-  // model group of this workgroup: models [m0, m1), basis rows [m0*r, m1*r) padded to oc
-  const int m0 = by * a.mpg, m1 = min(a.M, m0 + a.mpg);
-  const int row0 = m0 * a.r, oc = ((m1 - m0) * a.r + 15) & ~15;  // <= kOC
+  // model group(s) of this workgroup: group by (models [by*mpg, ...)), or with group_loop
+  // every group in turn over the same box sums (one workgroup per list chunk: the box-sum
+  // gathers run once instead of once per group)
+  const int ngl = a.group_loop ? (a.M + a.mpg - 1) / a.mpg : 1;
   const int fts = max(D * kFP, kFP * (kOC + 1));
   // the group's basis window goes straight to LDS (global_load_lds: no VGPR staging, the
   // score role would otherwise spill in the tick kernel); element e = j*kBlock + tid lands
-  // at qw[e] (wave-uniform base + lane*4); retired by the vmcnt(0) before the GEMM barrier
-  {
+  // at qw[e] (wave-uniform base + lane*4); retired by a vmcnt(0) before the GEMM barrier
+  auto issue_window = [&](int grp) {
     constexpr int kQW = 160 * kOC / kBlock;  // window floats per lane at the largest D
+    const int g0 = grp * a.mpg, g1 = min(a.M, g0 + a.mpg);
+    const int row0 = g0 * a.r, oc = ((g1 - g0) * a.r + 15) & ~15;  // <= kOC
     float* qwl = ssm + fts;
     const int wave = tid >> 6;
 #pragma unroll 4
@@ -560,7 +563,8 @@ __device__ __forceinline__ void score_list_body(const SparseSearch& b, int bx, i
       if (e < D * oc)
         __builtin_amdgcn_global_load_lds(a.qt + (int64_t)d * Qs + row0 + o, qwl + j * kBlock + wave * 64, 4, 0, 0);
     }
-  }
+  };
+  issue_window(by);
   const int n = (int)fcnt[a.epoch & 1];
   const int nch = (n + kFP - 1) / kFP;  // list chunks; chunk c -> workgroups c mod gdx
   if (bx >= nch) {
@@ -569,8 +573,10 @@ __device__ __forceinline__ void score_list_body(const SparseSearch& b, int bx, i
     return;
   }
   float* fT = ssm;                    // D x kFP (k-major box features)
-  float* qv = ssm;                    // kFP x (kOC+1), aliases fT after the GEMM
   float* qw = ssm + fts;              // D x oc: this group's whole basis window
+  // kFP x (kOC+1) projections after the GEMM: over fT, or with group_loop (fT serves every
+  // group) over the window (the host checks D * kOC >= kFP * (kOC + 1))
+  float* qv = a.group_loop ? qw : ssm;
   float* ffv = qw + D * kOC;
   int* gate = reinterpret_cast<int*>(ffv + kFP);
   int* hrow = gate + kFP;
@@ -680,76 +686,87 @@ __device__ __forceinline__ void score_list_body(const SparseSearch& b, int bx, i
       for (int d = 0; d < D; ++d) s = __builtin_fmaf(fT[d * kFP + tid], fT[d * kFP + tid], s);
       ffv[tid] = s;
     }
-    // GEMM: thread (tp, to): positions 2*tp, 2*tp+1; basis rows 4*to .. 4*to+3 of the group
-    const int tp = tid & 15, to = tid >> 4;
-    const bool active = 4 * to < oc;
-    float acc[2][4];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) acc[i][q] = 0.0f;
-    if (active) {
-#pragma unroll 4
-      for (int d = 0; d < D; ++d) {
-        const float2 f = *reinterpret_cast<const float2*>(&fT[d * kFP + 2 * tp]);
-        const float4 q = *reinterpret_cast<const float4*>(&qw[d * oc + 4 * to]);
-        acc[0][0] = __builtin_fmaf(f.x, q.x, acc[0][0]);
-        acc[0][1] = __builtin_fmaf(f.x, q.y, acc[0][1]);
-        acc[0][2] = __builtin_fmaf(f.x, q.z, acc[0][2]);
-        acc[0][3] = __builtin_fmaf(f.x, q.w, acc[0][3]);
-        acc[1][0] = __builtin_fmaf(f.y, q.x, acc[1][0]);
-        acc[1][1] = __builtin_fmaf(f.y, q.y, acc[1][1]);
-        acc[1][2] = __builtin_fmaf(f.y, q.z, acc[1][2]);
-        acc[1][3] = __builtin_fmaf(f.y, q.w, acc[1][3]);
+    for (int gi = 0; gi < ngl; ++gi) {
+      const int grp = by + gi;  // by == 0 with group_loop
+      const int m0 = grp * a.mpg, m1 = min(a.M, m0 + a.mpg);
+      const int oc = ((m1 - m0) * a.r + 15) & ~15;  // <= kOC
+      if (a.group_loop && (gi > 0 || ch != bx)) {  // this group's window is not in LDS yet
+        lds_barrier();  // the previous group's projections (aliasing the window) are read
+        issue_window(grp);
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
       }
-    }
-    lds_barrier();  // qv aliases fT
-    C3H_SPROF(3);
-    if (active) {
+      // GEMM: thread (tp, to): positions 2*tp, 2*tp+1; basis rows 4*to .. 4*to+3 of the group
+      const int tp = tid & 15, to = tid >> 4;
+      const bool active = 4 * to < oc;
+      float acc[2][4];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) qv[(2 * tp + i) * (kOC + 1) + 4 * to + q] = acc[i][q];
-    }
-    lds_barrier();
-    const int nm = m1 - m0;
-    for (int e = tid; e < kFP * nm; e += kBlock) {
-      const int mm = e / kFP, pp = e - mm * kFP;
-      double sc = -2.0;
-      if (gate[pp]) {
-        float q2 = 0.0f;
-        const float* q = qv + pp * (kOC + 1) + mm * a.r;
-#pragma unroll 4  // reads issued four at a time (a dependent LDS round trip per element otherwise)
-        for (int i = 0; i < a.r; ++i) q2 = __builtin_fmaf(q[i], q[i], q2);
-        sc = sqrt((double)q2) / sqrt((double)ffv[pp]);
-        const long long en = ent[pp];
-        const ModeGeom& md = a.md[(int)(en >> 40)];
-        fscores[md.offset + (int64_t)(m0 + mm) * md.P + (en & ((1ll << 40) - 1))] = sc;
-      }
-      bsc[e] = sc;
-    }
-    C3H_SPROF(4);
-    if (fpart) {
-      lds_barrier();
-      for (int mm = tid; mm < nm; mm += kBlock) {  // (score desc, scan order asc)
-        double best = -2.0;
-        long long bo = -1;
-        for (int pp = 0; pp < kFP; ++pp) {
-          if (!gate[pp]) continue;
-          const double sc = bsc[mm * kFP + pp];
-          const long long en = ent[pp];
-          const long long o = a.order_base[(int)(en >> 40)] + (en & ((1ll << 40) - 1));
-          if (sc > best || (sc == best && o < bo)) {
-            best = sc;
-            bo = o;
-          }
+        for (int q = 0; q < 4; ++q) acc[i][q] = 0.0f;
+      if (active) {
+#pragma unroll 4
+        for (int d = 0; d < D; ++d) {
+          const float2 f = *reinterpret_cast<const float2*>(&fT[d * kFP + 2 * tp]);
+          const float4 q = *reinterpret_cast<const float4*>(&qw[d * oc + 4 * to]);
+          acc[0][0] = __builtin_fmaf(f.x, q.x, acc[0][0]);
+          acc[0][1] = __builtin_fmaf(f.x, q.y, acc[0][1]);
+          acc[0][2] = __builtin_fmaf(f.x, q.z, acc[0][2]);
+          acc[0][3] = __builtin_fmaf(f.x, q.w, acc[0][3]);
+          acc[1][0] = __builtin_fmaf(f.y, q.x, acc[1][0]);
+          acc[1][1] = __builtin_fmaf(f.y, q.y, acc[1][1]);
+          acc[1][2] = __builtin_fmaf(f.y, q.z, acc[1][2]);
+          acc[1][3] = __builtin_fmaf(f.y, q.w, acc[1][3]);
         }
-        ScorePartial* q = fpart + (int64_t)ch * a.M + m0 + mm;
-        if (flists) {  // handed to another workgroup inside this launch: sc1 stores
-          __hip_atomic_store(&q->score, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(&q->order, bo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-          *q = ScorePartial{best, bo};
+      }
+      lds_barrier();  // qv aliases fT (or the window, with group_loop)
+      C3H_SPROF(3);
+      if (active) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) qv[(2 * tp + i) * (kOC + 1) + 4 * to + q] = acc[i][q];
+      }
+      lds_barrier();
+      const int nm = m1 - m0;
+      for (int e = tid; e < kFP * nm; e += kBlock) {
+        const int mm = e / kFP, pp = e - mm * kFP;
+        double sc = -2.0;
+        if (gate[pp]) {
+          float q2 = 0.0f;
+          const float* q = qv + pp * (kOC + 1) + mm * a.r;
+#pragma unroll 4  // reads issued four at a time (a dependent LDS round trip per element otherwise)
+          for (int i = 0; i < a.r; ++i) q2 = __builtin_fmaf(q[i], q[i], q2);
+          sc = sqrt((double)q2) / sqrt((double)ffv[pp]);
+          const long long en = ent[pp];
+          const ModeGeom& md = a.md[(int)(en >> 40)];
+          fscores[md.offset + (int64_t)(m0 + mm) * md.P + (en & ((1ll << 40) - 1))] = sc;
+        }
+        bsc[e] = sc;
+      }
+      C3H_SPROF(4);
+      if (fpart) {
+        lds_barrier();
+        for (int mm = tid; mm < nm; mm += kBlock) {  // (score desc, scan order asc)
+          double best = -2.0;
+          long long bo = -1;
+          for (int pp = 0; pp < kFP; ++pp) {
+            if (!gate[pp]) continue;
+            const double sc = bsc[mm * kFP + pp];
+            const long long en = ent[pp];
+            const long long o = a.order_base[(int)(en >> 40)] + (en & ((1ll << 40) - 1));
+            if (sc > best || (sc == best && o < bo)) {
+              best = sc;
+              bo = o;
+            }
+          }
+          ScorePartial* q = fpart + (int64_t)ch * a.M + m0 + mm;
+          if (flists) {  // handed to another workgroup inside this launch: sc1 stores
+            __hip_atomic_store(&q->score, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&q->order, bo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else {
+            *q = ScorePartial{best, bo};
+          }
         }
       }
     }
