@@ -41,11 +41,16 @@ constexpr int kMfWaves = kBlock / 64;
 constexpr int kMfCh = 12;
 constexpr int kMfK = 14;    // 13 offsets + the centre's own channels
 constexpr int kMfLoad = 2;  // (row, dword) items per lane of a layer (<= 18 rows x 5 dwords)
+#ifndef C3H_MF_TWO
+#define C3H_MF_TWO 1  // two-step layers with the lane-group-contiguous position map
+#endif
 #ifndef C3H_MF_EXP
 #define C3H_MF_EXP 0  // diagnostics variants: 1 no K steps, 2 no conversion, 4 no bin epilogue
 #endif
 
 __host__ __device__ inline int mf_pitch(int lx) { return (lx + 2 + 3) & ~3; }
+// items per lane of a layer for tiles up to lx x ly: (ly + 2) rows x pitch / 4 dwords
+__host__ __device__ inline int mf_load_items(int lx, int ly) { return ((ly + 2) * (mf_pitch(lx) >> 2) + 63) / 64; }
 // byte of position 0 in a plane: (off0 + PW) % 16 == 0 (the K origin), >= 16 bytes of
 // headroom for the dy = -1 reads of the first K step
 __host__ __device__ inline int mf_off0(int pw) { return 16 + ((16 - (pw & 15)) & 15); }
@@ -167,11 +172,97 @@ __device__ __forceinline__ void mf_layer_ksteps(const uint8_t* pp, const uint8_t
   }
 }
 
+// Layers of exactly two K steps (S <= 10 tiles: pitch 12, 12 rows -> 128 positions): lane
+// group h takes the 32 consecutive positions 32 h .. 32 h + 31 over both steps (K step ks
+// gets 32 h + 16 ks + i; the position -> (step, lane group, byte) map is a bijection and A,
+// B and the mask use the same one, so the integer sums are unchanged).  A plane row then
+// costs NB = 3-4 ds_read_b128 for both steps instead of 2 x 2-3: 16 instead of 22 reads
+// per layer, and the centre mask (the same plane for every layer) stays in registers.
+template <int DYR, int DXLO, int DXHI>
+struct MfRow2 {
+  static constexpr int B0 = mf_fdiv16(DYR + DXLO), NB = mf_fdiv16(DYR + DXHI + 31) - B0 + 1;
+  uint32_t w[4 * NB];
+  __device__ __forceinline__ void load(const uint8_t* row) {
+    const uint8_t* p = static_cast<const uint8_t*>(__builtin_assume_aligned(row, 16));
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      mf_u4 v = *reinterpret_cast<const mf_u4*>(p + 16 * (B0 + b));
+      __asm__("" : "+v"(v));  // keep the whole block: a narrowed ds_read_b32 bank-conflicts
+      w[4 * b] = v.x; w[4 * b + 1] = v.y; w[4 * b + 2] = v.z; w[4 * b + 3] = v.w;
+    }
+  }
+  template <int DX, int KS>
+  __device__ __forceinline__ mf_v4i frag() const {
+    constexpr int e = DYR + DX + 16 * KS - 16 * B0, d = e >> 2, sh = e & 3;
+    mf_v4i f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      f[i] = sh ? (int)__builtin_amdgcn_alignbyte(w[d + i + 1], w[d + i], sh) : (int)w[d + i];
+    return f;
+  }
+};
+
+template <int R>
+__device__ __forceinline__ void mf_layer_ksteps2(const uint8_t* pp, const uint8_t* pc, const mf_u4 (&mk)[2],
+                                                 int pw16, int h4, mf_v4i (&acc)[kMfK]) {
+  const int o = 32 * h4;
+  mf_v4i A0, A1;
+  {
+    // dz = 0: row 0 (the centres and dx = -1)
+    MfRow2<0, -1, 0> c0;
+    c0.load(pc + o);
+    const mf_v4i a0 = c0.template frag<0, 0>(), a1 = c0.template frag<0, 1>();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      A0[i] = (int)(((uint32_t)a0[i] & mk[0][i]) | (0x80808080u & ~mk[0][i]));
+      A1[i] = (int)(((uint32_t)a1[i] & mk[1][i]) | (0x80808080u & ~mk[1][i]));
+    }
+    acc[13] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0, A0, acc[13], 0, 0, 0);  // own channels
+    acc[13] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1, A1, acc[13], 0, 0, 0);
+    acc[12] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0, c0.template frag<-1, 0>(), acc[12], 0, 0, 0);  // (-1, 0, 0)
+    acc[12] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1, c0.template frag<-1, 1>(), acc[12], 0, 0, 0);
+  }
+#define C3H_MF2(ROW, DX, K)                                                                                 \
+  acc[K] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0, ROW.template frag<DX, 0>(), acc[K], 0, 0, 0);      \
+  acc[K] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1, ROW.template frag<DX, 1>(), acc[K], 0, 0, 0);
+  {
+    MfRow2<-R, -1, 1> cm;  // dz = 0, dy = -1: k = 9 + dx + 1
+    cm.load(pc + o - pw16);
+    C3H_MF2(cm, -1, 9)
+    C3H_MF2(cm, 0, 10)
+    C3H_MF2(cm, 1, 11)
+  }
+  {
+    MfRow2<-R, -1, 1> r;  // dz = -1, dy = -1: k = 3 (dx + 1)
+    r.load(pp + o - pw16);
+    C3H_MF2(r, -1, 0)
+    C3H_MF2(r, 0, 3)
+    C3H_MF2(r, 1, 6)
+  }
+  {
+    MfRow2<0, -1, 1> r;  // dz = -1, dy = 0
+    r.load(pp + o);
+    C3H_MF2(r, -1, 1)
+    C3H_MF2(r, 0, 4)
+    C3H_MF2(r, 1, 7)
+  }
+  {
+    MfRow2<R, -1, 1> r;  // dz = -1, dy = +1
+    r.load(pp + o + pw16);
+    C3H_MF2(r, -1, 2)
+    C3H_MF2(r, 0, 5)
+    C3H_MF2(r, 1, 8)
+  }
+#undef C3H_MF2
+}
+
 // plane p -> (type, reference channel); p >= 12 is padding
 __device__ __forceinline__ int mf_type(int p) { return (p >> 1) & 1; }
 __device__ __forceinline__ int mf_chan(int p) { return 2 * (p >> 2) + (p & 1); }
 
-// wave wid of nw (all waves of this launch for frame fy); smem = mf_lds_bytes(a.mf_pb)
+// wave wid of nw (all waves of this launch for frame fy); smem = mf_lds_bytes(a.mf_pb);
+// LOAD = grid-word items per lane of a layer (1 when every tile's layer fits one pass)
+template <int LOAD>
 __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int nw, int fy_, uint32_t* smem) {
   const int64_t fy = fy_;
   const int wid = wid_;
@@ -231,10 +322,10 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
     }
     // layer items (row, dword q) of lane + 64 i: x = x0 - 1 + 4 q + j, valid x bits, the
     // row (-1 when out of the tile or the grid) and the item's byte in a plane
-    int it_gy[kMfLoad], it_x[kMfLoad], it_dst[kMfLoad];
-    uint32_t it_xm[kMfLoad];
+    int it_gy[LOAD], it_x[LOAD], it_dst[LOAD];
+    uint32_t it_xm[LOAD];
 #pragma unroll
-    for (int i = 0; i < kMfLoad; ++i) {
+    for (int i = 0; i < LOAD; ++i) {
       const int e = lane + 64 * i, row = e / ipr, q = e - row * ipr, gy = y0 - 1 + row;
       it_gy[i] = e < nitem && (unsigned)gy < (unsigned)a.gy ? gy : -1;
       it_x[i] = x0 - 1 + 4 * q;
@@ -244,12 +335,12 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
       for (int j = 0; j < 4; ++j) xm |= (4 * q + j < TW && (unsigned)(it_x[i] + j) < (unsigned)a.gx ? 1u : 0u) << j;
       it_xm[i] = xm;
     }
-    uint32_t wv[2][kMfLoad][4];
-    auto load_layer = [&](int L, uint32_t (&w)[kMfLoad][4]) {
+    uint32_t wv[2][LOAD][4];
+    auto load_layer = [&](int L, uint32_t (&w)[LOAD][4]) {
       const int gz = z0 - 1 + L;
       const bool zin = (unsigned)gz < (unsigned)a.gz;
 #pragma unroll
-      for (int i = 0; i < kMfLoad; ++i) {
+      for (int i = 0; i < LOAD; ++i) {
         const bool rowin = zin && it_gy[i] >= 0;
         const uint32_t* src = fgrid + (((int64_t)gz * a.gy + it_gy[i]) * a.gx + it_x[i]);
 #pragma unroll
@@ -258,13 +349,13 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
     };
     // 12 channel planes of layer L: per voxel and colour one table read gives the 4 channel
     // bytes, a 4 x 4 byte transpose packs them per channel (4 voxels per dword)
-    auto store_layer = [&](int L, const uint32_t (&w)[kMfLoad][4]) {
+    auto store_layer = [&](int L, const uint32_t (&w)[LOAD][4]) {
 #if C3H_MF_EXP & 2
       return;
 #endif
       uint8_t* slot = wl + (L % 3) * SS;
 #pragma unroll
-      for (int i = 0; i < kMfLoad; ++i) {
+      for (int i = 0; i < LOAD; ++i) {
         if (it_dst[i] < 0) continue;
         // empty voxels read entry 768 (all channels 0, i.e. 0x80 each)
         uint32_t t[3][4];
@@ -302,16 +393,26 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
     const uint8_t* cpad = cplanes + (nk == 15 ? PBM : 0) + korg;
     const uint8_t* pmask = realk ? mask + korg : cplanes + 2 * PBM + korg;
     const int pw16 = PW & ~15;
+    mf_u4 mk2[2] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};  // two-step layers: the mask, once per tile
+    if (nks == 2) {
+      mf_compiler_fence();  // the mask plane was written above by this wave
+      mk2[0] = *reinterpret_cast<const mf_u4*>(__builtin_assume_aligned(pmask + 32 * h4k, 16));
+      mk2[1] = *reinterpret_cast<const mf_u4*>(__builtin_assume_aligned(pmask + 32 * h4k + 16, 16));
+    }
     for (int z = 0; z < lz; ++z) {
       mf_compiler_fence();  // same-wave LDS accesses complete in order; keep the compiler's too
       const uint8_t* pp = realk ? wl + ((z % 3) * SS + nk * PB + korg) : cpad;        // dz = -1
       const uint8_t* pc = realk ? wl + (((z + 1) % 3) * SS + nk * PB + korg) : cpad;  // dz = 0
 #if !(C3H_MF_EXP & 1)
-      switch (PW & 15) {
-        case 0: mf_layer_ksteps<0>(pp, pc, pmask, pw16, nks, h4k, acc); break;
-        case 4: mf_layer_ksteps<4>(pp, pc, pmask, pw16, nks, h4k, acc); break;
-        case 8: mf_layer_ksteps<8>(pp, pc, pmask, pw16, nks, h4k, acc); break;
-        default: mf_layer_ksteps<12>(pp, pc, pmask, pw16, nks, h4k, acc); break;
+      if (C3H_MF_TWO && nks == 2 && (PW & 15) == 12) {  // S <= 10 tiles: pitch 12
+        mf_layer_ksteps2<12>(pp, pc, mk2, pw16, h4k, acc);
+      } else {
+        switch (PW & 15) {
+          case 0: mf_layer_ksteps<0>(pp, pc, pmask, pw16, nks, h4k, acc); break;
+          case 4: mf_layer_ksteps<4>(pp, pc, pmask, pw16, nks, h4k, acc); break;
+          case 8: mf_layer_ksteps<8>(pp, pc, pmask, pw16, nks, h4k, acc); break;
+          default: mf_layer_ksteps<12>(pp, pc, pmask, pw16, nks, h4k, acc); break;
+        }
       }
 #endif
       mf_compiler_fence();
