@@ -3,6 +3,8 @@
 // (pipeline.hip).  Bodies take their block coordinates and LDS base explicitly so one
 // launch can host several stages (block-role dispatch).  See c3hlac.hip for the method.
 #pragma once
+#include <type_traits>
+
 #include "c3h_internal.h"
 
 namespace c3h {
@@ -141,6 +143,13 @@ constexpr int kOccBitsMax = 1 << 18;  // 32 KB of LDS bits (512^3 at S >= 8)
 #endif
 #ifndef C3H_OCC_PIPE
 #define C3H_OCC_PIPE 0
+#endif
+// rolling load ring over the whole chunks of the row-wave fast path (see there): 1 buffer
+// loads, 2 global loads.  Off: the stream alone gets 1.3 % faster with it, but the whole
+// tick 5-8 % slower -- a stream that never drains keeps the HBM queue longer for the
+// latency-bound roles (profiles/r3/occ_ring_ab/)
+#ifndef C3H_OCC_RING
+#define C3H_OCC_RING 0
 #endif
 constexpr int kOccBitsUnroll = C3H_OCC_UNROLL;  // 16-B non-temporal loads per lane per chunk
 constexpr bool kOccPipe = C3H_OCC_PIPE;         // next chunk's loads issued before this one is used
@@ -287,8 +296,95 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
     auto chunk_of = [&](int64_t i) {
       return oa.contiguous ? (i < per ? bx * per + i : nch) : i * gdx + (bx + i) % gdx;
     };
+#if C3H_OCC_RING
+    // Rolling ring over whole chunks: slot j of the next chunk is loaded the moment slot j
+    // of this chunk has been read, so each lane keeps kOccBitsUnroll loads in flight all
+    // the time (the oldest is always the one waited for: vmcnt(unroll - 1)) instead of
+    // draining to zero at every chunk end.  The loads carry no predicate (whole chunks
+    // only), so none is sunk into a branch (a predicated load forces vmcnt(0) before the
+    // first use).  A partial last chunk, if any, takes the loop below.
+    const int64_t nfull = n4 / kChunk4;
+    int64_t ri = 0;
+    if (chunk_of(0) < nfull) {
+      // buffer loads off a per-chunk descriptor: one address VGPR (tid * 16) for all
+      // slots, the slot offset j * 4 KB in an SGPR, non-temporal (aux 2)
+      const uint32_t voff = (uint32_t)tid * 16u;
+#if C3H_OCC_RING == 2  // diagnostics: global loads off a per-chunk base
+      auto chunk_rsrc = [&](int64_t c) { return reinterpret_cast<const char*>(g4 + c * kChunk4); };
+      auto ring_load = [&](const char* r, int j) {
+        return __builtin_nontemporal_load(reinterpret_cast<const v4u*>(r + voff + j * kBlock * 16));
+      };
+#else
+      auto chunk_rsrc = [&](int64_t c) {
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(g4 + c * kChunk4), (short)0, kChunk4 * 16, 0x00020000);
+      };
+      auto ring_load = [&](__amdgpu_buffer_rsrc_t r, int j) {
+        return __builtin_amdgcn_raw_buffer_load_b128(r, voff, j * kBlock * 16, 2);
+      };
+#endif
+      int64_t cur = chunk_of(0);
+      {
+        const auto r = chunk_rsrc(cur);
+#pragma unroll
+        for (int j = 0; j < kOccBitsUnroll; ++j) {
+          const v4u t = ring_load(r, j);
+          w[j] = make_uint4(t.x, t.y, t.z, t.w);
+        }
+      }
+      // one chunk; kIssue: slot j of chunk nxt is loaded right after slot j is read
+      auto run_chunk = [&](auto issue, int64_t c, int64_t nxt) {
+        const uint32_t row0 = (uint32_t)(((uint64_t)c * kChunk4 * 4 + (uint64_t)wv * 256) >> lg);
+        int y = (int)(row0 % (uint32_t)gy), z = (int)(row0 / (uint32_t)gy);
+        const auto rn = chunk_rsrc(decltype(issue)::value ? nxt : c);
+        auto refill = [&](int j) {  // slot j of the next chunk, once slot j is consumed
+          if constexpr (decltype(issue)::value) {
+            const v4u t = ring_load(rn, j);
+            w[j] = make_uint4(t.x, t.y, t.z, t.w);
+          }
+        };
+#pragma unroll
+        for (int j = 0; j < kOccBitsUnroll; ++j) {
+          if (j > 0) refill(j - 1);  // the previous slot is dead: its registers are reused
+          const uint32_t ws[4] = {w[j].x, w[j].y, w[j].z, w[j].w};
+          const int yj = y, zjj = z;
+          y += rpj;
+          while (y >= gy) {
+            y -= gy;
+            ++z;
+          }
+          if (__ballot((ws[0] | ws[1] | ws[2] | ws[3]) != 0u) == 0ull || zjj >= gz) continue;
+          const int a = __builtin_amdgcn_readfirstlane(my[yj]), b = __builtin_amdgcn_readfirstlane(mz[zjj]);
+          if (a < 0 || b < 0) continue;  // uniform: not a centre row
+          const int tyz = ns0 * (a + ns1 * b);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int t = tx0[k] + tyz;
+            if (ws[k] && tx0[k] >= 0 && t != last) {
+              last = t;
+              atomicOr(&s_bits[t >> 5], 1u << (t & 31));
+            }
+          }
+        }
+        refill(kOccBitsUnroll - 1);
+      };
+      for (;;) {  // chunk_of is increasing: the ring covers exactly the chunks below nfull
+        const int64_t nxt = chunk_of(ri + 1);
+        ++ri;
+        if (nxt < nfull) {  // uniform
+          run_chunk(std::true_type{}, cur, nxt);
+          cur = nxt;
+        } else {
+          run_chunk(std::false_type{}, cur, 0);
+          break;
+        }
+      }
+    }
+    for (int64_t i = ri; i * gdx < nch; ++i) {
+      if (chunk_of(i) < nfull) continue;  // streamed by the ring (uniform)
+#else
     if (kOccPipe && chunk_of(0) < nch) load_chunk(w, chunk_of(0) * kChunk4);
     for (int64_t i = 0; i * gdx < nch; ++i) {
+#endif
       const int64_t cidx = chunk_of(i);
       if (cidx >= nch) continue;  // uniform: the last, partial round of chunks
       const int64_t c0 = cidx * kChunk4;
