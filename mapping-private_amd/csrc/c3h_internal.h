@@ -176,6 +176,15 @@ struct VoxBatchArgs {
   uint32_t* grid[kMaxBatch];          // canvas grids of this set's frame slots (all slots)
   VoxFrameRec* info;                  // [nf]
   int32_t* lim;                       // [nf][4]: the frame's subdivisions per axis (0 = none)
+  // tile stamps of the tick's occupancy role, set by the scatter instead (stamp = 1): the
+  // tick then skips the occupancy stream over these canvases (OccArgs of the batch's C3 launch)
+  int stamp;
+  const int16_t* axmap;               // [C0 + C1 + C2] voxel coordinate -> subdivision (-1: none)
+  int ns0, ns1;                       // subdivisions along x, y
+  uint32_t epoch;
+  uint32_t* tf;                       // per frame: [2] reserved | [2] work counters | stamps
+  int32_t* work;                      // per frame: the non-empty tile list
+  int64_t s_tf, s_work;
 };
 int vb_chunk();  // points per accumulate block
 hipError_t launch_vox_batch(const VoxBatchArgs& a, hipStream_t s);
@@ -453,6 +462,7 @@ struct c3h_ctx {
   c3h::DevBuf<uint32_t> tileflags;  // [2] reserved | [2] work counters | [ntiles] stamps
   c3h::DevBuf<int32_t> work;        // non-empty tiles of the last extract
   uint32_t tile_epoch = 0;
+  int cap_h2d = 0;  // tables / stamp resets extract_frames enqueued (counts; points-in ordering)
   int64_t tf_stride = -1;           // tile-stamp layout the counters were zeroed for
   int tf_frames = 0;
   int nframes_feat = 1;             // frames of the last extract (frame 0 = the API view)
@@ -522,6 +532,7 @@ struct c3h_ctx {
     c3h::SparseCompress sc;
     int nf;
     int age;
+    bool stamped = false;  // tile stamps already set (points-in scatter): no occupancy role
   };
   struct PipeKey {
     int32_t div_b[3], min_b[3];

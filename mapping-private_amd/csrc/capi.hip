@@ -1175,6 +1175,7 @@ int extract_frames(c3h_ctx* ctx, const uint32_t* const* grids, int nf, const c3h
       ENSURE(ctx->axmap, ctx->h_axmap.size());
       HIPCHK(hipMemcpyAsync(ctx->axmap.p, ctx->h_axmap.data(), ctx->h_axmap.size() * 2,
                             hipMemcpyHostToDevice, ctx->stream));
+      ++ctx->cap_h2d;
     }
     Timed t(ctx, 1, nf);  // the whole C3 stage: occupancy pass + tile kernel (+ finalize)
     // per frame: [2] reserved | [2] work-list counters | [ntiles] epoch stamps.
@@ -1185,6 +1186,7 @@ int extract_frames(c3h_ctx* ctx, const uint32_t* const* grids, int nf, const c3h
     if (ctx->tileflags.n < tf_n || s_tf != ctx->tf_stride || nf != ctx->tf_frames || ++ctx->tile_epoch == 0) {
       ENSURE(ctx->tileflags, tf_n);
       HIPCHK(hipMemsetAsync(ctx->tileflags.p, 0, ctx->tileflags.n * 4, ctx->stream));
+      ++ctx->cap_h2d;
       ctx->tile_epoch = 1;
       ctx->tf_stride = s_tf;
       ctx->tf_frames = nf;
@@ -1901,7 +1903,7 @@ struct PipeScope {
 int pipe_tick(c3h_ctx* ctx, const c3h_ctx::PipeBatch* fresh) {
   c3h::TickParts tp;
   tp.prof = &ctx->prof;
-  if (fresh) tp.occ = &fresh->l;
+  if (fresh && !fresh->stamped) tp.occ = &fresh->l;
   for (auto& b : ctx->pipe) {
     if (b.age == 1) tp.tile = &b.l;
     if (b.age == 2) {
@@ -1948,11 +1950,12 @@ int pipe_quiesce(c3h_ctx* ctx) {
   return pipe_flush(ctx);
 }
 
-// Prepares nb frames as the next batch on its buffer set and launches its first tick.
-// Returns > 0 (modes searched), 0 when the configuration does not fit the tick (only
-// possible for the first batch of a stream: the caller then runs the lanes), < 0 on error.
-int pipe_push(c3h_ctx* ctx, const uint32_t* const* grids, c3h_det* const* outs, int nb,
-              const c3h_ctx::PipeKey& k, const int32_t* lim = nullptr) {
+// Captures nb frames as the next batch on its buffer set (no launch: its tile stamps may
+// come from elsewhere first).  Returns > 0 (modes searched), 0 when the configuration does
+// not fit the tick (only possible for the first batch of a stream: the caller then runs
+// the lanes), < 0 on error.
+int pipe_prepare(c3h_ctx* ctx, const uint32_t* const* grids, c3h_det* const* outs, int nb,
+                 const c3h_ctx::PipeKey& k, const int32_t* lim, c3h_ctx::PipeBatch* fresh) {
   c3h_ctx* c = pipe_set(ctx, ctx->pipe_seq);
   c->capture = true;
   c->cap_c3_valid = c->cap_search_valid = false;
@@ -1972,13 +1975,28 @@ int pipe_push(c3h_ctx* ctx, const uint32_t* const* grids, c3h_det* const* outs, 
     return 0;
   }
   c->nframes_feat = 1;  // slot 0 is the context's view from here on
-  const c3h_ctx::PipeBatch fresh{c->cap_c3, c->cap_q, c->cap_sc, nb, 0};
+  *fresh = c3h_ctx::PipeBatch{c->cap_c3, c->cap_q, c->cap_sc, nb, 0};
+  return rc;
+}
+
+// Launches a prepared batch's first tick; rc: pipe_prepare's result (> 0)
+int pipe_commit(c3h_ctx* ctx, const c3h_ctx::PipeBatch& fresh, const c3h_ctx::PipeKey& k, int rc) {
   int trc = pipe_tick(ctx, &fresh);
   if (trc != C3H_OK) return trc;
   ctx->pipe_seq++;
   ctx->pipe_key = k;
   ctx->pipe_nm = rc;
   return rc;
+}
+
+// Prepares nb frames as the next batch on its buffer set and launches its first tick.
+// Returns as pipe_prepare.
+int pipe_push(c3h_ctx* ctx, const uint32_t* const* grids, c3h_det* const* outs, int nb,
+              const c3h_ctx::PipeKey& k, const int32_t* lim = nullptr) {
+  c3h_ctx::PipeBatch fresh{};
+  const int rc = pipe_prepare(ctx, grids, outs, nb, k, lim, &fresh);
+  if (rc <= 0) return rc;
+  return pipe_commit(ctx, fresh, k, rc);
 }
 
 c3h_ctx::PipeKey pipe_key(c3h_ctx* ctx, const int32_t div_b[3], const int32_t min_b[3], float leaf,
@@ -2180,6 +2198,12 @@ int point_frame_single(c3h_ctx* ctx, const float* pts, int64_t n, int on_device,
 
 extern "C" {
 
+// points-in batches: the scatter stamps the tick's tiles (0: the tick streams the canvases)
+#ifndef C3H_POINT_STAMP
+#define C3H_POINT_STAMP 1
+#endif
+constexpr bool kPointStamp = C3H_POINT_STAMP;
+
 int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n, int32_t nframes, int on_device,
                          float leaf, float z_limit, const int32_t canvas[3], const c3h_extract_params* p,
                          const int32_t range[3], int32_t exist_threshold, int32_t rotate, c3h_det* d_out,
@@ -2268,10 +2292,15 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
     if (!ctx->pb_vox_ev) HIPCHK(hipEventCreateWithFlags(&ctx->pb_vox_ev, hipEventDisableTiming));
     for (hipEvent_t& e : ctx->pb_tick_ev)
       if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    // overlap pays where the tick is light: 512 x 128^3 frames 51k -> 74k frames/s, while at
-    // 256^3 the tick's 67 MB grid stream and the voxeliser's atomics slow each other down
-    // (33k -> 30k; profiles/r3/points_overlap/), so large canvases stay on one stream
-    const bool overlap = cvox <= ((int64_t)1 << 22);
+    // overlap pays where the tick is light: 512 x 128^3 frames 51k -> 74k frames/s.  While
+    // the tick streamed the canvases, 256^3 lost with it (33k -> 30k: the 67 MB grid stream
+    // and the voxeliser's atomics slowed each other down, profiles/r3/points_overlap/); with
+    // the scatter's stamps (no canvas stream) it gains there too: 41k -> 45k frames/s
+    // (profiles/r3/point_stamp/).  Canvases up to 2^25 voxels (256^3 and a little beyond)
+#ifndef C3H_POINT_OVERLAP_VOX
+#define C3H_POINT_OVERLAP_VOX (1 << 25)
+#endif
+    const bool overlap = cvox <= (int64_t)C3H_POINT_OVERLAP_VOX;
     const hipStream_t vs = overlap ? ctx->pb_vstream : ctx->stream;
     // every exit (errors included) leaves the voxeliser stream idle: the next call may
     // reallocate the buffers its work reads
@@ -2352,6 +2381,35 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
         return fail(ctx, C3H_ERR_STATE, "c3h_run_point_frames: internal: frame slots");
       va.info = ctx->pb_info.p + f0;
       va.lim = c->pb_lim.p;
+      const uint32_t* grids[c3h::kMaxBatch];
+      c3h_det* outs[c3h::kMaxBatch];
+      for (int j = 0; j < nb; ++j) {
+        grids[j] = c->pb_grid.p + (size_t)j * cvox;
+        outs[j] = d_out + (size_t)(f0 + j) * per_frame;
+      }
+      // the batch's launches are captured first: the scatter sets its tile stamps and work
+      // lists (the occupancy stream's job), so its first tick carries no occupancy role and
+      // no canvas is streamed (128^3: 8.4 MB, 256^3: 67 MB per frame)
+      c3h_ctx::PipeBatch fresh{};
+      const int h2d0 = c->cap_h2d;
+      rc = pipe_prepare(ctx, grids, outs, nb, k, c->pb_lim.p, &fresh);
+      if (rc == 0) rc = fail(ctx, C3H_ERR_STATE, "c3h_run_point_frames: the canvas does not fit the pipeline");
+      if (rc < 0) break;
+      const c3h::C3Launch& cl = fresh.l;
+      va.stamp = (kPointStamp && cl.gx == canvas[0] && cl.gy == canvas[1] && cl.gz == canvas[2]) ? 1 : 0;
+      va.axmap = cl.axmap;
+      va.ns0 = cl.nseg[0];
+      va.ns1 = cl.nseg[1];
+      va.epoch = cl.epoch;
+      va.tf = cl.tf;
+      va.work = cl.work;
+      va.s_tf = cl.s_tf;
+      va.s_work = cl.s_work;
+      // tables / stamp resets the capture enqueued precede the stamps (first batches only)
+      if (va.stamp && vs != ctx->stream && c->cap_h2d != h2d0) {
+        HIPCHK(hipEventRecord(ctx->pb_vox_ev, ctx->stream));
+        HIPCHK(hipStreamWaitEvent(vs, ctx->pb_vox_ev, 0));
+      }
       // the set's grids and gate limits were last read by the tick pushed two batches ago
       // (tile role: one tick after the batch's own, gate role: two), so this batch's voxels
       // overlap the previous batch's tick
@@ -2365,14 +2423,8 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
       c->pb_prev_nf = nb;
       c->pb_prev_total = va.total;
       c->pb_prev_blk0.assign(va.blk0, va.blk0 + nb + 1);
-      const uint32_t* grids[c3h::kMaxBatch];
-      c3h_det* outs[c3h::kMaxBatch];
-      for (int j = 0; j < nb; ++j) {
-        grids[j] = c->pb_grid.p + (size_t)j * cvox;
-        outs[j] = d_out + (size_t)(f0 + j) * per_frame;
-      }
-      rc = pipe_push(ctx, grids, outs, nb, k, c->pb_lim.p);
-      if (rc == 0) rc = fail(ctx, C3H_ERR_STATE, "c3h_run_point_frames: the canvas does not fit the pipeline");
+      fresh.stamped = va.stamp != 0;
+      rc = pipe_commit(ctx, fresh, k, rc);
       if (rc > 0) nm = rc;
       if (rc >= 0) HIPCHK(hipEventRecord(ctx->pb_tick_ev[ch & 3], ctx->stream));
     }

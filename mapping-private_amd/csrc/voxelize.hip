@@ -951,32 +951,60 @@ __global__ __launch_bounds__(kBlock) void voxb_scatter_kernel(VoxBatchArgs a) {
   ulonglong2* __restrict__ acc = a.acc + f * a.s_acc;
   uint32_t* __restrict__ Mg = a.accM + f * a.s_acc;
   uint32_t* __restrict__ grid = a.grid[f];
+  // the tick's tile stamps (occupancy_bits_body's rule: a centre voxel of subdivision
+  // t = mx[x] + ns0 (my[y] + ns1 mz[z]) stamps t; the first stamper lists it)
+  const int16_t* __restrict__ ax = a.axmap;
+  uint32_t* __restrict__ flags = a.stamp ? a.tf + f * a.s_tf + 4 : nullptr;
+  uint32_t* cnt = a.stamp ? a.tf + f * a.s_tf + 2 + (a.epoch & 1) : nullptr;
+  int32_t* __restrict__ work = a.stamp ? a.work + f * a.s_work : nullptr;
+  const int lane = tid & 63;
   uint32_t flagged = 0;
-  for (int i = tid; i < nseg; i += kBlock) {
-    const uint32_t t = vl[i];
-    const ulonglong2 v = acc[t];
-    const uint32_t m = Mg[t];
-    acc[t] = make_ulonglong2(0ull, 0ull);
-    Mg[t] = kNoMargin;
-    // offsets from min_b: the toroidal coordinates minus min_b, modulo 2^tb
-    const uint32_t cx = ((t & mx_) - (uint32_t)lo[0]) & mx_;
-    const uint32_t cy = (((t >> sy) & my_) - (uint32_t)lo[1]) & my_;
-    const uint32_t cz = (((t >> sz) & mz_) - (uint32_t)lo[2]) & mz_;
-    // an extent beyond the canvas (flagged by the reduction) may land past it: clamp
-    const uint32_t idx = min(cx, (uint32_t)Cx - 1) +
-                         (uint32_t)Cx * (min(cy, (uint32_t)Cy - 1) + (uint32_t)Cy * min(cz, (uint32_t)a.C[2] - 1));
-    const uint32_t count = (uint32_t)(v.x >> 40);
-    const float c = (float)count;
-    const uint32_t r = (uint32_t)(int)__fdiv_rn((float)(v.x & 0xffffffffffull), c);
-    const uint32_t g = (uint32_t)(int)__fdiv_rn((float)(v.y & 0xffffffffull), c);
-    const uint32_t bl = (uint32_t)(int)__fdiv_rn((float)(v.y >> 32), c);
-    grid[idx] = kOcc | (r << 16) | (g << 8) | bl;
-    wl[i] = idx;
-    // the exact centroid test of vox_scatter_kernel on the absolute cell
-    const int ax_ = lo[0] + (int)cx, ay_ = lo[1] + (int)cy, az_ = lo[2] + (int)cz;
-    const int cmag = max(max(abs(ax_), abs(ay_)), abs(az_)) + 1;
-    const float eps = (float)(count + 4) * (float)cmag * 0x1p-22f;
-    if (__uint_as_float(m) < eps || eps >= __uint_as_float(kMarginFlush)) ++flagged;
+  for (int i0 = 0; i0 < nseg; i0 += kBlock) {  // wave-uniform trip count (the stamp ballots)
+    const int i = i0 + tid;
+    int tile = -1;
+    if (i < nseg) {
+      const uint32_t t = vl[i];
+      const ulonglong2 v = acc[t];
+      const uint32_t m = Mg[t];
+      acc[t] = make_ulonglong2(0ull, 0ull);
+      if (m != kNoMargin) Mg[t] = kNoMargin;  // only the rare near-face voxels changed it
+      // offsets from min_b: the toroidal coordinates minus min_b, modulo 2^tb
+      const uint32_t cx = ((t & mx_) - (uint32_t)lo[0]) & mx_;
+      const uint32_t cy = (((t >> sy) & my_) - (uint32_t)lo[1]) & my_;
+      const uint32_t cz = (((t >> sz) & mz_) - (uint32_t)lo[2]) & mz_;
+      // an extent beyond the canvas (flagged by the reduction) may land past it: clamp
+      const uint32_t kx = min(cx, (uint32_t)Cx - 1), ky = min(cy, (uint32_t)Cy - 1), kz = min(cz, (uint32_t)a.C[2] - 1);
+      const uint32_t idx = kx + (uint32_t)Cx * (ky + (uint32_t)Cy * kz);
+      const uint32_t count = (uint32_t)(v.x >> 40);
+      const float c = (float)count;
+      const uint32_t r = (uint32_t)(int)__fdiv_rn((float)(v.x & 0xffffffffffull), c);
+      const uint32_t g = (uint32_t)(int)__fdiv_rn((float)(v.y & 0xffffffffull), c);
+      const uint32_t bl = (uint32_t)(int)__fdiv_rn((float)(v.y >> 32), c);
+      grid[idx] = kOcc | (r << 16) | (g << 8) | bl;
+      wl[i] = idx;
+      if (a.stamp) {
+        const int sx = ax[kx], sy_ = ax[Cx + ky], sz_ = ax[Cx + Cy + kz];
+        if (sx >= 0 && sy_ >= 0 && sz_ >= 0) tile = sx + a.ns0 * (sy_ + a.ns1 * sz_);
+      }
+      // the exact centroid test of vox_scatter_kernel on the absolute cell
+      const int ax_ = lo[0] + (int)cx, ay_ = lo[1] + (int)cy, az_ = lo[2] + (int)cz;
+      const int cmag = max(max(abs(ax_), abs(ay_)), abs(az_)) + 1;
+      const float eps = (float)(count + 4) * (float)cmag * 0x1p-22f;
+      if (__uint_as_float(m) < eps || eps >= __uint_as_float(kMarginFlush)) ++flagged;
+    }
+    if (a.stamp) {  // uniform
+      // neighbouring entries were first touched by neighbouring points: mostly one tile
+      const int tp = __shfl_up(tile, 1, 64);
+      const bool cand = tile >= 0 && !(lane > 0 && tp == tile) && flags[tile] != a.epoch;
+      const bool fresh = cand && atomicExch(&flags[tile], a.epoch) != a.epoch;
+      const unsigned long long bm = __ballot(fresh);
+      if (bm) {
+        uint32_t b0 = 0;
+        if (lane == 0) b0 = atomicAdd(cnt, (uint32_t)__popcll(bm));
+        b0 = __shfl(b0, 0, 64);
+        if (fresh) work[b0 + __popcll(bm & ((1ull << lane) - 1))] = tile;
+      }
+    }
   }
   flagged = wave_reduce(flagged, [](uint32_t u, uint32_t v) { return u + v; });
   if ((tid & 63) == 0 && flagged) atomicAdd(&a.info[f].flagged, flagged);
