@@ -179,3 +179,43 @@ def test_mixed_geometries_in_one_batch(ctx, bases):
         assert list(info["div_b"][i]) == list(gi.div_b) and list(info["min_b"][i]) == list(gi.min_b), i
         assert info["n_occ"][i] == gi.n_occ
     ctx.set_batch(32)
+
+
+def test_points_in_256_canvas_overlap_and_repeat(ctx):
+    """256^3 canvases (C3-HLAC-117 + 3 models): the batch scatter stamps the tick's tiles
+    (no occupancy stream), the voxeliser runs on its own stream beside the tick.  Two calls
+    on one context (the second reuses the buffer sets, epochs and word lists of the first)
+    give identical records, and sampled frames equal the single-frame path bit for bit."""
+    import torch
+    dev = torch.device("cuda", 0)
+    g2, leaf2 = 256, 0.01
+    base = [synth.kinect_scene(1_000_000, grid=g2, leaf=leaf2, seed=synth.BASE_SEED + 1400 + s) for s in range(3)]
+    bdev = [torch.from_numpy(b).to(dev) for b in base]
+    nfr = 40
+    frames = []
+    for i in range(nfr):
+        t = bdev[i % 3].clone()
+        t[:, 3] = (t[:, 3].view(torch.int32) ^ ((i * 0x2F1D37) & 0xFFFFFF)).view(torch.float32)
+        t[:, 0] = (t[:, 0].double() + (i % 5) * leaf2).float()
+        frames.append(t)
+    torch.cuda.synchronize()
+    axis_t, var, axis_q = synth.random_bases(117, D, 3, R, seed=synth.BASE_SEED + 34)
+    ctx.search_setup(axis_t, var, axis_q)
+    ctx.set_rank(1)
+    ctx.set_batch(16)
+    a = torch.zeros((nfr, 9), dtype=torch.int64, device=dev)
+    b = torch.zeros((nfr, 9), dtype=torch.int64, device=dev)
+    _, ia = ctx.run_point_frames(frames, leaf2, (g2,) * 3, 117, THR, S, BOX, EXIST, True, a)
+    _, ib = ctx.run_point_frames(frames[::-1], leaf2, (g2,) * 3, 117, THR, S, BOX, EXIST, True, b)
+    assert (ia["status"] == 0).all(), ia["status"]
+    ga = a.cpu().numpy().view(c3hlac.DET_DTYPE).reshape(nfr, 3)
+    gb = b.cpu().numpy().view(c3hlac.DET_DTYPE).reshape(nfr, 3)
+    assert np.array_equal(ga, gb[::-1])
+    assert (ga["score"] > 0).all()
+    for i in (0, 7, 13, 22, 39):
+        ctx.voxelize(frames[i], leaf2, float("inf"))
+        ctx.extract(117, THR, S)
+        ctx.set_rank(1)
+        ref, _ = ctx.search(BOX, EXIST)
+        assert np.array_equal(ga[i], ref[:, 0]), (i, ga[i], ref[:, 0])
+    ctx.set_batch(32)
