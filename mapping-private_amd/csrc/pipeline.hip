@@ -39,6 +39,7 @@ struct TickArgs {
   OccArgs oa;                        // occupancy role
   int o_grid;
   int order;                         // role ids in dispatch order, 4 bits each (first in the low bits)
+  int xcd;                           // bit r: role r keeps each frame's workgroups on one XCD
   long long* prof;                   // diagnostics (C3H_TICK_PROF): [block][2] start, end
 };
 
@@ -77,33 +78,50 @@ __device__ __forceinline__ int tick_canonical_block(const TickArgs& t) {
 #define C3H_SETPRIO(p) \
   if constexpr ((p) > 0) __builtin_amdgcn_s_setprio(p)
 
+// role-local block b -> (frame, block of that frame) for g blocks per frame.  XCD-placed:
+// blocks b and b + 8 share an XCD under the observed round-robin dispatch (speed only, never
+// correctness), so frame f takes the blocks with b % 8 == f % 8 -- every role of a frame
+// then runs on one XCD tick after tick: halo rows shared by neighbouring tiles and the rows
+// the next role re-reads (features, compressed rows) can be found in that XCD's L2
+__device__ __forceinline__ void role_frame(int b, int g, bool xcd, int& f, int& local) {
+  if (xcd) {
+    const int q = b >> 3, k = q / g;
+    f = (b & 7) + 8 * k;
+    local = q - k * g;
+  } else {
+    f = b / g;
+    local = b - f * g;
+  }
+}
+
 __device__ __forceinline__ void tick_roles(const TickArgs& t, uint32_t* tick_smem) {
   int b = t.order == 0x3210 ? (int)blockIdx.x : tick_canonical_block(t);
+  int f, r;
   if (b < t.n_occ) {
     C3H_SETPRIO(C3H_TICK_PRIO_OCC);
-    const int f = b / t.o_grid;
-    occupancy_bits_body<true>(t.oa, b - f * t.o_grid, f, t.o_grid, tick_smem);
+    role_frame(b, t.o_grid, t.xcd & 1, f, r);
+    occupancy_bits_body<true>(t.oa, r, f, t.o_grid, tick_smem);
     return;
   }
   b -= t.n_occ;
   if (b < t.n_tile) {
     C3H_SETPRIO(C3H_TICK_PRIO_TILE);
-    const int f = b / t.t_grid;
-    if (t.ka.wave117) c3hlac_wave117_body(t.ka, b - f * t.t_grid, f, t.t_grid, tick_smem);
-    else c3hlac_tile_body(t.ka, b - f * t.t_grid, f, t.t_grid, tick_smem);
+    role_frame(b, t.t_grid, t.xcd & 2, f, r);
+    if (t.ka.wave117) c3hlac_wave117_body(t.ka, r, f, t.t_grid, tick_smem);
+    else c3hlac_tile_body(t.ka, r, f, t.t_grid, tick_smem);
     return;
   }
   b -= t.n_tile;
   if (b < t.n_cg) {
     C3H_SETPRIO(C3H_TICK_PRIO_CG);
-    const int per = t.g_ngate + t.g_ncomp, f = b / per, r = b - f * per;
+    role_frame(b, t.g_ngate + t.g_ncomp, t.xcd & 4, f, r);
     if (r < t.g_ngate) gate_body(t.gq, r, f);
     else compress_rows_body(t.cr, r - t.g_ngate, t.g_ncomp, f, reinterpret_cast<float*>(tick_smem));
     return;
   }
   b -= t.n_cg;
   C3H_SETPRIO(C3H_TICK_PRIO_SCORE);
-  const int per = t.s_gx * t.s_groups, f = b / per, r = b - f * per;
+  role_frame(b, t.s_gx * t.s_groups, t.xcd & 8, f, r);
   score_list_body(t.sq, r % t.s_gx, r / t.s_gx, f, t.s_gx, t.s_groups, reinterpret_cast<float*>(tick_smem));
 }
 
@@ -258,6 +276,22 @@ hipError_t launch_tick(const TickParts& p, hipStream_t s) {
   }
   const int total = t.n_score + t.n_cg + t.n_tile + t.n_occ;
   if (total == 0) return hipSuccess;
+  // XCD placement per role: its frame count a multiple of 8 and its first block at a
+  // multiple of 8 in the launch (default dispatch order only)
+#ifndef C3H_TICK_XCD
+#define C3H_TICK_XCD 15
+#endif
+  t.xcd = 0;
+  if (t.order == 0x3210) {
+    const int nb[4] = {t.n_occ, t.n_tile, t.n_cg, t.n_score};
+    const int per[4] = {t.o_grid, t.t_grid, t.g_ngate + t.g_ncomp, t.s_gx * t.s_groups};
+    int base = 0;
+    for (int r = 0; r < 4; ++r) {
+      if (nb[r] > 0 && per[r] > 0 && base % 8 == 0 && (nb[r] / per[r]) % 8 == 0) t.xcd |= 1 << r;
+      base += nb[r];
+    }
+    t.xcd &= C3H_TICK_XCD;
+  }
   if (diag_env("C3H_TICK_PROF") && p.prof) {  // diagnostics builds only; synchronises
     DevBuf<long long>& b = *p.prof;
     if (b.n < (size_t)2 * total) {
