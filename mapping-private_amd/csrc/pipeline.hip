@@ -169,15 +169,17 @@ void tick_prof_dump(const TickArgs& t, long long* d_prof, int total, hipStream_t
               (smax - t0) * 0.01, (emax - t0) * 0.01, dsum / n[r] * 0.01);
       if (r == 0 && t.o_grid > 0) {  // occupancy: end-time spread across frames and within them
         double fmin = 1e30, fmax = 0, wmax = 0;
-        for (int f0 = b0; f0 < b0 + n[r]; f0 += t.o_grid) {
-          long long lo = LLONG_MAX, hi = 0;
-          for (int b = f0; b < f0 + t.o_grid; ++b) {
-            lo = std::min(lo, v[2 * b + 1]);
-            hi = std::max(hi, v[2 * b + 1]);
-          }
-          fmin = std::min(fmin, (hi - t0) * 0.01);
-          fmax = std::max(fmax, (hi - t0) * 0.01);
-          wmax = std::max(wmax, (hi - lo) * 0.01);
+        const int nfr = n[r] / t.o_grid;
+        std::vector<long long> lo(nfr, LLONG_MAX), hi(nfr, 0);
+        for (int b = 0; b < n[r]; ++b) {  // the device's block -> frame map (role_frame)
+          const int f = (t.xcd & 1) ? (b & 7) + 8 * ((b >> 3) / t.o_grid) : b / t.o_grid;
+          lo[f] = std::min(lo[f], v[2 * (b0 + b) + 1]);
+          hi[f] = std::max(hi[f], v[2 * (b0 + b) + 1]);
+        }
+        for (int f = 0; f < nfr; ++f) {
+          fmin = std::min(fmin, (hi[f] - t0) * 0.01);
+          fmax = std::max(fmax, (hi[f] - t0) * 0.01);
+          wmax = std::max(wmax, (hi[f] - lo[f]) * 0.01);
         }
         fprintf(fp, " occ_frame_end[%.1f..%.1f within<=%.1f]", fmin, fmax, wmax);
         std::vector<double> ends;  // workgroup end times: the balance of the stream
