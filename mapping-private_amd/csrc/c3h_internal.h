@@ -332,6 +332,10 @@ struct SparseSearch {
   // position passes only when it lies inside them (search.cpp:218-317 over the frame's
   // subdiv_b), so the canvas' extra empty subdivisions add no position
   const int32_t* lim = nullptr;    // [frame][4] (nullable)
+  // the score buffers hold the previous search of this layout: a gated-out position whose
+  // model-0 score is already -1 has -1 for every model (writers always fill all models of
+  // a position), so the gate rewrites only positions that passed last time
+  int sparse_scores = 0;
 };
 bool score_mfma_ok(int D);  // D fits score_mfma_kernel
 // sparse compress fused into the gate launch (nullable in launch_sparse_search)
@@ -500,6 +504,9 @@ struct c3h_ctx {
   bool g_valid = false;
   c3h::DevBuf<double> scores;
   int64_t scores_n = 0;
+  // layout of the score buffers' last search (modes' offsets and sizes, M, frames, buffer):
+  // an equal layout lets the gate skip the -1 fill of positions already gated out
+  std::vector<int64_t> scores_layout;
   c3h::DevBuf<float> qt;            // D x Opad transposed model basis (fast score path)
   int Opad = 0;
   c3h::DevBuf<c3h::ScorePartial> partials;

@@ -345,6 +345,12 @@ int sync_host_lists(c3h_ctx* ctx) {
 // setData + search for the nf frames of the last extract_frames (frame f's results at
 // f * stride; d_out + f * M * rank).  clean: 0 = continue from the lists, 1 = cleanMax
 // first, 2 = reset the lists as setRank does (batched frames start fresh).
+// gate: -1 fill only for positions not already gated out (0: every gated-out position)
+#ifndef C3H_SPARSE_SCORES
+#define C3H_SPARSE_SCORES 1
+#endif
+constexpr int kSparseScores = C3H_SPARSE_SCORES;
+
 int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int32_t rotate,
                   c3h_det* const* d_outs, int clean) {
   if (!ctx->have_feat) return fail(ctx, C3H_ERR_STATE, "c3h_search: no features (call c3h_extract)");
@@ -381,6 +387,13 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
   }
   ENSURE(ctx->scores, (size_t)nf * std::max<int64_t>(total, 1));
   ctx->scores_n = total;
+  std::vector<int64_t> layout{(int64_t)(intptr_t)ctx->scores.p, nf, ctx->M, rm.n};
+  for (int i = 0; i < rm.n; ++i) {
+    layout.push_back(rm.m[i].offset);
+    layout.push_back(rm.m[i].P);
+  }
+  const bool same_layout = layout == ctx->scores_layout;
+  ctx->scores_layout.swap(layout);
   ENSURE(ctx->G, (size_t)nf * H * ctx->D);
   // sparse compress: only the non-empty rows of the extract's list (the rest stay stale
   // and every consumer gates them on exist)
@@ -458,6 +471,7 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
     q.Opad = ctx->Opad;
     q.mpg = std::max(1, 64 / ctx->r);
     q.scores = ctx->scores.p;
+    q.sparse_scores = same_layout ? kSparseScores : 0;
     q.nmodes = rm.n;
     q.score_mfma = mf ? 1 : 0;
     if (mf && ctx->prec16 && ctx->Kq16 > 0) {  // fp16 search precision: f16 operands

@@ -395,6 +395,8 @@ __device__ __forceinline__ void gate_body(const SparseSearch& a, int bid, int64_
     const int x = (int)(p % md.xe), y = (int)((p / md.xe) % md.ye), z = (int)(p / xye);
     const int xyn = a.xn * a.yn;
     const int h = z * xyn + y * a.xn + x;
+    // model 0's score of the previous search of this layout (issued with the exist loads)
+    const double prev = a.sparse_scores ? fscores[md.offset + p] : 0.0;
     int e = 0;  // SearchObj::clipValue<int> on exist_voxel_num (search.cpp:484-535), exact
     for (int dz = 0; dz < md.zr; ++dz)
       for (int dy = 0; dy < md.yr; ++dy)
@@ -405,7 +407,7 @@ __device__ __forceinline__ void gate_body(const SparseSearch& a, int bid, int64_
       pass = pass && x + md.xr <= L[0] && y + md.yr <= L[1] && z + md.zr <= L[2];
     }
     entry = ((int64_t)mi << 40) | p;
-    if (!pass)
+    if (!pass && prev != -1.0)  // (a dense fill without sparse_scores: prev is 0)
       for (int m = 0; m < a.M; ++m) fscores[md.offset + (int64_t)m * md.P + p] = -1.0;
   }
   const unsigned long long m = __ballot(pass);
