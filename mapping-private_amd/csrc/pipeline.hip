@@ -12,8 +12,10 @@
 // Dependencies run only from one tick to the next (stream order), so no workgroup ever
 // waits on another role; the batches use four rotating buffer sets (c3h_ctx lanes).
 // Roles are dispatched occupancy first (one streaming workgroup per CU from the first
-// cycle), then tile, compress+gate and scoring in the remaining workgroup slots; other
-// orders measured slower (profiles/r1/o2_tick_order.log).
+// cycle), then scoring, tile and compress+gate in the remaining workgroup slots: the score
+// role's workgroups are the longest chains (one per list chunk running every model group),
+// dispatched last they started ~550 us into a 64-frame tick and set its end; dispatched
+// second they finish under the stream (profiles/r3/tick_order/: frac 0.662 -> 0.693).
 #include <algorithm>
 #include <climits>
 #include <cstdio>
@@ -211,9 +213,14 @@ hipError_t launch_tick(const TickParts& p, hipStream_t s) {
   TickArgs t{};
   size_t lds = 16;
   // dispatch order: occupancy first (it streams for the whole tick from the first cycle),
-  // then tile, compress+gate and scoring in the remaining workgroup slots.
-  // C3H_TICK_ORDER="3210" etc. (diagnostics) lists role ids first-dispatched first.
-  t.order = 0x3210;
+  // then scoring, tile and compress+gate in the remaining workgroup slots.
+  // C3H_TICK_ORDER="0312" etc. (diagnostics) lists role ids first-dispatched first.
+#ifndef C3H_TICK_ORDER_DEFAULT
+#define C3H_TICK_ORDER_DEFAULT 0x2130
+#endif
+  // (without an occupancy role -- points-in batches, drain ticks -- the chains keep the
+  // tile-first order: 128^3 points-in frames 1 % faster, profiles/r3/tick_order/)
+  t.order = p.occ ? C3H_TICK_ORDER_DEFAULT : 0x3210;
   if (const char* o = diag_env("C3H_TICK_ORDER"))
     if (strlen(o) == 4) {
       t.order = 0;
@@ -279,16 +286,17 @@ hipError_t launch_tick(const TickParts& p, hipStream_t s) {
   const int total = t.n_score + t.n_cg + t.n_tile + t.n_occ;
   if (total == 0) return hipSuccess;
   // XCD placement per role: its frame count a multiple of 8 and its first block at a
-  // multiple of 8 in the launch (default dispatch order only)
+  // multiple of 8 in the launch
 #ifndef C3H_TICK_XCD
 #define C3H_TICK_XCD 15
 #endif
   t.xcd = 0;
-  if (t.order == 0x3210) {
+  {
     const int nb[4] = {t.n_occ, t.n_tile, t.n_cg, t.n_score};
     const int per[4] = {t.o_grid, t.t_grid, t.g_ngate + t.g_ncomp, t.s_gx * t.s_groups};
-    int base = 0;
-    for (int r = 0; r < 4; ++r) {
+    int base = 0;  // the role's first block in the launch (dispatch order)
+    for (int i = 0; i < 4; ++i) {
+      const int r = (t.order >> (4 * i)) & 15;
       if (nb[r] > 0 && per[r] > 0 && base % 8 == 0 && (nb[r] / per[r]) % 8 == 0) t.xcd |= 1 << r;
       base += nb[r];
     }
