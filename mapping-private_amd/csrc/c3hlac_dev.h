@@ -127,6 +127,11 @@ struct OccArgs {
   int32_t* work;   // per frame: [ntiles]
   int64_t s_tf, s_work;
   int contiguous;  // 1: workgroup b streams one contiguous chunk range (large stand-alone grids)
+  // tail stealing (the tick, row-wave fast path only): each frame's chunks from steal_from
+  // on are cut into units of steal_unit chunks and pooled over the nframes frames; a
+  // workgroup done with its own chunks takes units off the pool (counter tf[0] of frame 0;
+  // steal_wgs workgroups in the launch), streaming and flushing each into its frame's stamps
+  int steal_from = 0, steal_unit = 0, steal_units = 0, nframes = 0, steal_wgs = 0;
 };
 
 // Bitmap variant (every tile one bit of LDS, ntiles <= kOccBitsMax): an occupied centre
@@ -296,6 +301,35 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
     auto chunk_of = [&](int64_t i) {
       return oa.contiguous ? (i < per ? bx * per + i : nch) : i * gdx + (bx + i) % gdx;
     };
+    // the tick's tail stealing (row-wave path, no ring): this frame's own chunks end at nstat
+    const int64_t nstat = (!C3H_OCC_RING && oa.steal_unit > 0) ? oa.steal_from : nch;
+    // rows are mostly empty: skip a row unless some lane of the wave holds a voxel of it
+    // (one ballot), look its (y, z) segment up only then
+    auto proc = [&](uint32_t row0) {
+      int y = (int)(row0 % (uint32_t)gy), z = (int)(row0 / (uint32_t)gy);
+#pragma unroll
+      for (int j = 0; j < kOccBitsUnroll; ++j) {
+        const int yj = y, zjj = z;
+        y += rpj;
+        while (y >= gy) {
+          y -= gy;
+          ++z;
+        }
+        const uint32_t ws[4] = {w[j].x, w[j].y, w[j].z, w[j].w};
+        if (__ballot((ws[0] | ws[1] | ws[2] | ws[3]) != 0u) == 0ull || zjj >= gz) continue;
+        const int a = __builtin_amdgcn_readfirstlane(my[yj]), b = __builtin_amdgcn_readfirstlane(mz[zjj]);
+        if (a < 0 || b < 0) continue;  // uniform: not a centre row
+        const int tyz = ns0 * (a + ns1 * b);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int t = tx0[k] + tyz;
+          if (ws[k] && tx0[k] >= 0 && t != last) {
+            last = t;
+            atomicOr(&s_bits[t >> 5], 1u << (t & 31));
+          }
+        }
+      }
+    };
 #if C3H_OCC_RING
     // Rolling ring over whole chunks: slot j of the next chunk is loaded the moment slot j
     // of this chunk has been read, so each lane keeps kOccBitsUnroll loads in flight all
@@ -386,7 +420,7 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
     for (int64_t i = 0; i * gdx < nch; ++i) {
 #endif
       const int64_t cidx = chunk_of(i);
-      if (cidx >= nch) continue;  // uniform: the last, partial round of chunks
+      if (cidx >= nstat) continue;  // uniform: the last, partial round / the pooled tail
       const int64_t c0 = cidx * kChunk4;
       uint4 nx[kOccBitsUnroll];
       if constexpr (kOccPipe) {  // the next chunk's loads in flight while this one is processed
@@ -407,33 +441,7 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
         continue;
       }
 #endif
-      // rows are mostly empty: skip a row unless some lane of the wave holds a voxel of it
-      // (one ballot), look its (y, z) segment up only then
-      {
-        int y = (int)(row0 % (uint32_t)gy), z = (int)(row0 / (uint32_t)gy);
-#pragma unroll
-        for (int j = 0; j < kOccBitsUnroll; ++j) {
-          const int yj = y, zjj = z;
-          y += rpj;
-          while (y >= gy) {
-            y -= gy;
-            ++z;
-          }
-          const uint32_t ws[4] = {w[j].x, w[j].y, w[j].z, w[j].w};
-          if (__ballot((ws[0] | ws[1] | ws[2] | ws[3]) != 0u) == 0ull || zjj >= gz) continue;
-          const int a = __builtin_amdgcn_readfirstlane(my[yj]), b = __builtin_amdgcn_readfirstlane(mz[zjj]);
-          if (a < 0 || b < 0) continue;  // uniform: not a centre row
-          const int tyz = ns0 * (a + ns1 * b);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int t = tx0[k] + tyz;
-            if (ws[k] && tx0[k] >= 0 && t != last) {
-              last = t;
-              atomicOr(&s_bits[t >> 5], 1u << (t & 31));
-            }
-          }
-        }
-      }
+      proc(row0);
       if constexpr (kOccPipe) {
 #pragma unroll
         for (int j = 0; j < kOccBitsUnroll; ++j) w[j] = nx[j];
@@ -441,6 +449,37 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
     }
     __syncthreads();
     occ_flush_bits(s_bits, nwords, s_list, s_wsum, epoch, flags, cnt, work);
+    if (!C3H_OCC_RING && oa.steal_unit > 0) {  // the pooled tails of every frame of the launch
+      // self-resetting: every workgroup's last dequeue fails; the last of those (counted in
+      // tf[1]) returns both words to 0 for the next launch on this buffer set
+      uint32_t* pool = oa.tf;
+      for (;;) {
+        __syncthreads();  // the flush is done with the bitmap, list and scan scratch
+        if (tid == 0) s_wsum[15] = (int)atomicAdd(pool, 1u);
+        __syncthreads();
+        const int u = s_wsum[15];
+        if (u >= oa.steal_units) {  // uniform
+          if (tid == 0 && atomicAdd(oa.tf + 1, 1u) == (uint32_t)oa.steal_wgs - 1) {
+            atomicExch(pool, 0u);
+            atomicExch(oa.tf + 1, 0u);
+          }
+          break;
+        }
+        const int fu = u % oa.nframes, ju = u / oa.nframes;
+        for (int i = tid; i < nwords; i += kBlock) s_bits[i] = 0u;
+        last = -1;  // another frame's bitmap
+        g4 = reinterpret_cast<const uint4*>(oa.grid[fu]);
+        __syncthreads();
+        const int64_t cb = nstat + (int64_t)ju * oa.steal_unit, ce = min(nch, cb + oa.steal_unit);
+        for (int64_t c = cb; c < ce; ++c) {
+          load_chunk(w, c * kChunk4);
+          proc((uint32_t)(((uint64_t)c * kChunk4 * 4 + (uint64_t)wv * 256) >> lg));
+        }
+        __syncthreads();
+        occ_flush_bits(s_bits, nwords, s_list, s_wsum, epoch, oa.tf + fu * oa.s_tf + 4,
+                       oa.tf + fu * oa.s_tf + 2 + (epoch & 1), oa.work + fu * oa.s_work);
+      }
+    }
     return;
   }
   uint4 w[kOccBitsUnroll];

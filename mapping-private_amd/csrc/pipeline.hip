@@ -275,6 +275,27 @@ hipError_t launch_tick(const TickParts& p, hipStream_t s) {
     t.o_grid = std::max(1, std::min(c.g1, env_int("C3H_TICK_OCC", std::max(1, 256 / std::max(1, c.nframes)))));
     t.n_occ = t.o_grid * c.nframes;
     lds = std::max(lds, c.occ_lds);
+    // tail stealing: the last 1/kStealDiv of every frame's chunks go to a pool shared by the
+    // launch's streaming workgroups, in units of kStealUnit chunks (row-wave path only)
+#ifndef C3H_TICK_STEAL_DIV
+#define C3H_TICK_STEAL_DIV 8
+#endif
+#ifndef C3H_TICK_STEAL_UNIT
+#define C3H_TICK_STEAL_UNIT 16
+#endif
+    const int64_t n4 = (int64_t)c.oa.gx * c.oa.gy * c.oa.gz / 4;
+    const int64_t nch = (n4 + (int64_t)kBlock * kOccBitsUnroll - 1) / ((int64_t)kBlock * kOccBitsUnroll);
+    const bool rowwave = c.ax && (c.oa.gx & 255) == 0 && 1024 % c.oa.gx == 0;
+    const int div = env_int("C3H_TICK_STEAL_DIV", C3H_TICK_STEAL_DIV);
+    const int unit = env_int("C3H_TICK_STEAL_UNIT", C3H_TICK_STEAL_UNIT);
+    if (rowwave && !C3H_OCC_RING && div > 0 && unit > 0 && nch >= 2 * div) {
+      const int64_t tail = nch / div;
+      t.oa.steal_from = (int)(nch - tail);
+      t.oa.steal_unit = unit;
+      t.oa.steal_units = (int)(c.nframes * ((tail + unit - 1) / unit));
+      t.oa.nframes = c.nframes;
+      t.oa.steal_wgs = t.n_occ;
+    }
   }
   if (const char* m = diag_env("C3H_TICK_ROLES")) {  // diagnostics only: bit mask of roles run
     const int mask = atoi(m);                       // 1 score, 2 compress+gate, 4 tile, 8 occupancy
