@@ -278,10 +278,10 @@ hipError_t launch_tick(const TickParts& p, hipStream_t s) {
     // tail stealing: the last 1/kStealDiv of every frame's chunks go to a pool shared by the
     // launch's streaming workgroups, in units of kStealUnit chunks (row-wave path only)
 #ifndef C3H_TICK_STEAL_DIV
-#define C3H_TICK_STEAL_DIV 8
+#define C3H_TICK_STEAL_DIV 16
 #endif
 #ifndef C3H_TICK_STEAL_UNIT
-#define C3H_TICK_STEAL_UNIT 16
+#define C3H_TICK_STEAL_UNIT 8
 #endif
     const int64_t n4 = (int64_t)c.oa.gx * c.oa.gy * c.oa.gz / 4;
     const int64_t nch = (n4 + (int64_t)kBlock * kOccBitsUnroll - 1) / ((int64_t)kBlock * kOccBitsUnroll);
