@@ -301,8 +301,8 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
     auto chunk_of = [&](int64_t i) {
       return oa.contiguous ? (i < per ? bx * per + i : nch) : i * gdx + (bx + i) % gdx;
     };
-    // the tick's tail stealing (row-wave path, no ring): this frame's own chunks end at nstat
-    const int64_t nstat = (!C3H_OCC_RING && oa.steal_unit > 0) ? oa.steal_from : nch;
+    // the tick's tail stealing (row-wave path): this frame's own chunks end at nstat
+    const int64_t nstat = oa.steal_unit > 0 ? oa.steal_from : nch;
     // rows are mostly empty: skip a row unless some lane of the wave holds a voxel of it
     // (one ballot), look its (y, z) segment up only then
     auto proc = [&](uint32_t row0) {
@@ -337,7 +337,7 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
     // draining to zero at every chunk end.  The loads carry no predicate (whole chunks
     // only), so none is sunk into a branch (a predicated load forces vmcnt(0) before the
     // first use).  A partial last chunk, if any, takes the loop below.
-    const int64_t nfull = n4 / kChunk4;
+    const int64_t nfull = min(n4 / kChunk4, nstat);  // whole chunks of this frame's own share
     int64_t ri = 0;
     if (chunk_of(0) < nfull) {
       // buffer loads off a per-chunk descriptor: one address VGPR (tid * 16) for all
@@ -449,7 +449,7 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
     }
     __syncthreads();
     occ_flush_bits(s_bits, nwords, s_list, s_wsum, epoch, flags, cnt, work);
-    if (!C3H_OCC_RING && oa.steal_unit > 0) {  // the pooled tails of every frame of the launch
+    if (oa.steal_unit > 0) {  // the pooled tails of every frame of the launch
       // self-resetting: every workgroup's last dequeue fails; the last of those (counted in
       // tf[1]) returns both words to 0 for the next launch on this buffer set
       uint32_t* pool = oa.tf;

@@ -288,7 +288,7 @@ hipError_t launch_tick(const TickParts& p, hipStream_t s) {
     const bool rowwave = c.ax && (c.oa.gx & 255) == 0 && 1024 % c.oa.gx == 0;
     const int div = env_int("C3H_TICK_STEAL_DIV", C3H_TICK_STEAL_DIV);
     const int unit = env_int("C3H_TICK_STEAL_UNIT", C3H_TICK_STEAL_UNIT);
-    if (rowwave && !C3H_OCC_RING && div > 0 && unit > 0 && nch >= 2 * div) {
+    if (rowwave && div > 0 && unit > 0 && nch >= 2 * div) {
       const int64_t tail = nch / div;
       t.oa.steal_from = (int)(nch - tail);
       t.oa.steal_unit = unit;
