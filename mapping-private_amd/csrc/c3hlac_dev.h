@@ -149,6 +149,10 @@ constexpr int kOccBitsMax = 1 << 18;  // 32 KB of LDS bits (512^3 at S >= 8)
 #ifndef C3H_OCC_PIPE
 #define C3H_OCC_PIPE 0
 #endif
+// occupied rows: a lane's (at most two) subdivisions precomputed (row-wave fast path)
+#ifndef C3H_OCC_PAIR
+#define C3H_OCC_PAIR 1
+#endif
 // rolling load ring over the whole chunks of the row-wave fast path (see there): 1 buffer
 // loads, 2 global loads.  Off: the stream alone gets 1.3 % faster with it, but the whole
 // tick 5-8 % slower -- a stream that never drains keeps the HBM queue longer for the
@@ -288,6 +292,27 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
     int tx0[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) tx0[k] = mx[xl + k];
+    // A lane's 4 voxels lie in at most two subdivisions along x when S >= 4: precompute
+    // them (tA, tB) and which voxels each holds (mA, mB), so an occupied row costs a lane
+    // two masked LDS ors from a 4-bit occupancy code instead of four tests and ors
+    // (the stream's per-slot instructions are on the tick's critical path)
+    int tA = -1, tB = -1;
+    uint32_t mA = 0, mB = 0;
+    bool cplx = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (tx0[k] < 0) continue;
+      if (tA < 0 || tx0[k] == tA) {
+        tA = tx0[k];
+        mA |= 1u << k;
+      } else if (tB < 0 || tx0[k] == tB) {
+        tB = tx0[k];
+        mB |= 1u << k;
+      } else {
+        cplx = true;
+      }
+    }
+    const bool pair_ok = C3H_OCC_PAIR && __ballot(cplx) == 0ull;  // uniform
     // Chunk i of this workgroup is chunk i * gdx + (bx + i) % gdx of the frame: rotated, so
     // every workgroup visits every y band of the grid (a fixed stride would give workgroup
     // bx the same rows of every plane, and frames' occupancy varies with y: the workgroups of
@@ -320,6 +345,13 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
         const int a = __builtin_amdgcn_readfirstlane(my[yj]), b = __builtin_amdgcn_readfirstlane(mz[zjj]);
         if (a < 0 || b < 0) continue;  // uniform: not a centre row
         const int tyz = ns0 * (a + ns1 * b);
+        if (pair_ok) {  // occupied voxel words are kOcc | rgb (< 2^25): bit 24 is occupancy
+          const uint32_t o = (ws[0] >> 24) | ((ws[1] >> 23) & 2u) | ((ws[2] >> 22) & 4u) | ((ws[3] >> 21) & 8u);
+          const int ta = tA + tyz, tb = tB + tyz;
+          if (o & mA) atomicOr(&s_bits[ta >> 5], 1u << (ta & 31));
+          if (o & mB) atomicOr(&s_bits[tb >> 5], 1u << (tb & 31));
+          continue;
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int t = tx0[k] + tyz;
