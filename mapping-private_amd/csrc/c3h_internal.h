@@ -209,6 +209,10 @@ struct C3Launch {
   int32_t* exist;
   unsigned long long* acc64;
   const int16_t* axmap;   // per-axis centre coordinate -> segment index (-1 = none)
+  // the y and z maps in closed form, when they are: c >= off ? (c - off) / S : -1
+  // (ar_s = S, 0 = use the maps; the division by S as a multiply-high by ar_magic)
+  int ar_s = 0, ar_oy = 0, ar_oz = 0;
+  uint32_t ar_magic = 0;
   int32_t* work;          // ntiles: non-empty tiles (pass 1 output)
   int32_t* rows;          // direct mode: non-empty subdivision list output (nullable)
   uint32_t epoch;

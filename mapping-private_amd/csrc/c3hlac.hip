@@ -378,6 +378,10 @@ C3Args build_c3_args(const C3Launch& l) {
   oa.gy = l.gy;
   oa.gz = l.gz;
   oa.axmap = l.axmap;
+  oa.ar_s = kOccArith ? l.ar_s : 0;
+  oa.ar_oy = l.ar_oy;
+  oa.ar_oz = l.ar_oz;
+  oa.ar_magic = l.ar_magic;
   oa.ns0 = l.nseg[0];
   oa.ns1 = l.nseg[1];
   oa.epoch = l.epoch;

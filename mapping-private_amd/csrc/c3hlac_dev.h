@@ -132,6 +132,8 @@ struct OccArgs {
   // workgroup done with its own chunks takes units off the pool (counter tf[0] of frame 0;
   // steal_wgs workgroups in the launch), streaming and flushing each into its frame's stamps
   int steal_from = 0, steal_unit = 0, steal_units = 0, nframes = 0, steal_wgs = 0;
+  int ar_s = 0, ar_oy = 0, ar_oz = 0;  // closed-form y / z maps (C3Launch), 0 = the LDS maps
+  uint32_t ar_magic = 0;
 };
 
 // Bitmap variant (every tile one bit of LDS, ntiles <= kOccBitsMax): an occupied centre
@@ -149,6 +151,11 @@ constexpr int kOccBitsMax = 1 << 18;  // 32 KB of LDS bits (512^3 at S >= 8)
 #ifndef C3H_OCC_PIPE
 #define C3H_OCC_PIPE 0
 #endif
+// occupied rows: a row's (y, z) subdivision by scalar arithmetic when the maps are uniform
+#ifndef C3H_OCC_ARITH
+#define C3H_OCC_ARITH 1
+#endif
+constexpr bool kOccArith = C3H_OCC_ARITH;
 // occupied rows: a lane's (at most two) subdivisions precomputed (row-wave fast path)
 #ifndef C3H_OCC_PAIR
 #define C3H_OCC_PAIR 1
@@ -342,7 +349,14 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
         }
         const uint32_t ws[4] = {w[j].x, w[j].y, w[j].z, w[j].w};
         if (__ballot((ws[0] | ws[1] | ws[2] | ws[3]) != 0u) == 0ull || zjj >= gz) continue;
-        const int a = __builtin_amdgcn_readfirstlane(my[yj]), b = __builtin_amdgcn_readfirstlane(mz[zjj]);
+        int a, b;
+        if (oa.ar_s) {  // uniform: scalar arithmetic, no LDS round trip
+          a = yj >= oa.ar_oy ? (int)__umulhi((uint32_t)(yj - oa.ar_oy), oa.ar_magic) : -1;
+          b = zjj >= oa.ar_oz ? (int)__umulhi((uint32_t)(zjj - oa.ar_oz), oa.ar_magic) : -1;
+        } else {
+          a = __builtin_amdgcn_readfirstlane(my[yj]);
+          b = __builtin_amdgcn_readfirstlane(mz[zjj]);
+        }
         if (a < 0 || b < 0) continue;  // uniform: not a centre row
         const int tyz = ns0 * (a + ns1 * b);
         if (pair_ok) {  // occupied voxel words are kOcc | rgb (< 2^25): bit 24 is occupancy

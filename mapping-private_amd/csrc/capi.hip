@@ -1236,6 +1236,35 @@ int extract_frames(c3h_ctx* ctx, const uint32_t* const* grids, int nf, const c3h
     l.exist = ctx->exist.p;
     l.acc64 = ctx->acc64.p;
     l.axmap = ctx->axmap.p;
+    {  // closed-form y / z maps (uniform subdivisions from an offset): the occupancy stream
+       // computes a row's segment with two scalar multiplies instead of two LDS lookups
+      const int16_t* my = ctx->h_axmap.data() + div[0];
+      const int16_t* mz = my + div[1];
+      auto first = [](const int16_t* m, int n) {
+        for (int c = 0; c < n; ++c)
+          if (m[c] == 0) return c;
+        return -1;
+      };
+      const int oy = first(my, div[1]), oz = first(mz, div[2]);
+      int S = 0;
+      if (oy >= 0) {
+        while (oy + S < div[1] && my[oy + S] == 0) ++S;
+      }
+      const uint32_t magic = S > 0 ? (uint32_t)(0x100000000ull / (uint64_t)S) + 1u : 0u;
+      auto closed = [&](const int16_t* m, int n, int off) {
+        if (off < 0) return false;
+        for (int c = 0; c < n; ++c) {
+          const int v = c >= off ? (int)(((uint64_t)(uint32_t)(c - off) * magic) >> 32) : -1;
+          if (v != m[c]) return false;
+        }
+        return true;
+      };
+      const bool ok = S > 0 && oz >= 0 && closed(my, div[1], oy) && closed(mz, div[2], oz);
+      l.ar_s = ok ? S : 0;
+      l.ar_oy = oy;
+      l.ar_oz = oz;
+      l.ar_magic = magic;
+    }
     ENSURE(ctx->work, (size_t)nf * ntiles);
     l.tf = ctx->tileflags.p;
     l.work = ctx->work.p;
