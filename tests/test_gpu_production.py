@@ -275,3 +275,39 @@ def test_config4_shape_voxelise_and_run_frames(ctx):
             assert np.array_equal(words, exp), "frame %d grid" % i
             _check_det(got[i], sc.reshape(1, -1), (P2, P2, P2), "frame %d" % i)
     assert (got[:, 0, 0].view(np.float64) > 0).all()
+
+
+def test_pipeline_offset_subdivisions_vs_oracle(ctx, prod):
+    """The tick with an offset and another subdivision size (S = 7 from (1, 2, 3)): the
+    occupancy stream's closed-form (y, z) subdivisions and per-lane subdivision pairs, the
+    pooled chunk tails and the dense memsets of a not-fully-covered grid, every frame's
+    detections against the float64 oracle on its grid."""
+    import torch
+    s7, off = 7, (1, 2, 3)
+    ngrid = 8
+    axis_t, var, axis_q = synth.random_bases(F, D, M, R, seed=synth.BASE_SEED)
+    ap = synth.whiten(axis_t, var)
+
+    def oracle(i):
+        g, layout, cloud = po.grid_inputs(prod["grids"][i], (G,) * 3, LEAF)
+        fe, sb, _ = po.c3hlac(g, layout, cloud, F, THR, LEAF, s7, off, exact=True)
+        ex = po.exist(fe)
+        _, _, sc = po.search(sb, fe, ex, ap, axis_q, BOX, 1, EXIST, dbl=True, want_scores=True)
+        return sb, sc
+
+    with cf.ThreadPoolExecutor(8) as pool:
+        ref = list(pool.map(oracle, range(ngrid)))
+    nfr = 40  # two full batches of 16 and a ragged one
+    ptrs = np.array([prod["d_grids"][i % ngrid].data_ptr() for i in range(nfr)], np.uint64)
+    d_out = torch.zeros((nfr, M * 3), dtype=torch.int64, device="cuda:0")
+    torch.cuda.synchronize()
+    ctx.set_batch(16)
+    ctx.set_pipeline(True)
+    ctx.run_frames(ptrs, (G,) * 3, (0, 0, 0), LEAF, F, THR, s7, BOX, EXIST, True, d_out.data_ptr(), offset=off)
+    ctx.synchronize()
+    got = d_out.cpu().numpy().reshape(nfr, M, 3)
+    for i in range(nfr):
+        sb, sc = ref[i % ngrid]
+        shape = tuple(int(n) - b + 1 for n, b in zip(sb[::-1], BOX))  # (z, y, x) positions
+        _check_det(got[i], sc.reshape(M, -1), shape, "frame %d" % i)
+    ctx.set_batch(32)
