@@ -297,6 +297,8 @@ def test_pipeline_offset_subdivisions_vs_oracle(ctx, prod):
 
     with cf.ThreadPoolExecutor(8) as pool:
         ref = list(pool.map(oracle, range(ngrid)))
+    ctx.search_setup(axis_t, var, axis_q)  # (other tests of the module set other axes)
+    ctx.set_rank(1)
     nfr = 40  # two full batches of 16 and a ragged one
     ptrs = np.array([prod["d_grids"][i % ngrid].data_ptr() for i in range(nfr)], np.uint64)
     d_out = torch.zeros((nfr, M * 3), dtype=torch.int64, device="cuda:0")
