@@ -181,6 +181,7 @@ struct VoxBatchArgs {
   int stamp;
   const int16_t* axmap;               // [C0 + C1 + C2] voxel coordinate -> subdivision (-1: none)
   int ns0, ns1;                       // subdivisions along x, y
+  int ntiles;                         // subdivisions of the canvas (<= 2^18: an LDS bitmap)
   uint32_t epoch;
   uint32_t* tf;                       // per frame: [2] reserved | [2] work counters | stamps
   int32_t* work;                      // per frame: the non-empty tile list

@@ -2439,10 +2439,12 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
       if (rc == 0) rc = fail(ctx, C3H_ERR_STATE, "c3h_run_point_frames: the canvas does not fit the pipeline");
       if (rc < 0) break;
       const c3h::C3Launch& cl = fresh.l;
-      va.stamp = (kPointStamp && cl.gx == canvas[0] && cl.gy == canvas[1] && cl.gz == canvas[2]) ? 1 : 0;
+      va.stamp = (kPointStamp && cl.gx == canvas[0] && cl.gy == canvas[1] && cl.gz == canvas[2] &&
+                  cl.ntiles <= ((int64_t)1 << 18)) ? 1 : 0;
       va.axmap = cl.axmap;
       va.ns0 = cl.nseg[0];
       va.ns1 = cl.nseg[1];
+      va.ntiles = (int)cl.ntiles;
       va.epoch = cl.epoch;
       va.tf = cl.tf;
       va.work = cl.work;

@@ -936,6 +936,9 @@ __global__ __launch_bounds__(kBlock) void voxb_reduce_kernel(VoxBatchArgs a) {
   rec.err = (err ? 1u : 0u) | (over ? 2u : 0u);
 }
 
+#ifndef C3H_VB_STAMP_DEDUP
+#define C3H_VB_STAMP_DEDUP 1  // the scatter's tile stamps deduplicated per workgroup in LDS
+#endif
 __global__ __launch_bounds__(kBlock) void voxb_scatter_kernel(VoxBatchArgs a) {
   const int b = blockIdx.x, tid = threadIdx.x;
   const int f = vb_frame(a.blk0, a.nf, b);
@@ -958,6 +961,12 @@ __global__ __launch_bounds__(kBlock) void voxb_scatter_kernel(VoxBatchArgs a) {
   uint32_t* cnt = a.stamp ? a.tf + f * a.s_tf + 2 + (a.epoch & 1) : nullptr;
   int32_t* __restrict__ work = a.stamp ? a.work + f * a.s_work : nullptr;
   const int lane = tid & 63;
+  // tiles this workgroup stamped already: one global exchange per (workgroup, tile)
+  extern __shared__ uint32_t vb_stamped[];
+  if (a.stamp) {
+    for (int i = tid; i < (a.ntiles + 31) / 32; i += kBlock) vb_stamped[i] = 0u;
+    __syncthreads();
+  }
   uint32_t flagged = 0;
   for (int i0 = 0; i0 < nseg; i0 += kBlock) {  // wave-uniform trip count (the stamp ballots)
     const int i = i0 + tid;
@@ -995,7 +1004,13 @@ __global__ __launch_bounds__(kBlock) void voxb_scatter_kernel(VoxBatchArgs a) {
     if (a.stamp) {  // uniform
       // neighbouring entries were first touched by neighbouring points: mostly one tile
       const int tp = __shfl_up(tile, 1, 64);
-      const bool cand = tile >= 0 && !(lane > 0 && tp == tile) && flags[tile] != a.epoch;
+      bool cand = tile >= 0 && !(lane > 0 && tp == tile);
+      if (C3H_VB_STAMP_DEDUP && cand) {
+        const uint32_t bit = 1u << (tile & 31);
+        cand = (atomicOr(&vb_stamped[tile >> 5], bit) & bit) == 0u;
+      } else if (cand) {  // (diagnostics: a plain read of the stamp instead)
+        cand = flags[tile] != a.epoch;
+      }
       const bool fresh = cand && atomicExch(&flags[tile], a.epoch) != a.epoch;
       const unsigned long long bm = __ballot(fresh);
       if (bm) {
@@ -1019,7 +1034,7 @@ hipError_t launch_vox_batch(const VoxBatchArgs& a, hipStream_t s) {
   if (g > 0) voxb_accum_kernel<<<(unsigned)g, kBT, 0, s>>>(a);
   if (a.total > 0) {
     voxb_reduce_kernel<<<(unsigned)a.nf, kBlock, 0, s>>>(a);
-    voxb_scatter_kernel<<<(unsigned)a.total, kBlock, 0, s>>>(a);
+    voxb_scatter_kernel<<<(unsigned)a.total, kBlock, a.stamp ? 4 * (size_t)((a.ntiles + 31) / 32) : 0, s>>>(a);
   }
   return hipGetLastError();
 }
