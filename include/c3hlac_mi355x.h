@@ -35,6 +35,17 @@ extern "C" {
 #define C3H_VARIANT_981 981  /* C3HLAC981Estimation (rotation-variant) */
 #define C3H_VARIANT_117 117  /* C3HLAC117Estimation (rotation-invariant) */
 
+/* setColor of the estimator (c3h_extract_params.color_mode): the six colour channels a
+ * voxel contributes (r, r_, g, g_, b, b_).  C3HLAC{,_RI}Estimation (color_chlac/include/
+ * color_chlac/color_chlac.hpp:155-179; c3_hlac_core's twin): r = 255 sin(v theta),
+ * r_ = 255 cos(v theta), theta = float(M_PI / 510), with sin / cos in double (the 2011
+ * build's ::sin(double); v = 255 -> (254, 0)) or float (std::sin(float); -> (255, 0)).
+ * ColorCHLAC{,_RI}Estimation (color_chlac.hpp:148-153): r_ = 255 - r.  Bins and
+ * normalisation constants are shared (color_chlac.h:38-53). */
+#define C3H_COLOR_C3_FLOAT 0
+#define C3H_COLOR_C3_DOUBLE 1  /* the default */
+#define C3H_COLOR_CHLAC 2
+
 /* SearchMode (color_voxel_recognition/include/color_voxel_recognition/search.h:48) */
 enum { C3H_S_MODE_1 = 0, C3H_S_MODE_2, C3H_S_MODE_3, C3H_S_MODE_4, C3H_S_MODE_5, C3H_S_MODE_6 };
 
@@ -59,7 +70,7 @@ typedef struct {
   int32_t thr[3];     /* setColorThreshold r,g,b (c3_hlac.h:92) */
   int32_t subdiv;     /* subdivision_size (0 = one vector for the whole grid) */
   int32_t offset[3];  /* offset_x/y/z */
-  int32_t lut_double; /* setColor's sin/cos in double (1, default; v=255 -> 254) or float (0) */
+  int32_t color_mode; /* C3H_COLOR_*: setColor's channels (C3H_COLOR_C3_DOUBLE by default) */
 } c3h_extract_params;
 
 /* one ranked detection: maxDot/maxX/maxY/maxZ/maxMode (search.h:99-126) */
@@ -179,7 +190,7 @@ int c3h_get_feature_info(c3h_ctx* ctx, int32_t subdiv_out[3], int64_t* hist_num,
  * the setGRSD rule.  c3h_get_rsd: r_min / r_max and the type per occupied voxel (leaf
  * layout order); returns their count.
  * c3h_extract_vosch: extractVOSCH (:832-843): [GRSD-20 | C3-HLAC-117] = 137 floats per
- * subdivision (the C3 part as c3h_extract with variant 117, thr, lut_double), exist by
+ * subdivision (the C3 part as c3h_extract with variant 117, thr, color_mode), exist by
  * the setVOSCH rule; the next c3h_search uses them (search_setup with F = 137).
  * The PCL algorithms are restated (PCL is not part of the reference tree); radius-search
  * ties are broken by point index. */
@@ -193,7 +204,7 @@ int c3h_compute_normals(c3h_ctx* ctx, float radius, const float viewpoint[3]);
 int c3h_get_normals(c3h_ctx* ctx, float* out, int on_device);
 int c3h_extract_grsd(c3h_ctx* ctx, const c3h_grsd_params* p, int32_t subdiv_out[3], int64_t* hist_num);
 int c3h_get_rsd(c3h_ctx* ctx, float* radii, int32_t* types, int on_device);
-int c3h_extract_vosch(c3h_ctx* ctx, const c3h_grsd_params* p, const int32_t thr[3], int32_t lut_double,
+int c3h_extract_vosch(c3h_ctx* ctx, const c3h_grsd_params* p, const int32_t thr[3], int32_t color_mode,
                       int32_t subdiv_out[3], int64_t* hist_num);
 /* SearchObj::setData(subdiv_b, feature) (search.cpp:539-658) with features computed
  * elsewhere (VOSCH / ConVOSCH / GRSD extractors, search_new.h:34-76, or stored C3-HLAC

@@ -10,11 +10,14 @@ import ctypes as C
 import numpy as np
 
 from . import _capi
-from ._capi import DET_DTYPE, TIMER_NAMES, check, i32x3, ptr
+from ._capi import DET_DTYPE, TIMER_NAMES, C3HError, check, i32x3, ptr  # noqa: F401
 
 FRAME_INFO_DTYPE = np.dtype([("div_b", "<i4", 3), ("min_b", "<i4", 3), ("subdiv_b", "<i4", 3), ("status", "<i4"),
                              ("n_valid", "<i8"), ("n_occ", "<i8")])
 S_MODE = {"S_MODE_%d" % (i + 1): i for i in range(6)}
+# setColor of the estimator (c3h_extract_params.color_mode, include/c3hlac_mi355x.h):
+# C3HLAC with sin/cos in float or in double (the default), or ColorCHLAC's (v, 255 - v)
+COLOR_C3_FLOAT, COLOR_C3_DOUBLE, COLOR_CHLAC = 0, 1, 2
 DIM_C3HLAC_981_1_3_ALL = 981
 DIM_C3HLAC_117_1_3_ALL = 117
 
@@ -140,13 +143,13 @@ class Context:
         return out
 
     # --- C3-HLAC ----------------------------------------------------------------------
-    def extract(self, variant, thr, subdiv=0, offset=(0, 0, 0), lut_double=True):
+    def extract(self, variant, thr, subdiv=0, offset=(0, 0, 0), color_mode=COLOR_C3_DOUBLE):
         p = _capi.ExtractParams()
         p.variant = int(variant)
         p.thr = (C.c_int32 * 3)(*[int(t) for t in thr])
         p.subdiv = int(subdiv)
         p.offset = (C.c_int32 * 3)(*[int(o) for o in offset])
-        p.lut_double = int(bool(lut_double))
+        p.color_mode = int(color_mode)
         sb = (C.c_int32 * 3)()
         hn = C.c_int64()
         self._chk(self.lib.c3h_extract(self.h, C.byref(p), sb, C.byref(hn)), "extract")
@@ -194,12 +197,12 @@ class Context:
         self._chk(self.lib.c3h_get_rsd(self.h, ptr(radii), ptr(types), 0), "get_rsd")
         return radii, types
 
-    def extract_vosch(self, thr, subdiv=0, offset=(0, 0, 0), rsd_radius=0.01, normalize=False, lut_double=True):
+    def extract_vosch(self, thr, subdiv=0, offset=(0, 0, 0), rsd_radius=0.01, normalize=False, color_mode=COLOR_C3_DOUBLE):
         sb = (C.c_int32 * 3)()
         hn = C.c_int64()
         p = self._grsd_params(subdiv, offset, rsd_radius, normalize)
         t = (C.c_int32 * 3)(*[int(x) for x in thr])
-        self._chk(self.lib.c3h_extract_vosch(self.h, C.byref(p), t, int(bool(lut_double)), sb, C.byref(hn)),
+        self._chk(self.lib.c3h_extract_vosch(self.h, C.byref(p), t, int(color_mode), sb, C.byref(hn)),
                   "extract_vosch")
         self.hist_num, self.subdiv, self.variant = int(hn.value), tuple(int(x) for x in sb), 137
         return self.subdiv, self.hist_num
@@ -278,7 +281,7 @@ class Context:
                                                    int(bool(rotate)), ptr(d_out)), "search_async")
 
     def run_frames(self, grid_ptrs, div_b, min_b, leaf, variant, thr, subdiv, ranges, exist_threshold,
-                   rotate=True, d_out=None, offset=(0, 0, 0), lut_double=True, stream=False):
+                   rotate=True, d_out=None, offset=(0, 0, 0), color_mode=COLOR_C3_DOUBLE, stream=False):
         """c3h_run_frames (stream=True: c3h_stream_frames, the pipeline stays filled;
         call stream_flush() before reading the last batches): grid_ptrs = uint64 numpy
         array of device pointers."""
@@ -289,7 +292,7 @@ class Context:
         p.thr = (C.c_int32 * 3)(*[int(t) for t in thr])
         p.subdiv = int(subdiv)
         p.offset = (C.c_int32 * 3)(*[int(o) for o in offset])
-        p.lut_double = int(bool(lut_double))
+        p.color_mode = int(color_mode)
         nm = self._chk(fn(self.h, ptr(gp), gp.size, i32x3(div_b), i32x3(min_b), float(leaf),
                           C.byref(p), i32x3(ranges), int(exist_threshold),
                           int(bool(rotate)), ptr(d_out)), "run_frames")
@@ -298,7 +301,7 @@ class Context:
         return nm
 
     def run_point_frames(self, frames, leaf, canvas, variant, thr, subdiv, ranges, exist_threshold, rotate=True,
-                         d_out=None, z_limit=float("inf"), offset=(0, 0, 0), lut_double=True):
+                         d_out=None, z_limit=float("inf"), offset=(0, 0, 0), color_mode=COLOR_C3_DOUBLE):
         """c3h_run_point_frames: frames = list of (n, 4) float32 point clouds, all numpy host
         arrays (pinned or not) or all torch device tensors; d_out = device pointer (int) or
         tensor of len(frames) * M * rank records.  Returns (modes, info) with info a numpy
@@ -322,7 +325,7 @@ class Context:
         p.thr = (C.c_int32 * 3)(*[int(t) for t in thr])
         p.subdiv = int(subdiv)
         p.offset = (C.c_int32 * 3)(*[int(o) for o in offset])
-        p.lut_double = int(bool(lut_double))
+        p.color_mode = int(color_mode)
         info = (_capi.FrameInfo * max(len(frames), 1))()
         nm = self._chk(self.lib.c3h_run_point_frames(self.h, ptr(ptrs), ptr(ns), len(frames), int(on_dev),
                                                      float(leaf), float(z_limit), i32x3(canvas), C.byref(p),

@@ -31,7 +31,7 @@ class GridInfo(C.Structure):
 
 class ExtractParams(C.Structure):
     _fields_ = [("variant", C.c_int32), ("thr", C.c_int32 * 3), ("subdiv", C.c_int32),
-                ("offset", C.c_int32 * 3), ("lut_double", C.c_int32)]
+                ("offset", C.c_int32 * 3), ("color_mode", C.c_int32)]
 
 
 class GrsdParams(C.Structure):

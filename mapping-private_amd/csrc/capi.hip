@@ -107,12 +107,17 @@ struct Timed {
   }
 };
 
-void host_lut(int lut_double, uint32_t* out) {
+// setColor as a 256-entry table of packed (r | r_ << 8) channel pairs, one table per
+// C3H_COLOR_* mode (color_chlac.hpp:148-179)
+void host_lut(int color_mode, uint32_t* out) {
   const float angle_norm = M_PI / 510;  // color_chlac/include/color_chlac/color_chlac.h:9
   for (int v = 0; v < 256; ++v) {
     const float a = v * angle_norm;
     int s, c;
-    if (lut_double) {
+    if (color_mode == C3H_COLOR_CHLAC) {  // ColorCHLAC: r_ = 255 - r
+      s = v;
+      c = 255 - v;
+    } else if (color_mode == C3H_COLOR_C3_DOUBLE) {
       s = (int)(255 * std::sin((double)a));
       c = (int)(255 * std::cos((double)a));
     } else {
@@ -639,10 +644,9 @@ int c3h_create(int hip_device, c3h_ctx** out) {
 
   if (hipHostMalloc(&ctx->h_small, 64 * sizeof(uint32_t)) != hipSuccess) return bail(C3H_ERR_HIP);
   if (ensure(ctx, ctx->scratch, 64) != C3H_OK) return bail(C3H_ERR_NOMEM);
-  if (ensure(ctx, ctx->lut, 512) != C3H_OK) return bail(C3H_ERR_NOMEM);
-  uint32_t lut[512];
-  host_lut(1, lut);
-  host_lut(0, lut + 256);
+  if (ensure(ctx, ctx->lut, 3 * 256) != C3H_OK) return bail(C3H_ERR_NOMEM);
+  uint32_t lut[3 * 256];
+  for (int m = 0; m < 3; ++m) host_lut(m, lut + 256 * m);  // indexed by C3H_COLOR_*
   if (hipMemcpy(ctx->lut.p, lut, sizeof(lut), hipMemcpyHostToDevice) != hipSuccess)
     return bail(C3H_ERR_HIP);
   ctx->rank = 1;
@@ -1092,11 +1096,16 @@ int c3h_set_grid(c3h_ctx* ctx, const uint32_t* words, const int32_t div_b[3],
 // C3HLAC{981,117}Estimation::setVoxelFilter + compute for nf frames of one geometry
 // (grids[f], dims / min_b / leaf of ctx->info) in one set of launches; frame f's
 // per-frame buffers (features, exist, tile stamps, work / row lists) sit at f * stride.
+static bool extract_params_ok(const c3h_extract_params* p) {
+  return (p->variant == 981 || p->variant == 117) && p->color_mode >= C3H_COLOR_C3_FLOAT &&
+         p->color_mode <= C3H_COLOR_CHLAC;
+}
+
 int extract_frames(c3h_ctx* ctx, const uint32_t* const* grids, int nf, const c3h_extract_params* p,
                    int32_t subdiv_out[3], int64_t* hist_num_out) {
   if (!ctx || !p) return C3H_ERR_ARG;
-  if (p->variant != 981 && p->variant != 117)
-    return fail(ctx, C3H_ERR_ARG, "c3h_extract: variant must be 981 or 117");
+  if (!extract_params_ok(p))
+    return fail(ctx, C3H_ERR_ARG, "c3h_extract: variant must be 981 or 117, color_mode a C3H_COLOR_* value");
   if (!ctx->have_grid) return fail(ctx, C3H_ERR_STATE, "c3h_extract: no grid");
   if (nf < 1 || nf > c3h::kMaxBatch) return fail(ctx, C3H_ERR_ARG, "extract: bad frame count");
   HIPCHK(hipSetDevice(ctx->device));
@@ -1231,7 +1240,7 @@ int extract_frames(c3h_ctx* ctx, const uint32_t* const* grids, int nf, const c3h
     l.sby = mode1 ? 1 : sb[1];
     l.variant = F;
     l.atomic = atomic ? 1 : 0;
-    l.lut = ctx->lut.p + (p->lut_double ? 0 : 256);
+    l.lut = ctx->lut.p + 256 * p->color_mode;
     l.feat = ctx->feat.p;
     l.exist = ctx->exist.p;
     l.acc64 = ctx->acc64.p;
@@ -1547,7 +1556,7 @@ int c3h_get_rsd(c3h_ctx* ctx, float* radii, int32_t* types, int on_device) {
 }
 
 // extractVOSCH (grsd_colorCHLAC_tools.hpp:832-843): [GRSD-20 | C3-HLAC-117] per subdivision
-int c3h_extract_vosch(c3h_ctx* ctx, const c3h_grsd_params* p, const int32_t thr[3], int32_t lut_double,
+int c3h_extract_vosch(c3h_ctx* ctx, const c3h_grsd_params* p, const int32_t thr[3], int32_t color_mode,
                       int32_t subdiv_out[3], int64_t* hist_num) {
   if (!ctx || !p || !thr) return C3H_ERR_ARG;
   QUIESCE(ctx);
@@ -1564,7 +1573,7 @@ int c3h_extract_vosch(c3h_ctx* ctx, const c3h_grsd_params* p, const int32_t thr[
     e.offset[a] = p->offset[a];
   }
   e.subdiv = p->subdiv;
-  e.lut_double = lut_double;
+  e.color_mode = color_mode;
   const uint32_t* g = ctx->grid_ptr;
   int32_t sb2[3];
   int64_t H2 = 0;
@@ -2120,6 +2129,7 @@ int c3h_run_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nframes
   if (!ctx || !d_grids || nframes < 0 || !div_b || !min_b || !p || !range || !d_out)
     return C3H_ERR_ARG;
   if (!ctx->have_setup) return fail(ctx, C3H_ERR_STATE, "c3h_run_frames: no axes (call c3h_search_setup)");
+  if (!extract_params_ok(p)) return fail(ctx, C3H_ERR_ARG, "c3h_run_frames: variant / color_mode");
   HIPCHK(hipSetDevice(ctx->device));
   {
     int rc = pipe_flush(ctx);  // an open stream completes first
@@ -2187,6 +2197,7 @@ int c3h_stream_frames(c3h_ctx* ctx, const uint32_t* const* d_grids, int32_t nfra
   if (!ctx || !d_grids || nframes < 0 || !div_b || !min_b || !p || !range || !d_out)
     return C3H_ERR_ARG;
   if (!ctx->have_setup) return fail(ctx, C3H_ERR_STATE, "c3h_stream_frames: no axes (call c3h_search_setup)");
+  if (!extract_params_ok(p)) return fail(ctx, C3H_ERR_ARG, "c3h_stream_frames: variant / color_mode");
   if (nframes == 0) return ctx->pipe_nm;
   HIPCHK(hipSetDevice(ctx->device));
   const int B = std::max(1, std::min(ctx->nbatch, c3h::kMaxBatch));
@@ -2257,6 +2268,8 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
     if (n[i] < 0 || (n[i] > 0 && !pts[i]) || n[i] >= ((int64_t)1 << 24))
       return fail(ctx, C3H_ERR_ARG, "c3h_run_point_frames: frame point counts must be in [0, 16,777,215]");
   if (p->variant != 981 && p->variant != 117) return fail(ctx, C3H_ERR_ARG, "c3h_run_point_frames: variant");
+  if (p->color_mode < C3H_COLOR_C3_FLOAT || p->color_mode > C3H_COLOR_CHLAC)
+    return fail(ctx, C3H_ERR_ARG, "c3h_run_point_frames: color_mode");
   int64_t cvox = 1;
   for (int a = 0; a < 3; ++a) {
     if (canvas[a] < 1) return fail(ctx, C3H_ERR_ARG, "c3h_run_point_frames: canvas dims must be >= 1");

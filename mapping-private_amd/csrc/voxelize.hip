@@ -21,14 +21,16 @@
 //   vox_scatter every block reduces the partial records (bounds, totals), then converts
 //               its segment's voxels: cell - min_b -> linear index (PCL's
 //               (floor(p * inv) - min_b) . divb_mul), the canonical colour mean
-//               kOcc | r<<16 | g<<8 | b with r = (int)(float(sum_r) / float(count)), the
-//               grid word, and the safety test below.
+//               kOcc | r<<16 | g<<8 | b with r = (int)(float(sum_r) * (1 / float(count)))
+//               (Eigen 3.0's scalar quotient, see pcl_colour_word), the grid word, and the
+//               safety test below.
 // Integer sums are exact and order-independent, so the grid is deterministic.
 //
 // Centroids.  C3-HLAC takes a voxel's subdivision (floor(c / voxel_size)) and neighbour
-// base (PCL getNeighborCentroidIndices: floor(c * inv_leaf)) from its float centroid c,
-// the fp32 sequential mean of its points in input order (the oracle's reading of PCL's
-// sort-then-sum).  That can leave the voxel's own cell only when c lies within the sum's
+// base (the reference's PCL 1.0 getNeighborCentroidIndices: floor(c / leaf_size)) from its
+// float centroid c = (fp32 sequential sum of its points in input order) * (1 / count), as
+// PCL 1.0's VoxelGrid on Eigen 3.0 computes it (pinned by the reference's shape_data
+// feature files, tests/test_shape_fixtures.py).  That can leave the voxel's own cell only when c lies within the sum's
 // rounding of a cell boundary; vox_scatter flags a voxel when its closest point's margin
 // is below (count + 4) * 2^-22 * (|cell| + 1) cells (4x the error bound of the mean, the
 // multiply and the divide).  Only then (and for c3h_get_downsampled) the exact pass runs:
@@ -68,6 +70,18 @@ constexpr int kCellBias = 1 << 20;
 // is below it except for very dense far voxels, which it then flags conservatively
 constexpr uint32_t kMarginFlush = 0x3c800000u;  // 1/64
 static_assert(sizeof(VoxSlot) == 32, "one 32-B slot per voxel");
+
+// PCL VoxelGrid's colour of a voxel (the reference's PCL 1.0 on Eigen 3.0): the channel
+// sums divided by the point count, which Eigen 3.0 evaluates as sum * (1 / n) in float,
+// truncated to int and repacked (kOcc marks the word occupied)
+__device__ __forceinline__ uint32_t pcl_colour_word(unsigned long long sr, unsigned long long sg,
+                                                    unsigned long long sb, uint32_t count) {
+  const float rn = __fdiv_rn(1.0f, (float)count);
+  const uint32_t r = (uint32_t)(int)__fmul_rn((float)sr, rn);
+  const uint32_t g = (uint32_t)(int)__fmul_rn((float)sg, rn);
+  const uint32_t b = (uint32_t)(int)__fmul_rn((float)sb, rn);
+  return kOcc | (r << 16) | (g << 8) | b;
+}
 
 __device__ __forceinline__ bool point_valid(const float4& p, float z_limit) {
   return isfinite(p.x) && isfinite(p.y) && isfinite(p.z) && p.z < z_limit;
@@ -405,11 +419,7 @@ __global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
     const int64_t idx = (x - t.mn[0]) + (int64_t)t.dv[0] * ((y - t.mn[1]) + (int64_t)t.dv[1] * (z - t.mn[2]));
     const unsigned long long A = ka.y, B = bm.x;
     const uint32_t count = (uint32_t)(A >> 40);
-    const float c = (float)count;
-    const uint32_t r = (uint32_t)(int)__fdiv_rn((float)(A & 0xffffffffffull), c);
-    const uint32_t g = (uint32_t)(int)__fdiv_rn((float)(B & 0xffffffffull), c);
-    const uint32_t bl = (uint32_t)(int)__fdiv_rn((float)(B >> 32), c);
-    a.grid[idx] = kOcc | (r << 16) | (g << 8) | bl;
+    a.grid[idx] = pcl_colour_word(A & 0xffffffffffull, B & 0xffffffffull, B >> 32, count);
     tl[i] = (uint32_t)idx;
     a.tab[s].pos = (uint32_t)(seg + i);
     // margins >= kMarginFlush were not recorded: conservative when the bound exceeds it
@@ -496,8 +506,8 @@ __global__ __launch_bounds__(kBlock) void vox_centroid_kernel(VoxArgs a, const u
       sy += p.y;
       sz += p.z;
     }
-    const float fc = (float)m;
-    const float c[3] = {__fdiv_rn(sx, fc), __fdiv_rn(sy, fc), __fdiv_rn(sz, fc)};
+    const float rn = __fdiv_rn(1.0f, (float)m);  // Eigen 3.0: centroid / n == centroid * (1 / n)
+    const float c[3] = {__fmul_rn(sx, rn), __fmul_rn(sy, rn), __fmul_rn(sz, rn)};
     const uint32_t idx = tl[q];
     cent[q] = make_float4(c[0], c[1], c[2], __uint_as_float(a.grid[idx] & 0x00ffffffu));
     int own[3];
@@ -506,8 +516,8 @@ __global__ __launch_bounds__(kBlock) void vox_centroid_kernel(VoxArgs a, const u
     bool moved = false;
 #pragma unroll
     for (int ax = 0; ax < 3; ++ax) {
-      nb[ax] = (int)floorf(c[ax] * a.inv);             // getNeighborCentroidIndices
-      sb[ax] = (int)floorf(__fdiv_rn(c[ax], a.leaf));  // c3_hlac.cpp:349-354
+      nb[ax] = (int)floorf(__fdiv_rn(c[ax], a.leaf));  // PCL 1.0 getNeighborCentroidIndices: floor(p / leaf)
+      sb[ax] = nb[ax];                                  // c3_hlac.cpp:349-354: floor(p / voxel_size)
       moved = moved || nb[ax] != own[ax] || sb[ax] != own[ax];
     }
     if (moved) {
@@ -985,11 +995,7 @@ __global__ __launch_bounds__(kBlock) void voxb_scatter_kernel(VoxBatchArgs a) {
       const uint32_t kx = min(cx, (uint32_t)Cx - 1), ky = min(cy, (uint32_t)Cy - 1), kz = min(cz, (uint32_t)a.C[2] - 1);
       const uint32_t idx = kx + (uint32_t)Cx * (ky + (uint32_t)Cy * kz);
       const uint32_t count = (uint32_t)(v.x >> 40);
-      const float c = (float)count;
-      const uint32_t r = (uint32_t)(int)__fdiv_rn((float)(v.x & 0xffffffffffull), c);
-      const uint32_t g = (uint32_t)(int)__fdiv_rn((float)(v.y & 0xffffffffull), c);
-      const uint32_t bl = (uint32_t)(int)__fdiv_rn((float)(v.y >> 32), c);
-      grid[idx] = kOcc | (r << 16) | (g << 8) | bl;
+      grid[idx] = pcl_colour_word(v.x & 0xffffffffffull, v.y & 0xffffffffull, v.y >> 32, count);
       wl[i] = idx;
       if (a.stamp) {
         const int sx = ax[kx], sy_ = ax[Cx + ky], sz_ = ax[Cx + Cy + kz];

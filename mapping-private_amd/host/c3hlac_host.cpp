@@ -33,7 +33,7 @@ Vector3i v3(const int32_t* p) {
 // getSubdivNum().
 Vector3i extract(VoxelGrid& grid, int variant, std::vector<std::vector<float> >& feature, int thr_r,
                  int thr_g, int thr_b, float voxel_size, int subdiv, int ox, int oy, int oz,
-                 bool lut_double) {
+                 int color_mode) {
   feature.resize(0);
   if (grid.leaf() != 0.0f && voxel_size != grid.leaf())
     throw Error(C3H_ERR_ARG, "extractC3HLACSignature: voxel_size differs from the grid's leaf size");
@@ -46,7 +46,7 @@ Vector3i extract(VoxelGrid& grid, int variant, std::vector<std::vector<float> >&
   p.offset[0] = ox;
   p.offset[1] = oy;
   p.offset[2] = oz;
-  p.lut_double = lut_double ? 1 : 0;
+  p.color_mode = color_mode;
   int32_t sb[3];
   int64_t hist_num = 0;
   const Context& ctx = grid.context();
@@ -268,7 +268,7 @@ bool voxel_filter(const VoxelGrid& grid, int subdiv, const int off[3], Vector3i&
   return true;
 }
 
-int64_t compute_feature(VoxelGrid& grid, int dim, const int thr[3], int subdiv, const int off[3], bool lut_double,
+int64_t compute_feature(VoxelGrid& grid, int dim, const int thr[3], int subdiv, const int off[3], int color_mode,
                         std::vector<float>& flat) {
   if (thr[0] < 0 || thr[1] < 0 || thr[2] < 0) {  // computeFeature's silent return (c3_hlac.cpp:306-309)
     std::cerr << "Invalid color_threshold: " << thr[0] << " " << thr[1] << " " << thr[2] << std::endl;
@@ -276,7 +276,7 @@ int64_t compute_feature(VoxelGrid& grid, int dim, const int thr[3], int subdiv, 
     return 0;
   }
   std::vector<std::vector<float> > rows;
-  extract(grid, dim, rows, thr[0], thr[1], thr[2], grid.leaf(), subdiv, off[0], off[1], off[2], lut_double);
+  extract(grid, dim, rows, thr[0], thr[1], thr[2], grid.leaf(), subdiv, off[0], off[1], off[2], color_mode);
   flat.resize(rows.size() * (size_t)dim);
   for (size_t h = 0; h < rows.size(); ++h) std::copy(rows[h].begin(), rows[h].end(), flat.begin() + h * dim);
   return (int64_t)rows.size();
@@ -299,28 +299,51 @@ template class C3HLAC117Estimation<PointXYZRGBNormal, C3HLACSignature117>;
 template class C3HLAC117Estimation<PointXYZRGBNormal, C3HLACSignature981>;
 template class C3HLAC981Estimation<PointXYZRGBNormal, C3HLACSignature117>;
 template class C3HLAC981Estimation<PointXYZRGBNormal, C3HLACSignature981>;
+template class ColorCHLAC_RI_Estimation<PointXYZRGB, C3HLACSignature117>;
+template class ColorCHLACEstimation<PointXYZRGB, C3HLACSignature981>;
+template class ColorCHLAC_RI_Estimation<PointXYZRGBNormal, C3HLACSignature117>;
+template class ColorCHLACEstimation<PointXYZRGBNormal, C3HLACSignature981>;
 
 Vector3i extractC3HLACSignature981(VoxelGrid& grid, std::vector<std::vector<float> >& feature, int r,
                                    int g, int b, float voxel_size, int subdiv, int ox, int oy, int oz,
-                                   bool lut_double) {
-  return extract(grid, C3H_VARIANT_981, feature, r, g, b, voxel_size, subdiv, ox, oy, oz, lut_double);
+                                   int color_mode) {
+  return extract(grid, C3H_VARIANT_981, feature, r, g, b, voxel_size, subdiv, ox, oy, oz, color_mode);
 }
 void extractC3HLACSignature981(VoxelGrid& grid, std::vector<float>& feature, int r, int g, int b,
-                               float voxel_size, bool lut_double) {
+                               float voxel_size, int color_mode) {
   std::vector<std::vector<float> > tmp;
-  extract(grid, C3H_VARIANT_981, tmp, r, g, b, voxel_size, 0, 0, 0, 0, lut_double);
+  extract(grid, C3H_VARIANT_981, tmp, r, g, b, voxel_size, 0, 0, 0, 0, color_mode);
   feature = tmp.empty() ? std::vector<float>() : tmp[0];
 }
 Vector3i extractC3HLACSignature117(VoxelGrid& grid, std::vector<std::vector<float> >& feature, int r,
                                    int g, int b, float voxel_size, int subdiv, int ox, int oy, int oz,
-                                   bool lut_double) {
-  return extract(grid, C3H_VARIANT_117, feature, r, g, b, voxel_size, subdiv, ox, oy, oz, lut_double);
+                                   int color_mode) {
+  return extract(grid, C3H_VARIANT_117, feature, r, g, b, voxel_size, subdiv, ox, oy, oz, color_mode);
 }
 void extractC3HLACSignature117(VoxelGrid& grid, std::vector<float>& feature, int r, int g, int b,
-                               float voxel_size, bool lut_double) {
+                               float voxel_size, int color_mode) {
   std::vector<std::vector<float> > tmp;
-  extract(grid, C3H_VARIANT_117, tmp, r, g, b, voxel_size, 0, 0, 0, 0, lut_double);
+  extract(grid, C3H_VARIANT_117, tmp, r, g, b, voxel_size, 0, 0, 0, 0, color_mode);
   feature = tmp.empty() ? std::vector<float>() : tmp[0];
+}
+
+// extractColorCHLACSignature981/117 (color_chlac/include/color_chlac/grsd_colorCHLAC_tools.hpp:
+// 680-747): the same flow with ColorCHLAC{,_RI}Estimation, whose setColor is (v, 255 - v)
+Vector3i extractColorCHLACSignature981(VoxelGrid& grid, std::vector<std::vector<float> >& feature, int r,
+                                       int g, int b, float voxel_size, int subdiv, int ox, int oy, int oz) {
+  return extract(grid, C3H_VARIANT_981, feature, r, g, b, voxel_size, subdiv, ox, oy, oz, C3H_COLOR_CHLAC);
+}
+void extractColorCHLACSignature981(VoxelGrid& grid, std::vector<float>& feature, int r, int g, int b,
+                                   float voxel_size) {
+  extractC3HLACSignature981(grid, feature, r, g, b, voxel_size, C3H_COLOR_CHLAC);
+}
+Vector3i extractColorCHLACSignature117(VoxelGrid& grid, std::vector<std::vector<float> >& feature, int r,
+                                       int g, int b, float voxel_size, int subdiv, int ox, int oy, int oz) {
+  return extract(grid, C3H_VARIANT_117, feature, r, g, b, voxel_size, subdiv, ox, oy, oz, C3H_COLOR_CHLAC);
+}
+void extractColorCHLACSignature117(VoxelGrid& grid, std::vector<float>& feature, int r, int g, int b,
+                                   float voxel_size) {
+  extractC3HLACSignature117(grid, feature, r, g, b, voxel_size, C3H_COLOR_CHLAC);
 }
 
 // ------------------------------------------------------------------------- VOSCH / GRSD
@@ -801,7 +824,7 @@ static void set_c3hlac(SearchObj& so, int F, int thr_r, int thr_g, int thr_b, co
   p.thr[2] = thr_b;
   p.subdiv = subdiv;
   p.offset[0] = p.offset[1] = p.offset[2] = 0;
-  p.lut_double = 1;
+  p.color_mode = C3H_COLOR_C3_DOUBLE;
   int32_t sb[3];
   int64_t hist_num = 0;
   ctx.check(c3h_extract(ctx.get(), &p, sb, &hist_num), "c3h_extract");

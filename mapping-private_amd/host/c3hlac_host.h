@@ -102,24 +102,25 @@ void getVoxelGrid(VoxelGrid& grid, const std::vector<PointXYZRGB>& input,
                   std::vector<PointXYZRGB>& output, float voxel_size,
                   float z_limit = std::numeric_limits<float>::infinity());
 
-// extractC3HLACSignature981/117 (c3_hlac_tools.hpp:134-202).  `lut_double` selects the
-// setColor sin/cos evaluation (true = double, the reference build's default).
+// extractC3HLACSignature981/117 (c3_hlac_tools.hpp:134-202).  `color_mode` selects the
+// setColor table (C3H_COLOR_*: C3 sin/cos in double -- the reference build's default -- or
+// float; C3H_COLOR_CHLAC is extractColorCHLACSignature*'s, below).
 Vector3i extractC3HLACSignature981(VoxelGrid& grid, std::vector<std::vector<float> >& feature,
                                    int color_threshold_r, int color_threshold_g,
                                    int color_threshold_b, float voxel_size,
                                    int subdivision_size = 0, int offset_x = 0, int offset_y = 0,
-                                   int offset_z = 0, bool lut_double = true);
+                                   int offset_z = 0, int color_mode = C3H_COLOR_C3_DOUBLE);
 void extractC3HLACSignature981(VoxelGrid& grid, std::vector<float>& feature, int color_threshold_r,
                                int color_threshold_g, int color_threshold_b, float voxel_size,
-                               bool lut_double = true);
+                               int color_mode = C3H_COLOR_C3_DOUBLE);
 Vector3i extractC3HLACSignature117(VoxelGrid& grid, std::vector<std::vector<float> >& feature,
                                    int color_threshold_r, int color_threshold_g,
                                    int color_threshold_b, float voxel_size,
                                    int subdivision_size = 0, int offset_x = 0, int offset_y = 0,
-                                   int offset_z = 0, bool lut_double = true);
+                                   int offset_z = 0, int color_mode = C3H_COLOR_C3_DOUBLE);
 void extractC3HLACSignature117(VoxelGrid& grid, std::vector<float>& feature, int color_threshold_r,
                                int color_threshold_g, int color_threshold_b, float voxel_size,
-                               bool lut_double = true);
+                               int color_mode = C3H_COLOR_C3_DOUBLE);
 
 // ---- the pcl::Feature-style estimators (c3_hlac/include/c3_hlac/c3_hlac.h:42-220) -----
 const int DIM_C3HLAC_981_1_3 = 495;
@@ -154,7 +155,7 @@ bool voxel_filter(const VoxelGrid& grid, int subdiv, const int off[3], Vector3i&
 // computeFeature (c3_hlac.cpp:303-324, 395-416) on the grid's device context: hist_num rows
 // of `dim` floats (0 rows for the silent-empty cases)
 int64_t compute_feature(VoxelGrid& grid, int dim, const int thr[3], int subdiv, const int off[3],
-                        bool lut_double, std::vector<float>& flat);
+                        int color_mode, std::vector<float>& flat);
 int64_t grid_occupied(const VoxelGrid& grid);  // n_occ of the grid (-1: not from getVoxelGrid)
 }  // namespace detail
 
@@ -198,7 +199,8 @@ class C3HLAC117Estimation {
   template <class Tree>
   void setSearchMethod(const Tree&) {}
   // setColor's sin/cos evaluation (double = the reference build's, see c3h_extract_params)
-  void setLUTDouble(bool lut_double) { lut_double_ = lut_double; }
+  void setLUTDouble(bool lut_double) { color_mode_ = lut_double ? C3H_COLOR_C3_DOUBLE : C3H_COLOR_C3_FLOAT; }
+  void setColorMode(int color_mode) { color_mode_ = color_mode; }  // C3H_COLOR_*
   const std::string& getFeatureName() const { return feature_name_; }
   // Feature::compute -> computeFeature: one PointOutT per subdivision (hist_num of them)
   void compute(std::vector<PointOutT>& output) {
@@ -213,7 +215,7 @@ class C3HLAC117Estimation {
       throw Error(C3H_ERR_ARG, feature_name_ + "::compute: the output type holds fewer than " + std::to_string(d) +
                                    " floats");
     std::vector<float> flat;
-    const int64_t hn = detail::compute_feature(*grid_, d, thr_, subdiv_, off_, lut_double_, flat);
+    const int64_t hn = detail::compute_feature(*grid_, d, thr_, subdiv_, off_, color_mode_, flat);
     output.assign((size_t)hn, PointOutT());
     for (int64_t h = 0; h < hn; ++h) {
       float* dst = reinterpret_cast<float*>(&output[h]);
@@ -230,7 +232,8 @@ class C3HLAC117Estimation {
   int thr_[3] = {-1, -1, -1};  // the constructor's -1 (c3_hlac.cpp:178): compute() then returns empty
   int subdiv_ = 0, off_[3] = {0, 0, 0};
   float voxel_size_ = 0.0f;
-  bool filter_ok_ = false, lut_double_ = true;
+  bool filter_ok_ = false;
+  int color_mode_ = C3H_COLOR_C3_DOUBLE;
   Vector3i subdiv_b_;
 };
 
@@ -243,6 +246,40 @@ class C3HLAC981Estimation : public C3HLAC117Estimation<PointT, PointOutT> {
  protected:
   int dim() const override { return DIM_C3HLAC_981_1_3_ALL; }
 };
+
+// ColorCHLAC_RI_Estimation / ColorCHLACEstimation (color_chlac/include/color_chlac/
+// color_chlac.h): the same estimators with ColorCHLAC's setColor (r_ = 255 - r,
+// color_chlac.hpp:148-153); bins and normalisation constants are the C3 ones.
+template <typename PointT, typename PointOutT>
+class ColorCHLAC_RI_Estimation : public C3HLAC117Estimation<PointT, PointOutT> {
+ public:
+  ColorCHLAC_RI_Estimation() {
+    this->feature_name_ = "ColorCHLAC_RI_Estimation";
+    this->color_mode_ = C3H_COLOR_CHLAC;
+  }
+};
+template <typename PointT, typename PointOutT>
+class ColorCHLACEstimation : public C3HLAC117Estimation<PointT, PointOutT> {
+ public:
+  ColorCHLACEstimation() {
+    this->feature_name_ = "ColorCHLACEstimation";
+    this->color_mode_ = C3H_COLOR_CHLAC;
+  }
+
+ protected:
+  int dim() const override { return DIM_C3HLAC_981_1_3_ALL; }
+};
+// extractColorCHLACSignature981/117 (grsd_colorCHLAC_tools.hpp:680-747)
+Vector3i extractColorCHLACSignature981(VoxelGrid& grid, std::vector<std::vector<float> >& feature, int thR,
+                                       int thG, int thB, float voxel_size, int subdivision_size = 0,
+                                       int offset_x = 0, int offset_y = 0, int offset_z = 0);
+void extractColorCHLACSignature981(VoxelGrid& grid, std::vector<float>& feature, int thR, int thG, int thB,
+                                   float voxel_size);
+Vector3i extractColorCHLACSignature117(VoxelGrid& grid, std::vector<std::vector<float> >& feature, int thR,
+                                       int thG, int thB, float voxel_size, int subdivision_size = 0,
+                                       int offset_x = 0, int offset_y = 0, int offset_z = 0);
+void extractColorCHLACSignature117(VoxelGrid& grid, std::vector<float>& feature, int thR, int thG, int thB,
+                                   float voxel_size);
 
 // VOSCH / GRSD (color_chlac/include/color_chlac/grsd_colorCHLAC_tools.h:27-32, .hpp:63-296,
 // 832-843) on the grid's cloud: computeNormal (radius normals_radius_search) runs on the

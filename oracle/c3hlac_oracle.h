@@ -35,16 +35,24 @@ typedef struct {
   float inv_leaf;
 } orc_grid;
 
-/* LUT of C3HLAC setColor (color_chlac.hpp:168-179): lut[2v] = 255*sin(v*theta),
- * lut[2v+1] = 255*cos(v*theta), theta = float(M_PI/510).  lut_double selects sin/cos
- * evaluated in double (v=255 -> (254,0)) or float (v=255 -> (255,0)). */
-void orc_lut(int lut_double, int32_t* lut /* 512 */);
+/* Colour channels of setColor.  ORC_COLOR_C3_DOUBLE / _FLOAT: C3HLAC (color_chlac.hpp:
+ * 155-179): lut[2v] = 255*sin(v*theta), lut[2v+1] = 255*cos(v*theta), theta =
+ * float(M_PI/510), sin/cos in double (v=255 -> (254,0)) or float (v=255 -> (255,0)).
+ * ORC_COLOR_CHLAC: ColorCHLAC{,_RI}Estimation (color_chlac.hpp:148-153): (v, 255 - v). */
+#define ORC_COLOR_C3_FLOAT 0
+#define ORC_COLOR_C3_DOUBLE 1
+#define ORC_COLOR_CHLAC 2
+void orc_lut(int color_mode, int32_t* lut /* 512 */);
+/* 1 (default): the voxel-grid arithmetic of the reference's PCL 1.0 / Eigen 3.0 (centroid
+ * = sum * (1/n), neighbour base floor(c / leaf)); 0: later PCL (see c3hlac_oracle.c). */
+void orc_set_voxel_semantics(int pcl_era);
 
 /* Bounds pass of PCL VoxelGrid::applyFilter (+ detect_object.cpp:68-87 limitPoint). */
 int orc_voxel_bounds(const float* pts /* n*4: x,y,z,rgb-bits */, int64_t n, float leaf,
                      float z_limit, orc_grid* g);
 /* Fill pass: leaf_layout (div product ints, -1 = empty), downsampled cloud (n_occ*4,
- * ascending linear index, xyz = float mean in input order, rgb = canonical mean). */
+ * ascending linear index, xyz = fp32 sum in input order times 1/n, rgb = per-channel
+ * fp32 sums times 1/n, truncated). */
 int orc_voxel_fill(const float* pts, int64_t n, float z_limit, orc_grid* g,
                    int32_t* leaf_layout, float* cloud_out);
 
@@ -54,7 +62,7 @@ int orc_voxel_fill(const float* pts, int64_t n, float z_limit, orc_grid* g,
  * feat_out must hold hist_num*variant floats (query with feat_out=NULL first). */
 int64_t orc_c3hlac(const orc_grid* g, const int32_t* leaf_layout, const float* cloud,
                    int variant, int thr_r, int thr_g, int thr_b, float voxel_size,
-                   int subdiv, int ox, int oy, int oz, int lut_double, int exact,
+                   int subdiv, int ox, int oy, int oz, int color_mode, int exact,
                    float* feat_out, int32_t subdiv_out[3]);
 
 /* exist_voxel_num of SearchC3HLAC::setC3HLAC (search_c3_hlac.h:60-61). */

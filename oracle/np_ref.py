@@ -21,10 +21,14 @@ def binmap(dim):
     return json.loads((GOLDEN / ("binmap_%d.json" % dim)).read_text())
 
 
-def lut(lut_double=True):
+def lut(color_mode=1):
+    """setColor channel pairs: 0 C3 float sin/cos, 1 C3 double (default), 2 ColorCHLAC."""
+    if color_mode == 2:  # ColorCHLAC{,_RI}Estimation::setColor (color_chlac.hpp:148-153)
+        v = np.arange(256, dtype=np.int64)
+        return np.stack([v, 255 - v], 1)
     an = F32(np.pi / 510)
     v = np.arange(256, dtype=np.float32) * an  # float multiply, as v * angle_norm
-    if lut_double:
+    if color_mode == 1:
         s = np.trunc(255 * np.sin(v.astype(np.float64))).astype(np.int64)
         c = np.trunc(255 * np.cos(v.astype(np.float64))).astype(np.int64)
     else:
@@ -55,8 +59,9 @@ def voxelize(pts, leaf, z_limit=np.inf):
     sums = [np.bincount(idx, weights=c.astype(np.float64), minlength=nvox) for c in chans]
     occ = cnt > 0
     words = np.zeros(nvox, np.uint32)
-    cf = cnt[occ].astype(np.float32)
-    means = [np.trunc(s[occ].astype(np.float32) / cf).astype(np.uint32) for s in sums]
+    # PCL 1.0 on Eigen 3.0: the channel sums times (1 / n) in float, truncated
+    rn = F32(1) / cnt[occ].astype(np.float32)
+    means = [np.trunc(s[occ].astype(np.float32) * rn).astype(np.uint32) for s in sums]
     words[occ] = (1 << 24) | (means[0] << 16) | (means[1] << 8) | means[2]
     layout = np.full(nvox, -1, np.int32)
     layout[occ] = np.arange(int(occ.sum()), dtype=np.int32)
@@ -86,7 +91,7 @@ def subdivisions(div, subdiv, offset):
     return sb, sb[0] * sb[1] * sb[2], True
 
 
-def c3hlac(words, variant, thr, subdiv=0, offset=(0, 0, 0), lut_double=True):
+def c3hlac(words, variant, thr, subdiv=0, offset=(0, 0, 0), color_mode=1):
     """Exact-integer C3-HLAC on a dense packed grid words[z,y,x] -> (feat, exist, sb)."""
     Z, Y, X = words.shape
     div = (X, Y, Z)
@@ -97,7 +102,7 @@ def c3hlac(words, variant, thr, subdiv=0, offset=(0, 0, 0), lut_double=True):
     r = ((words >> 16) & 255).astype(np.int64)
     g = ((words >> 8) & 255).astype(np.int64)
     b = (words & 255).astype(np.int64)
-    L = lut(lut_double)
+    L = lut(color_mode)
     a = np.stack([L[r, 0], L[r, 1], L[g, 0], L[g, 1], L[b, 0], L[b, 1]]) * occ
     br, bg, bb = (r > thr[0]).astype(np.int64), (g > thr[1]).astype(np.int64), (b > thr[2]).astype(np.int64)
     be = np.stack([br, 1 - br, bg, 1 - bg, bb, 1 - bb]) * occ

@@ -43,6 +43,7 @@ def load():
                                    P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                    C.c_int, C.c_int, P, P, P, P, P, P]
         lib.orc_remove_overlap.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P, P]
+        lib.orc_set_voxel_semantics.argtypes = [C.c_int]
         lib.orc_pca_read.argtypes = [C.c_char_p, C.c_int, P, P, P, C.POINTER(C.c_int), C.c_int]
         _lib = lib
     return _lib
@@ -52,10 +53,20 @@ def _p(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
 
 
-def lut(lut_double=True):
+COLOR_C3_FLOAT, COLOR_C3_DOUBLE, COLOR_CHLAC = 0, 1, 2  # c3hlac_oracle.h ORC_COLOR_*
+
+
+def lut(color_mode=COLOR_C3_DOUBLE):
     out = np.zeros(512, np.int32)
-    load().orc_lut(int(lut_double), _p(out))
+    load().orc_lut(int(color_mode), _p(out))
     return out.reshape(256, 2)
+
+
+def set_voxel_semantics(pcl_era=True):
+    """True (default): the reference's PCL 1.0 / Eigen 3.0 voxel-grid arithmetic (centroid =
+    sum * (1/n), neighbour base floor(c / leaf)); False: later PCL (true division, base
+    floor(c * (1/leaf))).  Process-wide; the fixture test switches it to show the difference."""
+    load().orc_set_voxel_semantics(int(bool(pcl_era)))
 
 
 def voxelize(pts, leaf, z_limit=float("inf")):
@@ -77,14 +88,14 @@ def voxelize(pts, leaf, z_limit=float("inf")):
 
 
 def c3hlac(g, layout, cloud, variant, thr, voxel_size, subdiv=0, offset=(0, 0, 0),
-           lut_double=True, exact=False):
+           color_mode=COLOR_C3_DOUBLE, exact=False):
     lib = load()
     layout = np.ascontiguousarray(layout, np.int32)
     cloud = np.ascontiguousarray(cloud, np.float32)
     sb = np.zeros(3, np.int32)
     args = (C.byref(g), _p(layout), _p(cloud), int(variant), int(thr[0]), int(thr[1]), int(thr[2]),
             float(voxel_size), int(subdiv), int(offset[0]), int(offset[1]), int(offset[2]),
-            int(lut_double), int(exact))
+            int(color_mode), int(exact))
     hn = lib.orc_c3hlac(*args, None, _p(sb))
     if hn < 0:
         return np.zeros((0, variant), np.float32), tuple(int(x) for x in sb), int(hn)

@@ -116,15 +116,38 @@ def test_kat_pair_per_offset(ctx, k):
         assert np.array_equal(ctx.features(), fn)
 
 
-@pytest.mark.parametrize("lut_double", [True, False])
-def test_colour_255_lut_flag(ctx, lut_double):
+@pytest.mark.parametrize("color_mode", [c3hlac.COLOR_C3_DOUBLE, c3hlac.COLOR_C3_FLOAT, c3hlac.COLOR_CHLAC])
+def test_colour_255_lut_flag(ctx, color_mode):
+    """v = 255 under every setColor table (C3 double: (254, 0), C3 float: (255, 0),
+    ColorCHLAC: (255, 0)), against the numpy restatement."""
     words = synth.random_words(12, 0.5, seed=5, colour_max=255)
     words[words != 0] |= np.uint32(0xFF0000)  # force r = 255
     ctx.set_grid(words.reshape(-1), (12, 12, 12))
     for variant in (981, 117):
-        ctx.extract(variant, THR, 4, lut_double=lut_double)
-        fn, ex, _ = npr.c3hlac(words, variant, THR, 4, lut_double=lut_double)
+        ctx.extract(variant, THR, 4, color_mode=color_mode)
+        fn, ex, _ = npr.c3hlac(words, variant, THR, 4, color_mode=color_mode)
         assert np.array_equal(ctx.features(), fn)
+
+
+@pytest.mark.parametrize("color_mode", [c3hlac.COLOR_C3_FLOAT, c3hlac.COLOR_CHLAC])
+def test_colour_modes_random_grids(ctx, color_mode):
+    """The other setColor tables on random colours, every variant / subdivision shape, on
+    the tile kernels and (dense) the matrix-core body."""
+    for occ, dims in ((0.05, (33, 27, 21)), (1.0, (24, 24, 24))):
+        words = synth.random_words(dims, occ, seed=17, colour_max=255)
+        ctx.set_grid(words.reshape(-1), dims)
+        for variant, S, off in ((981, 10, (0, 0, 0)), (117, 6, (1, 2, 3)), (117, 0, (0, 0, 0))):
+            ctx.extract(variant, (100, 200, 50), S, off, color_mode=color_mode)
+            fn, ex, _ = npr.c3hlac(words, variant, (100, 200, 50), S, off, color_mode=color_mode)
+            assert np.array_equal(ctx.features(), fn), (occ, variant, S, off)
+            assert np.array_equal(ctx.exist(), ex)
+
+
+def test_colour_mode_rejected(ctx):
+    words = synth.random_words(8, 0.5, seed=5)
+    ctx.set_grid(words.reshape(-1), (8, 8, 8))
+    with pytest.raises(c3hlac.C3HError):
+        ctx.extract(117, THR, 4, color_mode=3)
 
 
 @pytest.mark.parametrize("occ", [0.02, 0.3, 1.0])
