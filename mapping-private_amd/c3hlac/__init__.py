@@ -312,14 +312,27 @@ class Context:
         ns = np.zeros(len(frames), np.int64)
         for i, fr in enumerate(frames):
             if on_dev:
-                assert fr.is_contiguous() and fr.shape[-1] == 4
+                import torch
+                if fr.dtype != torch.float32 or fr.ndim != 2 or fr.shape[1] != 4 or not fr.is_contiguous():
+                    raise ValueError("run_point_frames: frame %d must be a contiguous (n, 4) float32 tensor" % i)
+                if fr.device.type != "cuda" or (fr.device.index or 0) != self.device:
+                    raise ValueError("run_point_frames: frame %d is on %s, the context on cuda:%d"
+                                     % (i, fr.device, self.device))
                 ptrs[i] = fr.data_ptr()
             else:
                 fr = np.ascontiguousarray(fr, dtype=np.float32)
-                assert fr.ndim == 2 and fr.shape[1] == 4
+                if fr.ndim != 2 or fr.shape[1] != 4:
+                    raise ValueError("run_point_frames: frame %d must be (n, 4)" % i)
                 keep.append(fr)
                 ptrs[i] = fr.ctypes.data
             ns[i] = fr.shape[0]
+        if d_out is not None and hasattr(d_out, "data_ptr"):
+            need = len(frames) * max(self.M, 1) * self.rank * DET_DTYPE.itemsize
+            have = d_out.numel() * d_out.element_size()
+            if have < need or not d_out.is_contiguous() or d_out.device.type != "cuda" or \
+                    (d_out.device.index or 0) != self.device:
+                raise ValueError("run_point_frames: d_out must be a contiguous tensor of >= %d bytes on cuda:%d"
+                                 % (need, self.device))
         p = _capi.ExtractParams()
         p.variant = int(variant)
         p.thr = (C.c_int32 * 3)(*[int(t) for t in thr])

@@ -511,7 +511,10 @@ struct c3h_ctx {
   int64_t scores_n = 0;
   // layout of the score buffers' last search (modes' offsets and sizes, M, frames, buffer):
   // an equal layout lets the gate skip the -1 fill of positions already gated out
+  // layout of the last search whose gate was enqueued on `scores` (empty: unknown); a search
+  // of the same layout writes -1 only where that one had not gated the position out already
   std::vector<int64_t> scores_layout;
+  std::vector<int64_t> cap_layout;  // a captured (pipelined) search's layout, until its gate runs
   c3h::DevBuf<float> qt;            // D x Opad transposed model basis (fast score path)
   int Opad = 0;
   c3h::DevBuf<c3h::ScorePartial> partials;
@@ -545,6 +548,8 @@ struct c3h_ctx {
     int nf;
     int age;
     bool stamped = false;  // tile stamps already set (points-in scatter): no occupancy role
+    c3h_ctx* set = nullptr;       // the buffer set (context) the batch was captured on
+    std::vector<int64_t> layout;  // its score-array layout, recorded there once its gate is enqueued
   };
   struct PipeKey {
     int32_t div_b[3], min_b[3];

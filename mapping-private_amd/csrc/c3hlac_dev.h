@@ -359,8 +359,8 @@ __device__ __forceinline__ void occupancy_bits_body(const OccArgs& oa, int bx, i
         }
         if (a < 0 || b < 0) continue;  // uniform: not a centre row
         const int tyz = ns0 * (a + ns1 * b);
-        if (pair_ok) {  // occupied voxel words are kOcc | rgb (< 2^25): bit 24 is occupancy
-          const uint32_t o = (ws[0] >> 24) | ((ws[1] >> 23) & 2u) | ((ws[2] >> 22) & 4u) | ((ws[3] >> 21) & 8u);
+        if (pair_ok) {  // any non-zero word is occupied (as in the general path and the tile pass)
+          const uint32_t o = min(ws[0], 1u) | (min(ws[1], 1u) << 1) | (min(ws[2], 1u) << 2) | (min(ws[3], 1u) << 3);
           const int ta = tA + tyz, tb = tB + tyz;
           if (o & mA) atomicOr(&s_bits[ta >> 5], 1u << (ta & 31));
           if (o & mB) atomicOr(&s_bits[tb >> 5], 1u << (tb & 31));

@@ -398,7 +398,7 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
     layout.push_back(rm.m[i].P);
   }
   const bool same_layout = layout == ctx->scores_layout;
-  ctx->scores_layout.swap(layout);
+  ctx->scores_layout.clear();  // recorded again once this search's gate is enqueued (below)
   ENSURE(ctx->G, (size_t)nf * H * ctx->D);
   // sparse compress: only the non-empty rows of the extract's list (the rest stay stale
   // and every consumer gates them on exist)
@@ -539,6 +539,7 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
       ctx->g_sparse = true;
     }
     if (ctx->capture) {  // pipelined c3h_run_frames: the tick kernel runs these stages
+      ctx->cap_layout.swap(layout);  // recorded by pipe_tick when the gate role is enqueued
       ctx->cap_q = q;
       ctx->cap_sc = sc;
       ctx->cap_sparse_g = sparse_g;
@@ -558,6 +559,7 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
       Timed t(ctx, 3, nf);
       HIPCHK(c3h::launch_sparse_search(q, sparse_g ? &sc : nullptr, ctx->stream));
     }
+    ctx->scores_layout.swap(layout);  // the gate writes every position of this layout
     if (q.prof) {
       int rc = prof_dump(ctx, "score_list_kernel", nparts);
       if (rc != C3H_OK) return rc;
@@ -579,6 +581,7 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
       Timed t(ctx, 3);
       for (auto& a : launches) HIPCHK(c3h::launch_score(a, ctx->stream));
     }
+    ctx->scores_layout.swap(layout);
     Timed t(ctx, 4);
     HIPCHK(c3h::launch_replay(ctx->scores.p, rm, ctx->M, ctx->rank, range[0], range[1], range[2], clean,
                               ctx->d_lists.p, d_outs ? d_outs[0] : nullptr, ctx->stream));
@@ -1969,6 +1972,8 @@ int pipe_tick(c3h_ctx* ctx, const c3h_ctx::PipeBatch* fresh) {
     hipError_t e = c3h::launch_tick(tp, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, "launch_tick", e);
   }
+  for (auto& b : ctx->pipe)  // this tick enqueued the batch's gate: its layout is written
+    if (b.age == 2 && b.set) b.set->scores_layout = b.layout;
   std::vector<c3h_ctx::PipeBatch> next;
   for (auto& b : ctx->pipe)
     if (b.age < 3) {
@@ -2028,11 +2033,23 @@ int pipe_prepare(c3h_ctx* ctx, const uint32_t* const* grids, c3h_det* const* out
   }
   c->nframes_feat = 1;  // slot 0 is the context's view from here on
   *fresh = c3h_ctx::PipeBatch{c->cap_c3, c->cap_q, c->cap_sc, nb, 0};
+  fresh->set = c;
+  fresh->layout = c->cap_layout;
   return rc;
 }
 
 // Launches a prepared batch's first tick; rc: pipe_prepare's result (> 0)
 int pipe_commit(c3h_ctx* ctx, const c3h_ctx::PipeBatch& fresh, const c3h_ctx::PipeKey& k, int rc) {
+  if (ctx->pipe.empty()) {
+    // a stream starts: the occupancy role's tail-stealing pool (words 0-1 of each buffer
+    // set's tile flags) resets itself at the end of every launch; zero it here as well, so
+    // a launch that ended early (an aborted stream) cannot leave it counting
+    for (int sidx = 0; sidx < kPipeDepth; ++sidx) {
+      c3h_ctx* c = sidx == 0 ? ctx : (sidx - 1 < (int)ctx->lanes.size() ? ctx->lanes[sidx - 1] : nullptr);
+      if (c && c->tileflags.p && c->tileflags.n >= 2)
+        HIPCHK(hipMemsetAsync(c->tileflags.p, 0, 2 * sizeof(uint32_t), ctx->stream));
+    }
+  }
   int trc = pipe_tick(ctx, &fresh);
   if (trc != C3H_OK) return trc;
   ctx->pipe_seq++;

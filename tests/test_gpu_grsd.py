@@ -125,5 +125,14 @@ def test_grsd_leaf_wider_than_four_normal_radii(ctx):
     feat_ref, _, radii_ref, types_ref = go.grsd(pts, dn, g, layout, cloud, 0.1)
     radii, types = ctx.rsd()
     np.testing.assert_allclose(radii, radii_ref, rtol=1e-5, atol=1e-7)
-    if np.array_equal(types, types_ref):
+    # get_type (grsd_colorCHLAC_tools.hpp:104-118) on radii equal within 1e-5: a voxel may
+    # only change type where a radius sits on one of its thresholds (a tie of the float
+    # orders); every other voxel's type must agree, and with all types equal the features
+    diff = np.flatnonzero(types != types_ref)
+    rmin, rmax = radii_ref[diff, 0].astype(np.float64), radii_ref[diff, 1].astype(np.float64)
+    near = lambda v, t: np.abs(v - t) <= 1e-5 * t + 1e-7  # noqa: E731
+    tie = near(rmin, 0.100) | near(rmax, 0.175) | near(rmin, 0.015) | (np.abs(rmax - rmin - 0.050) <= 1e-6)
+    assert tie.all(), diff[~tie]
+    assert len(diff) <= max(1, len(types) // 100)
+    if len(diff) == 0:
         assert np.array_equal(ctx.features()[0], feat_ref[0].astype(np.float32))

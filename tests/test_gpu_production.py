@@ -313,3 +313,34 @@ def test_pipeline_offset_subdivisions_vs_oracle(ctx, prod):
         shape = tuple(int(n) - b + 1 for n, b in zip(sb[::-1], BOX))  # (z, y, x) positions
         _check_det(got[i], sc.reshape(M, -1), shape, "frame %d" % i)
     ctx.set_batch(32)
+
+
+def test_score_layout_across_pipelined_and_single_searches(ctx, prod):
+    """The sparse -1 fill of the score arrays (a position is rewritten only where the last
+    search of the same layout had not gated it out) across single-frame searches and
+    pipelined batches of one frame on the same context, whose score arrays share that
+    layout (the layout is recorded once a search's gate is enqueued, not at
+    capture).  After every single search the whole score array equals the float64
+    oracle's: -1 exactly where the oracle gates the position out."""
+    import torch
+    d_out = torch.zeros((4, M * 3), dtype=torch.int64, device="cuda:0")
+    ctx.set_batch(1)
+    ctx.set_pipeline(True)
+    for k, (single, batch) in enumerate([(3, 11), (11, 3), (5, 5), (17, 29)]):
+        g = prod["d_grids"][single]
+        ctx.set_grid(g, (G,) * 3, leaf=LEAF)
+        ctx.extract(F, THR, S)
+        ctx.search(BOX, EXIST, rotate=True)
+        sc = ctx.scores()
+        ref = prod["ref"][single][2]
+        assert np.array_equal(sc < 0, ref < 0), k
+        ok = ref > 0
+        np.testing.assert_allclose(sc[ok], ref[ok], rtol=RTOL)
+        ptrs = np.array([prod["d_grids"][batch].data_ptr()], np.uint64)
+        ctx.run_frames(ptrs, (G,) * 3, (0, 0, 0), LEAF, F, THR, S, BOX, EXIST, True, d_out[k].data_ptr())
+        ctx.synchronize()
+        _check_det(d_out[k].cpu().numpy().reshape(M, 3), prod["ref"][batch][2].reshape(M, -1), (P1, P1, P1),
+                   "batch %d" % k)
+        sc = ctx.scores()  # the context holds the batch's frame
+        ref = prod["ref"][batch][2]
+        assert np.array_equal(sc < 0, ref < 0), ("batch", k)
