@@ -69,12 +69,17 @@ def algorithmic_bytes_c3(G, H, F):
     return G ** 3 * 4 + H * F * 4 + H * 4
 
 
+def scene_points(synth, rank, s):
+    """the 1M points of make_grids' scene s (grids 4 s .. 4 s + 3)"""
+    return synth.kinect_scene(N_RAYS, grid=GRID, leaf=LEAF, seed=synth.BASE_SEED + 1000 * rank + s)
+
+
 def make_grids(ctx, dev, nf, rank, synth, c3hlac, torch):
     """nf resident 256^3 grids: scenes voxelised on the GPU, plus x-shifted copies."""
-    grids, t_vox_ms, n_points, scene0 = [], [], 0, None
+    grids, t_vox_ms, n_points = [], [], 0
     per_scene = 4  # the scene and three x-shifts of it (distinct buffers)
     for s in range(-(-nf // per_scene)):
-        pts = synth.kinect_scene(N_RAYS, grid=GRID, leaf=LEAF, seed=synth.BASE_SEED + 1000 * rank + s)
+        pts = scene_points(synth, rank, s)
         d_pts = torch.from_numpy(pts).to(dev)
         torch.cuda.current_stream(dev).synchronize()
         # untimed first call per scene: a scene with more points than any before it grows the
@@ -250,6 +255,12 @@ def main():
     tick_avg_s = tick_ms / n_ticks / 1e3
     alg_bytes = algorithmic_bytes_c3(GRID, H, VARIANT) * B
     achieved = alg_bytes / tick_avg_s / 1e9
+    # the bytes the tick must move: the grid stream plus the rows of the non-empty
+    # subdivisions only (an empty subdivision keeps exist 0 and every reader gates on it)
+    # and exist, from the frames of the timed region (the context holds the last one)
+    nonempty = int((ctx.exist() > 0).sum())
+    min_bytes = (GRID ** 3 * 4 + nonempty * VARIANT * 4 + H * 4) * B
+    achieved_min = min_bytes / tick_avg_s / 1e9
     result = {
         "metric": "Mvoxels/s C3-HLAC + detections/s sliding-box, 256^3 grid",
         "value": voxels / elapsed / 1e6,
@@ -299,6 +310,13 @@ def main():
             "frames_per_launch": B,
             "launches": n_ticks,
             "avg_launch_ms": tick_avg_s * 1e3,
+            "achieved_min_bytes": achieved_min,
+            "frac_min_bytes": achieved_min / HBM_PEAK_GBS,
+            "min_bytes_per_frame": min_bytes // B,
+            "min_bytes_note": "the same tick time on the bytes the tick must move: the 4 B/voxel grid stream, "
+                              "feature rows of the %d non-empty subdivisions only (of %d) and exist; 'achieved' / "
+                              "'frac' use SURVEY 8(d)'s algorithmic bytes, which charge a row to every "
+                              "subdivision" % (nonempty, H),
         },
     }
     if args.point_frames > 0:
@@ -307,7 +325,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         f0 = args.warmup * B  # the first timed frame: the oracle re-computes it as it is timed
         rec0 = d[f0]
-        result["cpu_baseline"] = cpu_baseline(grids[f0 % nf].cpu().numpy().view(np.uint32), rec0, args.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline(grids[f0 % nf].cpu().numpy().view(np.uint32), rec0, args.cpu_seconds,
+                                              scene_points(synth, rank, (f0 % nf) // 4), grids[(f0 % nf) // 4 * 4])
+        if "points_in" in result:
+            result["points_in"]["cpu_baseline"] = cpu_baseline_points(synth, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result))
     ctx.close()
@@ -424,14 +445,29 @@ def host_cpu():
     return model, os.cpu_count(), avail
 
 
-def cpu_baseline(words, gpu_rec, seconds):
+def cpu_baseline(words, gpu_rec, seconds, scene_pts=None, scene_grid=None):
     """The oracle (single-threaded C restatement of the reference, -O2) on the same
     workload -- C3-HLAC-117 + exist + setData/search of the 10 models in the reference's
     fp32 order -- repeated on the first timed frame's grid until `seconds` elapse (at least
     once).  It is also the check of that frame: the GPU detection of every model must be
-    the float64 oracle's (position, mode) with the score within 1e-5."""
+    the float64 oracle's (position, mode) with the score within 1e-5.  The voxelise phase
+    of detect_object.cpp:182-186's split (getVoxelGrid on the 1M points) is timed on the
+    scene the frame's grid was voxelised from, and its grid checked against the GPU's."""
     import pyoracle as po
     from c3hlac import synth
+    t_vox, vox_check = None, None
+    if scene_pts is not None:
+        nv, tv0 = 0, time.perf_counter()
+        while nv == 0 or time.perf_counter() - tv0 < seconds / 4:
+            gv, lay_v, cl_v = po.voxelize(scene_pts, LEAF)
+            nv += 1
+        t_vox = (time.perf_counter() - tv0) / nv
+        if scene_grid is not None:  # packed words of the oracle's voxels vs the GPU's grid
+            w = scene_grid.cpu().numpy().view(np.uint32)
+            occ = np.flatnonzero(lay_v >= 0)
+            ok = (list(gv.div_b) == [GRID] * 3 and np.array_equal(np.flatnonzero(w), occ) and
+                  np.array_equal(w[occ] & np.uint32(0xFFFFFF), cl_v[lay_v[occ], 3].view(np.uint32)))
+            vox_check = "oracle getVoxelGrid of the scene == the GPU's grid: %s" % ("yes" if ok else "MISMATCH")
     g, layout, cloud = po.grid_inputs(words, (GRID,) * 3, LEAF)
     axis_t, var, axis_q = synth.random_bases(VARIANT, D, M, R, seed=synth.BASE_SEED)
     ap = synth.whiten(axis_t, var)
@@ -476,6 +512,46 @@ def cpu_baseline(words, gpu_rec, seconds):
         "cpus_available": avail,
         "frame_check": "GPU detections of the first timed frame vs the float64 oracle on its grid: %s" % (
             "all %d models equal (score within 1e-5)" % M if not bad else "MISMATCH in models %s" % bad),
+        "phases_s_per_frame": {"voxelize": t_vox, "c3hlac": t_c3 / n, "search": t_s / n},
+        "phases_note": "detect_object.cpp:182-186's split, one core: getVoxelGrid of the 1M-point scene (%s), "
+                       "C3-HLAC + exist, setData + search; 'value' covers the C3 + search phases over the 256^3 "
+                       "voxels (the metric's grid-resident region)" % (vox_check or "not timed"),
+        "frames_per_s_end_to_end": 1.0 / (t_vox + (t_c3 + t_s) / n) if t_vox else None,
+    }
+
+
+def cpu_baseline_points(synth, seconds):
+    """configs[3]'s unit of work on one core (single-thread frames/s): one
+    1M-point frame of the points-in pass through the oracle -- getVoxelGrid (128^3),
+    C3-HLAC-981 S=10 + exist, setData (981 -> 100) + search of 1 model x r=20 -- timed per
+    phase, repeated over the pass's base scenes until `seconds` elapse (at least once)."""
+    import pyoracle as po
+    axis_t, var, axis_q = synth.random_bases(P_VARIANT, D, P_M, R, seed=synth.BASE_SEED + 31)
+    ap = synth.whiten(axis_t, var)
+    tv = tc = ts = 0.0
+    n = 0
+    t_start = time.perf_counter()
+    while n == 0 or time.perf_counter() - t_start < seconds:
+        pts = synth.kinect_scene(N_RAYS, grid=P_GRID, leaf=P_LEAF, seed=synth.BASE_SEED + 7000 + n % 16)
+        t0 = time.perf_counter()
+        g, layout, cloud = po.voxelize(pts, P_LEAF)
+        t1 = time.perf_counter()
+        f, sb, _ = po.c3hlac(g, layout, cloud, P_VARIANT, THR, P_LEAF, SUBDIV)
+        ex = po.exist(f)
+        t2 = time.perf_counter()
+        po.search(sb, f, ex, ap, axis_q, BOX, RANK, EXIST_THR)
+        t3 = time.perf_counter()
+        tv, tc, ts = tv + t1 - t0, tc + t2 - t1, ts + t3 - t2
+        n += 1
+    tot = tv + tc + ts
+    return {
+        "value": n / tot,
+        "unit": "frames/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": "%d 1M-point frame(s) of the points-in pass's base scenes, one core: voxelize %.3f s, C3-HLAC-981 "
+                  "%.3f s, search %.3f s per frame" % (n, tv / n, tc / n, ts / n),
+        "phases_s_per_frame": {"voxelize": tv / n, "c3hlac": tc / n, "search": ts / n},
     }
 
 

@@ -343,6 +343,15 @@ int c3h_get_compressed(c3h_ctx* ctx, float* out, int on_device);
 int c3h_get_scores(c3h_ctx* ctx, double* out, int64_t* n_out, int on_device);
 /* SearchObjMulti::removeOverlap on host lists (pure host function, no context). */
 int c3h_remove_overlap(int32_t M, int32_t rank, const int32_t range[3], c3h_det* lists);
+/* SearchObj(Multi)::searchPart's sequential rank update (search.cpp:464-474 with checkOverlap
+ * :327-356) replayed on host score arrays in c3h_get_scores' layout: per mode of search()'s
+ * schedule for range / rotate (modes without a position skipped), M x P doubles in (z, y, x)
+ * scan order over subdiv_b, -1 = gated out.  lists (M x rank, host) continue from their
+ * state, as search() does.  Pure host function: merges the score arrays of the z-slabs of
+ * one scene (c3hlac/dist.py) into the whole scene's ranked lists.  Returns the number of
+ * searched modes. */
+int c3h_replay_scores(int32_t M, int32_t rank, const int32_t range[3], int32_t rotate, const int32_t subdiv_b[3],
+                      const double* scores, c3h_det* lists);
 
 /* PCA::read (color_voxel_recognition/src/pca.cpp:119-185): axis column-major dim x dim
  * (eigenvector i contiguous), variances, optional mean.  Returns dim or an error.

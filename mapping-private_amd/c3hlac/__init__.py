@@ -447,6 +447,17 @@ def write_feature(path, feat, remove_zero=True, fields=None):
           None, "feature_write")
 
 
+def replay_scores(scores, subdiv_b, ranges, lists, rotate=True):
+    """c3h_replay_scores: searchPart's rank update over score arrays in c3h_get_scores'
+    layout (host function); lists: (M, rank) DET_DTYPE, continued from their state."""
+    lists = np.ascontiguousarray(lists, dtype=DET_DTYPE)
+    M, rank = lists.shape
+    sc = np.ascontiguousarray(scores, dtype=np.float64)
+    check(_capi.load().c3h_replay_scores(M, rank, i32x3(ranges), int(bool(rotate)), i32x3(subdiv_b), ptr(sc),
+                                         ptr(lists)), None, "replay_scores")
+    return lists
+
+
 def remove_overlap(lists, ranges):
     """SearchObjMulti::removeOverlap on (M, rank) DET_DTYPE lists (host function)."""
     lists = np.ascontiguousarray(lists, dtype=DET_DTYPE)

@@ -119,9 +119,10 @@ def slab_search(ctx, words_zyx, variant, thr, subdiv, ranges, exist_threshold, r
     engine settings) are already set.  Returns (M,) c3h_det records with global z, or None
     when the slab owns no plane.
 
-    search_rank (SearchObj::setRank) must be 1: the rank > 1 update with checkOverlap
+    search_rank (SearchObj::setRank) must be 1 here: the rank > 1 update with checkOverlap
     (search.cpp:327-356, 464-474) is sequential over the whole scene's scan order, so
-    per-slab lists cannot be merged into it; C3HError(C3H_ERR_ARG) otherwise.
+    per-slab lists cannot be merged into it (C3HError(C3H_ERR_ARG) otherwise); rank > 1
+    goes through slab_scores + merge_slab_scores, which replay it over the whole scene.
 
     The slab is loaded from packed grid words (c3h_set_grid), so voxels are placed by their
     cell index.  A scene voxelised from points whose centroids round across a cell boundary
@@ -130,7 +131,7 @@ def slab_search(ctx, words_zyx, variant, thr, subdiv, ranges, exist_threshold, r
     import numpy as np
     from ._capi import C3HError, DET_DTYPE, ERRORS
     if int(search_rank) != 1:
-        raise C3HError("slab_search: search_rank %d: %s (only rank 1 merges across slabs)"
+        raise C3HError("slab_search: search_rank %d: %s (rank > 1: slab_scores + merge_slab_scores)"
                        % (search_rank, ERRORS.get(-1, -1)))
     gz, gy, gx = words_zyx.shape
     zr_max = max(mode_ranges(md, ranges)[2] for md in mode_schedule(ranges, rotate))
@@ -159,3 +160,138 @@ def gather_slab_lists(local, M, schedule, dist, device="cpu"):
     parts = [torch.empty_like(buf) for _ in range(dist.get_world_size())]
     dist.all_gather(parts, buf)
     return merge_slab_lists([p.cpu().numpy().reshape(-1).view(DET_DTYPE) for p in parts], schedule)
+
+
+# ---------------------------------------------------------------- rank > 1 over slabs
+# The rank > 1 lists depend on the whole scene's scan order: a candidate enters only above
+# the list's current rank-th score, and checkOverlap compares it with every entry ranked
+# before it, wherever in the scene that entry came from (search.cpp:327-356, 464-474).  So
+# per-slab lists cannot be merged; instead every rank sends the scores of the box positions
+# it owns (origins in its subdivision planes [p0, p1); its sub-grid's extra planes only
+# complete boxes that start inside the slab), and the sequential update is replayed over
+# the assembled whole-scene score arrays (c3h_replay_scores, host).  Scores of a position
+# are bit-identical on the slab and on the whole scene (integer-exact features, the same
+# box-sum order), so the lists are the whole-scene search's.
+
+def scene_subdivisions(grid_xyz, subdiv):
+    """setVoxelFilter's getSubdivNum without offsets (c3_hlac.cpp:210-225, float arithmetic)."""
+    import numpy as np
+    inv = np.float32(1.0 / subdiv)
+    return tuple(int(np.ceil(np.float32(g) * inv)) for g in grid_xyz)
+
+
+def _mode_geoms(sb, ranges, rotate):
+    """(mode, xe, ye, ze) of every scheduled mode with a position (the score layout's order)."""
+    out = []
+    for md in mode_schedule(ranges, rotate):
+        xr, yr, zr = mode_ranges(md, ranges)
+        xe, ye, ze = sb[0] - xr + 1, sb[1] - yr + 1, sb[2] - zr + 1
+        if xe > 0 and ye > 0 and ze > 0:
+            out.append((md, xe, ye, ze))
+    return out
+
+
+def slab_scores(ctx, words_zyx, variant, thr, subdiv, ranges, exist_threshold, rank, world, rotate=True):
+    """Extract + search of rank `rank`'s slab (as slab_search) -> (p0, blocks): per mode of
+    the whole scene's schedule the (M, nz, ye, xe) float64 scores of the positions whose
+    origin plane z is in [p0, min(p1, ze)), -1 where gated out; None when the slab owns no
+    plane.  The slab's own lists are not used (rank 1 on the fast path)."""
+    import numpy as np
+    gz, gy, gx = words_zyx.shape
+    zr_max = max(mode_ranges(md, ranges)[2] for md in mode_schedule(ranges, rotate))
+    ext = slab_extent(gz, subdiv, zr_max, rank, world)
+    if ext is None:
+        return None
+    p0, p1, vz0, vz1, zoff = ext
+    ctx.set_grid(np.ascontiguousarray(words_zyx[vz0:vz1]).reshape(-1), (gx, gy, vz1 - vz0))
+    sbl, _ = ctx.extract(variant, thr, subdiv, (0, 0, zoff))
+    ctx.set_rank(1)
+    ctx.search(ranges, exist_threshold, rotate=rotate)
+    return owned_blocks(ctx.scores(), sbl, p0, p1, (gx, gy, gz), subdiv, ranges, max(ctx.M, 1), rotate)
+
+
+def owned_blocks(scores_local, sb_local, p0, p1, grid_xyz, subdiv, ranges, M, rotate=True):
+    """A slab's score arrays (c3h_get_scores layout over its sub-grid's subdivisions
+    sb_local, plane 0 = the scene's plane p0) -> (p0, per whole-scene mode the (M, nz, ye,
+    xe) block of the positions with origin plane in [p0, min(p1, ze)))."""
+    import numpy as np
+    local, off, o = {}, {}, 0
+    for md, xe, ye, ze in _mode_geoms(sb_local, ranges, rotate):
+        local[md] = (xe, ye, ze)
+        off[md] = o
+        o += M * xe * ye * ze
+    assert o == scores_local.size or (o == 0 and scores_local.size <= 1), (o, scores_local.size)
+    blocks = []
+    for md, xe, ye, ze in _mode_geoms(scene_subdivisions(grid_xyz, subdiv), ranges, rotate):
+        nz = max(0, min(p1, ze) - p0)
+        if nz == 0:
+            blocks.append(np.zeros((M, 0, ye, xe)))
+            continue
+        lx, ly, lz = local[md]
+        assert (lx, ly) == (xe, ye) and lz >= nz
+        blk = scores_local[off[md]:off[md] + M * lx * ly * lz].reshape(M, lz, ly, lx)
+        blocks.append(np.ascontiguousarray(blk[:, :nz], dtype=np.float64))
+    return p0, blocks
+
+
+def merge_slab_scores(parts, grid_xyz, subdiv, ranges, search_rank, rotate=True, lists=None):
+    """parts: every rank's slab_scores result (None: no plane) -> (the whole scene's score
+    arrays in c3h_get_scores' layout, its (M, search_rank) lists replayed from `lists`
+    (default: setRank's state))."""
+    import numpy as np
+    from . import replay_scores
+    from ._capi import DET_DTYPE
+    parts = [p for p in parts if p is not None]
+    sbg = scene_subdivisions(grid_xyz, subdiv)
+    geoms = _mode_geoms(sbg, ranges, rotate)
+    M = parts[0][1][0].shape[0]
+    full = []
+    for i, (md, xe, ye, ze) in enumerate(geoms):
+        a = np.full((M, ze, ye, xe), np.nan)
+        for p0, blocks in parts:
+            b = blocks[i]
+            a[:, p0:p0 + b.shape[1]] = b
+        assert not np.isnan(a).any(), "a position no slab owns"
+        full.append(a.reshape(-1))
+    scores = np.concatenate(full) if full else np.zeros(0)
+    if lists is None:
+        lists = np.zeros((M, int(search_rank)), DET_DTYPE)
+    return scores, replay_scores(scores, sbg, ranges, lists, rotate=rotate)
+
+
+def gather_slab_scores(local, grid_xyz, subdiv, ranges, M, search_rank, dist, rotate=True, device="cpu"):
+    """All-gather every rank's slab_scores (padded to the largest slab) and merge them on
+    every rank -> (M, search_rank) lists of the whole scene."""
+    import numpy as np
+    sbg = scene_subdivisions(grid_xyz, subdiv)
+    geoms = _mode_geoms(sbg, ranges, rotate)
+    world = dist.get_world_size()
+    zr_max = max(mode_ranges(md, ranges)[2] for md in mode_schedule(ranges, rotate))
+    maxp = max(b - a for a, b in slab_planes(sbg[2], world))
+    per = [M * maxp * ye * xe for _, xe, ye, _ in geoms]
+    buf = np.full(1 + sum(per), -2.0)
+    if local is not None:
+        p0, blocks = local
+        buf[0] = p0
+        o = 1
+        for n, b in zip(per, blocks):
+            buf[o:o + b.size] = b.reshape(-1)
+            o += n
+    t = torch.from_numpy(buf).to(device)
+    got = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(got, t)
+    parts = []
+    for r, g in enumerate(got):
+        g = g.cpu().numpy()
+        if g[0] < 0:
+            continue
+        p0 = int(g[0])
+        ext = slab_extent(grid_xyz[2], subdiv, zr_max, r, world)
+        p1 = ext[1]
+        blocks, o = [], 1
+        for n, (_, xe, ye, ze) in zip(per, geoms):
+            nz = max(0, min(p1, ze) - p0)
+            blocks.append(g[o:o + M * nz * ye * xe].reshape(M, nz, ye, xe))
+            o += n
+        parts.append((p0, blocks))
+    return merge_slab_scores(parts, grid_xyz, subdiv, ranges, search_rank, rotate=rotate)[1]

@@ -2603,6 +2603,48 @@ int c3h_remove_overlap(int32_t M, int32_t rank, const int32_t range[3], c3h_det*
   return C3H_OK;
 }
 
+// searchPart's rank update (search.cpp:464-474 with checkOverlap :327-356) replayed on the
+// host over c3h_get_scores-layout arrays: per scheduled mode, per model, positions in
+// (z, y, x) scan order; a candidate reaches the update only above the current rank-th
+// score (that score never decreases: the replay kernel's rule)
+int c3h_replay_scores(int32_t M, int32_t rank, const int32_t range[3], int32_t rotate, const int32_t subdiv_b[3],
+                      const double* scores, c3h_det* lists) {
+  if (M < 1 || rank < 1 || !range || !subdiv_b || !scores || !lists) return C3H_ERR_ARG;
+  const int r1 = range[0], r2 = range[1], r3 = range[2];
+  if (r1 < 1 || r2 < 1 || r3 < 1) return C3H_ERR_ARG;
+  int modes[6];
+  const int nm = mode_schedule(r1, r2, r3, rotate, modes);
+  int64_t off = 0;
+  int searched = 0;
+  for (int i = 0; i < nm; ++i) {
+    int xr, yr, zr;
+    get_range(modes[i], r1, r2, r3, &xr, &yr, &zr);
+    const int xe = subdiv_b[0] - xr + 1, ye = subdiv_b[1] - yr + 1, ze = subdiv_b[2] - zr + 1;
+    if (!(xe > 0 && ye > 0 && ze > 0)) continue;
+    const int64_t P = (int64_t)xe * ye * ze;
+    for (int m = 0; m < M; ++m) {
+      c3h_det* L = lists + (size_t)m * rank;
+      const double* sc = scores + off + (int64_t)m * P;
+      for (int64_t p = 0; p < P; ++p) {
+        const double cs = sc[p];
+        if (!(cs > L[rank - 1].score)) continue;
+        const int x = (int)(p % xe), y = (int)((p / xe) % ye), z = (int)(p / ((int64_t)xe * ye));
+        for (int j = 0; j < rank; j++) {
+          if (cs > L[j].score) {
+            const int num = check_overlap(L, rank, r1, r2, r3, x, y, z, modes[i]);
+            for (int q = 0; q < num - j; q++) L[num - q] = L[num - 1 - q];
+            if (j <= num) L[j] = c3h_det{cs, x, y, z, modes[i]};
+            break;
+          }
+        }
+      }
+    }
+    off += P * M;
+    ++searched;
+  }
+  return searched;
+}
+
 int c3h_pca_read(const char* path, int32_t ascii, float* axis, float* var, float* mean,
                  int32_t* has_mean, int32_t max_dim) {
   const bool query = !axis && !var;  // size query: read the header only

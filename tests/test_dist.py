@@ -160,10 +160,96 @@ def test_slab_partition():
 
 
 def test_slab_search_rejects_rank_above_one():
-    """rank > 1 lists cannot be merged across slabs (the checkOverlap update is sequential
-    over the whole scene): slab_search fails with C3H_ERR_ARG before touching a context."""
+    """rank > 1 lists cannot be merged from per-slab lists (the checkOverlap update is
+    sequential over the whole scene): slab_search fails with C3H_ERR_ARG before touching a
+    context; rank > 1 goes through slab_scores + merge_slab_scores (below)."""
     from c3hlac import dist as cdist
     from c3hlac._capi import C3HError
     words = np.zeros((20, 20, 20), np.uint32)
     with pytest.raises(C3HError, match="C3H_ERR_ARG"):
         cdist.slab_search(None, words, 117, THR, 10, (2, 2, 2), 0, 0, 2, search_rank=3)
+
+
+def _oracle_scene(words, ranges, rank, offset=(0, 0, 0)):
+    """float64 oracle: (subdivisions, score arrays, rank-`rank` lists) of words[z, y, x]."""
+    import np_ref as npr
+    import pyoracle as po
+    from c3hlac import synth
+    from c3hlac._capi import DET_DTYPE
+    feat, ex, sb = npr.c3hlac(words, 117, THR, SLAB_S, offset)
+    axis_t, var, axis_q = synth.random_bases(117, 12, 3, 4, seed=7)
+    L, _, sc = po.search(sb, feat, ex, synth.whiten(axis_t, var), axis_q, ranges, rank, 10, dbl=True,
+                         want_scores=True)
+    rec = np.zeros((3, rank), DET_DTYPE)
+    for m in range(3):
+        for i in range(rank):
+            k = m * rank + i
+            rec[m, i] = (L.score[k], L.x[k], L.y[k], L.z[k], L.mode[k])
+    return sb, sc, rec
+
+
+def _slab_scores_worker(rank, world, port, ranges, srank, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from c3hlac.dist import gather_slab_scores, mode_ranges, mode_schedule, owned_blocks, slab_extent
+    words = _sparse_words()
+    zr_max = max(mode_ranges(md, ranges)[2] for md in mode_schedule(ranges))
+    ext = slab_extent(SLAB_G, SLAB_S, zr_max, rank, world)
+    local = None
+    if ext is not None:
+        p0, p1, vz0, vz1, zoff = ext
+        sbl, sc, _ = _oracle_scene(words[vz0:vz1], ranges, 1, (0, 0, zoff))
+        local = owned_blocks(sc, sbl, p0, p1, (SLAB_G,) * 3, SLAB_S, ranges, 3)
+    out = gather_slab_scores(local, (SLAB_G,) * 3, SLAB_S, ranges, 3, srank, dist)
+    q.put((rank, out.tobytes()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ranges,srank", [((2, 2, 2), 3), ((1, 2, 3), 4)])
+def test_gloo_two_ranks_scene_slabs_rank_above_one(ranges, srank):
+    """rank 3 / 4 over two z-slabs (gloo, world size 2): every rank's owned position scores
+    are gathered and the sequential update replayed over the whole scene; the lists equal
+    the whole-scene float64 oracle's (search.cpp:327-356, 464-474)."""
+    from c3hlac._capi import DET_DTYPE
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_slab_scores_worker, args=(r, 2, port, ranges, srank, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    _, _, ref = _oracle_scene(_sparse_words(), ranges, srank)
+    assert (ref["score"] > 0).sum() >= 2 * 3  # several entries per list: the update is exercised
+    for rank, raw in res:
+        got = np.frombuffer(raw, DET_DTYPE).reshape(3, srank)
+        for f in ("x", "y", "z", "mode"):
+            np.testing.assert_array_equal(got[f], ref[f])
+        np.testing.assert_allclose(got["score"], ref["score"], rtol=1e-12)
+
+
+@pytest.mark.parametrize("ranges", [(2, 2, 2), (1, 2, 3), (3, 1, 1)])
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_merge_slab_scores_equals_whole_scene_replay(ranges, world):
+    """In one process: the slabs' owned blocks reassemble the whole scene's score arrays
+    position for position, and c3h_replay_scores over them gives the oracle's rank-4 lists."""
+    from c3hlac.dist import merge_slab_scores, mode_ranges, mode_schedule, owned_blocks, slab_extent
+    words = _sparse_words()
+    sbw, scw, ref = _oracle_scene(words, ranges, 4)
+    zr_max = max(mode_ranges(md, ranges)[2] for md in mode_schedule(ranges))
+    parts = []
+    for r in range(world):
+        ext = slab_extent(SLAB_G, SLAB_S, zr_max, r, world)
+        if ext is None:
+            continue
+        p0, p1, vz0, vz1, zoff = ext
+        sbl, sc, _ = _oracle_scene(words[vz0:vz1], ranges, 1, (0, 0, zoff))
+        parts.append(owned_blocks(sc, sbl, p0, p1, (SLAB_G,) * 3, SLAB_S, ranges, 3))
+    scores, lists = merge_slab_scores(parts, (SLAB_G,) * 3, SLAB_S, ranges, 4)
+    np.testing.assert_allclose(scores, scw, rtol=1e-12)
+    assert np.array_equal(scores < 0, scw < 0)
+    for f in ("x", "y", "z", "mode"):
+        np.testing.assert_array_equal(lists[f], ref[f])
+    np.testing.assert_allclose(lists["score"], ref["score"], rtol=1e-12)

@@ -238,7 +238,11 @@ def test_config2_kinect_128(ctx):
     np.testing.assert_allclose(sc[ok], scd[ok], rtol=SCORE_RTOL_F64)
     np.testing.assert_allclose(sc[ok], sc32[ok], rtol=SCORE_RTOL_F32)
     best = Ld.records()[0][0]
-    assert (int(lists[0, 0]["x"]), int(lists[0, 0]["y"]), int(lists[0, 0]["z"])) == best[1:4]
+    got = (int(lists[0, 0]["x"]), int(lists[0, 0]["y"]), int(lists[0, 0]["z"]))
+    if got != best[1:4]:  # only a tie within the fp32 tolerance may pick another position
+        e = sb[0] - 1
+        p = (got[2] * e + got[1]) * e + got[0]
+        assert scd[p] >= best[0] * (1 - 2 * SCORE_RTOL_F64), (got, best)
     _assert_replay_matches(ctx, (2, 2, 2), 1, lists)
 
 
@@ -269,9 +273,14 @@ def test_config3_kinect_256_ri117_multimodel(ctx):
     ok = scd > 0
     np.testing.assert_allclose(sc[ok], scd[ok], rtol=SCORE_RTOL_F64)
     _assert_replay_matches(ctx, (2, 2, 2), M, lists)
-    # same detections as the float64 oracle (top entry of every model)
+    # same detections as the float64 oracle (top entry of every model), up to fp32 ties
+    e = sb[0] - 1
+    scm = scd.reshape(M, -1)
     for m in range(M):
-        assert (int(lists[m, 0]["x"]), int(lists[m, 0]["y"]), int(lists[m, 0]["z"])) == Ld.records()[m][0][1:4]
+        got = (int(lists[m, 0]["x"]), int(lists[m, 0]["y"]), int(lists[m, 0]["z"]))
+        best = Ld.records()[m][0]
+        if got != best[1:4]:
+            assert scm[m, (got[2] * e + got[1]) * e + got[0]] >= best[0] * (1 - 2 * SCORE_RTOL_F64), (m, got, best)
 
 
 @pytest.mark.parametrize("ranges", [(1, 2, 1), (1, 2, 3), (2, 1, 1), (3, 3, 1)])

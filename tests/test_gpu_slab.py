@@ -53,3 +53,30 @@ def test_slabs_config5_dense_512_eight_ranks(ctx):
     whole = _whole(ctx, words, 981, S, (2, 2, 2), 100)
     got = _split(ctx, words, 981, S, (2, 2, 2), 100, 8)
     assert np.array_equal(got, whole)
+
+
+@pytest.mark.parametrize("srank", [3, 4])
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("ranges", [(2, 2, 2), (1, 2, 3)])
+def test_slabs_rank_above_one_kinect_256(ctx, srank, world, ranges):
+    """rank 3 / 4 (SearchObj::setRank) over z-slabs: every slab's owned position scores
+    (slab_scores), reassembled and replayed with the sequential checkOverlap update on the
+    host (merge_slab_scores -> c3h_replay_scores), equal the whole-scene search's lists
+    (the GPU replay kernel) bit for bit, and the score arrays position for position."""
+    from c3hlac.dist import merge_slab_scores, slab_scores
+    pts = synth.kinect_scene(1_000_000, grid=256, leaf=0.01, seed=synth.BASE_SEED + 11)
+    gi = ctx.voxelize(pts, 0.01)
+    d = gi.div_b
+    words = ctx.grid().reshape(d[2], d[1], d[0])
+    axis_t, var, axis_q = synth.random_bases(117, 100, 10, 20, seed=4)
+    ctx.search_setup(axis_t, var, axis_q)
+    ctx.set_grid(np.ascontiguousarray(words).reshape(-1), (d[0], d[1], d[2]))
+    ctx.extract(117, THR, 10)
+    ctx.set_rank(srank)
+    whole, _ = ctx.search(ranges, 100)
+    whole_scores = ctx.scores()
+    assert (whole["score"] > 0).all()
+    parts = [slab_scores(ctx, words, 117, THR, 10, ranges, 100, r, world) for r in range(world)]
+    scores, lists = merge_slab_scores(parts, (d[0], d[1], d[2]), 10, ranges, srank)
+    assert np.array_equal(scores, whole_scores)
+    assert np.array_equal(lists, np.ascontiguousarray(whole))
