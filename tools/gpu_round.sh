@@ -8,7 +8,7 @@ R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 export C3H_REQUIRE_GPU=1
 if [ "${2:-tests}" = tests ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+  timeout -k 10 900 python -u -m pytest tests -m gpu ${PYTEST_X--x} -v --timeout 300 --timeout-method thread -p no:cacheprovider \
     > $R/gpurun_out/gpu_tests_$TAG.log 2>&1 || exit $?
 fi
 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $R/gpurun_out/bench_$TAG.json 2> $R/gpurun_out/bench_$TAG.err || exit 3
