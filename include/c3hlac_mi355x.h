@@ -309,11 +309,15 @@ int c3h_stream_flush(c3h_ctx* ctx);
  * canvas[0] x canvas[1] x canvas[2] voxels placed at the frame's own min_b, and go through
  * the software-pipelined tick of c3h_run_frames; a box position passes only inside the
  * frame's own subdivisions, so every frame's results are those of its own grid.  Frame i's
- * M x rank detections land in d_out + i * M * rank (device).  Frames the canvas path cannot
- * reproduce exactly -- extent beyond the canvas, a voxel centroid that may round across its
- * cell boundary (c3h_voxelize's exact pass), one subdivision where the canvas has several
- * (computeC3HLAC's hist_num == 1 rule), no valid point -- are recomputed on the
- * single-frame path after the batches (status 1).  info (host, nframes records, may be
+ * M x rank detections land in d_out + i * M * rank (device).  Voxels whose centroid may
+ * round across a cell face are summed exactly in the batch (their points in input order),
+ * and those whose centroid cell is another cell take it as subdivision and neighbour base
+ * (c3_hlac.cpp:349-377): their subdivisions are recomputed after the batch's C3 stage
+ * (n_moved in info).  Frames the canvas path cannot reproduce -- extent beyond the canvas,
+ * more than 4,096 such voxels (65,536 of their points) or 256 moved ones, a centroid cell
+ * past the last subdivision, one subdivision where the canvas has several (computeC3HLAC's
+ * hist_num == 1 rule), no valid point -- are recomputed on the single-frame path after the
+ * batches (status 1).  info (host, nframes records, may be
  * NULL): the frame's VoxelGrid geometry, getSubdivNum, point and voxel counts and status
  * (0 batched, 1 single-frame path, < 0 the C3H_ERR_* that frame failed with; its lists are
  * the fresh setRank state).  One host synchronisation per call (the frames' records).
@@ -322,6 +326,8 @@ int c3h_stream_flush(c3h_ctx* ctx);
 typedef struct {
   int32_t div_b[3], min_b[3], subdiv_b[3];
   int32_t status;
+  int32_t n_moved;  /* voxels whose centroid lies in another cell, corrected in the batch */
+  int32_t pad;
   int64_t n_valid, n_occ;
 } c3h_frame_info;
 int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n, int32_t nframes,

@@ -13,7 +13,7 @@ from . import _capi
 from ._capi import DET_DTYPE, TIMER_NAMES, C3HError, check, i32x3, ptr  # noqa: F401
 
 FRAME_INFO_DTYPE = np.dtype([("div_b", "<i4", 3), ("min_b", "<i4", 3), ("subdiv_b", "<i4", 3), ("status", "<i4"),
-                             ("n_valid", "<i8"), ("n_occ", "<i8")])
+                             ("n_moved", "<i4"), ("n_valid", "<i8"), ("n_occ", "<i8")])
 S_MODE = {"S_MODE_%d" % (i + 1): i for i in range(6)}
 # setColor of the estimator (c3h_extract_params.color_mode, include/c3hlac_mi355x.h):
 # C3HLAC with sin/cos in float or in double (the default), or ColorCHLAC's (v, 255 - v)
@@ -347,7 +347,7 @@ class Context:
         out = np.zeros(len(frames), FRAME_INFO_DTYPE)
         for i in range(len(frames)):
             r = info[i]
-            out[i] = (tuple(r.div_b), tuple(r.min_b), tuple(r.subdiv_b), r.status, r.n_valid, r.n_occ)
+            out[i] = (tuple(r.div_b), tuple(r.min_b), tuple(r.subdiv_b), r.status, r.n_moved, r.n_valid, r.n_occ)
         return nm, out
 
     def _refresh(self):

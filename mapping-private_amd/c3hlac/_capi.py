@@ -46,7 +46,8 @@ class Det(C.Structure):
 
 class FrameInfo(C.Structure):
     _fields_ = [("div_b", C.c_int32 * 3), ("min_b", C.c_int32 * 3), ("subdiv_b", C.c_int32 * 3),
-                ("status", C.c_int32), ("n_valid", C.c_int64), ("n_occ", C.c_int64)]
+                ("status", C.c_int32), ("n_moved", C.c_int32), ("pad", C.c_int32), ("n_valid", C.c_int64),
+                ("n_occ", C.c_int64)]
 
 
 DET_DTYPE = np.dtype([("score", "<f8"), ("x", "<i4"), ("y", "<i4"), ("z", "<i4"), ("mode", "<i4")])

@@ -151,8 +151,28 @@ struct VoxFrameRec {
   int32_t sb[3];        // the frame's own getSubdivNum (the gate's position limits)
   uint32_t n_valid, n_occ;
   uint32_t flagged;     // voxels whose centroid may round across their cell boundary
-  uint32_t err;         // bit 0: cell coordinates beyond +-2^20; bit 1: extent beyond the canvas
+  uint32_t err;         // bit 0: cell coordinates beyond +-2^20; bit 1: extent beyond the canvas;
+                        // bit 2: flagged voxels beyond the exact pass's capacity; bit 3: a
+                        // centroid cell past the last subdivision (the reference reads out of bounds)
+  uint32_t moved;       // voxels whose exact centroid lies in another cell (the fixup's)
+};
+// exact-centroid pass of the batched voxeliser (round 4): per frame, the voxels the scatter
+// flagged (their points are bucketed and summed in input order), and those whose centroid
+// cell differs from their own cell
+constexpr int kVbFlagCap = 4096;        // flagged voxels per frame
+constexpr int kVbBucketCap = 1 << 16;   // their points per frame
+constexpr int kVbMovedCap = 256;        // off-cell voxels per frame
+struct VoxFlag {
+  uint32_t t;       // toroidal accumulator key
+  uint32_t idx;     // canvas word index
+  uint32_t count;   // points
+  uint32_t off;     // first bucket word
+  uint32_t cur;     // bucket fill (atomic)
   uint32_t pad;
+};
+struct VoxMoved {
+  uint32_t idx;     // canvas word index of the voxel's own cell
+  int32_t base[3];  // canvas coordinates of its centroid's cell (floor(c / leaf) - min_b)
 };
 struct VoxBatchArgs {
   int nf, total;                      // frames, accumulate blocks of this batch
@@ -186,8 +206,39 @@ struct VoxBatchArgs {
   uint32_t* tf;                       // per frame: [2] reserved | [2] work counters | stamps
   int32_t* work;                      // per frame: the non-empty tile list
   int64_t s_tf, s_work;
+  // exact pass (nullable: flagged frames then take the single-frame path)
+  VoxFlag* flags;                     // [nf][kVbFlagCap]
+  uint32_t* bucket;                   // [nf][kVbBucketCap] point indices
+  VoxMoved* moved;                    // [nf][kVbMovedCap]
+  uint32_t* xcnt;                     // [nf][4]: flags, bucket words, moved, - (zeroed by voxb_reduce)
 };
 int vb_chunk();  // points per accumulate block
+// The off-cell correction of a points-in batch, run after the tick that ran the batch's
+// tile role and before the one that compresses it: every subdivision holding a voxel the
+// exact pass moved (its own cell's and its centroid cell's) is recomputed exactly with the
+// moved voxels as centres at their centroid cells (c3_hlac.cpp:349-377), normalised, its
+// exist gate rewritten, and a newly non-empty one appended to the row list.
+struct PointFixup {
+  int nf;
+  const uint32_t* grid[kMaxBatch];    // canvas grids
+  const VoxMoved* moved;              // [nf][kVbMovedCap]
+  const uint32_t* xcnt;               // [nf][4]
+  const VoxFrameRec* info;            // [nf] (min_b / max_b: the frame's grid)
+  int C[3];                           // canvas dims
+  const int16_t* axmap;               // canvas coordinate -> subdivision (-1: no centre)
+  const int32_t* segs;                // [3][seg_stride][3] start, len, subdivision
+  int ns0, ns1, seg_stride;
+  int sbx, sby;
+  int variant, thr[3];
+  const uint32_t* lut;
+  float* feat;
+  int32_t* exist;
+  int32_t* rows;
+  uint32_t* tf;                       // per frame: [2] reserved | [2] work counters | stamps
+  int64_t s_feat, s_h, s_tf;
+  uint32_t epoch;
+};
+hipError_t launch_point_fixup(const PointFixup& a, hipStream_t s);
 hipError_t launch_vox_batch(const VoxBatchArgs& a, hipStream_t s);
 
 struct C3Launch {
@@ -550,6 +601,8 @@ struct c3h_ctx {
     bool stamped = false;  // tile stamps already set (points-in scatter): no occupancy role
     c3h_ctx* set = nullptr;       // the buffer set (context) the batch was captured on
     std::vector<int64_t> layout;  // its score-array layout, recorded there once its gate is enqueued
+    bool fix = false;             // points-in batch: the off-cell fixup runs after its tile role
+    c3h::PointFixup fx{};
   };
   struct PipeKey {
     int32_t div_b[3], min_b[3];
@@ -564,6 +617,9 @@ struct c3h_ctx {
   // accumulators, the voxel lists, host-point staging, the frames' records.
   c3h::DevBuf<uint32_t> pb_grid, pb_wlist;
   c3h::DevBuf<int32_t> pb_part, pb_lim;
+  c3h::DevBuf<c3h::VoxFlag> pb_flags;    // the exact pass of this set's batch
+  c3h::DevBuf<uint32_t> pb_bucket, pb_xcnt;
+  c3h::DevBuf<c3h::VoxMoved> pb_moved;
   int64_t pb_cvox = 0;             // canvas voxels per slot the set's buffers hold
   int pb_slots = 0;
   int pb_prev_nf = 0, pb_prev_total = 0;

@@ -279,7 +279,140 @@ __global__ __launch_bounds__(64) void offcell_delta_kernel(OffcellArgs o) {
   offcell_contrib(o, w, sc, nb, 1);
 }
 
+// ---- off-cell fixup of points-in batches (round 4) --------------------------------------
+// After the tile role of a batch: for every voxel the exact pass moved (its centroid cell is
+// not its own), the subdivisions of its own cell and of its centroid cell are recomputed
+// from the canvas: every occupied cell of the subdivision as a centre at its own cell, except
+// the moved voxels, which take their centroid cell as subdivision and neighbour base
+// (c3_hlac.cpp:349-377).  Exact u32 sums in LDS, normalised as the tile role does; the exist
+// gate is rewritten; a subdivision the tile role never saw is stamped and appended to the
+// row list the compress role reads.  One workgroup per (frame, job), jobs deduplicated.
+constexpr int kFixThreads = 256;
+
+__device__ __forceinline__ int fix_centre_sub(const PointFixup& a, const int c[3], int* tile) {
+  for (int ax = 0; ax < 3; ++ax)
+    if (c[ax] < 0 || c[ax] >= a.C[ax]) return -1;
+  const int ix = a.axmap[c[0]], iy = a.axmap[a.C[0] + c[1]], iz = a.axmap[a.C[0] + a.C[1] + c[2]];
+  if (ix < 0 || iy < 0 || iz < 0) return -1;
+  *tile = ix + a.ns0 * (iy + a.ns1 * iz);
+  return a.segs[3 * ix + 2] + a.sbx * (a.segs[3 * (a.seg_stride + iy) + 2] +
+                                       a.sby * a.segs[3 * (2 * a.seg_stride + iz) + 2]);
+}
+
+// centre word w at neighbour base b (canvas coordinates; the frame's grid is [0, dv))
+__device__ void fix_contrib(const PointFixup& a, const uint32_t* __restrict__ grid, const uint32_t* lut,
+                            uint32_t w, const int b[3], const int dv[3], uint32_t* hist) {
+  const bool v981 = a.variant == 981;
+  int ca[6], be[6];
+  channels(w, lut, a.thr, ca, be);
+  const int z0 = v981 ? 495 : 63, pc0 = v981 ? 969 : 105, au0 = v981 ? 474 : 42;
+  for (int c = 0; c < 6; ++c) {
+    if (be[c]) atomicAdd(&hist[z0 + c], 1u);
+    atomicAdd(&hist[c], (uint32_t)ca[c]);
+    for (int n = c; n < 6; ++n) atomicAdd(&hist[au0 + tri6(c, n)], (uint32_t)(ca[c] * ca[n]));
+  }
+  for (int c = 0; c < 4; ++c)
+    for (int n = (c < 2 ? 2 : 4); n < 6; ++n)
+      if (be[c] && be[n]) atomicAdd(&hist[pc0 + (c < 2 ? 4 * c + (n - 2) : 8 + 2 * (c - 2) + (n - 4))], 1u);
+  for (int k = 0; k < 13; ++k) {  // relative coordinates, c3_hlac.cpp:177-202
+    const int rel[3] = {k < 9 ? k / 3 - 1 : (k < 12 ? k - 10 : -1), k < 9 ? k % 3 - 1 : (k < 12 ? -1 : 0),
+                        k < 9 ? -1 : 0};
+    int q[3];
+    bool in = true;
+    for (int ax = 0; ax < 3; ++ax) {
+      q[ax] = b[ax] + rel[ax];
+      in = in && q[ax] >= 0 && q[ax] < dv[ax];
+    }
+    if (!in) continue;
+    const uint32_t nw = grid[q[0] + (int64_t)a.C[0] * (q[1] + (int64_t)a.C[1] * q[2])];
+    if (!nw) continue;
+    int na[6], nbe[6];
+    channels(nw, lut, a.thr, na, nbe);
+    for (int c = 0; c < 6; ++c)
+      for (int n = 0; n < 6; ++n) {
+        const int bn = v981 ? bin981(k, c, n) : 6 + 6 * c + n;
+        atomicAdd(&hist[bn], (uint32_t)(ca[c] * na[n]));
+        if (be[c] && nbe[n]) atomicAdd(&hist[v981 ? 495 + bn : 63 + bn], 1u);
+      }
+  }
+}
+
+__global__ __launch_bounds__(kFixThreads) void point_fixup_kernel(PointFixup a) {
+  __shared__ uint32_t s_hist[981];
+  __shared__ uint32_t s_lut[256];
+  __shared__ VoxMoved s_mv[kVbMovedCap];
+  __shared__ int s_h[2 * kVbMovedCap], s_t[2 * kVbMovedCap];
+  const int f = blockIdx.y, tid = threadIdx.x;
+  const VoxFrameRec& rec = a.info[f];
+  const int nm = (int)min(a.xcnt[4 * f + 2], (uint32_t)kVbMovedCap);
+  if (nm == 0 || rec.err) return;  // uniform
+  if ((int)blockIdx.x >= 2 * nm) return;
+  const uint32_t* __restrict__ grid = a.grid[f];
+  const int Cx = a.C[0], Cy = a.C[1];
+  const int dv[3] = {rec.max_b[0] - rec.min_b[0] + 1, rec.max_b[1] - rec.min_b[1] + 1,
+                     rec.max_b[2] - rec.min_b[2] + 1};
+  for (int i = tid; i < 256; i += kFixThreads) s_lut[i] = a.lut[i];
+  for (int i = tid; i < nm; i += kFixThreads) {
+    const VoxMoved m = a.moved[(size_t)f * kVbMovedCap + i];
+    s_mv[i] = m;
+    const int own[3] = {(int)(m.idx % (uint32_t)Cx), (int)((m.idx / (uint32_t)Cx) % (uint32_t)Cy),
+                        (int)(m.idx / ((uint32_t)Cx * (uint32_t)Cy))};
+    int t0 = -1, t1 = -1;
+    s_h[2 * i] = fix_centre_sub(a, own, &t0);
+    s_h[2 * i + 1] = fix_centre_sub(a, m.base, &t1);
+    s_t[2 * i] = t0;
+    s_t[2 * i + 1] = t1;
+  }
+  __syncthreads();
+  float* ffeat = a.feat + (int64_t)f * a.s_feat;
+  int32_t* fexist = a.exist + (int64_t)f * a.s_h;
+  int32_t* frows = a.rows + (int64_t)f * a.s_h;
+  uint32_t* ftf = a.tf + (int64_t)f * a.s_tf;
+  for (int j = blockIdx.x; j < 2 * nm; j += gridDim.x) {
+    const int h = s_h[j], tile = s_t[j];
+    bool skip = h < 0;
+    for (int k = 0; k < j && !skip; ++k) skip = s_h[k] == h;  // recomputed by job k
+    if (skip) continue;  // uniform
+    for (int i = tid; i < 981; i += kFixThreads) s_hist[i] = 0u;
+    __syncthreads();
+    const int sx = tile % a.ns0, sy = (tile / a.ns0) % a.ns1, sz = tile / (a.ns0 * a.ns1);
+    const int x0 = a.segs[3 * sx], lx = a.segs[3 * sx + 1];
+    const int y0 = a.segs[3 * (a.seg_stride + sy)], ly = a.segs[3 * (a.seg_stride + sy) + 1];
+    const int z0 = a.segs[3 * (2 * a.seg_stride + sz)], lz = a.segs[3 * (2 * a.seg_stride + sz) + 1];
+    // the subdivision's centres at their own cells, the moved voxels excepted
+    for (int e = tid; e < lx * ly * lz; e += kFixThreads) {
+      const int c[3] = {x0 + e % lx, y0 + (e / lx) % ly, z0 + e / (lx * ly)};
+      const uint32_t idx = (uint32_t)c[0] + (uint32_t)Cx * ((uint32_t)c[1] + (uint32_t)Cy * (uint32_t)c[2]);
+      const uint32_t w = grid[idx];
+      if (!w) continue;
+      bool mv = false;
+      for (int i = 0; i < nm && !mv; ++i) mv = s_mv[i].idx == idx;
+      if (!mv) fix_contrib(a, grid, s_lut, w, c, dv, s_hist);
+    }
+    // the moved voxels whose centroid cell is in this subdivision
+    for (int i = tid; i < nm; i += kFixThreads)
+      if (s_h[2 * i + 1] == h) fix_contrib(a, grid, s_lut, grid[s_mv[i].idx], s_mv[i].base, dv, s_hist);
+    __syncthreads();
+    float* out = ffeat + (int64_t)h * a.variant;
+    for (int i = tid; i < a.variant; i += kFixThreads)
+      out[i] = (float)s_hist[i] * (a.variant == 981 ? norm981(i) : norm117(i));
+    if (tid == 0) {
+      fexist[h] = exist_from((float)s_hist[0], (float)s_hist[1]);
+      // a subdivision the tile role did not see: stamp it and list its row for the compress
+      if (atomicExch(&ftf[4 + tile], a.epoch) != a.epoch) frows[atomicAdd(&ftf[2 + (a.epoch & 1)], 1u)] = h;
+    }
+    __syncthreads();  // s_hist is reused by the next job
+  }
+}
+
 }  // namespace
+
+hipError_t launch_point_fixup(const PointFixup& a, hipStream_t s) {
+  if (a.nf <= 0) return hipSuccess;
+  // jobs per frame: 2 per moved voxel; frames without moved voxels exit at once
+  point_fixup_kernel<<<dim3(32, (unsigned)a.nf), kFixThreads, 0, s>>>(a);
+  return hipGetLastError();
+}
 
 hipError_t launch_offcell_delta(const int32_t* rec, int nrec, const C3Launch& l, int hist1, const int off[3],
                                 const int sb[3], float inv_s, hipStream_t s) {

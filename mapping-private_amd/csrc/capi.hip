@@ -733,6 +733,10 @@ void c3h_destroy(c3h_ctx* ctx) {
   release(ctx->pb_wlist);
   release(ctx->pb_part);
   release(ctx->pb_lim);
+  release(ctx->pb_flags);
+  release(ctx->pb_bucket);
+  release(ctx->pb_xcnt);
+  release(ctx->pb_moved);
   release(ctx->pb_acc);
   release(ctx->pb_accM);
   release(ctx->pb_fcnt);
@@ -1972,8 +1976,13 @@ int pipe_tick(c3h_ctx* ctx, const c3h_ctx::PipeBatch* fresh) {
     hipError_t e = c3h::launch_tick(tp, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, "launch_tick", e);
   }
-  for (auto& b : ctx->pipe)  // this tick enqueued the batch's gate: its layout is written
-    if (b.age == 2 && b.set) b.set->scores_layout = b.layout;
+  for (auto& b : ctx->pipe) {
+    if (b.age == 2 && b.set) b.set->scores_layout = b.layout;  // this tick enqueued its gate
+    if (b.age == 1 && b.fix) {  // its tile role ran in this tick: the off-cell fixup before its compress
+      hipError_t e = c3h::launch_point_fixup(b.fx, ctx->stream);
+      if (e != hipSuccess) return hip_fail(ctx, "launch_point_fixup", e);
+    }
+  }
   std::vector<c3h_ctx::PipeBatch> next;
   for (auto& b : ctx->pipe)
     if (b.age < 3) {
@@ -2274,6 +2283,12 @@ extern "C" {
 #define C3H_POINT_STAMP 1
 #endif
 constexpr bool kPointStamp = C3H_POINT_STAMP;
+// points-in batches: flagged voxels summed exactly and off-cell voxels fixed up in the batch
+// (0: frames with flagged voxels take the single-frame path, as in round 3)
+#ifndef C3H_POINT_EXACT
+#define C3H_POINT_EXACT 1
+#endif
+constexpr bool kPointExact = C3H_POINT_EXACT;
 
 int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n, int32_t nframes, int on_device,
                          float leaf, float z_limit, const int32_t canvas[3], const c3h_extract_params* p,
@@ -2303,6 +2318,7 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
   std::vector<c3h_frame_info> fi((size_t)nframes);
   std::vector<char> redo((size_t)nframes, 1);
   int nm = 0;
+  bool exact_any = false, exact_used = false;  // the batches ran the exact pass + fixup
   // canvas subdivisions: a frame with one subdivision where the canvas has several takes the
   // single-frame path (computeC3HLAC's hist_num == 1 rule puts every voxel in histogram 0)
   bool canvas_multi = false;
@@ -2408,6 +2424,10 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
         ENSURE(c->pb_lim, (size_t)B * 4);
         ENSURE(c->pb_part, (size_t)bc * c3h::vox_part_words());
         ENSURE(c->pb_wlist, (size_t)bc * chunk);
+        ENSURE(c->pb_flags, (size_t)B * c3h::kVbFlagCap);
+        ENSURE(c->pb_bucket, (size_t)B * c3h::kVbBucketCap);
+        ENSURE(c->pb_moved, (size_t)B * c3h::kVbMovedCap);
+        ENSURE(c->pb_xcnt, (size_t)B * 4);
         HIPCHK(hipMemsetAsync(c->pb_grid.p, 0, (size_t)B * cvox * 4, vs));
         c->pb_cvox = cvox;
         c->pb_slots = B;
@@ -2480,6 +2500,45 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
       va.work = cl.work;
       va.s_tf = cl.s_tf;
       va.s_work = cl.s_work;
+      // the exact pass + off-cell fixup: the tick's direct mode (a row list, one tile per
+      // subdivision) on the canvas itself; otherwise flagged frames take the single-frame path
+      const bool exact = kPointExact && cl.rows && cl.axmap && cl.gx == canvas[0] && cl.gy == canvas[1] &&
+                         cl.gz == canvas[2];
+      if (exact) {
+        va.flags = c->pb_flags.p;
+        va.bucket = c->pb_bucket.p;
+        va.moved = c->pb_moved.p;
+        va.xcnt = c->pb_xcnt.p;
+        c3h::PointFixup& fx = fresh.fx;
+        fx.nf = nb;
+        for (int j = 0; j < nb; ++j) fx.grid[j] = grids[j];
+        fx.moved = c->pb_moved.p;
+        fx.xcnt = c->pb_xcnt.p;
+        fx.info = ctx->pb_info.p + f0;
+        for (int a = 0; a < 3; ++a) {
+          fx.C[a] = canvas[a];
+          fx.thr[a] = cl.thr[a];
+        }
+        fx.axmap = cl.axmap;
+        fx.segs = cl.segs;
+        fx.ns0 = cl.nseg[0];
+        fx.ns1 = cl.nseg[1];
+        fx.seg_stride = cl.seg_stride;
+        fx.sbx = cl.sbx;
+        fx.sby = cl.sby;
+        fx.variant = cl.variant;
+        fx.lut = cl.lut;
+        fx.feat = cl.feat;
+        fx.exist = cl.exist;
+        fx.rows = cl.rows;
+        fx.tf = cl.tf;
+        fx.s_feat = cl.s_feat;
+        fx.s_h = cl.s_h;
+        fx.s_tf = cl.s_tf;
+        fx.epoch = cl.epoch;
+        fresh.fix = true;
+      }
+      exact_any = exact_any || exact;
       // tables / stamp resets the capture enqueued precede the stamps (first batches only)
       if (va.stamp && vs != ctx->stream && c->cap_h2d != h2d0) {
         HIPCHK(hipEventRecord(ctx->pb_vox_ev, ctx->stream));
@@ -2512,6 +2571,7 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
       return rc;
     }
     std::vector<c3h::VoxFrameRec> recs((size_t)nframes);
+    exact_used = exact_any;
     HIPCHK(hipMemcpyAsync(recs.data(), ctx->pb_info.p, recs.size() * sizeof(c3h::VoxFrameRec), hipMemcpyDeviceToHost,
                           ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -2527,10 +2587,11 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
       }
       o.n_valid = r.n_valid;
       o.n_occ = r.n_occ;
+      o.n_moved = (int32_t)r.moved;
       o.status = 0;
       const bool hist1_mismatch = p->subdiv > 0 && canvas_multi && one;
       const bool empty_sub = p->subdiv > 0 && (r.sb[0] == 0 || r.sb[1] == 0 || r.sb[2] == 0);
-      redo[i] = (r.err || r.flagged || r.n_valid == 0 || hist1_mismatch || empty_sub) ? 1 : 0;
+      redo[i] = (r.err || (r.flagged && !exact_used) || r.n_valid == 0 || hist1_mismatch || empty_sub) ? 1 : 0;
     }
   }
   for (int i = 0; i < nframes; ++i) {

@@ -944,6 +944,9 @@ __global__ __launch_bounds__(kBlock) void voxb_reduce_kernel(VoxBatchArgs a) {
   rec.n_occ = (uint32_t)tn;
   rec.flagged = 0;  // the scatter adds its flags
   rec.err = (err ? 1u : 0u) | (over ? 2u : 0u);
+  rec.moved = 0;
+  if (a.xcnt)
+    for (int k = 0; k < 4; ++k) a.xcnt[4 * f + k] = 0u;
 }
 
 #ifndef C3H_VB_STAMP_DEDUP
@@ -1005,7 +1008,18 @@ __global__ __launch_bounds__(kBlock) void voxb_scatter_kernel(VoxBatchArgs a) {
       const int ax_ = lo[0] + (int)cx, ay_ = lo[1] + (int)cy, az_ = lo[2] + (int)cz;
       const int cmag = max(max(abs(ax_), abs(ay_)), abs(az_)) + 1;
       const float eps = (float)(count + 4) * (float)cmag * 0x1p-22f;
-      if (__uint_as_float(m) < eps || eps >= __uint_as_float(kMarginFlush)) ++flagged;
+      if (__uint_as_float(m) < eps || eps >= __uint_as_float(kMarginFlush)) {
+        ++flagged;
+        if (a.flags) {  // to the exact pass: its points are bucketed and summed in input order
+          uint32_t* xc = a.xcnt + 4 * f;
+          const uint32_t k = atomicAdd(xc, 1u);
+          const uint32_t o = atomicAdd(xc + 1, count);
+          if (k < (uint32_t)kVbFlagCap && o + count <= (uint32_t)kVbBucketCap)
+            a.flags[(size_t)f * kVbFlagCap + k] = VoxFlag{t, idx, count, o, 0u, 0u};
+          else
+            atomicOr(&a.info[f].err, 4u);
+        }
+      }
     }
     if (a.stamp) {  // uniform
       // neighbouring entries were first touched by neighbouring points: mostly one tile
@@ -1031,6 +1045,129 @@ __global__ __launch_bounds__(kBlock) void voxb_scatter_kernel(VoxBatchArgs a) {
   if ((tid & 63) == 0 && flagged) atomicAdd(&a.info[f].flagged, flagged);
 }
 
+// ---- exact centroids of the flagged voxels (round 4) ---------------------------------
+// voxb_bucket: block b of the accumulate grid re-reads its frame's points (frames without
+// flagged voxels return at once) and files every point of a flagged voxel (an LDS hash of
+// the frame's flagged keys) into that voxel's bucket.
+constexpr int kVbFlagSlots = 2 * kVbFlagCap;
+static_assert((kVbFlagSlots & (kVbFlagSlots - 1)) == 0, "flag hash");
+__global__ __launch_bounds__(kBT) void voxb_bucket_kernel(VoxBatchArgs a) {
+  __shared__ uint32_t s_key[kVbFlagSlots];
+  __shared__ uint16_t s_rec[kVbFlagSlots];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int f = vb_frame(a.blk0, a.nf, b);
+  const uint32_t nflag = a.xcnt[4 * f];
+  if (nflag == 0 || a.info[f].err) return;  // uniform
+  const int nrec = (int)min(nflag, (uint32_t)kVbFlagCap);
+  VoxFlag* fl = a.flags + (size_t)f * kVbFlagCap;
+  uint32_t* bk = a.bucket + (size_t)f * kVbBucketCap;
+  for (int s = tid; s < kVbFlagSlots; s += kBT) s_key[s] = kNoT;
+  __syncthreads();
+  for (int r = tid; r < nrec; r += kBT) {
+    const uint32_t t = fl[r].t;
+    uint32_t h = (t * 0x9E3779B1u) >> (32 - __builtin_ctz(kVbFlagSlots));
+    while (atomicCAS(&s_key[h], kNoT, t) != kNoT) h = (h + 1) & (kVbFlagSlots - 1);
+    s_rec[h] = (uint16_t)r;
+  }
+  __syncthreads();
+  const int64_t base = (int64_t)(b - a.blk0[f]) * kBChunk;
+  const float4* __restrict__ pts = a.pts[f];
+  const int64_t n = a.n[f];
+  const uint32_t mx_ = (1u << a.tb[0]) - 1, my_ = (1u << a.tb[1]) - 1, mz_ = (1u << a.tb[2]) - 1;
+  const int sy = a.tb[0], sz = a.tb[0] + a.tb[1];
+  VoxArgs q{};
+  q.inv = a.inv;
+  for (int j = 0; j < kBPer; ++j) {
+    const int64_t i = base + (int64_t)j * kBT + tid;
+    if (i >= n) break;
+    const float4 p = pts[i];
+    int c[3];
+    float margin;
+    if (!point_valid(p, a.z_limit) || !point_cell(q, p, c, &margin)) continue;
+    const uint32_t t = ((uint32_t)c[0] & mx_) | (((uint32_t)c[1] & my_) << sy) | (((uint32_t)c[2] & mz_) << sz);
+    uint32_t h = (t * 0x9E3779B1u) >> (32 - __builtin_ctz(kVbFlagSlots));
+    for (;;) {
+      const uint32_t k = s_key[h];
+      if (k == kNoT) break;
+      if (k == t) {
+        VoxFlag& r = fl[s_rec[h]];
+        bk[r.off + atomicAdd(&r.cur, 1u)] = (uint32_t)i;
+        break;
+      }
+      h = (h + 1) & (kVbFlagSlots - 1);
+    }
+  }
+}
+
+// voxb_exact: block f, a thread per flagged voxel: its points in input order (shell sort of
+// the bucket), the fp32 sequential sum times 1/n (PCL 1.0 on Eigen 3.0, as the single-frame
+// path and the oracle), the centroid cell floor(c / leaf); a voxel whose centroid cell is
+// not its own cell goes to the frame's moved list (the fixup after the tile role).  A
+// centroid cell past the frame's last subdivision (where the reference reads beyond its
+// histograms) sends the frame to the single-frame path.
+__global__ __launch_bounds__(kBlock) void voxb_exact_kernel(VoxBatchArgs a) {
+  const int f = blockIdx.x, tid = threadIdx.x;
+  VoxFrameRec& rec = a.info[f];
+  const uint32_t nflag = a.xcnt[4 * f];
+  if (nflag == 0 || rec.err) return;
+  const int nrec = (int)min(nflag, (uint32_t)kVbFlagCap);
+  const VoxFlag* fl = a.flags + (size_t)f * kVbFlagCap;
+  uint32_t* bks = a.bucket + (size_t)f * kVbBucketCap;
+  const float4* __restrict__ pts = a.pts[f];
+  const int Cx = a.C[0], Cy = a.C[1];
+  for (int r = tid; r < nrec; r += kBlock) {
+    const VoxFlag e = fl[r];
+    const int m = (int)e.count;
+    uint32_t* bk = bks + e.off;
+    const int gaps[8] = {701, 301, 132, 57, 23, 10, 4, 1};
+    for (int gi = 0; gi < 8; ++gi) {
+      const int gap = gaps[gi];
+      for (int u = gap; u < m; ++u) {
+        const uint32_t t = bk[u];
+        int v = u;
+        for (; v >= gap && bk[v - gap] > t; v -= gap) bk[v] = bk[v - gap];
+        bk[v] = t;
+      }
+    }
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f;
+    for (int u = 0; u < m; ++u) {
+      const float4 p = pts[bk[u]];
+      sx += p.x;
+      sy += p.y;
+      sz += p.z;
+    }
+    const float rn = __fdiv_rn(1.0f, (float)m);
+    const float c[3] = {__fmul_rn(sx, rn), __fmul_rn(sy, rn), __fmul_rn(sz, rn)};
+    const int own[3] = {(int)(e.idx % (uint32_t)Cx), (int)((e.idx / (uint32_t)Cx) % (uint32_t)Cy),
+                        (int)(e.idx / ((uint32_t)Cx * (uint32_t)Cy))};
+    int bc[3];
+    bool moved = false;
+    for (int ax = 0; ax < 3; ++ax) {
+      bc[ax] = (int)floorf(__fdiv_rn(c[ax], a.leaf)) - rec.min_b[ax];  // canvas coordinates
+      moved = moved || bc[ax] != own[ax];
+    }
+    if (!moved) continue;
+    if (a.subdiv > 0) {  // computeC3HLAC's subdivision of the centroid (c3_hlac.cpp:349-362)
+      bool centre = true, past = false;
+      for (int ax = 0; ax < 3; ++ax) {
+        const int tmp = bc[ax] - a.off[ax];
+        centre = centre && tmp >= 0;
+        past = past || (tmp >= 0 && (int)floorf((float)tmp * a.inv_s) >= rec.sb[ax]);
+      }
+      if (centre && past) {
+        atomicOr(&rec.err, 8u);
+        continue;
+      }
+    }
+    const uint32_t k = atomicAdd(a.xcnt + 4 * f + 2, 1u);
+    if (k < (uint32_t)kVbMovedCap)
+      a.moved[(size_t)f * kVbMovedCap + k] = VoxMoved{e.idx, {bc[0], bc[1], bc[2]}};
+    else
+      atomicOr(&rec.err, 4u);
+    atomicAdd(&rec.moved, 1u);
+  }
+}
+
 }  // namespace
 
 int vb_chunk() { return kBChunk; }
@@ -1041,6 +1178,10 @@ hipError_t launch_vox_batch(const VoxBatchArgs& a, hipStream_t s) {
   if (a.total > 0) {
     voxb_reduce_kernel<<<(unsigned)a.nf, kBlock, 0, s>>>(a);
     voxb_scatter_kernel<<<(unsigned)a.total, kBlock, a.stamp ? 4 * (size_t)((a.ntiles + 31) / 32) : 0, s>>>(a);
+    if (a.flags) {
+      voxb_bucket_kernel<<<(unsigned)a.total, kBT, 0, s>>>(a);
+      voxb_exact_kernel<<<(unsigned)a.nf, kBlock, 0, s>>>(a);
+    }
   }
   return hipGetLastError();
 }
