@@ -273,6 +273,7 @@ struct C3Launch {
   int64_t ntiles;
   long long* prof;  // diagnostics (C3H_PROF)
   int debug;
+  uint32_t* dense = nullptr;  // stand-alone large grids: the density probe's verdict word
 };
 
 int64_t c3hlac_grid(const C3Launch& a);  // persistent grid of the tile kernel
@@ -619,6 +620,7 @@ struct c3h_ctx {
   c3h::DevBuf<int32_t> pb_part, pb_lim;
   c3h::DevBuf<c3h::VoxFlag> pb_flags;    // the exact pass of this set's batch
   c3h::DevBuf<uint32_t> pb_bucket, pb_xcnt;
+  c3h::DevBuf<uint32_t> dense_flag;  // density probe of large stand-alone extracts
   c3h::DevBuf<c3h::VoxMoved> pb_moved;
   int64_t pb_cvox = 0;             // canvas voxels per slot the set's buffers hold
   int pb_slots = 0;

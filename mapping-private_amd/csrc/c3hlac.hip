@@ -50,6 +50,38 @@ namespace {
 
 // kAx: the axis map lives in LDS, so the per-voxel tile lookup is LDS-only (no global
 // load in the chain behind the stream data)
+// Large stand-alone grids (config 5, >= 65,536 tiles): a sampled density check before the
+// occupancy stream.  Every block reads the same 4,096 sampled words (a multiplicative-hash
+// spread over the grid); when at least half of them are occupied the grid is dense -- the
+// matrix-core body then takes every tile anyway (>= half non-empty) -- so every tile is
+// stamped and listed (identity work list) and the 4 B/voxel occupancy stream is skipped.
+// Empty tiles of such a grid are computed as zero rows with exist 0: the same result.
+constexpr int kDenseSamples = 4096;
+__global__ __launch_bounds__(kBlock) void dense_probe_kernel(OccArgs oa, uint32_t* dense) {
+  __shared__ int s_cnt;
+  const int tid = threadIdx.x;
+  if (tid == 0) s_cnt = 0;
+  __syncthreads();
+  const uint32_t* __restrict__ grid = oa.grid[0];
+  const uint64_t nvox = (uint64_t)oa.gx * oa.gy * oa.gz;
+  int c = 0;
+  for (int j = tid; j < kDenseSamples; j += kBlock) {
+    const uint64_t v = (((uint64_t)j + 1) * 0x9E3779B97F4A7C15ull >> 16) % nvox;
+    c += grid[v] != 0u;
+  }
+  atomicAdd(&s_cnt, c);
+  __syncthreads();
+  const bool dn = 2 * s_cnt >= kDenseSamples;
+  if (blockIdx.x == 0 && tid == 0) *dense = dn ? 1u : 0u;
+  if (!dn) return;
+  uint32_t* __restrict__ flags = oa.tf + 4;
+  for (int t = blockIdx.x * kBlock + tid; t < oa.ntiles; t += gridDim.x * kBlock) {
+    flags[t] = oa.epoch;
+    oa.work[t] = t;
+  }
+  if (blockIdx.x == 0 && tid == 0) oa.tf[2 + (oa.epoch & 1)] = (uint32_t)oa.ntiles;
+}
+
 template <bool kVec, bool kAx>
 __global__ __launch_bounds__(kBlock) void c3_occupancy_kernel(OccArgs oa) {
   const int f = blockIdx.y;
@@ -610,6 +642,10 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
 #endif
   c.oa.contiguous = C3H_OCC_CONTIG && l.ntiles >= 65536 ? 1 : 0;  // large grids (config 5): contiguous chunk ranges
   const dim3 g1d((unsigned)c.g1, (unsigned)l.nframes);
+  if (l.dense && l.nframes == 1 && c.bits && mf) {  // config 5: skip the stream of a dense grid
+    dense_probe_kernel<<<64, kBlock, 0, s>>>(c.oa, l.dense);
+    c.oa.dense = l.dense;
+  }
   if (c.bits) {
     if (c.ax)
       c3_occupancy_bits_kernel<true><<<g1d, kBlock, c.occ_lds, s>>>(c.oa);

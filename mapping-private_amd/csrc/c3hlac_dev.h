@@ -134,6 +134,9 @@ struct OccArgs {
   int steal_from = 0, steal_unit = 0, steal_units = 0, nframes = 0, steal_wgs = 0;
   int ar_s = 0, ar_oy = 0, ar_oz = 0;  // closed-form y / z maps (C3Launch), 0 = the LDS maps
   uint32_t ar_magic = 0;
+  // stand-alone large grids: dense_probe_kernel's verdict (non-zero: every tile was listed
+  // and stamped, the stream is skipped); nullptr elsewhere (the tick)
+  const uint32_t* dense = nullptr;
 };
 
 // Bitmap variant (every tile one bit of LDS, ntiles <= kOccBitsMax): an occupied centre
@@ -593,6 +596,7 @@ namespace {
 template <bool kAx>
 __global__ __launch_bounds__(kBlock) void c3_occupancy_bits_kernel(OccArgs oa) {
   extern __shared__ __attribute__((aligned(16))) uint32_t occ_smem[];
+  if (oa.dense && *oa.dense) return;  // uniform: a dense grid's tiles are all listed already
   occupancy_bits_body<kAx>(oa, blockIdx.x, blockIdx.y, gridDim.x, occ_smem);
 }
 }  // namespace

@@ -733,6 +733,7 @@ void c3h_destroy(c3h_ctx* ctx) {
   release(ctx->pb_wlist);
   release(ctx->pb_part);
   release(ctx->pb_lim);
+  release(ctx->dense_flag);
   release(ctx->pb_flags);
   release(ctx->pb_bucket);
   release(ctx->pb_xcnt);
@@ -1103,6 +1104,12 @@ int c3h_set_grid(c3h_ctx* ctx, const uint32_t* words, const int32_t div_b[3],
 // C3HLAC{981,117}Estimation::setVoxelFilter + compute for nf frames of one geometry
 // (grids[f], dims / min_b / leaf of ctx->info) in one set of launches; frame f's
 // per-frame buffers (features, exist, tile stamps, work / row lists) sit at f * stride.
+// large stand-alone extracts: the sampled density probe may skip the occupancy stream
+#ifndef C3H_DENSE_PROBE
+#define C3H_DENSE_PROBE 1
+#endif
+constexpr bool kDenseProbe = C3H_DENSE_PROBE;
+
 static bool extract_params_ok(const c3h_extract_params* p) {
   return (p->variant == 981 || p->variant == 117) && p->color_mode >= C3H_COLOR_C3_FLOAT &&
          p->color_mode <= C3H_COLOR_CHLAC;
@@ -1299,6 +1306,11 @@ int extract_frames(c3h_ctx* ctx, const uint32_t* const* grids, int nf, const c3h
     l.ntiles = ntiles;
     l.debug = 0;
     l.prof = nullptr;
+    l.dense = nullptr;
+    if (!ctx->capture && nf == 1 && ntiles >= 65536 && l.zero_empty && !atomic && kDenseProbe) {
+      ENSURE(ctx->dense_flag, 1);
+      l.dense = ctx->dense_flag.p;
+    }
     if (const char* dbg = c3h::diag_env("C3H_C3_DEBUG")) l.debug = atoi(dbg);  // diagnostics only
     const int64_t tgrid = c3h::c3hlac_grid(l);
     if (nf == 1) {

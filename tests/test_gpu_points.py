@@ -5,9 +5,9 @@ per-frame host round trip.
 
 - configs[3] at its stated size on one GPU: 512 independent 1M-point frames at 128^3
   (C3-HLAC-981, S = 10, compress 981 -> 100, 1 model x r = 20, box 2x2x2, rank 1), frames
-  on the device; every 32nd frame re-computed by the oracle from its points (grid
-  geometry and counts exact, detection within 1e-5 of the float64 oracle); the whole
-  batch bit-identical to the single-frame path.
+  on the device; every 4th frame (128 of 512) re-computed by the oracle from its points
+  (grid geometry and counts exact, detection within 1e-5 of the float64 oracle); sampled
+  frames bit-identical to the single-frame path.
 - host-resident frames (the H2D-inclusive path) give the same records as device frames.
 - mixed geometries in one batch: frames of different extents and min_b inside the canvas,
   a frame beyond the canvas, an empty frame, a frame whose centroids may round across a
@@ -81,7 +81,7 @@ def test_config4_512_frames_points_in(ctx, bases):
     assert np.array_equal(info["min_b"][:, 0], np.arange(nfr) // 8)  # the x shift moves min_b
     assert (info["subdiv_b"] == 13).all()
     assert (got["score"] > 0).all()
-    # the oracle from the points, every 32nd frame
+    # the oracle from the points, every 4th frame
     P = (-(-G // S) - BOX[0] + 1,) * 3
 
     def oracle(i):
@@ -93,7 +93,7 @@ def test_config4_512_frames_points_in(ctx, bases):
         return i, g, cloud, sc
 
     with cf.ThreadPoolExecutor(8) as pool:  # the C oracle releases the GIL
-        for i, g, cloud, sc in pool.map(oracle, range(5, nfr, 32)):
+        for i, g, cloud, sc in pool.map(oracle, range(1, nfr, 4)):  # 128 of the 512 frames
             assert list(info["div_b"][i]) == list(g.div_b) and list(info["min_b"][i]) == list(g.min_b), i
             assert info["n_valid"][i] == g.n_valid and info["n_occ"][i] == g.n_occ == len(cloud), i
             e = got[i, 0]
@@ -131,8 +131,8 @@ def test_host_frames_equal_device_frames(ctx, bases):
 
 def test_mixed_geometries_in_one_batch(ctx, bases):
     """Frames of different extents / origins share one canvas; each frame's positions are
-    bounded by its own subdivisions.  Statuses: 0 batched, 1 recomputed on the
-    single-frame path (beyond the canvas, empty, centroid near a cell boundary)."""
+    bounded by its own subdivisions.  Statuses: 0 batched (a centroid near a cell boundary
+    too: the exact pass), 1 recomputed on the single-frame path (beyond the canvas, empty)."""
     import torch
     dev = torch.device("cuda", 0)
     axis_t, var, axis_q = synth.random_bases(117, D, 3, R, seed=synth.BASE_SEED + 33)
@@ -156,11 +156,11 @@ def test_mixed_geometries_in_one_batch(ctx, bases):
     expect_status.append(1)
     frames.append(np.full((1000, 4), np.nan, np.float32))  # no valid point
     expect_status.append(1)
-    edge = frames[3].copy()  # a point right on a cell face: its voxel's centroid is flagged
-    k = np.flatnonzero(np.isfinite(edge[:, 0]))[7]
+    edge = frames[3].copy()  # a point right on a cell face: its voxel's centroid is flagged,
+    k = np.flatnonzero(np.isfinite(edge[:, 0]))[7]  # summed exactly in the batch (round 4)
     edge[k, 0] = np.float32(np.floor(edge[k, 0] / np.float32(LEAF)) * np.float32(LEAF))
     frames.append(edge)
-    expect_status.append(1)
+    expect_status.append(0)
     nfr = len(frames)
     devf = [torch.from_numpy(f).to(dev) for f in frames]
     torch.cuda.synchronize()
