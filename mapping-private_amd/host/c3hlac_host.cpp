@@ -224,7 +224,8 @@ void getVoxelGrid(VoxelGrid& grid, const std::vector<PointXYZRGBNormal>& input,
   output.assign(cent.size(), PointXYZRGBNormal());
   if (cent.empty()) return;
   // VoxelGrid::filter averages every float field of the voxel's points: the normal and the
-  // curvature in fp32, input order (the centroid's xyz and colour come from the device)
+  // curvature in fp32, input order, times 1 / n as Eigen 3.0 divides (the centroid's xyz and
+  // colour come from the device, with the same arithmetic)
   const std::vector<int> layout = grid.getLeafLayout();
   const Vector3i mn = grid.getMinBoxCoordinates(), dv = grid.getNrDivisions();
   const float inv = 1.0f / voxel_size;
@@ -243,9 +244,9 @@ void getVoxelGrid(VoxelGrid& grid, const std::vector<PointXYZRGBNormal>& input,
     ++cnt[o];
   }
   for (size_t o = 0; o < cent.size(); ++o) {
-    const float c = (float)cnt[o];
-    output[o] = PointXYZRGBNormal{cent[o].x, cent[o].y, cent[o].z, cent[o].rgb, acc[4 * o] / c, acc[4 * o + 1] / c,
-                                  acc[4 * o + 2] / c, acc[4 * o + 3] / c};
+    const float rn = 1.0f / (float)cnt[o];
+    output[o] = PointXYZRGBNormal{cent[o].x, cent[o].y, cent[o].z, cent[o].rgb, acc[4 * o] * rn, acc[4 * o + 1] * rn,
+                                  acc[4 * o + 2] * rn, acc[4 * o + 3] * rn};
   }
 }
 

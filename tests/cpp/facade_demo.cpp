@@ -270,6 +270,19 @@ static int estim(const std::string& pdir, const std::string& pcd, const std::str
   for (size_t h = 0; h < sig.size(); ++h) rows[h].assign(sig[h].histogram, sig[h].histogram + DIM_C3HLAC_981_1_3_ALL);
   writeFeature((prefix + "_estim.pcd").c_str(), rows);
   const Vector3i sb = est.getSubdivNum();
+  // ColorCHLAC (color_chlac.h): the RI estimator vs the free function, and vs C3 (the
+  // colour tables differ, so the rows must too)
+  std::vector<std::vector<float> > cc117;
+  extractColorCHLACSignature117(grid, cc117, thr_r, thr_g, thr_b, voxel_size, subdivision_size);
+  ColorCHLAC_RI_Estimation<PointXYZRGB, C3HLACSignature117> ecc;
+  ecc.setColorThreshold(thr_r, thr_g, thr_b);
+  ecc.setVoxelFilter(grid, subdivision_size, 0, 0, 0, voxel_size);
+  std::vector<C3HLACSignature117> scc;
+  ecc.compute(scc);
+  bool same_cc = scc.size() == cc117.size() && !cc117.empty();
+  for (size_t h = 0; same_cc && h < scc.size(); ++h)
+    same_cc = std::equal(cc117[h].begin(), cc117[h].end(), scc[h].histogram);
+  writeFeature((prefix + "_cc117.pcd").c_str(), cc117);
   // rotation-invariant 117 into both output types
   std::vector<std::vector<float> > f117;
   extractC3HLACSignature117(grid, f117, thr_r, thr_g, thr_b, voxel_size, subdivision_size, 1, 2, 0);
@@ -340,11 +353,11 @@ static int estim(const std::string& pdir, const std::string& pcd, const std::str
   printf("{\"filter_ok\": %d, \"rows\": %zu, \"free_rows\": %zu, \"same981\": %d, \"subdiv\": [%d, %d, %d], "
          "\"subdiv_free\": [%d, %d, %d], \"same117\": %d, \"rows117\": %zu, \"wide117\": %d, \"narrow_throws\": %d, "
          "\"normal_down_same\": %d, \"normal_same981\": %d, \"offset_false\": %d, \"negative_subdiv_false\": %d, "
-         "\"negative_thr_empty\": %d, \"unset_throws\": %d, \"name\": \"%s\"}\n",
+         "\"negative_thr_empty\": %d, \"unset_throws\": %d, \"name\": \"%s\", \"same_cc117\": %d, \"cc_name\": \"%s\"}\n",
          ok, sig.size(), c3_hlac.size(), same_rows<PointXYZRGB>(c3_hlac, sig, DIM_C3HLAC_981_1_3_ALL), sb[0], sb[1], sb[2],
          sb_free[0], sb_free[1], sb_free[2], same117, s117.size(), wide_ok, narrow_throws, down_same,
          same_rows<PointXYZRGBNormal>(c3_hlac, sn, DIM_C3HLAC_981_1_3_ALL), off_false, neg_sub_false, empty.empty(),
-         unset_throws, est.getFeatureName().c_str());
+         unset_throws, est.getFeatureName().c_str(), same_cc, ecc.getFeatureName().c_str());
   return 0;
 }
 

@@ -259,6 +259,14 @@ def test_facade_estimation_classes(demo, tmp_path):
     assert j["normal_down_same"] == 1 and j["normal_same981"] == 1
     assert j["offset_false"] == 1 and j["negative_subdiv_false"] == 1 and j["negative_thr_empty"] == 1
     assert j["unset_throws"] == 1 and j["name"] == "C3HLAC981Estimation"
+    # ColorCHLAC_RI_Estimation == extractColorCHLACSignature117 == the oracle's ColorCHLAC table
+    assert j["same_cc117"] == 1 and j["cc_name"] == "ColorCHLAC_RI_Estimation"
+    cc = c3hlac.read_feature(tmp_path / "f_cc117.pcd")
+    fc, _, _ = po.c3hlac(*po.voxelize(pts, 0.02), 117, (147, 146, 148), 0.02, 10, color_mode=po.COLOR_CHLAC,
+                         exact=True)
+    fc = fc[(fc != 0).any(1)]
+    assert cc.shape == fc.shape
+    np.testing.assert_allclose(cc, fc, atol=5e-7, rtol=1e-6)
     est = c3hlac.read_feature(tmp_path / "f_estim.pcd")
     free = c3hlac.read_feature(tmp_path / "f_free.pcd")
     assert np.array_equal(est, free)
