@@ -322,6 +322,8 @@ def main():
     if args.point_frames > 0:
         result["points_in"] = points_pass(ctx, dev, rank, world, dist, torch, synth, c3hlac, args.point_frames,
                                           args.host_point_frames)
+        if world == 1:
+            result["points_in_real_views"] = real_views_pass(ctx, dev, torch, synth, c3hlac)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         f0 = args.warmup * B  # the first timed frame: the oracle re-computes it as it is timed
         rec0 = d[f0]
@@ -414,6 +416,44 @@ def points_pass(ctx, dev, rank, world, dist, torch, synth, c3hlac, n_total, n_ho
         res["h2d_note"] = "%d frames per GPU from pinned host memory (16 MB each), H2D inside the timed call" % len(hf)
         res["h2d_equals_device"] = bool(torch.equal(hout, out[:len(hf)]))
     return res
+
+
+def real_views_pass(ctx, dev, torch, synth, c3hlac, reps=10):
+    """The reference's own sensor frames through c3h_run_point_frames: the committed sample
+    of 126 captured Kinect object views (tests/golden/kinect_views_126.npz, 258..19,005
+    points each; quantised depth puts many points on cell faces), leaf 0.01 on a 40^3 canvas,
+    C3-HLAC-117 S = 4 + 3 models x r = 5 (117 -> 30), rank 1, views resident in HBM.  Reports
+    the batched share, the voxels whose centroid lies in another cell (corrected in the
+    batch) and frames/s (best of `reps` calls)."""
+    f = ROOT / "tests" / "golden" / "kinect_views_126.npz"
+    if not f.exists():
+        return None
+    with np.load(f, allow_pickle=False) as z:
+        st, P = z["starts"], z["pts"]
+        frames = [torch.from_numpy(np.ascontiguousarray(P[st[i]:st[i + 1]])).to(dev) for i in range(len(st) - 1)]
+    M = 3
+    axis_t, var, axis_q = synth.random_bases(117, 30, M, 5, seed=synth.BASE_SEED + 91)
+    ctx.search_setup(axis_t, var, axis_q)
+    ctx.set_rank(1)
+    out = torch.zeros((len(frames), 3 * M), dtype=torch.int64, device=dev)
+    args = (0.01, (40, 40, 40), 117, THR, 4, BOX, 4, True, out)
+    ctx.run_point_frames(frames, *args)  # untimed: sizes the buffers
+    torch.cuda.synchronize(dev)
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        _, info = ctx.run_point_frames(frames, *args)
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        best = el if best is None else min(best, el)
+    return {
+        "frames": len(frames), "points": int(st[-1]),
+        "frames_batched": int((info["status"] == 0).sum()),
+        "views_with_offcell_voxels": int((info["n_moved"] > 0).sum()), "offcell_voxels": int(info["n_moved"].sum()),
+        "frames_per_s": len(frames) / best, "ms_per_call": best * 1e3,
+        "note": "126 captured Kinect views of color_feature_classification/demos/data (every 12th), leaf 0.01, "
+                "canvas 40^3, C3-HLAC-117 S=4, 117->30, 3 models x r=5, box 2x2x2, rank 1; one call, one host sync",
+    }
 
 
 def pmc_traffic(frames_per_tick):
