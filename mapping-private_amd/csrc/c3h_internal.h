@@ -546,6 +546,7 @@ struct c3h_ctx {
   // search
   bool have_setup = false;
   int D = 0, F = 0, M = 0, r = 0, Dpad = 0;
+  int D_user = 0;  // the caller's D (D is rounded up to a multiple of 4 with zero axes)
   bool compress = true;
   c3h::DevBuf<float> axis_pt;       // F x Dpad (transposed, whitened)
   c3h::DevBuf<_Float16> axis_pt16;  // 128 x Fp16 f16 copy (column-major) for the fp16 compress

@@ -1716,16 +1716,10 @@ int c3h_set_score_engine(c3h_ctx* ctx, int32_t engine) {
   return C3H_OK;
 }
 
-int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_t D, int32_t F,
-                     const float* axis_q, int32_t M, int32_t r, const float* feature_max,
-                     int32_t feature_max_len) {
-  if (!ctx) return C3H_ERR_ARG;
-  QUIESCE(ctx);
-  if (D < 1 || F < 1 || M < 1 || r < 1 || !axis_q || feature_max_len < 0 ||
-      (feature_max_len > 0 && !feature_max))
-    return fail(ctx, C3H_ERR_ARG, "c3h_search_setup: bad arguments");
-  if (!axis_p && D != F)
-    return fail(ctx, C3H_ERR_ARG, "c3h_search_setup: without compression D must equal F");
+// the bases on the device (D a multiple of 4 when D <= 160; see c3h_search_setup)
+static int search_setup_dev(c3h_ctx* ctx, const float* axis_p, const float* var, int32_t D, int32_t F,
+                            const float* axis_q, int32_t M, int32_t r, const float* feature_max,
+                            int32_t feature_max_len, int32_t D_user) {
   HIPCHK(hipSetDevice(ctx->device));
   // the bases are replaced with synchronous copies: queued kernels of this context may
   // still read them
@@ -1793,6 +1787,7 @@ int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_
   ++ctx->setup_version;
   ctx->compress = axis_p != nullptr;
   ctx->D = D;
+  ctx->D_user = D_user;
   ctx->F = F;
   ctx->M = M;
   ctx->r = r;
@@ -1801,6 +1796,33 @@ int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_
   ctx->g_valid = false;
   if (ctx->lists.M != M) init_lists(ctx);
   return C3H_OK;
+}
+
+int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_t D, int32_t F,
+                     const float* axis_q, int32_t M, int32_t r, const float* feature_max,
+                     int32_t feature_max_len) {
+  if (!ctx) return C3H_ERR_ARG;
+  QUIESCE(ctx);
+  if (D < 1 || F < 1 || M < 1 || r < 1 || !axis_q || feature_max_len < 0 ||
+      (feature_max_len > 0 && !feature_max))
+    return fail(ctx, C3H_ERR_ARG, "c3h_search_setup: bad arguments");
+  if (!axis_p && D != F)
+    return fail(ctx, C3H_ERR_ARG, "c3h_search_setup: without compression D must equal F");
+  if (D % 4 == 0 || D > 160)
+    return search_setup_dev(ctx, axis_p, var, D, F, axis_q, M, r, feature_max, feature_max_len, D);
+  // the sparse search, the pipeline and the matrix-core projection take D in 4-float chunks:
+  // zero axes (unit variance) are appended.  Their compressed values are 0, so every dot
+  // product and norm adds exact zeros: the scores are the caller's D's, bit for bit
+  const int Dp = (D + 3) / 4 * 4;
+  std::vector<float> ap, vp((size_t)Dp, 1.0f), qp((size_t)M * r * Dp, 0.0f);
+  if (axis_p) {  // (identity compression, D == F: the appended axes select no bin)
+    ap.assign((size_t)Dp * F, 0.0f);
+    std::copy(axis_p, axis_p + (size_t)D * F, ap.begin());
+  }
+  if (var) std::copy(var, var + D, vp.begin());
+  for (int c = 0; c < M * r; ++c) std::copy(axis_q + (size_t)c * D, axis_q + (size_t)(c + 1) * D, qp.begin() + (size_t)c * Dp);
+  return search_setup_dev(ctx, axis_p ? ap.data() : nullptr, var ? vp.data() : nullptr, Dp, F, qp.data(), M, r,
+                          feature_max, feature_max_len, D);
 }
 
 int c3h_set_rank(c3h_ctx* ctx, int32_t rank) {
@@ -1911,10 +1933,11 @@ int ensure_lanes(c3h_ctx* ctx, int n) {
         HIPCHK(hipStreamSynchronize(ctx->stream));
         synced = true;
       }
-      int rc = c3h_search_setup(c, ctx->h_axis_p.empty() ? nullptr : ctx->h_axis_p.data(),
+      int rc = search_setup_dev(c, ctx->h_axis_p.empty() ? nullptr : ctx->h_axis_p.data(),
                                 ctx->h_var.empty() ? nullptr : ctx->h_var.data(), ctx->D, ctx->F,
                                 ctx->h_axis_q.data(), ctx->M, ctx->r,
-                                ctx->h_fmax.empty() ? nullptr : ctx->h_fmax.data(), (int)ctx->h_fmax.size());
+                                ctx->h_fmax.empty() ? nullptr : ctx->h_fmax.data(), (int)ctx->h_fmax.size(),
+                                ctx->D_user);
       if (rc != C3H_OK) return fail(ctx, rc, std::string("c3h_run_frames: lane setup: ") + c->err);
       c->setup_version = ctx->setup_version;
     }
@@ -2633,6 +2656,25 @@ int c3h_get_compressed(c3h_ctx* ctx, float* out, int on_device) {
   QUIESCE(ctx);
   if (!ctx->g_valid) return fail(ctx, C3H_ERR_STATE, "no compressed features (run a search)");
   HIPCHK(hipSetDevice(ctx->device));
+  if (ctx->D_user != ctx->D) {  // appended zero axes: the caller's D columns of each row
+    const int W = ctx->D, Wu = ctx->D_user;
+    const float* src = ctx->G.p;
+    c3h::DevBuf<float> tmp;
+    hipError_t e = hipSuccess;
+    if (ctx->g_sparse) {  // rows of empty subdivisions were not written: 0
+      int rc = ensure(ctx, tmp, (size_t)ctx->hist_num * W);
+      if (rc != C3H_OK) return rc;
+      e = c3h::launch_masked_rows(ctx->G.p, ctx->exist.p, ctx->hist_num, W, tmp.p, ctx->stream);
+      src = tmp.p;
+    }
+    if (e == hipSuccess && ctx->hist_num > 0)
+      e = hipMemcpy2DAsync(out, (size_t)Wu * 4, src, (size_t)W * 4, (size_t)Wu * 4, (size_t)ctx->hist_num,
+                           on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    release(tmp);
+    if (e != hipSuccess) return fail(ctx, C3H_ERR_HIP, std::string("c3h_get_compressed: ") + hipGetErrorString(e));
+    return C3H_OK;
+  }
   const size_t n = (size_t)ctx->hist_num * ctx->D;
   if (!ctx->g_sparse) {
     HIPCHK(hipMemcpyAsync(out, ctx->G.p, n * 4, on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, ctx->stream));

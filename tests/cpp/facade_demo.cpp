@@ -12,6 +12,7 @@
 //   facade_demo readdata <F.bin> <N.bin> <dir> <dim>     (GPU: SearchObj::readData + search)
 //   facade_demo estim <param_dir> <cloud.pcd> <out_prefix> (GPU: extract_c3_hlac_scene.cpp's flow
 //                                                        through C3HLAC{981,117}Estimation)
+#include <cmath>
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -326,7 +327,8 @@ static int estim(const std::string& pdir, const std::string& pcd, const std::str
   for (size_t i = 0; down_same && i < down_n.size(); ++i)
     down_same = down_n[i].x == cloud_downsampled[i].x && down_n[i].y == cloud_downsampled[i].y &&
                 down_n[i].z == cloud_downsampled[i].z && down_n[i].rgb == cloud_downsampled[i].rgb &&
-                down_n[i].normal_z == 1.0f && down_n[i].curvature == 0.25f;
+                // n x 1.0 times fl(1/n) (PCL 1.0 on Eigen 3.0): within an ulp of the value
+                std::fabs(down_n[i].normal_z - 1.0f) <= 0x1p-23f && std::fabs(down_n[i].curvature - 0.25f) <= 0x1p-25f;
   C3HLAC981Estimation<PointXYZRGBNormal, C3HLACSignature981> en;
   en.setColorThreshold(thr_r, thr_g, thr_b);
   en.setVoxelFilter(grid_n, subdivision_size, 0, 0, 0, voxel_size);

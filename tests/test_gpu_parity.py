@@ -331,6 +331,15 @@ def test_search_without_rotation_and_feature_max(ctx):
     ok = scd > 0
     np.testing.assert_allclose(sc[ok], scd[ok], rtol=SCORE_RTOL_F64)
     _assert_replay_matches(ctx, (1, 2, 3), 2, lists, rotate=False)
+    # D = 30 runs on 32 internal axes (two zero axes appended): the readback holds the
+    # caller's 30, equal to the float64 compress of the normalised features
+    G = ctx.compressed()
+    assert G.shape == (hn, 30)
+    fn = f.astype(np.float64)
+    fn = np.where(fmax > 0, fn / np.where(fmax > 0, fmax, 1), 0.0)  # setData's normalisation (oracle)
+    Gd = fn @ synth.whiten(axis_t, var).astype(np.float64).T
+    live = ex > 0
+    np.testing.assert_allclose(G[live], Gd[live], rtol=1e-4, atol=1e-4 * np.abs(Gd[live]).max())
 
 
 def test_no_compression_path(ctx):
