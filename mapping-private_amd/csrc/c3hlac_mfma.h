@@ -44,6 +44,9 @@ constexpr int kMfLoad = 2;  // (row, dword) items per lane of a layer (<= 18 row
 #ifndef C3H_MF_TWO
 #define C3H_MF_TWO 1  // two-step layers with the lane-group-contiguous position map
 #endif
+#ifndef C3H_MF_GAP
+#define C3H_MF_GAP 16  // diagnostics: 0 = the round-3 plane placement of the two-step layers
+#endif
 #ifndef C3H_MF_EXP
 #define C3H_MF_EXP 0  // diagnostics variants: 1 no K steps, 2 no conversion, 4 no bin epilogue
 #endif
@@ -67,7 +70,8 @@ __host__ __device__ inline int mf_plane_bytes(int lx, int ly) {
   return ((m - 32 + 255) & ~255) + 32;
 }
 __host__ __device__ inline int mf_r256(int x) { return (x + 255) & ~255; }
-__host__ __device__ inline int mf_slot_stride(int pb) { return mf_r256(kMfCh * pb); }
+// (+16: the two-step layers put planes 4..11 one 16-byte block further, see mf_layer_ksteps2)
+__host__ __device__ inline int mf_slot_stride(int pb) { return mf_r256(kMfCh * pb + 16); }
 __host__ __device__ inline int mf_wave_stride(int pb) { return 3 * mf_slot_stride(pb) + mf_r256(pb); }
 __host__ __device__ inline int mf_const_bytes(int pb) { return mf_r256(128 + 3 * pb); }
 // 3 x 256 channel-byte tables | 128 B | 3 constant planes (0x00, 0x01, 0xff) | per-wave
@@ -178,6 +182,12 @@ __device__ __forceinline__ void mf_layer_ksteps(const uint8_t* pp, const uint8_t
 // B and the mask use the same one, so the integer sums are unchanged).  A plane row then
 // costs NB = 3-4 ds_read_b128 for both steps instead of 2 x 2-3: 16 instead of 22 reads
 // per layer, and the centre mask (the same plane for every layer) stays in registers.
+// Banks: lane (h, n) reads plane n at 32 h, so with planes at a 288-byte stride (18 blocks
+// of 16 B) the 4-bank block of every lane is even and a ds_read_b128 lane group (lanes
+// {0-3, 12-15, 20-27} = (h 0, n 0-3 / 12-15), (h 1, n 4-11), ...) met its own blocks twice
+// (2-way, every read).  Planes 4..11 then sit one block further (odd blocks): the 12 real
+// lanes of each group hit 12 distinct blocks and the constant planes (blocks 8, 10) the
+// rest.  The one-step layout (16 h) is conflict-free without the shift.
 template <int DYR, int DXLO, int DXHI>
 struct MfRow2 {
   static constexpr int B0 = mf_fdiv16(DYR + DXLO), NB = mf_fdiv16(DYR + DXHI + 31) - B0 + 1;
@@ -309,6 +319,8 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
     const int PB = mf_plane_bytes(lx, ly);
     const int ipr = PW >> 2, nitem = TY * ipr;
     const int SS = mf_slot_stride(PB);
+    const bool two = C3H_MF_TWO && nks == 2 && (PW & 15) == 12;  // mf_layer_ksteps2's layers
+    const int gap = two ? C3H_MF_GAP : 0;  // planes 4..11 shifted (banks, see mf_layer_ksteps2)
     uint8_t* mask = wl + 3 * SS;
     // centre mask of the K positions PW + 4 j + b: rows 1..ly, columns 1..lx
     for (int j = lane; j < 16 * nks; j += 64) {
@@ -374,7 +386,7 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
           const uint32_t o[4] = {__builtin_amdgcn_perm(u2, u0, 0x05040100u), __builtin_amdgcn_perm(u2, u0, 0x07060302u),
                                  __builtin_amdgcn_perm(u3, u1, 0x05040100u), __builtin_amdgcn_perm(u3, u1, 0x07060302u)};
 #pragma unroll
-          for (int s2 = 0; s2 < 4; ++s2) *reinterpret_cast<uint32_t*>(dst + (4 * col + s2) * PB) = o[s2];
+          for (int s2 = 0; s2 < 4; ++s2) *reinterpret_cast<uint32_t*>(dst + (4 * col + s2) * PB + (col ? gap : 0)) = o[s2];
         }
       }
     };
@@ -401,10 +413,11 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
     }
     for (int z = 0; z < lz; ++z) {
       mf_compiler_fence();  // same-wave LDS accesses complete in order; keep the compiler's too
-      const uint8_t* pp = realk ? wl + ((z % 3) * SS + nk * PB + korg) : cpad;        // dz = -1
-      const uint8_t* pc = realk ? wl + (((z + 1) % 3) * SS + nk * PB + korg) : cpad;  // dz = 0
+      const int pn = nk * PB + (nk >= 4 ? gap : 0) + korg;
+      const uint8_t* pp = realk ? wl + ((z % 3) * SS + pn) : cpad;        // dz = -1
+      const uint8_t* pc = realk ? wl + (((z + 1) % 3) * SS + pn) : cpad;  // dz = 0
 #if !(C3H_MF_EXP & 1)
-      if (C3H_MF_TWO && nks == 2 && (PW & 15) == 12) {  // S <= 10 tiles: pitch 12
+      if (two) {  // S <= 10 tiles: pitch 12
         mf_layer_ksteps2<12>(pp, pc, mk2, pw16, h4k, acc);
       } else {
         switch (PW & 15) {

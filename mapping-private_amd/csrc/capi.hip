@@ -402,7 +402,10 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
   ENSURE(ctx->G, (size_t)nf * H * ctx->D);
   // sparse compress: only the non-empty rows of the extract's list (the rest stay stale
   // and every consumer gates them on exist)
-  const bool sparse_g = !ctx->g_valid && fast && ctx->rows_valid &&
+  int64_t npos = 0;  // positions of every mode (0: no box fits the subdivisions)
+  for (int i = 0; i < rm.n; ++i) npos += rm.m[i].P;
+  // (no positions: nothing of the sparse search launches, so the compress is the dense one)
+  const bool sparse_g = !ctx->g_valid && fast && ctx->rows_valid && npos > 0 &&
                         c3h::compress_rows_ok(ctx->F, ctx->Dpad);
   if (ctx->capture && !sparse_g) return 0;  // not pipelinable: the caller falls back
   if (!ctx->g_valid && !sparse_g) {  // dense compress of every frame of the extract
@@ -492,7 +495,10 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
     }
     const int64_t ptot = q.pstart[rm.n];
     ENSURE(ctx->glist, (size_t)nf * std::max<int64_t>(ptot, 1));
-    if (!ctx->gcnt.p || ctx->gcnt_frames != nf || ctx->gcnt.n < (size_t)nf * 4 || ++ctx->search_epoch == 0) {
+    // an epoch per launched gate (its first workgroup resets the next epoch's counters): a
+    // search with no positions launches nothing and keeps the epoch
+    if (!ctx->gcnt.p || ctx->gcnt_frames != nf || ctx->gcnt.n < (size_t)nf * 4 ||
+        (ptot > 0 && ++ctx->search_epoch == 0)) {
       // per frame: [2] list counters | [2] finished-workgroup counters
       ENSURE(ctx->gcnt, (size_t)nf * 4);
       HIPCHK(hipMemsetAsync(ctx->gcnt.p, 0, ctx->gcnt.n * 4, ctx->stream));

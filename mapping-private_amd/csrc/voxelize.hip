@@ -63,6 +63,9 @@ constexpr int kVoxRound = kVoxPer;             // loads in flight per thread (on
 #ifndef C3H_VOX_SLOTS
 #define C3H_VOX_SLOTS 2048
 #endif
+#ifndef C3H_VOX_MERGE
+#define C3H_VOX_MERGE 1  // the run merge (0: every point updates the LDS table itself)
+#endif
 constexpr int kLSlots = C3H_VOX_SLOTS;        // LDS hash slots per workgroup
 constexpr int kLProbe = 48;                   // LDS probes before a point goes straight to the global table
 constexpr int kCellBias = 1 << 20;
@@ -187,6 +190,12 @@ __device__ __forceinline__ void vox_clear_prev(const VoxArgs& a) {
   }
 }
 
+// DPP row_shr:o (within 16-lane rows); lanes without a source read 0
+template <int O>
+__device__ __forceinline__ uint32_t vrow_shr(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 | O, 0xf, 0xf, true);
+}
+
 __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
   __shared__ unsigned long long s_key[kLSlots];
   __shared__ unsigned long long s_gb[kLSlots];  // b << 32 | g
@@ -230,6 +239,7 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
     atomicAdd(&a.tab[s].b, B);
     if (m < kMarginFlush) atomicMin(&a.tab[s].margin, m);
   };
+  const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1);  // lanes <= this one
   for (int j0 = 0; j0 < kVoxPer; j0 += kVoxRound) {
   float4 p[kVoxRound];
 #pragma unroll
@@ -244,37 +254,65 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
   }
 #pragma unroll
   for (int j = 0; j < kVoxRound; ++j) {
-    if (!point_valid(p[j], a.z_limit)) continue;
-    int c[3];
-    float margin;
-    if (!point_cell(a, p[j], c, &margin)) {
+    int c[3] = {0, 0, 0};
+    float margin = 1.0f;
+    bool valid = point_valid(p[j], a.z_limit);
+    if (valid && !point_cell(a, p[j], c, &margin)) {
       err = true;
-      continue;
+      valid = false;
     }
-    ++nv;
+    unsigned long long key = kNoKey;
+    uint32_t w0 = 0, w1 = 0, mb = kNoMargin;
+    if (valid) {
+      ++nv;
 #pragma unroll
-    for (int ax = 0; ax < 3; ++ax) {
-      mn[ax] = min(mn[ax], c[ax]);
-      mx[ax] = max(mx[ax], c[ax]);
+      for (int ax = 0; ax < 3; ++ax) {
+        mn[ax] = min(mn[ax], c[ax]);
+        mx[ax] = max(mx[ax], c[ax]);
+      }
+      key = pack_cell(c[0], c[1], c[2]);
+      const uint32_t rgb = __float_as_uint(p[j].w);
+      w0 = ((rgb >> 16) & 0xffu) | (((rgb >> 8) & 0xffu) << 12) | (1u << 24);  // r | g << 12 | count << 24
+      w1 = rgb & 0xffu;                                                         // b
+      const uint32_t mbits = __float_as_uint(margin);
+      mb = mbits < kMarginFlush ? mbits : kNoMargin;
     }
-    const unsigned long long key = pack_cell(c[0], c[1], c[2]);
-    const uint32_t rgb = __float_as_uint(p[j].w);
-    const uint32_t r = (rgb >> 16) & 0xffu, g = (rgb >> 8) & 0xffu, b = rgb & 0xffu;
-    const uint32_t mb = __float_as_uint(margin);
+    // a depth camera's neighbouring pixels hit one voxel in runs: inside each 16-lane row
+    // the runs are summed by a segmented DPP scan (as voxb_accum) and only a run's last
+    // lane updates the LDS table (same-address LDS atomics serialise)
+    const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);
+    const bool head = !C3H_VOX_MERGE || !valid || (lane & 15) == 0 || vrow_shr<1>(klo) != klo ||
+                      vrow_shr<1>(khi) != khi;
+    const uint64_t hm = __ballot(head);
+    const int o0 = lane - (63 - __clzll(hm & le));  // lanes before this one in its run
+    uint32_t s0, s1, sm;
+    s0 = vrow_shr<1>(w0); s1 = vrow_shr<1>(w1); sm = vrow_shr<1>(mb);
+    if (o0 >= 1) { w0 += s0; w1 += s1; mb = min(mb, sm); }
+    s0 = vrow_shr<2>(w0); s1 = vrow_shr<2>(w1); sm = vrow_shr<2>(mb);
+    if (o0 >= 2) { w0 += s0; w1 += s1; mb = min(mb, sm); }
+    s0 = vrow_shr<4>(w0); s1 = vrow_shr<4>(w1); sm = vrow_shr<4>(mb);
+    if (o0 >= 4) { w0 += s0; w1 += s1; mb = min(mb, sm); }
+    s0 = vrow_shr<8>(w0); s1 = vrow_shr<8>(w1); sm = vrow_shr<8>(mb);
+    if (o0 >= 8) { w0 += s0; w1 += s1; mb = min(mb, sm); }
+    const bool tail = valid && ((lane & 15) == 15 || ((hm >> (lane + 1)) & 1));
+    if (!tail) continue;
+    // the run's totals: count <= 16, channel sums <= 4080
+    const unsigned long long cr = ((unsigned long long)(w0 >> 24) << 32) | (w0 & 0xfffu);
+    const unsigned long long gb = ((unsigned long long)w1 << 32) | ((w0 >> 12) & 0xfffu);
     uint32_t h = mix64(key) & (kLSlots - 1);
     bool done = false;
     for (int probe = 0; probe < kLProbe; ++probe) {
       const unsigned long long prev = atomicCAS(&s_key[h], kNoKey, key);
       if (prev == kNoKey || prev == key) {
-        atomicAdd(&s_cr[h], (1ull << 32) | r);
-        atomicAdd(&s_gb[h], ((unsigned long long)b << 32) | g);
-        if (mb < kMarginFlush) atomicMin(&s_m[h], mb);
+        atomicAdd(&s_cr[h], cr);
+        atomicAdd(&s_gb[h], gb);
+        if (mb != kNoMargin) atomicMin(&s_m[h], mb);
         done = true;
         break;
       }
       h = (h + 1) & (kLSlots - 1);
     }
-    if (!done) add_global(key, (1ull << 40) | r, ((unsigned long long)b << 32) | g, mb);  // LDS table full
+    if (!done) add_global(key, ((cr >> 32) << 40) | (cr & 0xffffffffull), gb, mb);  // LDS table full
   }
   }
   // flush: one global insert + two (three near a cell boundary) atomics per (workgroup, voxel)
@@ -691,11 +729,6 @@ __device__ __forceinline__ int vb_frame(const int* blk0, int nf, int b) {
   return lo;
 }
 
-// DPP row_shr:o (within 16-lane rows); lanes without a source read 0
-template <int O>
-__device__ __forceinline__ uint32_t row_shr(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 | O, 0xf, 0xf, true);
-}
 
 __global__ __launch_bounds__(kBT) void voxb_accum_kernel(VoxBatchArgs a) {
   __shared__ uint32_t s_key[kBSlots];
@@ -782,19 +815,19 @@ __global__ __launch_bounds__(kBT) void voxb_accum_kernel(VoxBatchArgs a) {
     }
     // runs of equal keys inside each 16-lane row: a lane starts a run when it is invalid,
     // the row's first lane, or its key differs from the previous lane's
-    const uint32_t tp = row_shr<1>(t);
+    const uint32_t tp = vrow_shr<1>(t);
     const bool head = !C3H_VB_MERGE || !valid || (lane & 15) == 0 || tp != t;
     const uint64_t hm = __ballot(head);
     const int hpos = 63 - __clzll(hm & le);  // this lane's run start
     const int o0 = lane - hpos;              // lanes before this one in its run
     uint32_t s0, s1, sm;
-    s0 = row_shr<1>(w0); s1 = row_shr<1>(w1); sm = row_shr<1>(mb);
+    s0 = vrow_shr<1>(w0); s1 = vrow_shr<1>(w1); sm = vrow_shr<1>(mb);
     if (o0 >= 1) { w0 += s0; w1 += s1; mb = min(mb, sm); }
-    s0 = row_shr<2>(w0); s1 = row_shr<2>(w1); sm = row_shr<2>(mb);
+    s0 = vrow_shr<2>(w0); s1 = vrow_shr<2>(w1); sm = vrow_shr<2>(mb);
     if (o0 >= 2) { w0 += s0; w1 += s1; mb = min(mb, sm); }
-    s0 = row_shr<4>(w0); s1 = row_shr<4>(w1); sm = row_shr<4>(mb);
+    s0 = vrow_shr<4>(w0); s1 = vrow_shr<4>(w1); sm = vrow_shr<4>(mb);
     if (o0 >= 4) { w0 += s0; w1 += s1; mb = min(mb, sm); }
-    s0 = row_shr<8>(w0); s1 = row_shr<8>(w1); sm = row_shr<8>(mb);
+    s0 = vrow_shr<8>(w0); s1 = vrow_shr<8>(w1); sm = vrow_shr<8>(mb);
     if (o0 >= 8) { w0 += s0; w1 += s1; mb = min(mb, sm); }
     const bool tail = C3H_VB_DIAG < 2 && valid && ((lane & 15) == 15 || ((hm >> (lane + 1)) & 1));
     if (tail) {  // the run's totals: count <= 16, channel sums <= 4080

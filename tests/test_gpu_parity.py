@@ -312,6 +312,37 @@ def test_rotation_modes_and_rank(ctx, ranges):
     assert np.array_equal(c3hlac.remove_overlap(l4, ranges), l3)
 
 
+def test_search_after_a_frame_without_positions(ctx):
+    """A frame whose subdivisions hold no box (xe, ye or ze < 1: searchPart runs no
+    position) launches nothing; the next frame's sparse search must not inherit stale
+    list counters (round 4: every later frame lost its records)."""
+    axis_t, var, axis_q = synth.random_bases(117, 24, 3, 6, seed=17)
+    ctx.search_setup(axis_t, var, axis_q)
+    small = synth.kinect_scene(20_000, grid=12, leaf=0.02, seed=17)
+    big = synth.kinect_scene(100_000, grid=40, leaf=0.02, seed=18)
+    ctx.voxelize(small, 0.02)
+    sb, _ = ctx.extract(117, THR, 6)
+    assert min(sb) < 3, sb  # no 3 x 3 x 3 box fits
+    ctx.set_rank(1)
+    lists0, _ = ctx.search((3, 3, 3), 10)
+    assert (lists0["score"] == 0).all()
+    for _ in range(2):  # and again after a frame that did search
+        ctx.voxelize(big, 0.02)
+        sb, _ = ctx.extract(117, THR, 6)
+        f, ex = ctx.features(), ctx.exist()
+        ctx.set_rank(1)
+        lists, _ = ctx.search((3, 3, 3), 10)
+        L, _, scd = po.search(sb, f, ex, synth.whiten(axis_t, var), axis_q, (3, 3, 3), 1, 10, dbl=True,
+                              want_scores=True)
+        for m in range(3):
+            want = L.records()[m][0][0]
+            assert want > 0 and abs(float(lists[m, 0]["score"]) - want) <= SCORE_RTOL_F64 * want, (m, want)
+        ctx.voxelize(small, 0.02)
+        ctx.extract(117, THR, 6)
+        ctx.set_rank(1)
+        assert (ctx.search((3, 3, 3), 10)[0]["score"] == 0).all()
+
+
 def test_search_without_rotation_and_feature_max(ctx):
     pts = synth.kinect_scene(200_000, grid=64, leaf=0.02, seed=5)
     ctx.voxelize(pts, 0.02)
