@@ -91,11 +91,13 @@ enum {
   kVcValid = 6,   // u64 valid points
   kVcSlots = 8,   // [2] voxels listed by the frame of each epoch parity
   kVcFlag = 10,   // voxels whose centroid may leave their cell
-  kVcErr = 11,    // cell range / table overflow
+  kVcErr = 11,    // kVcErrRange | kVcErrFull
   kVcOver = 12,   // grid buffer too small (scatter not run)
   kVcOff = 13,    // off-cell voxels recorded by the exact pass
   kVcWords = 16
 };
+constexpr uint32_t kVcErrRange = 1;  // cell coordinates beyond +-2^20
+constexpr uint32_t kVcErrFull = 2;   // the global table had no room (the frame runs again, table x2)
 // one voxel of the voxeliser's global hash table (32 B: one load / clear)
 struct VoxSlot {
   unsigned long long key;  // absolute cell (21 bits per axis, biased), ~0 = empty
@@ -490,6 +492,7 @@ struct c3h_ctx {
   c3h::DevBuf<uint32_t> vlists, vcnt;
   c3h::DevBuf<int32_t> vpart;
   uint64_t vtsize = 0, vlcap = 0;
+  uint64_t vocc_hint = 0;  // voxels of the last frame: sizes the next frame's table
   int vpar = 0, vblk_cap = 0;
   int vblk_prev = 0;                // accum blocks of the previous frame (its lists to clear)
   bool vgrid_tracked = false;       // grid buffer is zero outside the previous frame's list

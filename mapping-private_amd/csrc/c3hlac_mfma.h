@@ -192,12 +192,28 @@ template <int DYR, int DXLO, int DXHI>
 struct MfRow2 {
   static constexpr int B0 = mf_fdiv16(DYR + DXLO), NB = mf_fdiv16(DYR + DXHI + 31) - B0 + 1;
   uint32_t w[4 * NB];
+  mf_u4 q[NB];
   __device__ __forceinline__ void load(const uint8_t* row) {
     const uint8_t* p = static_cast<const uint8_t*>(__builtin_assume_aligned(row, 16));
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       mf_u4 v = *reinterpret_cast<const mf_u4*>(p + 16 * (B0 + b));
       __asm__("" : "+v"(v));  // keep the whole block: a narrowed ds_read_b32 bank-conflicts
+      w[4 * b] = v.x; w[4 * b + 1] = v.y; w[4 * b + 2] = v.z; w[4 * b + 3] = v.w;
+    }
+  }
+  // prefetch: issue() the reads, pin() where the row is first used -- the whole-block
+  // barrier then sits after the work issued in between, which hides the LDS latency
+  __device__ __forceinline__ void issue(const uint8_t* row) {
+    const uint8_t* p = static_cast<const uint8_t*>(__builtin_assume_aligned(row, 16));
+#pragma unroll
+    for (int b = 0; b < NB; ++b) q[b] = *reinterpret_cast<const mf_u4*>(p + 16 * (B0 + b));
+  }
+  __device__ __forceinline__ void pin() {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      mf_u4 v = q[b];
+      __asm__("" : "+v"(v));
       w[4 * b] = v.x; w[4 * b + 1] = v.y; w[4 * b + 2] = v.z; w[4 * b + 3] = v.w;
     }
   }
@@ -212,11 +228,57 @@ struct MfRow2 {
   }
 };
 
+#ifndef C3H_MF_PREFETCH
+#define C3H_MF_PREFETCH 1  // two-step layers: each plane row's reads issued one row ahead
+#endif
 template <int R>
 __device__ __forceinline__ void mf_layer_ksteps2(const uint8_t* pp, const uint8_t* pc, const mf_u4 (&mk)[2],
                                                  int pw16, int h4, mf_v4i (&acc)[kMfK]) {
   const int o = 32 * h4;
   mf_v4i A0, A1;
+#define C3H_MF2(ROW, DX, K)                                                                                 \
+  acc[K] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0, ROW.template frag<DX, 0>(), acc[K], 0, 0, 0);      \
+  acc[K] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1, ROW.template frag<DX, 1>(), acc[K], 0, 0, 0);
+  if (C3H_MF_PREFETCH) {
+    MfRow2<0, -1, 0> c0;   // dz = 0, dy = 0: the centres and dx = -1
+    MfRow2<-R, -1, 1> cm;  // dz = 0, dy = -1: k = 9 + dx + 1
+    c0.issue(pc + o);
+    cm.issue(pc + o - pw16);
+    c0.pin();
+    const mf_v4i a0 = c0.template frag<0, 0>(), a1 = c0.template frag<0, 1>();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      A0[i] = (int)(((uint32_t)a0[i] & mk[0][i]) | (0x80808080u & ~mk[0][i]));
+      A1[i] = (int)(((uint32_t)a1[i] & mk[1][i]) | (0x80808080u & ~mk[1][i]));
+    }
+    acc[13] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0, A0, acc[13], 0, 0, 0);  // own channels
+    acc[13] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1, A1, acc[13], 0, 0, 0);
+    acc[12] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0, c0.template frag<-1, 0>(), acc[12], 0, 0, 0);  // (-1, 0, 0)
+    acc[12] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1, c0.template frag<-1, 1>(), acc[12], 0, 0, 0);
+    MfRow2<-R, -1, 1> rm;  // dz = -1, dy = -1: k = 3 (dx + 1)
+    rm.issue(pp + o - pw16);
+    cm.pin();
+    C3H_MF2(cm, -1, 9)
+    C3H_MF2(cm, 0, 10)
+    C3H_MF2(cm, 1, 11)
+    MfRow2<0, -1, 1> r0;  // dz = -1, dy = 0
+    r0.issue(pp + o);
+    rm.pin();
+    C3H_MF2(rm, -1, 0)
+    C3H_MF2(rm, 0, 3)
+    C3H_MF2(rm, 1, 6)
+    MfRow2<R, -1, 1> rp;  // dz = -1, dy = +1
+    rp.issue(pp + o + pw16);
+    r0.pin();
+    C3H_MF2(r0, -1, 1)
+    C3H_MF2(r0, 0, 4)
+    C3H_MF2(r0, 1, 7)
+    rp.pin();
+    C3H_MF2(rp, -1, 2)
+    C3H_MF2(rp, 0, 5)
+    C3H_MF2(rp, 1, 8)
+    return;
+  }
   {
     // dz = 0: row 0 (the centres and dx = -1)
     MfRow2<0, -1, 0> c0;
@@ -232,9 +294,6 @@ __device__ __forceinline__ void mf_layer_ksteps2(const uint8_t* pp, const uint8_
     acc[12] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0, c0.template frag<-1, 0>(), acc[12], 0, 0, 0);  // (-1, 0, 0)
     acc[12] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1, c0.template frag<-1, 1>(), acc[12], 0, 0, 0);
   }
-#define C3H_MF2(ROW, DX, K)                                                                                 \
-  acc[K] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0, ROW.template frag<DX, 0>(), acc[K], 0, 0, 0);      \
-  acc[K] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1, ROW.template frag<DX, 1>(), acc[K], 0, 0, 0);
   {
     MfRow2<-R, -1, 1> cm;  // dz = 0, dy = -1: k = 9 + dx + 1
     cm.load(pc + o - pw16);

@@ -815,68 +815,84 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
       d_pts = reinterpret_cast<const float4*>(ctx->pts.p);
     }
   }
-  // tables: >= 2x the points (load <= 1/2); (re)allocation starts from all-empty state
-  uint64_t ts = 1024;
-  while (ts < 2 * (uint64_t)n) ts <<= 1;
+  // the global table holds ~4x the voxels expected (the last frame's count; n / 4 before
+  // the first) rather than 2x the points: 58k voxels of a 1M-point frame then fill 256k
+  // slots (8 MB) instead of 2M (64 MB), so the flush's atomics stay in cache.  A frame that
+  // fills it (kGProbe probes without room) runs again on a table twice the size; the table
+  // only grows.  Slot lists and partial records: one segment of the block's points per block
+  uint64_t pcap = 512;
+  while (pcap < (uint64_t)n) pcap <<= 1;
+  const uint64_t hint = ctx->vocc_hint ? ctx->vocc_hint : (uint64_t)n / 4;
+  uint64_t ts_want = 4096;
+  while (ts_want < 4 * hint && ts_want < 2 * pcap) ts_want <<= 1;
   const int nblk = (int)c3h::vox_blocks(n);
-  if (ctx->vtsize < ts || !ctx->vcnt.p || ctx->vblk_cap < nblk) {
-    ctx->vtsize = 0;
-    const int bcap = (int)c3h::vox_blocks((int64_t)(ts / 2));
-    ENSURE(ctx->vtab[0], ts);
-    ENSURE(ctx->vtab[1], ts);
-    ENSURE(ctx->vlists, 4 * (size_t)c3h::vox_positions((int64_t)(ts / 2)));
-    ENSURE(ctx->vpart, 2 * (size_t)bcap * c3h::vox_part_words());
-    ENSURE(ctx->vcnt, c3h::kVcWords);
-    HIPCHK(hipMemsetAsync(ctx->vpart.p, 0, ctx->vpart.n * 4, ctx->stream));
-    for (int t = 0; t < 2; ++t) {  // empty slots: key ~0, sums 0, margin ~0
-      HIPCHK(hipMemset2DAsync(&ctx->vtab[t].p[0].key, sizeof(c3h::VoxSlot), 0xff, 8, ts, ctx->stream));
-      HIPCHK(hipMemset2DAsync(&ctx->vtab[t].p[0].a, sizeof(c3h::VoxSlot), 0, 16, ts, ctx->stream));
-      HIPCHK(hipMemset2DAsync(&ctx->vtab[t].p[0].margin, sizeof(c3h::VoxSlot), 0xff, 8, ts, ctx->stream));
-    }
-    HIPCHK(hipMemsetAsync(ctx->vcnt.p, 0, c3h::kVcWords * 4, ctx->stream));
-    ctx->vtsize = ts;
-    ctx->vlcap = (uint64_t)c3h::vox_positions((int64_t)(ts / 2));
-    ctx->vblk_cap = bcap;
-    ctx->vblk_prev = 0;
-    ctx->vgrid_tracked = false;
-  }
-  // the previous frame's grid words are cleared through its list only when its scatter
-  // completed (tracked); otherwise the whole buffer is zeroed once
-  const bool clear_grid = ctx->vgrid_tracked && ctx->grid.n;
-  if (!ctx->vgrid_tracked && ctx->grid.n) HIPCHK(hipMemsetAsync(ctx->grid.p, 0, ctx->grid.n * 4, ctx->stream));
-  ctx->vgrid_tracked = false;  // until this frame's scatter completes
   c3h::VoxArgs a{};
-  a.pts = d_pts;
-  a.n = n;
-  a.z_limit = z_limit;
-  a.inv = gi.inv_leaf;
-  a.leaf = leaf;
-  a.tab = ctx->vtab[ctx->vpar].p;
-  a.tab_prev = ctx->vtab[ctx->vpar ^ 1].p;
-  a.tmask = ctx->vtsize - 1;
-  a.lists = ctx->vlists.p;
-  a.lcap = ctx->vlcap;
-  a.part = ctx->vpart.p;
-  a.nblk = nblk;
-  a.nblk_prev = ctx->vblk_prev;
-  a.nblk_cap = ctx->vblk_cap;
-  a.cnt = ctx->vcnt.p;
-  a.grid = ctx->grid.p;
-  a.grid_cap = (int64_t)ctx->grid.n;
-  a.par = ctx->vpar;
-  a.clear_tables = 1;
-  a.clear_grid = clear_grid ? 1 : 0;
-  {
-    Timed t(ctx, 0);
-    HIPCHK(c3h::launch_voxelize(a, ctx->stream));
-  }
   uint32_t* hc = ctx->h_small;
-  HIPCHK(hipMemcpyAsync(hc, ctx->vcnt.p, c3h::kVcWords * 4, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(hipStreamSynchronize(ctx->stream));
+  for (int attempt = 0;; ++attempt) {
+    if (ctx->vtsize < ts_want || !ctx->vcnt.p || ctx->vblk_cap < nblk) {  // (re)allocation: all-empty state
+      const uint64_t ts = std::max<uint64_t>(ts_want, ctx->vtsize);
+      ctx->vtsize = 0;
+      const int bcap = (int)std::max<int64_t>(c3h::vox_blocks((int64_t)pcap), ctx->vblk_cap);
+      ENSURE(ctx->vtab[0], ts);
+      ENSURE(ctx->vtab[1], ts);
+      ENSURE(ctx->vlists, 4 * (size_t)bcap * c3h::vox_positions(1));
+      ENSURE(ctx->vpart, 2 * (size_t)bcap * c3h::vox_part_words());
+      ENSURE(ctx->vcnt, c3h::kVcWords);
+      HIPCHK(hipMemsetAsync(ctx->vpart.p, 0, ctx->vpart.n * 4, ctx->stream));
+      for (int t = 0; t < 2; ++t) {  // empty slots: key ~0, sums 0, margin ~0
+        HIPCHK(hipMemset2DAsync(&ctx->vtab[t].p[0].key, sizeof(c3h::VoxSlot), 0xff, 8, ts, ctx->stream));
+        HIPCHK(hipMemset2DAsync(&ctx->vtab[t].p[0].a, sizeof(c3h::VoxSlot), 0, 16, ts, ctx->stream));
+        HIPCHK(hipMemset2DAsync(&ctx->vtab[t].p[0].margin, sizeof(c3h::VoxSlot), 0xff, 8, ts, ctx->stream));
+      }
+      HIPCHK(hipMemsetAsync(ctx->vcnt.p, 0, c3h::kVcWords * 4, ctx->stream));
+      ctx->vtsize = ts;
+      ctx->vlcap = (uint64_t)bcap * (uint64_t)c3h::vox_positions(1);
+      ctx->vblk_cap = bcap;
+      ctx->vblk_prev = 0;
+      ctx->vgrid_tracked = false;
+    }
+    // the previous frame's grid words are cleared through its list only when its scatter
+    // completed (tracked); otherwise the whole buffer is zeroed once
+    const bool clear_grid = ctx->vgrid_tracked && ctx->grid.n;
+    if (!ctx->vgrid_tracked && ctx->grid.n) HIPCHK(hipMemsetAsync(ctx->grid.p, 0, ctx->grid.n * 4, ctx->stream));
+    ctx->vgrid_tracked = false;  // until this frame's scatter completes
+    a = c3h::VoxArgs{};
+    a.pts = d_pts;
+    a.n = n;
+    a.z_limit = z_limit;
+    a.inv = gi.inv_leaf;
+    a.leaf = leaf;
+    a.tab = ctx->vtab[ctx->vpar].p;
+    a.tab_prev = ctx->vtab[ctx->vpar ^ 1].p;
+    a.tmask = ctx->vtsize - 1;
+    a.lists = ctx->vlists.p;
+    a.lcap = ctx->vlcap;
+    a.part = ctx->vpart.p;
+    a.nblk = nblk;
+    a.nblk_prev = ctx->vblk_prev;
+    a.nblk_cap = ctx->vblk_cap;
+    a.cnt = ctx->vcnt.p;
+    a.grid = ctx->grid.p;
+    a.grid_cap = (int64_t)ctx->grid.n;
+    a.par = ctx->vpar;
+    a.clear_tables = 1;
+    a.clear_grid = clear_grid ? 1 : 0;
+    {
+      Timed t(ctx, 0);
+      HIPCHK(c3h::launch_voxelize(a, ctx->stream));
+    }
+    HIPCHK(hipMemcpyAsync(hc, ctx->vcnt.p, c3h::kVcWords * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (!(hc[c3h::kVcErr] & c3h::kVcErrFull) || (hc[c3h::kVcErr] & c3h::kVcErrRange)) break;
+    if (attempt >= 8 || ctx->vtsize >= ((uint64_t)1 << 28))
+      return fail(ctx, C3H_ERR_NOMEM, "c3h_voxelize: internal: voxel table still full");
+    ts_want = 2 * ctx->vtsize;  // the frame again, from all-empty tables twice the size
+    ctx->vtsize = 0;
+  }
   // from here the tables hold this frame's entries (listed under parity a.par)
   ctx->vpar ^= 1;
   ctx->vblk_prev = nblk;
-  if (hc[c3h::kVcErr]) {
+  if (hc[c3h::kVcErr] & c3h::kVcErrRange) {
     return fail(ctx, C3H_ERR_RANGE, "c3h_voxelize: leaf size too small (cell coordinates beyond +-2^20)");
   }
   uint64_t nvalid;
@@ -918,6 +934,7 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
   ctx->vgrid_tracked = true;
   ctx->vargs = a;
   ctx->vns = hc[c3h::kVcSlots + a.par];
+  ctx->vocc_hint = ctx->vns;
   gi.n_occ = ctx->vns;
   ctx->info = gi;
   ctx->grid_ptr = ctx->grid.p;

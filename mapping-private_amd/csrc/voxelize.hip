@@ -118,11 +118,12 @@ __device__ __forceinline__ uint32_t mix64(unsigned long long k) {
   return (uint32_t)k;
 }
 
-// global table insert: returns the slot (or -1 when the table is full, which the host
-// sizing at >= 2x the point count excludes); *fresh = this call inserted the key
+// global table insert: returns the slot (or -1 when kGProbe probes found no room: the host
+// runs the frame again on a table twice the size); *fresh = this call inserted the key
+constexpr uint64_t kGProbe = 64;  // global probes before the table counts as full (load <= 1/4 by sizing)
 __device__ __forceinline__ int64_t global_slot(const VoxArgs& a, unsigned long long key, bool* fresh) {
   uint64_t h = mix64(key) & a.tmask;
-  for (uint64_t probes = 0; probes <= a.tmask; ++probes) {
+  for (uint64_t probes = 0; probes < kGProbe && probes <= a.tmask; ++probes) {
     const unsigned long long prev = atomicCAS(&a.tab[h].key, kNoKey, key);
     if (prev == kNoKey) {
       *fresh = true;
@@ -220,18 +221,31 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
     a.cnt[kVcSlots + a.par] = 0;
     a.cnt[kVcFlag] = a.cnt[kVcErr] = a.cnt[kVcOver] = a.cnt[kVcOff] = 0;
   }
-  vox_clear_prev(a);
   const int64_t base = blockIdx.x * (int64_t)kVoxChunk;
+  // the points' loads are in flight while the previous frame is cleared (one round)
+  static_assert(kVoxPer == kVoxRound, "one round of point loads");
+  float4 p[kVoxRound];
+#pragma unroll
+  for (int j = 0; j < kVoxRound; ++j) {
+    const int64_t i = base + j * kVB + tid;
+    if (i < a.n) {  // streamed once: non-temporal
+      const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.pts) + i);
+      p[j] = make_float4(v.x, v.y, v.z, v.w);
+    } else {
+      p[j] = make_float4(NAN, NAN, NAN, 0.0f);
+    }
+  }
+  vox_clear_prev(a);
   uint32_t* sl = a.lists + (size_t)a.par * a.lcap + (size_t)blockIdx.x * kVoxChunk;
   __syncthreads();
   int mn[3] = {INT_MAX, INT_MAX, INT_MAX}, mx[3] = {INT_MIN, INT_MIN, INT_MIN};
   int nv = 0;
-  bool err = false;
+  int err = 0;  // kVcErrRange | kVcErrFull
   auto add_global = [&](unsigned long long key, unsigned long long A, unsigned long long B, uint32_t m) {
     bool fresh = false;
     const int64_t s = global_slot(a, key, &fresh);
     if (s < 0) {
-      err = true;
+      err |= kVcErrFull;
       return;
     }
     if (fresh) sl[atomicAdd(&s_nnew, 1u)] = (uint32_t)s;
@@ -240,25 +254,14 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
     if (m < kMarginFlush) atomicMin(&a.tab[s].margin, m);
   };
   const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1);  // lanes <= this one
-  for (int j0 = 0; j0 < kVoxPer; j0 += kVoxRound) {
-  float4 p[kVoxRound];
-#pragma unroll
-  for (int j = 0; j < kVoxRound; ++j) {  // a round of loads in flight together
-    const int64_t i = base + (j0 + j) * kVB + tid;
-    if (i < a.n) {  // streamed once: non-temporal
-      const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.pts) + i);
-      p[j] = make_float4(v.x, v.y, v.z, v.w);
-    } else {
-      p[j] = make_float4(NAN, NAN, NAN, 0.0f);
-    }
-  }
+  {
 #pragma unroll
   for (int j = 0; j < kVoxRound; ++j) {
     int c[3] = {0, 0, 0};
     float margin = 1.0f;
     bool valid = point_valid(p[j], a.z_limit);
     if (valid && !point_cell(a, p[j], c, &margin)) {
-      err = true;
+      err |= kVcErrRange;
       valid = false;
     }
     unsigned long long key = kNoKey;
@@ -315,13 +318,41 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
     if (!done) add_global(key, ((cr >> 32) << 40) | (cr & 0xffffffffull), gb, mb);  // LDS table full
   }
   }
-  // flush: one global insert + two (three near a cell boundary) atomics per (workgroup, voxel)
+  // flush: one global insert + two (three near a cell boundary) atomics per (workgroup, voxel);
+  // a thread's first probes are all issued before any result is used (round trips)
   __syncthreads();  // every point's LDS update is in
-  for (int s = tid; s < kLSlots; s += kVB) {
-    const unsigned long long key = s_key[s];
-    if (key == kNoKey) continue;
-    const unsigned long long cr = s_cr[s];
-    add_global(key, ((cr >> 32) << 40) | (cr & 0xffffffffull), s_gb[s], s_m[s]);
+  {
+    constexpr int kFl = (kLSlots + kVB - 1) / kVB;
+    unsigned long long key[kFl], prev[kFl];
+    uint64_t h[kFl];
+#pragma unroll
+    for (int k = 0; k < kFl; ++k) {
+      const int s = tid + k * kVB;
+      key[k] = s < kLSlots ? s_key[s] : kNoKey;
+      h[k] = mix64(key[k]) & a.tmask;
+      prev[k] = key[k] != kNoKey ? atomicCAS(&a.tab[h[k]].key, kNoKey, key[k]) : kNoKey;
+    }
+#pragma unroll
+    for (int k = 0; k < kFl; ++k) {
+      if (key[k] == kNoKey) continue;
+      const int s = tid + k * kVB;
+      // collisions: linear probing as global_slot (the host sizes the table at >= 2x points)
+      uint64_t probes = 1;
+      while (prev[k] != kNoKey && prev[k] != key[k] && probes < kGProbe && probes <= a.tmask) {
+        h[k] = (h[k] + 1) & a.tmask;
+        prev[k] = atomicCAS(&a.tab[h[k]].key, kNoKey, key[k]);
+        ++probes;
+      }
+      if (prev[k] != kNoKey && prev[k] != key[k]) {
+        err |= kVcErrFull;
+        continue;
+      }
+      const unsigned long long cr = s_cr[s];
+      if (prev[k] == kNoKey) sl[atomicAdd(&s_nnew, 1u)] = (uint32_t)h[k];
+      atomicAdd(&a.tab[h[k]].a, ((cr >> 32) << 40) | (cr & 0xffffffffull));
+      atomicAdd(&a.tab[h[k]].b, s_gb[s]);
+      if (s_m[s] < kMarginFlush) atomicMin(&a.tab[h[k]].margin, s_m[s]);
+    }
   }
   // bounds, counts and the slot list go to this block's partial record: no same-address
   // atomics across blocks (they serialise at the memory side)
@@ -331,7 +362,7 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
     mx[ax] = wave_reduce(mx[ax], [](int x, int y) { return max(x, y); });
   }
   nv = wave_reduce(nv, [](int x, int y) { return x + y; });
-  const int e = wave_reduce(err ? 1 : 0, [](int x, int y) { return x | y; });
+  const int e = wave_reduce(err, [](int x, int y) { return x | y; });
   if (lane == 0) {
     for (int ax = 0; ax < 3; ++ax) {
       s_red[w][ax] = mn[ax];
@@ -425,7 +456,7 @@ __device__ VoxTotals vox_reduce(const VoxArgs& a, bool publish) {
     a.cnt[kVcValid] = (uint32_t)tv;
     a.cnt[kVcValid + 1] = 0;
     a.cnt[kVcSlots + a.par] = (uint32_t)tn;
-    if (te) a.cnt[kVcErr] = 1;
+    if (te) a.cnt[kVcErr] = (uint32_t)te;
   }
   return t;
 }
@@ -434,24 +465,35 @@ __device__ __forceinline__ int seg_count(const VoxArgs& a, int b) {
   return part_of(a, a.par)[(size_t)b * kPartW + kPNew];
 }
 
-// one block per accum block: its listed voxels (the block's segment of the slot list)
+// one block per accum block: its listed voxels (the block's segment of the slot list).  The
+// first round of the segment's slots is loaded before the totals are reduced (neither
+// depends on the other): the reduction's round trip hides the slots' latency
 __global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
+  const int b = blockIdx.x;
+  const int nn = seg_count(a, b);
+  const size_t seg = (size_t)b * kVoxChunk;
+  const uint32_t* sl = a.lists + (size_t)a.par * a.lcap + seg;
+  uint32_t* tl = a.lists + (size_t)(2 + a.par) * a.lcap + seg;
+  constexpr int kPre = 2;  // slots per thread loaded ahead (a segment averages ~1.5 rounds)
+  uint32_t ps[kPre];
+  ulonglong2 pka[kPre], pbm[kPre];
+#pragma unroll
+  for (int k = 0; k < kPre; ++k) {
+    const int i = threadIdx.x + k * kBlock;
+    ps[k] = i < nn ? sl[i] : 0u;
+    if (i < nn) {
+      pka[k] = *reinterpret_cast<const ulonglong2*>(&a.tab[ps[k]].key);
+      pbm[k] = *reinterpret_cast<const ulonglong2*>(&a.tab[ps[k]].b);
+    }
+  }
   const VoxTotals t = vox_reduce(a, blockIdx.x == 0);
   if (!t.any) return;
   if (t.nvox > a.grid_cap || t.nvox > INT_MAX) {  // the host grows the grid and runs this again
     if (blockIdx.x == 0 && threadIdx.x == 0) a.cnt[kVcOver] = 1;
     return;
   }
-  const int b = blockIdx.x;
-  const int nn = seg_count(a, b);
-  const size_t seg = (size_t)b * kVoxChunk;
-  const uint32_t* sl = a.lists + (size_t)a.par * a.lcap + seg;
-  uint32_t* tl = a.lists + (size_t)(2 + a.par) * a.lcap + seg;
   uint32_t flagged = 0;
-  for (int i = threadIdx.x; i < nn; i += kBlock) {
-    const uint32_t s = sl[i];
-    const ulonglong2 ka = *reinterpret_cast<const ulonglong2*>(&a.tab[s].key);
-    const ulonglong2 bm = *reinterpret_cast<const ulonglong2*>(&a.tab[s].b);
+  auto convert = [&](int i, uint32_t s, const ulonglong2& ka, const ulonglong2& bm) {
     int x, y, z;
     unpack_cell(ka.x, x, y, z);
     const int64_t idx = (x - t.mn[0]) + (int64_t)t.dv[0] * ((y - t.mn[1]) + (int64_t)t.dv[1] * (z - t.mn[2]));
@@ -464,6 +506,15 @@ __global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
     const int cmag = max(max(abs(x), abs(y)), abs(z)) + 1;
     const float eps = (float)(count + 4) * (float)cmag * 0x1p-22f;
     if (__uint_as_float((uint32_t)bm.y) < eps || eps >= __uint_as_float(kMarginFlush)) ++flagged;
+  };
+#pragma unroll
+  for (int k = 0; k < kPre; ++k) {
+    const int i = threadIdx.x + k * kBlock;
+    if (i < nn) convert(i, ps[k], pka[k], pbm[k]);
+  }
+  for (int i = threadIdx.x + kPre * kBlock; i < nn; i += kBlock) {
+    const uint32_t s = sl[i];
+    convert(i, s, *reinterpret_cast<const ulonglong2*>(&a.tab[s].key), *reinterpret_cast<const ulonglong2*>(&a.tab[s].b));
   }
   flagged = wave_reduce(flagged, [](uint32_t u, uint32_t v) { return u + v; });
   if ((threadIdx.x & 63) == 0 && flagged) atomicAdd(a.cnt + kVcFlag, flagged);

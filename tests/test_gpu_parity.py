@@ -208,6 +208,29 @@ def test_multipoint_voxel_colour_mean(ctx):
     assert np.array_equal(ds.view(np.uint32), cloud.view(np.uint32))
 
 
+def test_voxel_table_regrows(ctx):
+    """The single-frame voxeliser sizes its hash table from the previous frame's voxel count
+    (round 4): a small frame followed by 400k scattered points (~400k voxels) fills it, and
+    the frame runs again on larger tables -- the grid, colours and downsampled cloud are the
+    oracle's, and a small frame after it is exact too."""
+    rng = np.random.default_rng(11)
+
+    def cloud(n, span):
+        xyz = (rng.random((n, 3)) * span).astype(np.float32)
+        col = rng.integers(0, 256, (n, 3))
+        return np.concatenate([xyz, synth.pack_rgb(col[:, 0], col[:, 1], col[:, 2])[:, None]], 1).astype(np.float32)
+
+    for pts in (cloud(2000, 0.05), cloud(400_000, 1.0), cloud(3000, 0.08)):
+        gi = ctx.voxelize(pts, 0.01)
+        g, layout, cl = po.voxelize(pts, 0.01)
+        assert list(gi.div_b) == list(g.div_b) and gi.n_occ == (layout >= 0).sum()
+        assert np.array_equal(ctx.leaf_layout(), layout)
+        words = ctx.grid()
+        occ = layout >= 0
+        assert np.array_equal(words[occ], (1 << 24) | cl[layout[occ], 3].view(np.uint32)) and not words[~occ].any()
+        assert np.array_equal(ctx.downsampled().view(np.uint32), cl.view(np.uint32))
+
+
 def test_config2_kinect_128(ctx):
     """Config 2: 1M-pt Kinect-style scene, 128^3, C3-HLAC-981 + 1-model search."""
     pts = synth.kinect_scene(1_000_000, grid=128, leaf=0.02, seed=synth.BASE_SEED)
