@@ -72,7 +72,12 @@ __host__ __device__ inline int mf_plane_bytes(int lx, int ly) {
 __host__ __device__ inline int mf_r256(int x) { return (x + 255) & ~255; }
 // (+16: the two-step layers put planes 4..11 one 16-byte block further, see mf_layer_ksteps2)
 __host__ __device__ inline int mf_slot_stride(int pb) { return mf_r256(kMfCh * pb + 16); }
-__host__ __device__ inline int mf_wave_stride(int pb) { return 3 * mf_slot_stride(pb) + mf_r256(pb); }
+#ifndef C3H_MF_SLOTS
+#define C3H_MF_SLOTS 3  // layer slots per wave (2: layer z + 2 reuses layer z's slot after its K steps)
+#endif
+constexpr int kMfSlots = C3H_MF_SLOTS;
+static_assert(kMfSlots == 2 || kMfSlots == 3, "layer slots");
+__host__ __device__ inline int mf_wave_stride(int pb) { return kMfSlots * mf_slot_stride(pb) + mf_r256(pb); }
 __host__ __device__ inline int mf_const_bytes(int pb) { return mf_r256(128 + 3 * pb); }
 // 3 x 256 channel-byte tables | 128 B | 3 constant planes (0x00, 0x01, 0xff) | per-wave
 // regions: 3 layer slots of 12 planes, the centre mask
@@ -380,7 +385,7 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
     const int SS = mf_slot_stride(PB);
     const bool two = C3H_MF_TWO && nks == 2 && (PW & 15) == 12;  // mf_layer_ksteps2's layers
     const int gap = two ? C3H_MF_GAP : 0;  // planes 4..11 shifted (banks, see mf_layer_ksteps2)
-    uint8_t* mask = wl + 3 * SS;
+    uint8_t* mask = wl + kMfSlots * SS;
     // centre mask of the K positions PW + 4 j + b: rows 1..ly, columns 1..lx
     for (int j = lane; j < 16 * nks; j += 64) {
       uint32_t m = 0;
@@ -424,7 +429,7 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
 #if C3H_MF_EXP & 2
       return;
 #endif
-      uint8_t* slot = wl + (L % 3) * SS;
+      uint8_t* slot = wl + (L % kMfSlots) * SS;
 #pragma unroll
       for (int i = 0; i < LOAD; ++i) {
         if (it_dst[i] < 0) continue;
@@ -473,8 +478,8 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
     for (int z = 0; z < lz; ++z) {
       mf_compiler_fence();  // same-wave LDS accesses complete in order; keep the compiler's too
       const int pn = nk * PB + (nk >= 4 ? gap : 0) + korg;
-      const uint8_t* pp = realk ? wl + ((z % 3) * SS + pn) : cpad;        // dz = -1
-      const uint8_t* pc = realk ? wl + (((z + 1) % 3) * SS + pn) : cpad;  // dz = 0
+      const uint8_t* pp = realk ? wl + ((z % kMfSlots) * SS + pn) : cpad;        // dz = -1
+      const uint8_t* pc = realk ? wl + (((z + 1) % kMfSlots) * SS + pn) : cpad;  // dz = 0
 #if !(C3H_MF_EXP & 1)
       if (two) {  // S <= 10 tiles: pitch 12
         mf_layer_ksteps2<12>(pp, pc, mk2, pw16, h4k, acc);
