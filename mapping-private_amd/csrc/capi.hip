@@ -822,7 +822,10 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
   // only grows.  Slot lists and partial records: one segment of the block's points per block
   uint64_t pcap = 512;
   while (pcap < (uint64_t)n) pcap <<= 1;
-  const uint64_t hint = ctx->vocc_hint ? ctx->vocc_hint : (uint64_t)n / 4;
+#ifndef C3H_VOX_ADAPTIVE
+#define C3H_VOX_ADAPTIVE 1  // diagnostics: 0 = the table at 2x the points (round 3)
+#endif
+  const uint64_t hint = C3H_VOX_ADAPTIVE ? (ctx->vocc_hint ? ctx->vocc_hint : (uint64_t)n / 4) : 2 * pcap;
   uint64_t ts_want = 4096;
   while (ts_want < 4 * hint && ts_want < 2 * pcap) ts_want <<= 1;
   const int nblk = (int)c3h::vox_blocks(n);

@@ -63,6 +63,9 @@ constexpr int kVoxRound = kVoxPer;             // loads in flight per thread (on
 #ifndef C3H_VOX_SLOTS
 #define C3H_VOX_SLOTS 2048
 #endif
+#ifndef C3H_VOX_EARLY_LOAD
+#define C3H_VOX_EARLY_LOAD 1  // the points' loads issued before the previous frame's clear
+#endif
 #ifndef C3H_VOX_MERGE
 #define C3H_VOX_MERGE 1  // the run merge (0: every point updates the LDS table itself)
 #endif
@@ -234,6 +237,10 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
     } else {
       p[j] = make_float4(NAN, NAN, NAN, 0.0f);
     }
+  }
+  if (!C3H_VOX_EARLY_LOAD) {  // diagnostics: the points' loads wait for the clear
+    __syncthreads();
+    __builtin_amdgcn_s_waitcnt(0);
   }
   vox_clear_prev(a);
   uint32_t* sl = a.lists + (size_t)a.par * a.lcap + (size_t)blockIdx.x * kVoxChunk;
