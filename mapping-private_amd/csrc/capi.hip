@@ -815,15 +815,17 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
       d_pts = reinterpret_cast<const float4*>(ctx->pts.p);
     }
   }
-  // the global table holds ~4x the voxels expected (the last frame's count; n / 4 before
-  // the first) rather than 2x the points: 58k voxels of a 1M-point frame then fill 256k
-  // slots (8 MB) instead of 2M (64 MB), so the flush's atomics stay in cache.  A frame that
-  // fills it (kGProbe probes without room) runs again on a table twice the size; the table
-  // only grows.  Slot lists and partial records: one segment of the block's points per block
+  // the global table: 2x the points (load <= 1/2).  C3H_VOX_ADAPTIVE=1 sizes it at ~4x the
+  // voxels expected instead (the last frame's count; 256k slots for a 1M-point Kinect frame
+  // of 58k voxels instead of 2M): measured 2 us slower per frame (profiles/r4/vox_ab/) --
+  // the flush's device-scope atomics serialise per cache line, and a denser table puts more
+  // voxels on each line.  A frame that fills the table (kGProbe probes without room) runs
+  // again on a table twice the size; the table only grows.  Slot lists and partial
+  // records: one segment of the block's points per block
   uint64_t pcap = 512;
   while (pcap < (uint64_t)n) pcap <<= 1;
 #ifndef C3H_VOX_ADAPTIVE
-#define C3H_VOX_ADAPTIVE 1  // diagnostics: 0 = the table at 2x the points (round 3)
+#define C3H_VOX_ADAPTIVE 0  // diagnostics: 1 = the table at ~4x the expected voxels
 #endif
   const uint64_t hint = C3H_VOX_ADAPTIVE ? (ctx->vocc_hint ? ctx->vocc_hint : (uint64_t)n / 4) : 2 * pcap;
   uint64_t ts_want = 4096;
