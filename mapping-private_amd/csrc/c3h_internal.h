@@ -385,6 +385,7 @@ struct SparseSearch {
   float* gbox = nullptr;   // large grids: box-summed G rows of every position (pstart order)
   int64_t s_gbox = 0;
   int score_mfma = 0;      // project on the matrix cores (score_mfma_kernel; needs gbox, nframes 1)
+  int skip_empty = 1;      // box sums skip rows with exist 0 (C3 extracts: exist 0 <=> no centre voxel)
   const _Float16* qt16 = nullptr;  // fp16 search precision: the basis as f16, [Opad][16 * Kq16]
   int Kq16 = 0;                    // 16-wide k steps (D rounded up to 16, / 16)
   // canvas frames (c3h_run_point_frames): per frame its own subdivision counts; a box
@@ -549,6 +550,10 @@ struct c3h_ctx {
   // search
   bool have_setup = false;
   int D = 0, F = 0, M = 0, r = 0, Dpad = 0;
+  // exist 0 implies an all-zero feature row (C3 extracts: every centre voxel adds >= 1 to
+  // the exist value); GRSD / VOSCH / caller features do not promise it (a row of a few
+  // GRSD transitions has exist 0), so their box sums add every row as searchPart does
+  bool exist_gates_rows = false;
   int D_user = 0;  // the caller's D (D is rounded up to a multiple of 4 with zero axes)
   bool compress = true;
   c3h::DevBuf<float> axis_pt;       // F x Dpad (transposed, whitened)

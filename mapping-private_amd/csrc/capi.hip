@@ -482,6 +482,7 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
     q.sparse_scores = same_layout ? kSparseScores : 0;
     q.nmodes = rm.n;
     q.score_mfma = mf ? 1 : 0;
+    q.skip_empty = ctx->exist_gates_rows ? 1 : 0;
     if (mf && ctx->prec16 && ctx->Kq16 > 0) {  // fp16 search precision: f16 operands
       q.qt16 = ctx->qt16.p;
       q.Kq16 = ctx->Kq16;
@@ -1154,6 +1155,7 @@ int extract_frames(c3h_ctx* ctx, const uint32_t* const* grids, int nf, const c3h
   ctx->have_feat = false;
   ctx->g_valid = false;
   ctx->rows_valid = false;
+  ctx->exist_gates_rows = true;
   const int F = p->variant;
   const int* div = ctx->info.div_b;
   int32_t sb[3] = {0, 0, 0};
@@ -1569,6 +1571,7 @@ int c3h_extract_grsd(c3h_ctx* ctx, const c3h_grsd_params* p, int32_t subdiv_out[
   ctx->have_feat = false;
   ctx->g_valid = false;
   ctx->rows_valid = false;
+  ctx->exist_gates_rows = false;
   int32_t sb[3];
   int64_t H = 0;
   int rc = grsd_frames(ctx, p, sb, &H);
@@ -1634,6 +1637,7 @@ int c3h_extract_vosch(c3h_ctx* ctx, const c3h_grsd_params* p, const int32_t thr[
   ctx->feat_sparse = false;
   ctx->g_valid = false;
   ctx->rows_valid = false;
+  ctx->exist_gates_rows = false;
   if (subdiv_out) memcpy(subdiv_out, sb, sizeof(sb));
   if (hist_num) *hist_num = H;
   return C3H_OK;
@@ -1656,6 +1660,7 @@ int c3h_set_features(c3h_ctx* ctx, const float* feat, const int32_t subdiv_b[3],
   ctx->have_feat = false;
   ctx->g_valid = false;
   ctx->rows_valid = false;
+  ctx->exist_gates_rows = false;
   ENSURE(ctx->feat, (size_t)H * dim);
   ENSURE(ctx->exist, (size_t)H);
   if (H > 0) {

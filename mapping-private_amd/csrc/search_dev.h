@@ -441,7 +441,7 @@ __device__ __forceinline__ void boxsum_body(const SparseSearch& a, int64_t e, in
     for (int dy = 0; dy < md.yr; ++dy)
       for (int dx = 0; dx < md.xr; ++dx) {
         const int hh = h + dz * xyn + dy * a.xn + dx;
-        if (fexist[hh] != 0) {
+        if (!a.skip_empty || fexist[hh] != 0) {
           const float4 v = G4[(int64_t)hh * D4 + d4];
           s.x += v.x;
           s.y += v.y;
@@ -627,7 +627,8 @@ __device__ __forceinline__ void score_list_body(const SparseSearch& b, int bx, i
     } else {  // box sums in the fixed (dz, dy, dx) order over non-empty rows; lane = position.
        // Cells go in batches of 4 x (this thread's d4 slots): every load of a batch is in
        // flight together.  Rows of empty subdivisions read as 0 (their G rows may be stale;
-       // +0 added to a sum that starts at +0 changes nothing).
+       // +0 added to a sum that starts at +0 changes nothing) -- for C3 extracts, where
+       // exist 0 means empty (skip_empty); other features add every row.
       const int pp = tid & (kFP - 1), dg = tid / kFP;
       constexpr int kDG = kBlock / kFP;  // d4 stride
       const bool ok = gate[pp];
@@ -649,7 +650,7 @@ __device__ __forceinline__ void score_list_body(const SparseSearch& b, int bx, i
             const int c = c0 + k;
             const int dx = c % xr, dy = (c / xr) % yr, dz = c / (xr * yr);
             const int hh = h + dz * xyn + dy * a.xn + dx;
-            lv[k] = c < ncell && fexist[c < ncell ? hh : h] != 0;
+            lv[k] = c < ncell && (!a.skip_empty || fexist[c < ncell ? hh : h] != 0);
 #pragma unroll
             for (int q = 0; q < kSlots; ++q) {
               const int d4 = d4b + dg + q * kDG;
