@@ -66,7 +66,13 @@ def test_external_features_with_reference_exist_rules(ctx, kind):
     else:  # GRSD-21: 20 surface-type pair counts + 1
         F = 21
         f = np.floor(rng.random((H, F)) * 60).astype(np.float32)
+        # rows of a few transitions: exist 0 with non-zero features, which the box sums
+        # must still add (searchPart sums every row; round 4 found the sparse search
+        # skipping them for caller features)
+        few = rng.random(H) < 0.25
+        f[few] = np.floor(rng.random((few.sum(), F)) * 2)
         exp = _grsd_exist(f)
+        assert ((exp == 0) & (f.sum(1) > 0)).sum() > 10
         rule = 2
         fmax = None
     ctx.set_features(f, sb, None, rule)
