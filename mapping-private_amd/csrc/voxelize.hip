@@ -63,8 +63,10 @@ constexpr int kVoxRound = kVoxPer;             // loads in flight per thread (on
 #ifndef C3H_VOX_SLOTS
 #define C3H_VOX_SLOTS 2048
 #endif
-#ifndef C3H_VOX_EARLY_LOAD
-#define C3H_VOX_EARLY_LOAD 1  // the points' loads issued before the previous frame's clear
+#ifndef C3H_VOX_DIAG_FLUSH
+#define C3H_VOX_DIAG_FLUSH 0  // diagnostics builds only: 1 = flush atomics at workgroup scope (wrong
+                              // across XCDs: times L2-local atomics), 2 = no global flush at all,
+                              // 3 = no LDS hash either
 #endif
 #ifndef C3H_VOX_MERGE
 #define C3H_VOX_MERGE 1  // the run merge (0: every point updates the LDS table itself)
@@ -176,10 +178,44 @@ __device__ __forceinline__ const int32_t* part_of(const VoxArgs& a, int par) {
   return a.part + (size_t)par * a.nblk_cap * kPartW;
 }
 
-// the previous frame's grid words and its table's slots (its segments b, b + nblk, ...)
-__device__ __forceinline__ void vox_clear_prev(const VoxArgs& a) {
+// the previous frame's grid words and its table's slots (its segments b, b + nblk, ...).
+// The first segment's list is loaded at the start of the accumulate (speculatively, all
+// kVoxChunk entries: no wait for its count) and cleared at its end, after the flush: the
+// clear is off the workgroup's dependency chain (this frame uses the other table; the
+// scatter, a later launch, writes the grid)
+constexpr int kClrPer = kVoxChunk / kVB;
+struct VoxClear {
+  int nn = 0;
+  uint32_t sl[kClrPer], tl[kClrPer];
+};
+__device__ __forceinline__ void vox_clear_issue(const VoxArgs& a, VoxClear& c) {
+  const int pp = a.par ^ 1, b = blockIdx.x;
+  if (b >= a.nblk_prev) return;  // uniform
+  c.nn = part_of(a, pp)[(size_t)b * kPartW + kPNew];
+  const uint32_t* sl = a.lists + (size_t)pp * a.lcap + (size_t)b * kVoxChunk;
+  const uint32_t* tl = a.lists + (size_t)(2 + pp) * a.lcap + (size_t)b * kVoxChunk;
+#pragma unroll
+  for (int k = 0; k < kClrPer; ++k) {
+    c.sl[k] = sl[threadIdx.x + k * kVB];
+    c.tl[k] = tl[threadIdx.x + k * kVB];
+  }
+}
+__device__ __forceinline__ void vox_clear_finish(const VoxArgs& a, const VoxClear& c) {
+#pragma unroll
+  for (int k = 0; k < kClrPer; ++k) {
+    if ((int)(threadIdx.x + k * kVB) >= c.nn) continue;
+    if (a.clear_tables) {
+      VoxSlot& t = a.tab_prev[c.sl[k]];
+      *reinterpret_cast<ulonglong2*>(&t.key) = make_ulonglong2(kNoKey, 0ull);
+      *reinterpret_cast<ulonglong2*>(&t.b) = make_ulonglong2(0ull, (unsigned long long)kNoMargin);
+    }
+    if (a.clear_grid) a.grid[c.tl[k]] = 0;
+  }
+}
+// the previous frame's segments beyond the first (more previous blocks than this launch's)
+__device__ __forceinline__ void vox_clear_prev(const VoxArgs& a, int b_first) {
   const int pp = a.par ^ 1;
-  for (int b = blockIdx.x; b < a.nblk_prev; b += gridDim.x) {
+  for (int b = b_first; b < a.nblk_prev; b += gridDim.x) {
     const int nn = part_of(a, pp)[(size_t)b * kPartW + kPNew];
     const uint32_t* sl = a.lists + (size_t)pp * a.lcap + (size_t)b * kVoxChunk;
     const uint32_t* tl = a.lists + (size_t)(2 + pp) * a.lcap + (size_t)b * kVoxChunk;
@@ -192,6 +228,16 @@ __device__ __forceinline__ void vox_clear_prev(const VoxArgs& a) {
       if (a.clear_grid) a.grid[tl[i]] = 0;
     }
   }
+}
+
+// the flush's slot claim (diagnostics: C3H_VOX_DIAG_FLUSH 1 at workgroup scope)
+__device__ __forceinline__ unsigned long long vox_cas(unsigned long long* p, unsigned long long cmp,
+                                                      unsigned long long val) {
+  if (C3H_VOX_DIAG_FLUSH == 1) {
+    __hip_atomic_compare_exchange_strong(p, &cmp, val, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return cmp;
+  }
+  return atomicCAS(p, cmp, val);
 }
 
 // DPP row_shr:o (within 16-lane rows); lanes without a source read 0
@@ -238,11 +284,8 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
       p[j] = make_float4(NAN, NAN, NAN, 0.0f);
     }
   }
-  if (!C3H_VOX_EARLY_LOAD) {  // diagnostics: the points' loads wait for the clear
-    __syncthreads();
-    __builtin_amdgcn_s_waitcnt(0);
-  }
-  vox_clear_prev(a);
+  VoxClear clr;
+  vox_clear_issue(a, clr);
   uint32_t* sl = a.lists + (size_t)a.par * a.lcap + (size_t)blockIdx.x * kVoxChunk;
   __syncthreads();
   int mn[3] = {INT_MAX, INT_MAX, INT_MAX}, mx[3] = {INT_MIN, INT_MIN, INT_MIN};
@@ -304,7 +347,7 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
     if (o0 >= 4) { w0 += s0; w1 += s1; mb = min(mb, sm); }
     s0 = vrow_shr<8>(w0); s1 = vrow_shr<8>(w1); sm = vrow_shr<8>(mb);
     if (o0 >= 8) { w0 += s0; w1 += s1; mb = min(mb, sm); }
-    const bool tail = valid && ((lane & 15) == 15 || ((hm >> (lane + 1)) & 1));
+    const bool tail = C3H_VOX_DIAG_FLUSH < 3 && valid && ((lane & 15) == 15 || ((hm >> (lane + 1)) & 1));
     if (!tail) continue;
     // the run's totals: count <= 16, channel sums <= 4080
     const unsigned long long cr = ((unsigned long long)(w0 >> 24) << 32) | (w0 & 0xfffu);
@@ -335,9 +378,9 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
 #pragma unroll
     for (int k = 0; k < kFl; ++k) {
       const int s = tid + k * kVB;
-      key[k] = s < kLSlots ? s_key[s] : kNoKey;
+      key[k] = s < kLSlots && C3H_VOX_DIAG_FLUSH < 2 ? s_key[s] : kNoKey;
       h[k] = mix64(key[k]) & a.tmask;
-      prev[k] = key[k] != kNoKey ? atomicCAS(&a.tab[h[k]].key, kNoKey, key[k]) : kNoKey;
+      prev[k] = key[k] != kNoKey ? vox_cas(&a.tab[h[k]].key, kNoKey, key[k]) : kNoKey;
     }
 #pragma unroll
     for (int k = 0; k < kFl; ++k) {
@@ -347,7 +390,7 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
       uint64_t probes = 1;
       while (prev[k] != kNoKey && prev[k] != key[k] && probes < kGProbe && probes <= a.tmask) {
         h[k] = (h[k] + 1) & a.tmask;
-        prev[k] = atomicCAS(&a.tab[h[k]].key, kNoKey, key[k]);
+        prev[k] = vox_cas(&a.tab[h[k]].key, kNoKey, key[k]);
         ++probes;
       }
       if (prev[k] != kNoKey && prev[k] != key[k]) {
@@ -356,11 +399,19 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
       }
       const unsigned long long cr = s_cr[s];
       if (prev[k] == kNoKey) sl[atomicAdd(&s_nnew, 1u)] = (uint32_t)h[k];
-      atomicAdd(&a.tab[h[k]].a, ((cr >> 32) << 40) | (cr & 0xffffffffull));
-      atomicAdd(&a.tab[h[k]].b, s_gb[s]);
+      if (C3H_VOX_DIAG_FLUSH == 1) {
+        __hip_atomic_fetch_add(&a.tab[h[k]].a, ((cr >> 32) << 40) | (cr & 0xffffffffull), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(&a.tab[h[k]].b, s_gb[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {
+        atomicAdd(&a.tab[h[k]].a, ((cr >> 32) << 40) | (cr & 0xffffffffull));
+        atomicAdd(&a.tab[h[k]].b, s_gb[s]);
+      }
       if (s_m[s] < kMarginFlush) atomicMin(&a.tab[h[k]].margin, s_m[s]);
     }
   }
+  vox_clear_finish(a, clr);
+  vox_clear_prev(a, blockIdx.x + gridDim.x);
   // bounds, counts and the slot list go to this block's partial record: no same-address
   // atomics across blocks (they serialise at the memory side)
 #pragma unroll
