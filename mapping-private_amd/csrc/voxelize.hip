@@ -66,7 +66,8 @@ constexpr int kVoxRound = kVoxPer;             // loads in flight per thread (on
 #ifndef C3H_VOX_DIAG_FLUSH
 #define C3H_VOX_DIAG_FLUSH 0  // diagnostics builds only: 1 = flush atomics at workgroup scope (wrong
                               // across XCDs: times L2-local atomics), 2 = no global flush at all,
-                              // 3 = no LDS hash either
+                              // 3 = no LDS hash either, 4 = the flush's CAS only, 5 = its adds
+                              // only (at the first probe slot, no claim)
 #endif
 #ifndef C3H_VOX_MERGE
 #define C3H_VOX_MERGE 1  // the run merge (0: every point updates the LDS table itself)
@@ -380,7 +381,7 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
       const int s = tid + k * kVB;
       key[k] = s < kLSlots && C3H_VOX_DIAG_FLUSH < 2 ? s_key[s] : kNoKey;
       h[k] = mix64(key[k]) & a.tmask;
-      prev[k] = key[k] != kNoKey ? vox_cas(&a.tab[h[k]].key, kNoKey, key[k]) : kNoKey;
+      prev[k] = key[k] != kNoKey && C3H_VOX_DIAG_FLUSH != 5 ? vox_cas(&a.tab[h[k]].key, kNoKey, key[k]) : kNoKey;
     }
 #pragma unroll
     for (int k = 0; k < kFl; ++k) {
@@ -399,6 +400,7 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
       }
       const unsigned long long cr = s_cr[s];
       if (prev[k] == kNoKey) sl[atomicAdd(&s_nnew, 1u)] = (uint32_t)h[k];
+      if (C3H_VOX_DIAG_FLUSH == 4) continue;  // diagnostics: the claim only
       if (C3H_VOX_DIAG_FLUSH == 1) {
         __hip_atomic_fetch_add(&a.tab[h[k]].a, ((cr >> 32) << 40) | (cr & 0xffffffffull), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
