@@ -112,6 +112,8 @@ struct VoxArgs {
   float z_limit, inv, leaf;
   VoxSlot* tab;             // this frame's hash table (the two tables alternate by parity)
   VoxSlot* tab_prev;        // the previous frame's, cleared by this frame's accum launch
+  unsigned long long* keys;       // the tables' keys, apart from the sums (C3H_VOX_SOA)
+  unsigned long long* keys_prev;
   uint64_t tmask;           // table size - 1 (power of two)
   uint32_t* lists;          // [slots parity 0 | slots parity 1 | grid words parity 0 | parity 1] x lcap,
   uint64_t lcap;            //   each a segment of 2048 per accum block
@@ -490,6 +492,7 @@ struct c3h_ctx {
   // voxeliser state (voxelize.hip): global hash table, slot / grid-word lists by epoch
   // parity, counters; what the previous frame listed is cleared by the next frame
   c3h::DevBuf<c3h::VoxSlot> vtab[2];
+  c3h::DevBuf<unsigned long long> vkeys[2];
   c3h::DevBuf<uint32_t> vlists, vcnt;
   c3h::DevBuf<int32_t> vpart;
   uint64_t vtsize = 0, vlcap = 0;

@@ -700,6 +700,8 @@ void c3h_destroy(c3h_ctx* ctx) {
   release(ctx->vosch_feat);
   release(ctx->vtab[0]);
   release(ctx->vtab[1]);
+  release(ctx->vkeys[0]);
+  release(ctx->vkeys[1]);
   release(ctx->vlists);
   release(ctx->vcnt);
   release(ctx->vpart);
@@ -841,12 +843,15 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
       const int bcap = (int)std::max<int64_t>(c3h::vox_blocks((int64_t)pcap), ctx->vblk_cap);
       ENSURE(ctx->vtab[0], ts);
       ENSURE(ctx->vtab[1], ts);
+      ENSURE(ctx->vkeys[0], ts);
+      ENSURE(ctx->vkeys[1], ts);
       ENSURE(ctx->vlists, 4 * (size_t)bcap * c3h::vox_positions(1));
       ENSURE(ctx->vpart, 2 * (size_t)bcap * c3h::vox_part_words());
       ENSURE(ctx->vcnt, c3h::kVcWords);
       HIPCHK(hipMemsetAsync(ctx->vpart.p, 0, ctx->vpart.n * 4, ctx->stream));
       for (int t = 0; t < 2; ++t) {  // empty slots: key ~0, sums 0, margin ~0
         HIPCHK(hipMemset2DAsync(&ctx->vtab[t].p[0].key, sizeof(c3h::VoxSlot), 0xff, 8, ts, ctx->stream));
+        HIPCHK(hipMemsetAsync(ctx->vkeys[t].p, 0xff, ts * 8, ctx->stream));
         HIPCHK(hipMemset2DAsync(&ctx->vtab[t].p[0].a, sizeof(c3h::VoxSlot), 0, 16, ts, ctx->stream));
         HIPCHK(hipMemset2DAsync(&ctx->vtab[t].p[0].margin, sizeof(c3h::VoxSlot), 0xff, 8, ts, ctx->stream));
       }
@@ -870,6 +875,8 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
     a.leaf = leaf;
     a.tab = ctx->vtab[ctx->vpar].p;
     a.tab_prev = ctx->vtab[ctx->vpar ^ 1].p;
+    a.keys = ctx->vkeys[ctx->vpar].p;
+    a.keys_prev = ctx->vkeys[ctx->vpar ^ 1].p;
     a.tmask = ctx->vtsize - 1;
     a.lists = ctx->vlists.p;
     a.lcap = ctx->vlcap;

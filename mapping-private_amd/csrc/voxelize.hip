@@ -124,13 +124,23 @@ __device__ __forceinline__ uint32_t mix64(unsigned long long k) {
   return (uint32_t)k;
 }
 
+#ifndef C3H_VOX_SOA
+#define C3H_VOX_SOA 1  // keys in their own array: the claims and the sums' atomics hit different lines
+#endif
+__device__ __forceinline__ unsigned long long& vkey(const VoxArgs& a, uint64_t h) {
+  return C3H_VOX_SOA ? a.keys[h] : a.tab[h].key;
+}
+__device__ __forceinline__ unsigned long long& vkey_prev(const VoxArgs& a, uint64_t h) {
+  return C3H_VOX_SOA ? a.keys_prev[h] : a.tab_prev[h].key;
+}
+
 // global table insert: returns the slot (or -1 when kGProbe probes found no room: the host
 // runs the frame again on a table twice the size); *fresh = this call inserted the key
 constexpr uint64_t kGProbe = 64;  // global probes before the table counts as full (load <= 1/4 by sizing)
 __device__ __forceinline__ int64_t global_slot(const VoxArgs& a, unsigned long long key, bool* fresh) {
   uint64_t h = mix64(key) & a.tmask;
   for (uint64_t probes = 0; probes < kGProbe && probes <= a.tmask; ++probes) {
-    const unsigned long long prev = atomicCAS(&a.tab[h].key, kNoKey, key);
+    const unsigned long long prev = atomicCAS(&vkey(a, h), kNoKey, key);
     if (prev == kNoKey) {
       *fresh = true;
       return (int64_t)h;
@@ -148,7 +158,7 @@ __device__ __forceinline__ int64_t global_slot(const VoxArgs& a, unsigned long l
 __device__ __forceinline__ int64_t find_slot(const VoxArgs& a, unsigned long long key) {
   uint64_t h = mix64(key) & a.tmask;
   for (uint64_t probes = 0; probes <= a.tmask; ++probes) {
-    const unsigned long long k = a.tab[h].key;
+    const unsigned long long k = vkey(a, h);
     if (k == key) return (int64_t)h;
     if (k == kNoKey) return -1;
     h = (h + 1) & a.tmask;
@@ -208,6 +218,7 @@ __device__ __forceinline__ void vox_clear_finish(const VoxArgs& a, const VoxClea
     if (a.clear_tables) {
       VoxSlot& t = a.tab_prev[c.sl[k]];
       *reinterpret_cast<ulonglong2*>(&t.key) = make_ulonglong2(kNoKey, 0ull);
+      if (C3H_VOX_SOA) vkey_prev(a, c.sl[k]) = kNoKey;
       *reinterpret_cast<ulonglong2*>(&t.b) = make_ulonglong2(0ull, (unsigned long long)kNoMargin);
     }
     if (a.clear_grid) a.grid[c.tl[k]] = 0;
@@ -224,6 +235,7 @@ __device__ __forceinline__ void vox_clear_prev(const VoxArgs& a, int b_first) {
       if (a.clear_tables) {
         VoxSlot& t = a.tab_prev[sl[i]];
         *reinterpret_cast<ulonglong2*>(&t.key) = make_ulonglong2(kNoKey, 0ull);
+        if (C3H_VOX_SOA) vkey_prev(a, sl[i]) = kNoKey;
         *reinterpret_cast<ulonglong2*>(&t.b) = make_ulonglong2(0ull, (unsigned long long)kNoMargin);
       }
       if (a.clear_grid) a.grid[tl[i]] = 0;
@@ -381,7 +393,7 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
       const int s = tid + k * kVB;
       key[k] = s < kLSlots && C3H_VOX_DIAG_FLUSH < 2 ? s_key[s] : kNoKey;
       h[k] = mix64(key[k]) & a.tmask;
-      prev[k] = key[k] != kNoKey && C3H_VOX_DIAG_FLUSH != 5 ? vox_cas(&a.tab[h[k]].key, kNoKey, key[k]) : kNoKey;
+      prev[k] = key[k] != kNoKey && C3H_VOX_DIAG_FLUSH != 5 ? vox_cas(&vkey(a, h[k]), kNoKey, key[k]) : kNoKey;
     }
 #pragma unroll
     for (int k = 0; k < kFl; ++k) {
@@ -391,7 +403,7 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
       uint64_t probes = 1;
       while (prev[k] != kNoKey && prev[k] != key[k] && probes < kGProbe && probes <= a.tmask) {
         h[k] = (h[k] + 1) & a.tmask;
-        prev[k] = vox_cas(&a.tab[h[k]].key, kNoKey, key[k]);
+        prev[k] = vox_cas(&vkey(a, h[k]), kNoKey, key[k]);
         ++probes;
       }
       if (prev[k] != kNoKey && prev[k] != key[k]) {
@@ -543,6 +555,7 @@ __global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
     ps[k] = i < nn ? sl[i] : 0u;
     if (i < nn) {
       pka[k] = *reinterpret_cast<const ulonglong2*>(&a.tab[ps[k]].key);
+      pka[k].x = vkey(a, ps[k]);
       pbm[k] = *reinterpret_cast<const ulonglong2*>(&a.tab[ps[k]].b);
     }
   }
@@ -574,7 +587,9 @@ __global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
   }
   for (int i = threadIdx.x + kPre * kBlock; i < nn; i += kBlock) {
     const uint32_t s = sl[i];
-    convert(i, s, *reinterpret_cast<const ulonglong2*>(&a.tab[s].key), *reinterpret_cast<const ulonglong2*>(&a.tab[s].b));
+    ulonglong2 ka = *reinterpret_cast<const ulonglong2*>(&a.tab[s].key);
+    ka.x = vkey(a, s);
+    convert(i, s, ka, *reinterpret_cast<const ulonglong2*>(&a.tab[s].b));
   }
   flagged = wave_reduce(flagged, [](uint32_t u, uint32_t v) { return u + v; });
   if ((threadIdx.x & 63) == 0 && flagged) atomicAdd(a.cnt + kVcFlag, flagged);
@@ -660,7 +675,7 @@ __global__ __launch_bounds__(kBlock) void vox_centroid_kernel(VoxArgs a, const u
     const uint32_t idx = tl[q];
     cent[q] = make_float4(c[0], c[1], c[2], __uint_as_float(a.grid[idx] & 0x00ffffffu));
     int own[3];
-    unpack_cell(a.tab[sl[q]].key, own[0], own[1], own[2]);
+    unpack_cell(vkey(a, sl[q]), own[0], own[1], own[2]);
     int nb[3], sb[3];
     bool moved = false;
 #pragma unroll
