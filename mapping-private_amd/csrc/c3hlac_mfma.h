@@ -330,6 +330,93 @@ __device__ __forceinline__ void mf_layer_ksteps2(const uint8_t* pp, const uint8_
 #undef C3H_MF2
 }
 
+#ifndef C3H_MF_U32
+#define C3H_MF_U32 0  // two-step layers: dx = +-1 and unaligned fragments as byte-offset ds_read_b32
+#endif
+// The two-step layers with every fragment not on a 16-byte boundary read as four 32-bit LDS
+// loads at its byte offset (CDNA4 serves a misaligned ds_read_b32 without a replay; wider
+// misaligned reads replay at 64 cycles, so each load is fenced from its neighbours to keep
+// the compiler from merging them) instead of whole blocks + v_alignbyte: ~80 fewer VALU
+// and ~150 more LDS cycles per layer.
+typedef uint32_t __attribute__((aligned(1))) mf_u32_ua;
+__device__ __forceinline__ uint32_t mf_ld32(const uint8_t* p) {
+  const uint32_t v = *reinterpret_cast<const mf_u32_ua*>(p);
+  mf_compiler_fence();
+  return v;
+}
+template <int OFF>
+__device__ __forceinline__ mf_v4i mf_frag32(const uint8_t* row) {
+  if constexpr ((OFF & 15) == 0) {
+    const mf_u4 v = *reinterpret_cast<const mf_u4*>(__builtin_assume_aligned(row + OFF, 16));
+    return mf_v4i{(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+  } else {
+    mf_v4i f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[i] = (int)mf_ld32(row + OFF + 4 * i);
+    return f;
+  }
+}
+// a plane row's fragments dx = -1 .. NDX - 2 of both K steps: 8 NDX loads issued together
+// (from row + DYR - 1, so every offset is a non-negative immediate)
+template <int DYR, int NDX>
+__device__ __forceinline__ void mf_rowu(const uint8_t* row, mf_v4i (&f)[NDX][2]) {
+  const uint8_t* b = row + DYR - 1;
+#pragma unroll
+  for (int d = 0; d < NDX; ++d)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) f[d][ks][i] = (int)mf_ld32(b + d + 16 * ks + 4 * i);
+}
+template <int R>
+__device__ __forceinline__ void mf_layer_ksteps2u(const uint8_t* pp, const uint8_t* pc, const mf_u4 (&mk)[2],
+                                                  int pw16, int h4, mf_v4i (&acc)[kMfK]) {
+  const int o = 32 * h4;
+  const uint8_t* c0 = static_cast<const uint8_t*>(__builtin_assume_aligned(pc + o, 16));
+  mf_v4i A0, A1;
+  {
+    const mf_u4 a0 = *reinterpret_cast<const mf_u4*>(c0), a1 = *reinterpret_cast<const mf_u4*>(c0 + 16);
+    mf_v4i fl[1][2];
+    mf_rowu<0, 1>(c0, fl);  // dx = -1
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      A0[i] = (int)((a0[i] & mk[0][i]) | (0x80808080u & ~mk[0][i]));
+      A1[i] = (int)((a1[i] & mk[1][i]) | (0x80808080u & ~mk[1][i]));
+    }
+    acc[13] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0, A0, acc[13], 0, 0, 0);  // own channels
+    acc[13] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1, A1, acc[13], 0, 0, 0);
+    acc[12] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0, fl[0][0], acc[12], 0, 0, 0);  // (-1, 0, 0)
+    acc[12] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1, fl[0][1], acc[12], 0, 0, 0);
+  }
+  auto row3 = [&](const mf_v4i (&f)[3][2], int k0, int kstep) {
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      acc[k0 + kstep * d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0, f[d][0], acc[k0 + kstep * d], 0, 0, 0);
+      acc[k0 + kstep * d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1, f[d][1], acc[k0 + kstep * d], 0, 0, 0);
+    }
+  };
+  {
+    mf_v4i f[3][2];
+    mf_rowu<-R, 3>(pc + o - pw16, f);  // dz = 0, dy = -1: k = 9 + dx + 1
+    row3(f, 9, 1);
+  }
+  {
+    mf_v4i f[3][2];
+    mf_rowu<-R, 3>(pp + o - pw16, f);  // dz = -1, dy = -1: k = 3 (dx + 1)
+    row3(f, 0, 3);
+  }
+  {
+    mf_v4i f[3][2];
+    mf_rowu<0, 3>(pp + o, f);  // dz = -1, dy = 0
+    row3(f, 1, 3);
+  }
+  {
+    mf_v4i f[3][2];
+    mf_rowu<R, 3>(pp + o + pw16, f);  // dz = -1, dy = +1
+    row3(f, 2, 3);
+  }
+}
+
 // plane p -> (type, reference channel); p >= 12 is padding
 __device__ __forceinline__ int mf_type(int p) { return (p >> 1) & 1; }
 __device__ __forceinline__ int mf_chan(int p) { return 2 * (p >> 2) + (p & 1); }
@@ -482,7 +569,8 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
       const uint8_t* pc = realk ? wl + (((z + 1) % kMfSlots) * SS + pn) : cpad;  // dz = 0
 #if !(C3H_MF_EXP & 1)
       if (two) {  // S <= 10 tiles: pitch 12
-        mf_layer_ksteps2<12>(pp, pc, mk2, pw16, h4k, acc);
+        if (C3H_MF_U32) mf_layer_ksteps2u<12>(pp, pc, mk2, pw16, h4k, acc);
+        else mf_layer_ksteps2<12>(pp, pc, mk2, pw16, h4k, acc);
       } else {
         switch (PW & 15) {
           case 0: mf_layer_ksteps<0>(pp, pc, pmask, pw16, nks, h4k, acc); break;
