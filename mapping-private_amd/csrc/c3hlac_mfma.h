@@ -330,6 +330,9 @@ __device__ __forceinline__ void mf_layer_ksteps2(const uint8_t* pp, const uint8_
 #undef C3H_MF2
 }
 
+#ifndef C3H_MF_LOADX4
+#define C3H_MF_LOADX4 0  // a layer item whose 4 words all lie in the grid: one 16-B load
+#endif
 #ifndef C3H_MF_U32
 #define C3H_MF_U32 0  // two-step layers: dx = +-1 and unaligned fragments as byte-offset ds_read_b32
 #endif
@@ -506,6 +509,12 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
       for (int i = 0; i < LOAD; ++i) {
         const bool rowin = zin && it_gy[i] >= 0;
         const uint32_t* src = fgrid + (((int64_t)gz * a.gy + it_gy[i]) * a.gx + it_x[i]);
+        if (C3H_MF_LOADX4 && rowin && it_xm[i] == 15u) {  // the item's 4 words in the grid: one load
+          typedef uint32_t u4a4 __attribute__((ext_vector_type(4), aligned(4)));
+          const u4a4 v = *reinterpret_cast<const u4a4*>(src);
+          w[i][0] = v.x; w[i][1] = v.y; w[i][2] = v.z; w[i][3] = v.w;
+          continue;
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) w[i][j] = rowin && ((it_xm[i] >> j) & 1u) ? src[j] : 0u;
       }
