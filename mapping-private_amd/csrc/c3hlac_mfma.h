@@ -331,16 +331,16 @@ __device__ __forceinline__ void mf_layer_ksteps2(const uint8_t* pp, const uint8_
 }
 
 #ifndef C3H_MF_LOADX4
-#define C3H_MF_LOADX4 0  // a layer item whose 4 words all lie in the grid: one 16-B load
+#define C3H_MF_LOADX4 1  // a layer item whose 4 words all lie in the grid: one 16-B load
 #endif
 #ifndef C3H_MF_U32
 #define C3H_MF_U32 0  // two-step layers: dx = +-1 and unaligned fragments as byte-offset ds_read_b32
 #endif
-// The two-step layers with every fragment not on a 16-byte boundary read as four 32-bit LDS
-// loads at its byte offset (CDNA4 serves a misaligned ds_read_b32 without a replay; wider
-// misaligned reads replay at 64 cycles, so each load is fenced from its neighbours to keep
-// the compiler from merging them) instead of whole blocks + v_alignbyte: ~80 fewer VALU
-// and ~150 more LDS cycles per layer.
+// Diagnostics: the two-step layers with every fragment not on a 16-byte boundary read as
+// four 32-bit LDS loads at its byte offset (each fenced from its neighbours so the compiler
+// does not merge them) instead of whole blocks + v_alignbyte: 68 fewer VALU per layer, but
+// a ds_read_b32 off a 4-byte boundary is replayed, and config 5 took 11.2 ms instead of
+// 1.43 (profiles/r4/config5_ab/): the alignbyte form stays.
 typedef uint32_t __attribute__((aligned(1))) mf_u32_ua;
 __device__ __forceinline__ uint32_t mf_ld32(const uint8_t* p) {
   const uint32_t v = *reinterpret_cast<const mf_u32_ua*>(p);
