@@ -69,6 +69,9 @@ constexpr int kVoxRound = kVoxPer;             // loads in flight per thread (on
                               // 3 = no LDS hash either, 4 = the flush's CAS only, 5 = its adds
                               // only (at the first probe slot, no claim)
 #endif
+#ifndef C3H_VOX_SPEC_ADD
+#define C3H_VOX_SPEC_ADD 1  // the flush's sums issued with its claim (see vox_accum_kernel)
+#endif
 #ifndef C3H_VOX_MERGE
 #define C3H_VOX_MERGE 1  // the run merge (0: every point updates the LDS table itself)
 #endif
@@ -388,17 +391,36 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
     constexpr int kFl = (kLSlots + kVB - 1) / kVB;
     unsigned long long key[kFl], prev[kFl];
     uint64_t h[kFl];
+    // Speculative sums (C3H_VOX_SPEC_ADD): the two adds go to the key's home slot together
+    // with its claim, not after the claim's round trip; a claim that finds another key there
+    // (a collision, ~3 % of voxels at the table's load) takes the sums back out (64-bit
+    // wrap-around subtraction: exact) and adds them where the probe lands.  The scatter
+    // reads the sums only after this launch, so the intermediate state is never seen.
+    bool spec[kFl];
 #pragma unroll
     for (int k = 0; k < kFl; ++k) {
       const int s = tid + k * kVB;
       key[k] = s < kLSlots && C3H_VOX_DIAG_FLUSH < 2 ? s_key[s] : kNoKey;
       h[k] = mix64(key[k]) & a.tmask;
       prev[k] = key[k] != kNoKey && C3H_VOX_DIAG_FLUSH != 5 ? vox_cas(&vkey(a, h[k]), kNoKey, key[k]) : kNoKey;
+      spec[k] = C3H_VOX_SPEC_ADD && C3H_VOX_DIAG_FLUSH == 0 && key[k] != kNoKey;
+      if (spec[k]) {
+        const unsigned long long cr = s_cr[s];
+        atomicAdd(&a.tab[h[k]].a, ((cr >> 32) << 40) | (cr & 0xffffffffull));
+        atomicAdd(&a.tab[h[k]].b, s_gb[s]);
+      }
     }
 #pragma unroll
     for (int k = 0; k < kFl; ++k) {
       if (key[k] == kNoKey) continue;
       const int s = tid + k * kVB;
+      const unsigned long long cr = s_cr[s];
+      const unsigned long long va = ((cr >> 32) << 40) | (cr & 0xffffffffull), vb = s_gb[s];
+      if (spec[k] && prev[k] != kNoKey && prev[k] != key[k]) {  // collision: undo at home
+        atomicAdd(&a.tab[h[k]].a, 0ull - va);
+        atomicAdd(&a.tab[h[k]].b, 0ull - vb);
+        spec[k] = false;
+      }
       // collisions: linear probing as global_slot (the host sizes the table at >= 2x points)
       uint64_t probes = 1;
       while (prev[k] != kNoKey && prev[k] != key[k] && probes < kGProbe && probes <= a.tmask) {
@@ -410,9 +432,12 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
         err |= kVcErrFull;
         continue;
       }
-      const unsigned long long cr = s_cr[s];
       if (prev[k] == kNoKey) sl[atomicAdd(&s_nnew, 1u)] = (uint32_t)h[k];
       if (C3H_VOX_DIAG_FLUSH == 4) continue;  // diagnostics: the claim only
+      if (spec[k]) {  // the sums are in already
+        if (s_m[s] < kMarginFlush) atomicMin(&a.tab[h[k]].margin, s_m[s]);
+        continue;
+      }
       if (C3H_VOX_DIAG_FLUSH == 1) {
         __hip_atomic_fetch_add(&a.tab[h[k]].a, ((cr >> 32) << 40) | (cr & 0xffffffffull), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
