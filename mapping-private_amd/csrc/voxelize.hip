@@ -70,7 +70,7 @@ constexpr int kVoxRound = kVoxPer;             // loads in flight per thread (on
                               // only (at the first probe slot, no claim)
 #endif
 #ifndef C3H_VOX_SPEC_ADD
-#define C3H_VOX_SPEC_ADD 1  // the flush's sums issued with its claim (see vox_accum_kernel)
+#define C3H_VOX_SPEC_ADD 0  // diagnostics: 1 = the flush's sums issued with its claim (measured neutral)
 #endif
 #ifndef C3H_VOX_MERGE
 #define C3H_VOX_MERGE 1  // the run merge (0: every point updates the LDS table itself)
