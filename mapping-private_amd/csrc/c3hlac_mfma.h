@@ -330,6 +330,9 @@ __device__ __forceinline__ void mf_layer_ksteps2(const uint8_t* pp, const uint8_
 #undef C3H_MF2
 }
 
+#ifndef C3H_MF_SHAPE_CACHE
+#define C3H_MF_SHAPE_CACHE 1  // the tile shape's mask and item map kept across same-shape tiles
+#endif
 #ifndef C3H_MF_LOADX4
 #define C3H_MF_LOADX4 1  // a layer item whose 4 words all lie in the grid: one 16-B load
 #endif
@@ -461,6 +464,9 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
   const int h4k = lane >> 4, nk = lane & 15;
   const bool realk = nk < kMfCh;
 
+  int shape_prev = -1;  // the tile shape whose mask and item map are current (C3H_MF_SHAPE_CACHE)
+  int it_row[LOAD], it_q[LOAD];
+  uint32_t it_xs[LOAD];
   for (int wi = wid; wi < nwork; wi += nw) {
     const int tile = fwork[wi];
     const int ix = tile % a.ns0, iy = (tile / a.ns0) % a.ns1, iz = tile / (a.ns0 * a.ns1);
@@ -476,15 +482,33 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
     const bool two = C3H_MF_TWO && nks == 2 && (PW & 15) == 12;  // mf_layer_ksteps2's layers
     const int gap = two ? C3H_MF_GAP : 0;  // planes 4..11 shifted (banks, see mf_layer_ksteps2)
     uint8_t* mask = wl + kMfSlots * SS;
-    // centre mask of the K positions PW + 4 j + b: rows 1..ly, columns 1..lx
-    for (int j = lane; j < 16 * nks; j += 64) {
-      uint32_t m = 0;
+    // The tile shape's centre mask and item map (divisions by the pitch: ~300 VALU) are
+    // built when the shape differs from this wave's previous tile; S-uniform grids give
+    // every interior tile one shape (the mask stays in the wave's LDS region, past the
+    // epilogue's staging)
+    const int shape = lx | (ly << 8);
+    if (!C3H_MF_SHAPE_CACHE || shape != shape_prev) {
+      shape_prev = shape;
+      // centre mask of the K positions PW + 4 j + b: rows 1..ly, columns 1..lx
+      for (int j = lane; j < 16 * nks; j += 64) {
+        uint32_t m = 0;
 #pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int p = PW + 4 * j + b, row = p / PW, col = p - row * PW;
-        m |= (row <= ly && col >= 1 && col <= lx ? 0xffu : 0u) << (8 * b);
+        for (int b = 0; b < 4; ++b) {
+          const int p = PW + 4 * j + b, row = p / PW, col = p - row * PW;
+          m |= (row <= ly && col >= 1 && col <= lx ? 0xffu : 0u) << (8 * b);
+        }
+        *reinterpret_cast<uint32_t*>(mask + off0 + PW + 4 * j) = m;
       }
-      *reinterpret_cast<uint32_t*>(mask + off0 + PW + 4 * j) = m;
+#pragma unroll
+      for (int i = 0; i < LOAD; ++i) {
+        const int e = lane + 64 * i, row = e / ipr, q = e - row * ipr;
+        it_row[i] = e < nitem ? row : -(1 << 20);
+        it_q[i] = q;
+        uint32_t xs = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xs |= (4 * q + j < TW ? 1u : 0u) << j;
+        it_xs[i] = xs;
+      }
     }
     // layer items (row, dword q) of lane + 64 i: x = x0 - 1 + 4 q + j, valid x bits, the
     // row (-1 when out of the tile or the grid) and the item's byte in a plane
@@ -492,13 +516,13 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
     uint32_t it_xm[LOAD];
 #pragma unroll
     for (int i = 0; i < LOAD; ++i) {
-      const int e = lane + 64 * i, row = e / ipr, q = e - row * ipr, gy = y0 - 1 + row;
-      it_gy[i] = e < nitem && (unsigned)gy < (unsigned)a.gy ? gy : -1;
+      const int row = it_row[i], q = it_q[i], gy = y0 - 1 + row;
+      it_gy[i] = row >= 0 && (unsigned)gy < (unsigned)a.gy ? gy : -1;
       it_x[i] = x0 - 1 + 4 * q;
-      it_dst[i] = e < nitem ? off0 + row * PW + 4 * q : -1;
+      it_dst[i] = row >= 0 ? off0 + row * PW + 4 * q : -1;
       uint32_t xm = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) xm |= (4 * q + j < TW && (unsigned)(it_x[i] + j) < (unsigned)a.gx ? 1u : 0u) << j;
+      for (int j = 0; j < 4; ++j) xm |= ((it_xs[i] >> j) & 1u) && (unsigned)(it_x[i] + j) < (unsigned)a.gx ? 1u << j : 0u;
       it_xm[i] = xm;
     }
     uint32_t wv[2][LOAD][4];
