@@ -231,7 +231,11 @@ int c3h_get_exist(c3h_ctx* ctx, int32_t* out, int on_device);
  *           NULL disables compression (compress_flg=false; then D must equal F).
  *   axis_q: M x r x D model subspaces as readAxis leaves them (search.cpp:153-165,
  *           819-837: transposed, MULTIPLE_SIMILARITY scaling already applied).
- *   feature_max: setNormalizeVal values (search.cpp:742-748), NULL/0 = none. */
+ *   feature_max: setNormalizeVal values (search.cpp:742-748), NULL/0 = none.
+ * Any D >= 1: a D <= 160 that is not a multiple of 4 is run on zero axes appended up to the
+ * next multiple (their compressed values are 0, so the scores are the caller's D's bit for
+ * bit), which keeps such searches on the sparse list path and the pipeline;
+ * c3h_get_compressed returns the caller's D columns. */
 int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_t D,
                      int32_t F, const float* axis_q, int32_t M, int32_t r,
                      const float* feature_max, int32_t feature_max_len);
@@ -247,7 +251,7 @@ int c3h_set_search_precision(c3h_ctx* ctx, int32_t fp16);
  * M x r x D products, search.cpp:915-968): 0 = automatic (default: the matrix cores for
  * grids of >= 65,536 subdivisions and for models with r > 64, the VALU list kernel
  * otherwise), 1 = VALU (score_list_kernel for r <= 64; the generic kernel beyond),
- * 2 = matrix cores (score_mfma_kernel, v_mfma_f32_32x32x2_f32; D <= 160, D % 4 == 0).
+ * 2 = matrix cores (score_mfma_kernel, v_mfma_f32_32x32x2_f32; D <= 160).
  * Both engines form every product as the same k-ordered fp32 fma chain, so the scores are
  * bit-identical.  Batched / pipelined searches (c3h_run_frames) always use the VALU kernel. */
 int c3h_set_score_engine(c3h_ctx* ctx, int32_t engine);
