@@ -14,7 +14,8 @@ so every view stays batched (status 0), and:
   - every view with a moved voxel, and every 8th other view, equals the float64 oracle run
     from the points (position and mode exact unless scores tie within 1e-5; score within
     1e-5).
-C3-HLAC-117 (S = 4) and C3-HLAC-981 (S = 5), both with offsets."""
+C3-HLAC-117 (S = 4) and C3-HLAC-981 (S = 5), both with offsets; and the other colour
+tables (ColorCHLAC's (v, 255 - v), C3's float sin/cos) on a sample of the views."""
 import numpy as np
 import pytest
 
@@ -97,3 +98,49 @@ def test_real_views_batched_with_offcell_fixup(ctx, variant, S, off):
             assert abs(float(e["score"]) - sc[m, p]) <= RTOL * sc[m, p], (i, m, float(e["score"]), sc[m, p])
             if p != best:
                 assert sc[m, p] >= sc[m, best] * (1 - 2 * RTOL), (i, m, p, best)
+
+
+@pytest.mark.parametrize("color_mode", [c3hlac.COLOR_CHLAC, c3hlac.COLOR_C3_FLOAT])
+def test_real_views_batched_colour_modes(ctx, color_mode):
+    """The other setColor tables through the points-in batch (round 4): ColorCHLAC's
+    (v, 255 - v) and C3's float sin/cos, every 5th of the committed views, records equal
+    to the single-frame path with the same table and the sampled views to the oracle."""
+    import torch
+    views = _views()[::5]
+    nfr = len(views)
+    dev = torch.device("cuda", 0)
+    frames = [torch.from_numpy(v).to(dev) for v in views]
+    M = 2
+    axis_t, var, axis_q = synth.random_bases(117, 24, M, 4, seed=synth.BASE_SEED + 92)
+    ap = synth.whiten(axis_t, var)
+    ctx.search_setup(axis_t, var, axis_q)
+    ctx.set_rank(1)
+    ctx.set_batch(16)
+    ctx.set_pipeline(True)
+    d_out = torch.zeros((nfr, 3 * M), dtype=torch.int64, device=dev)
+    _, info = ctx.run_point_frames(frames, LEAF, CANVAS, 117, THR, 4, BOX, EXIST, True, d_out, color_mode=color_mode)
+    got = d_out.cpu().numpy().view(c3hlac.DET_DTYPE).reshape(nfr, M)
+    assert (info["status"] == 0).all(), np.flatnonzero(info["status"])
+    for i in range(nfr):
+        ctx.voxelize(views[i], LEAF)
+        ctx.extract(117, THR, 4, color_mode=color_mode)
+        ctx.set_rank(1)
+        lists, _ = ctx.search(BOX, EXIST)
+        assert np.array_equal(got[i], lists[:, 0]), i
+    for i in range(0, nfr, 6):
+        g, layout, cloud = po.voxelize(views[i], LEAF)
+        fe, sb, hn = po.c3hlac(g, layout, cloud, 117, THR, LEAF, 4, color_mode=color_mode, exact=True)
+        if min(sb) < 2:
+            continue
+        ex = po.exist(fe)
+        _, _, sc = po.search(sb, fe, ex, ap, axis_q, BOX, 1, EXIST, dbl=True, want_scores=True)
+        sc = sc.reshape(M, -1)
+        xe, ye = sb[0] - 1, sb[1] - 1
+        for m in range(M):
+            e = got[i, m]
+            if sc[m].max() <= 0:
+                assert float(e["score"]) == 0.0, (i, m)
+                continue
+            p = (int(e["z"]) * ye + int(e["y"])) * xe + int(e["x"])
+            assert abs(float(e["score"]) - sc[m, p]) <= RTOL * sc[m, p], (i, m)
+            assert sc[m, p] >= sc[m].max() * (1 - 2 * RTOL), (i, m)
