@@ -1016,7 +1016,18 @@ hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc,
       // last round of workgroups
       if (sc->PT16) {  // fp16 search precision
         const int64_t rblocks = (sc->H + kMR - 1) / kMR;
-        const unsigned ncomp = (unsigned)std::min<int64_t>(rblocks, 2048);
+        unsigned ncomp = (unsigned)std::min<int64_t>(rblocks, 2048);
+#ifndef C3H_CF16_BALANCED
+#define C3H_CF16_BALANCED 0  // diagnostics: persistent workgroups in balanced rounds (3 per CU)
+#endif
+        if (C3H_CF16_BALANCED) {
+          int dev = 0, n_cu = 256;
+          (void)hipGetDevice(&dev);
+          (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+          const int64_t slots = std::max<int64_t>(1, 3 * (int64_t)n_cu / std::max(1u, nf));
+          const int64_t rounds = (rblocks + slots - 1) / slots;
+          ncomp = (unsigned)std::min<int64_t>(rblocks, (rblocks + rounds - 1) / rounds);
+        }
         compress_f16_kernel<<<dim3(ncomp, nf), kBlock, 0, s>>>(cr, sc->PT16, sc->Fp16);
         gate_kernel<<<dim3(ngate, nf), kBlock, 0, s>>>(a);
         goto score;
