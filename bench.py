@@ -61,7 +61,59 @@ def parse():
                     help="configs[3] points-in pass: frames over all ranks (0: skip)")
     ap.add_argument("--host-point-frames", type=int, default=128,
                     help="frames of the H2D-inclusive points-in pass per rank (pinned host memory)")
+    ap.add_argument("--single-frames", type=int, default=40,
+                    help="per-callback latency pass: 1M-point host clouds through voxelize/extract/search "
+                         "one at a time (0: skip; N = 1 only)")
     return ap.parse_args()
+
+
+def launch_plan(gpus, env, n_devices, argv, port=None):
+    """What `python bench.py --gpus N` does before anything touches the GPU.
+
+    Returns ("inline", None) when this process runs the bench itself (N = 1, or it is
+    already one rank of a torch.distributed launch: WORLD_SIZE set), ("spawn", cmd) when it
+    must start N ranks as a child `torch.distributed.run` (the parent only waits and relays
+    the child's JSON line and exit code -- it never execs and never initialises HIP), and
+    ("error", message) when the request cannot be met (fewer visible devices than N: never
+    a silent one-rank run under an N-GPU label).  C3H_BENCH_REHEARSAL=1 allows N ranks on
+    fewer devices (all on device 0, collectives staged over gloo; not a measurement)."""
+    if gpus < 1:
+        return "error", "--gpus must be >= 1 (got %d)" % gpus
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            return "error", "launched with WORLD_SIZE=%d but --gpus %d" % (world, gpus)
+        return "inline", None
+    if gpus == 1:
+        return "inline", None
+    rehearsal = env.get("C3H_BENCH_REHEARSAL") == "1"
+    if n_devices < gpus and not rehearsal:
+        return "error", "--gpus %d requested but only %d HIP device(s) are visible" % (gpus, n_devices)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port or 29500),
+           str(ROOT / "bench.py")] + list(argv)
+    return "spawn", cmd
+
+
+def child_env(env):
+    out = dict(env)
+    out["C3H_BENCH_CHILD"] = "1"
+    out.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this pool's driver
+    return out
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _visible_devices():
+    """HIP devices visible to this process, counted without initialising HIP
+    (torch.cuda.device_count() does not create a device context on this image)."""
+    import torch
+    return torch.cuda.device_count()
 
 
 def algorithmic_bytes_c3(G, H, F):
@@ -124,6 +176,9 @@ class _StagedGloo:
     def barrier(self):
         self.d.barrier()
 
+    def get_world_size(self):
+        return self.d.get_world_size()
+
     def destroy_process_group(self):
         self.d.destroy_process_group()
 
@@ -135,6 +190,14 @@ def torch_mod():
 
 def main():
     args = parse()
+    n_dev = _visible_devices() if args.gpus > 1 and "WORLD_SIZE" not in os.environ else 0
+    action, what = launch_plan(args.gpus, os.environ, n_dev, sys.argv[1:], port=_free_port())
+    if action == "error":
+        print("bench.py: " + what, file=sys.stderr)
+        sys.exit(2)
+    if action == "spawn":  # child launcher; this process never touches the GPU
+        import subprocess
+        sys.exit(subprocess.run(what, env=child_env(os.environ)).returncode)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -152,6 +215,7 @@ def main():
             dist = _StagedGloo(dist)
         else:
             dist.init_process_group("nccl", device_id=dev)
+        assert dist.get_world_size() == args.gpus == world, (dist.get_world_size(), args.gpus, world)
 
     import c3hlac
     from c3hlac import synth
@@ -208,9 +272,13 @@ def main():
     done_first = max(0, args.warmup - (PIPE_DEPTH - 1))
     done_last = args.warmup + args.steps - (PIPE_DEPTH - 1)
     n_done = max(0, done_last - done_first)
+    gather_ev = None
     if dist:  # gather every rank's completed detections (one RCCL all_gather) inside the timed region
         from c3hlac.dist import gather_records
+        gather_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        gather_ev[0].record(stream)  # the library's stream = torch's current stream
         gather_records(dets[done_first * B:done_last * B], n_done * B * world, rank, world, dist)
+        gather_ev[1].record(stream)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -283,7 +351,18 @@ def main():
             "step": "one batch of %d frames = one pipeline tick (steady state: the warmup steps fill the "
                     "pipeline, it is drained after the timer)" % B,
             "frames_per_step": B, "frames_completed_timed": frames_done * world,
+            "frames_per_rank": frames_done,
             "schedule": "software pipeline, %d batches in flight per GPU" % PIPE_DEPTH,
+        },
+        "distributed": {
+            "world_size": dist.get_world_size() if dist else 1,
+            "backend": ("gloo (rehearsal: every rank on device 0, collectives staged through host memory; "
+                        "not a measurement)" if rehearsal else "nccl (RCCL)") if dist else None,
+            "launch": ("self-launched torch.distributed.run child" if os.environ.get("C3H_BENCH_CHILD") == "1"
+                       else "torch.distributed.run") if dist else "single process",
+            "gather_ms_rank0": gather_ev[0].elapsed_time(gather_ev[1]) if gather_ev else None,
+            "gather_note": "HIP events on the library's stream around the all_gather of the timed region's "
+                           "detection records (starts when the rank's last tick completes)",
         },
         "detections_per_s": P * M * frames_done * world / elapsed,
         "detections_per_s_search_kernels": (P * M * max(kt_all["score"][1], 1) / (search_ms / 1e3)) if search_ms else None,
@@ -324,6 +403,8 @@ def main():
                                           args.host_point_frames)
         if world == 1:
             result["points_in_real_views"] = real_views_pass(ctx, dev, torch, synth, c3hlac)
+    if world == 1 and args.single_frames > 0:
+        result["single_frame"] = single_frame_pass(local, torch, synth, c3hlac, rank, args.single_frames)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         f0 = args.warmup * B  # the first timed frame: the oracle re-computes it as it is timed
         rec0 = d[f0]
@@ -416,6 +497,64 @@ def points_pass(ctx, dev, rank, world, dist, torch, synth, c3hlac, n_total, n_ho
         res["h2d_note"] = "%d frames per GPU from pinned host memory (16 MB each), H2D inside the timed call" % len(hf)
         res["h2d_equals_device"] = bool(torch.equal(hout, out[:len(hf)]))
     return res
+
+
+def single_frame_pass(local, torch, synth, c3hlac, rank, n_frames, n_scenes=4):
+    """The drop-in per-callback latency (detect_object.cpp:139-186, queue 1): one 1M-point
+    host cloud at a time (pageable numpy memory, as fromROSMsg leaves it) through
+    c3h_voxelize -> c3h_extract -> c3h_search at configs[2]'s shape (256^3, C3-HLAC-117 S=10,
+    117 -> 100, 10 models x r = 20, box 2^3, rank 1), detections back on the host.  Its own
+    context on its own stream.  Two timed loops over the same frames:
+    - end_to_end: the three calls back to back, exactly what the callback does (the host
+      syncs are the API's own: voxelize returns the grid info, search the lists);
+    - phases: the same with a device sync after extract, so the wall clock splits as the
+      reference prints it (detect_object.cpp:182-186), plus the HIP-event kernel time of
+      each phase (voxelize = its kernels, not the H2D copy)."""
+    ctx = c3hlac.Context(local)
+    try:
+        scenes = [scene_points(synth, rank, s) for s in range(n_scenes)]
+        axis_t, var, axis_q = synth.random_bases(VARIANT, D, M, R, seed=synth.BASE_SEED)
+        ctx.search_setup(axis_t, var, axis_q)
+        ctx.set_rank(RANK)
+
+        def frame(i, sync_phases):
+            t0 = time.perf_counter()
+            ctx.voxelize(scenes[i % n_scenes], LEAF)
+            t1 = time.perf_counter()
+            ctx.extract(VARIANT, THR, SUBDIV)
+            if sync_phases:
+                ctx.synchronize()
+            t2 = time.perf_counter()
+            lists, _ = ctx.search(BOX, EXIST_THR)
+            t3 = time.perf_counter()
+            assert float(lists[0, 0]["score"]) > 0, "no detection"
+            return t1 - t0, t2 - t1, t3 - t2
+
+        for i in range(2 * n_scenes):  # untimed: buffers sized for the scenes
+            frame(i, False)
+        e2e = [sum(frame(i, False)) for i in range(n_frames)]
+        ctx.timing(c3hlac.timing_mask("voxelize", "c3hlac", "compress", "score", "replay"))
+        ctx.kernel_times(reset=True)
+        ph = np.array([frame(i, True) for i in range(n_frames)])
+        kt = ctx.kernel_times(reset=True)
+        ctx.timing(False)
+    finally:
+        ctx.close()
+    med = lambda a: float(np.median(a)) * 1e3  # noqa: E731
+    kms = lambda *names: sum(kt[n][0] for n in names) / n_frames  # noqa: E731
+    return {
+        "ms_per_frame_end_to_end": med(e2e),
+        "ms_per_frame_end_to_end_mean": float(np.mean(e2e)) * 1e3,
+        "frames_per_s": 1e3 / med(e2e),
+        "phases_ms_per_frame": {"voxelize": med(ph[:, 0]), "c3hlac": med(ph[:, 1]), "search": med(ph[:, 2])},
+        "kernel_ms_per_frame": {"voxelize": kms("voxelize"), "c3hlac": kms("c3hlac"),
+                                "search": kms("compress", "score", "replay")},
+        "frames": n_frames,
+        "note": "detect_object.cpp's per-callback path, one frame at a time: %d 1M-point host clouds (pageable, %d "
+                "distinct Kinect scenes) -> c3h_voxelize (H2D inside) -> c3h_extract -> c3h_search (lists to the "
+                "host); medians; compare cpu_baseline.phases_s_per_frame (same scene shape, one core)"
+                % (n_frames, n_scenes),
+    }
 
 
 def real_views_pass(ctx, dev, torch, synth, c3hlac, reps=10):

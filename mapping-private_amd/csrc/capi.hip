@@ -897,8 +897,13 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
     HIPCHK(hipMemcpyAsync(hc, ctx->vcnt.p, c3h::kVcWords * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     if (!(hc[c3h::kVcErr] & c3h::kVcErrFull) || (hc[c3h::kVcErr] & c3h::kVcErrRange)) break;
-    if (attempt >= 8 || ctx->vtsize >= ((uint64_t)1 << 28))
+    if (attempt >= 8 || ctx->vtsize >= ((uint64_t)1 << 28)) {
+      // the failed attempt's keys and sums are still in the tables: the next call must
+      // start from all-empty ones (re-allocation path: memsets, untracked grid)
+      ctx->vtsize = 0;
+      ctx->vgrid_tracked = false;
       return fail(ctx, C3H_ERR_NOMEM, "c3h_voxelize: internal: voxel table still full");
+    }
     ts_want = 2 * ctx->vtsize;  // the frame again, from all-empty tables twice the size
     ctx->vtsize = 0;
   }

@@ -231,6 +231,35 @@ def test_voxel_table_regrows(ctx):
         assert np.array_equal(ctx.downsampled().view(np.uint32), cl.view(np.uint32))
 
 
+def _assert_pick(m, got, sb, feats, scd, Ld, L32):
+    """The GPU's rank-1 position of model m against the oracles (search.cpp:464-474: the
+    strict '>' over the scan order (mode, z, y, x) keeps the first of equal scores).
+
+    Accepted when it is the float64 oracle's pick, or:
+    (a) both boxes hold bit-identical feature sums (exact tie: the GPU's direct box sums
+        give equal scores, so the strict '>' keeps the earlier scan position -- the GPU's
+        must come first; the oracle's float64 summed-volume table differences break such a
+        tie by rounding: config 3's model 7, (7, 12, 17) vs (7, 13, 17), 3.5e-16 apart, moved
+        with round 4's PCL-1.0 centroid semantics, which changed the oracle's rounding, not
+        the boxes: they are equal under both semantics); or
+    (b) it is the fp32-reference-order oracle's pick; or
+    (c) the two float64 scores differ by < 1e-5 relative (a tie within the stated tolerance)."""
+    best = Ld.records()[m][0]
+    if got == tuple(best[1:4]):
+        return
+    e = sb[0] - 1
+    pg = (got[2] * e + got[1]) * e + got[0]
+    pb = (best[3] * e + best[2]) * e + best[1]
+    gap = (scd[pb] - scd[pg]) / scd[pb]
+    F = feats.reshape(sb[2], sb[1], sb[0], -1).astype(np.float64)
+    box = lambda x, y, z: F[z:z + 2, y:y + 2, x:x + 2].sum(axis=(0, 1, 2))  # noqa: E731
+    exact_tie = np.array_equal(box(*got), box(*best[1:4]))
+    f32 = tuple(L32.records()[m][0][1:4]) if L32 is not None else None
+    ok = (exact_tie and pg < pb) or got == f32 or abs(gap) < 1e-5
+    assert ok, ("model %d: GPU %s, f64 oracle %s, fp32 oracle %s, f64 gap %.3g, exact tie %s"
+                % (m, got, tuple(best[1:4]), f32, gap, exact_tie))
+
+
 def test_config2_kinect_128(ctx):
     """Config 2: 1M-pt Kinect-style scene, 128^3, C3-HLAC-981 + 1-model search."""
     pts = synth.kinect_scene(1_000_000, grid=128, leaf=0.02, seed=synth.BASE_SEED)
@@ -260,12 +289,8 @@ def test_config2_kinect_128(ctx):
     ok = scd > 0
     np.testing.assert_allclose(sc[ok], scd[ok], rtol=SCORE_RTOL_F64)
     np.testing.assert_allclose(sc[ok], sc32[ok], rtol=SCORE_RTOL_F32)
-    best = Ld.records()[0][0]
     got = (int(lists[0, 0]["x"]), int(lists[0, 0]["y"]), int(lists[0, 0]["z"]))
-    if got != best[1:4]:  # only a tie within the fp32 tolerance may pick another position
-        e = sb[0] - 1
-        p = (got[2] * e + got[1]) * e + got[0]
-        assert scd[p] >= best[0] * (1 - 2 * SCORE_RTOL_F64), (got, best)
+    _assert_pick(0, got, sb, ff, scd, Ld, L32)
     _assert_replay_matches(ctx, (2, 2, 2), 1, lists)
 
 
@@ -296,14 +321,13 @@ def test_config3_kinect_256_ri117_multimodel(ctx):
     ok = scd > 0
     np.testing.assert_allclose(sc[ok], scd[ok], rtol=SCORE_RTOL_F64)
     _assert_replay_matches(ctx, (2, 2, 2), M, lists)
-    # same detections as the float64 oracle (top entry of every model), up to fp32 ties
-    e = sb[0] - 1
+    # same detections as the float64 oracle (top entry of every model); the one pick that
+    # differs is an exact tie (model 7, see _assert_pick)
+    L32, _, _ = po.search(sb, f, ex, synth.whiten(axis_t, var), axis_q, (2, 2, 2), M, 100, dbl=False)
     scm = scd.reshape(M, -1)
     for m in range(M):
         got = (int(lists[m, 0]["x"]), int(lists[m, 0]["y"]), int(lists[m, 0]["z"]))
-        best = Ld.records()[m][0]
-        if got != best[1:4]:
-            assert scm[m, (got[2] * e + got[1]) * e + got[0]] >= best[0] * (1 - 2 * SCORE_RTOL_F64), (m, got, best)
+        _assert_pick(m, got, sb, f, scm[m], Ld, L32)
 
 
 @pytest.mark.parametrize("ranges", [(1, 2, 1), (1, 2, 3), (2, 1, 1), (3, 3, 1)])
