@@ -95,6 +95,27 @@ def launch_plan(gpus, env, n_devices, argv, port=None):
     return "spawn", cmd
 
 
+def relay(cmd, env, out=None, err=None):
+    """Run the launcher child; its stdout lines that are the bench's JSON object go to our
+    stdout (exactly one line from rank 0), anything else the ranks or their libraries print
+    there (gloo's connection banner, ...) goes to stderr.  Returns the child's exit code."""
+    import subprocess
+    out = out or sys.stdout
+    err = err or sys.stderr
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in p.stdout:
+        s = line.strip()
+        is_result = False
+        if s.startswith("{"):
+            try:
+                is_result = "metric" in json.loads(s)
+            except ValueError:
+                pass
+        (out if is_result else err).write(line if line.endswith("\n") else line + "\n")
+        (out if is_result else err).flush()
+    return p.wait()
+
+
 def child_env(env):
     out = dict(env)
     out["C3H_BENCH_CHILD"] = "1"
@@ -196,8 +217,7 @@ def main():
         print("bench.py: " + what, file=sys.stderr)
         sys.exit(2)
     if action == "spawn":  # child launcher; this process never touches the GPU
-        import subprocess
-        sys.exit(subprocess.run(what, env=child_env(os.environ)).returncode)
+        sys.exit(relay(what, child_env(os.environ)))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

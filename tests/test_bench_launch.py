@@ -53,6 +53,17 @@ def test_child_env_marks_child_and_keeps_dmabuf_ipc():
     assert env["C3H_BENCH_CHILD"] == "1" and env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
 
 
+def test_relay_keeps_only_the_result_line_on_stdout():
+    import io
+    script = ("import json, sys; print('[Gloo] Rank 0 is connected to 1 peer ranks'); "
+              "print(json.dumps({'metric': 'm', 'value': 1.0})); print('{not json'); sys.exit(3)")
+    out, err = io.StringIO(), io.StringIO()
+    rc = bench.relay([sys.executable, "-c", script], None, out=out, err=err)
+    assert rc == 3
+    assert out.getvalue().splitlines() == ['{"metric": "m", "value": 1.0}']
+    assert "[Gloo]" in err.getvalue() and "{not json" in err.getvalue()
+
+
 def test_bench_exits_nonzero_without_devices():
     """This container has no HIP device: --gpus 2 must fail loudly, not run one rank."""
     env = {k: v for k, v in __import__("os").environ.items() if k not in ("WORLD_SIZE", "C3H_BENCH_REHEARSAL")}
