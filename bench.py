@@ -347,6 +347,11 @@ def main():
     # subdivisions only (an empty subdivision keeps exist 0 and every reader gates on it)
     # and exist, from the frames of the timed region (the context holds the last one)
     nonempty = int((ctx.exist() > 0).sum())
+    # positions of the last frame that passed the exist gate (scored; the rest are -1)
+    try:
+        scored = int((ctx.scores().reshape(M, -1)[0] >= 0).sum())
+    except (c3hlac.C3HError, ValueError):
+        scored = 0
     min_bytes = (GRID ** 3 * 4 + nonempty * VARIANT * 4 + H * 4) * B
     achieved_min = min_bytes / tick_avg_s / 1e9
     result = {
@@ -385,6 +390,10 @@ def main():
                            "detection records (starts when the rank's last tick completes)",
         },
         "detections_per_s": P * M * frames_done * world / elapsed,
+        "detections_note": "detections_per_s counts every box position x model (SURVEY 8(d)); only the positions "
+                           "passing the exist gate are scored: scored_detections_per_s (gate-passing positions of "
+                           "the last frame, %d of %d, x models x frames/s)" % (scored, P),
+        "scored_detections_per_s": (scored * M * frames_done * world / elapsed) if scored else None,
         "detections_per_s_search_kernels": (P * M * max(kt_all["score"][1], 1) / (search_ms / 1e3)) if search_ms else None,
         "frames_per_s": frames_done * world / elapsed,
         "kernel_ms_avg": {k: (v[0] / v[1] if v[1] else None) for k, v in kt_all.items()},

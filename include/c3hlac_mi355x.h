@@ -362,6 +362,13 @@ int c3h_remove_overlap(int32_t M, int32_t rank, const int32_t range[3], c3h_det*
  * searched modes. */
 int c3h_replay_scores(int32_t M, int32_t rank, const int32_t range[3], int32_t rotate, const int32_t subdiv_b[3],
                       const double* scores, c3h_det* lists);
+/* c3h_replay_scores that also records every row's entry floor: row_floor[(m * ze + z) * ye
+ * + y] (per searched mode, in the scores' mode order) = model m's rank-th score before the
+ * row's first position.  A position at or below it cannot change the lists (searchPart
+ * updates only above lists[rank-1], which never decreases), so the z-slab merge
+ * (c3hlac/dist.py) can leave such positions out and verify that it did so safely. */
+int c3h_replay_scores_floor(int32_t M, int32_t rank, const int32_t range[3], int32_t rotate,
+                            const int32_t subdiv_b[3], const double* scores, c3h_det* lists, double* row_floor);
 
 /* PCA::read (color_voxel_recognition/src/pca.cpp:119-185): axis column-major dim x dim
  * (eigenvector i contiguous), variances, optional mean.  Returns dim or an error.

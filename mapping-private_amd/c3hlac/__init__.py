@@ -447,15 +447,30 @@ def write_feature(path, feat, remove_zero=True, fields=None):
           None, "feature_write")
 
 
-def replay_scores(scores, subdiv_b, ranges, lists, rotate=True):
+def replay_scores(scores, subdiv_b, ranges, lists, rotate=True, floors=False):
     """c3h_replay_scores: searchPart's rank update over score arrays in c3h_get_scores'
-    layout (host function); lists: (M, rank) DET_DTYPE, continued from their state."""
+    layout (host function); lists: (M, rank) DET_DTYPE, continued from their state.
+    floors=True (c3h_replay_scores_floor): returns (lists, row floors), the floors per
+    searched mode as M x ze x ye doubles, concatenated in the scores' mode order."""
     lists = np.ascontiguousarray(lists, dtype=DET_DTYPE)
     M, rank = lists.shape
     sc = np.ascontiguousarray(scores, dtype=np.float64)
-    check(_capi.load().c3h_replay_scores(M, rank, i32x3(ranges), int(bool(rotate)), i32x3(subdiv_b), ptr(sc),
-                                         ptr(lists)), None, "replay_scores")
-    return lists
+    lib = _capi.load()
+    if not floors:
+        check(lib.c3h_replay_scores(M, rank, i32x3(ranges), int(bool(rotate)), i32x3(subdiv_b), ptr(sc),
+                                    ptr(lists)), None, "replay_scores")
+        return lists
+    from .dist import mode_schedule, mode_ranges
+    n = 0
+    for md in mode_schedule(ranges, rotate):
+        xr, yr, zr = mode_ranges(md, ranges)
+        xe, ye, ze = subdiv_b[0] - xr + 1, subdiv_b[1] - yr + 1, subdiv_b[2] - zr + 1
+        if xe > 0 and ye > 0 and ze > 0:
+            n += M * ze * ye
+    fl = np.zeros(max(n, 1), np.float64)
+    check(lib.c3h_replay_scores_floor(M, rank, i32x3(ranges), int(bool(rotate)), i32x3(subdiv_b), ptr(sc),
+                                      ptr(lists), ptr(fl)), None, "replay_scores_floor")
+    return lists, fl[:n]
 
 
 def remove_overlap(lists, ranges):

@@ -103,6 +103,8 @@ _SIGS = {
     "c3h_remove_overlap": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(C.c_int32), _P]),
     "c3h_replay_scores": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.c_int32, C.POINTER(C.c_int32),
                                     _P, _P]),
+    "c3h_replay_scores_floor": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.c_int32,
+                                          C.POINTER(C.c_int32), _P, _P, _P]),
     "c3h_pca_read": (C.c_int, [C.c_char_p, C.c_int32, _P, _P, _P, C.POINTER(C.c_int32), C.c_int32]),
     "c3h_allgather_detections": (C.c_int, [_P, _P, _P, C.c_int64, _P]),
     "c3h_compute_normals": (C.c_int, [_P, C.c_float, _P]),

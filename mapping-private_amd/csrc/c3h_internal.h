@@ -89,43 +89,46 @@ enum {
   kVcMin = 0,     // int32[3] min cell
   kVcMax = 3,     // int32[3] max cell
   kVcValid = 6,   // u64 valid points
-  kVcSlots = 8,   // [2] voxels listed by the frame of each epoch parity
+  kVcSlots = 8,   // [2] occupied voxels (owning entries) of the frame of each epoch parity
   kVcFlag = 10,   // voxels whose centroid may leave their cell
-  kVcErr = 11,    // kVcErrRange | kVcErrFull
+  kVcErr = 11,    // kVcErrRange | kVcErrWrap
   kVcOver = 12,   // grid buffer too small (scatter not run)
   kVcOff = 13,    // off-cell voxels recorded by the exact pass
   kVcWords = 16
 };
 constexpr uint32_t kVcErrRange = 1;  // cell coordinates beyond +-2^20
-constexpr uint32_t kVcErrFull = 2;   // the global table had no room (the frame runs again, table x2)
-// one voxel of the voxeliser's global hash table (32 B: one load / clear)
-struct VoxSlot {
-  unsigned long long key;  // absolute cell (21 bits per axis, biased), ~0 = empty
-  unsigned long long a;    // count << 40 | sum r
-  unsigned long long b;    // sum b << 32 | sum g
-  uint32_t margin;         // min distance (cells, float bits) of a member point to the cell boundary
-  uint32_t pos;            // position (accum block * 2048 + i) in the frame's slot list
-};
+constexpr uint32_t kVcErrWrap = 4;   // the frame's extent exceeds the toroidal accumulator (the
+                                     // frame runs again on larger dims; the scatter wrote nothing)
+// Single-frame voxeliser state.  The accumulators are toroidal: voxel (x, y, z) sums at
+// t = (x mod 2^tb0) | (y mod 2^tb1) << tb0 | (z mod 2^tb2) << (tb0 + tb1), so a frame whose
+// extent fits 2^tb per axis maps its voxels one-to-one without a hash table.  Every
+// (accumulate block, voxel) pair is one list entry; its sums go out as non-returning
+// atomics, and the entry with the min (margin << 32 | entry id) owns the voxel in the
+// scatter, which converts it and returns the accumulator to zero.
 struct VoxArgs {
   const float4* pts;
   int64_t n;
   float z_limit, inv, leaf;
-  VoxSlot* tab;             // this frame's hash table (the two tables alternate by parity)
-  VoxSlot* tab_prev;        // the previous frame's, cleared by this frame's accum launch
-  unsigned long long* keys;       // the tables' keys, apart from the sums (C3H_VOX_SOA)
-  unsigned long long* keys_prev;
-  uint64_t tmask;           // table size - 1 (power of two)
-  uint32_t* lists;          // [slots parity 0 | slots parity 1 | grid words parity 0 | parity 1] x lcap,
-  uint64_t lcap;            //   each a segment of 2048 per accum block
+  ulonglong2* acc;          // [2^(tb0+tb1+tb2)] {count << 40 | sum r, sum b << 32 | sum g}, 0 between frames
+  unsigned long long* mo;   // [same] min over the voxel's entries of (margin bits << 32 | entry id), ~0 between frames
+  uint32_t* tpos;           // [same] list position of the voxel's owning entry (written by the scatter)
+  int tb[3];
+  uint32_t* lists;          // [entries parity 0 | entries parity 1 | grid words parity 0 | parity 1] x lcap,
+  uint64_t lcap;            //   each a segment of vox_positions(1) per accum block
+  uint32_t* lcnt;           // [lcap] this frame's owning entries' point counts (0: not owning)
   int32_t* part;            // per parity, per accum block: bounds, counts (vox_part_words() ints)
   int nblk, nblk_prev, nblk_cap;  // accum blocks of this / the previous frame, capacity
   uint32_t* cnt;            // kVcWords counters (totals published by the scatter)
   uint32_t* grid;           // packed grid buffer (capacity grid_cap words)
   int64_t grid_cap;
   int par;                  // epoch parity of this frame
-  int clear_tables, clear_grid;  // clear what the previous frame listed
+  int clear_grid;           // clear the grid words the previous frame listed
 };
 hipError_t launch_voxelize(const VoxArgs& a, hipStream_t s);
+#ifdef C3H_DIAG
+hipError_t launch_vox_dirty(const ulonglong2* acc, const unsigned long long* mo, int64_t tor, uint32_t* out,
+                            hipStream_t s);
+#endif
 hipError_t launch_vox_scatter(const VoxArgs& a, hipStream_t s);
 int64_t vox_blocks(int64_t n);
 int64_t vox_positions(int64_t n);
@@ -191,10 +194,11 @@ struct VoxBatchArgs {
   int subdiv, off[3];
   float inv_s;
   ulonglong2* acc;                    // [frame][2^(tb0+tb1+tb2)] {count << 40 | sum r, sum b << 32 | sum g}
-  uint32_t* accM;                     //                min boundary margin (float bits), ~0 = none
+  unsigned long long* accMO;          //                min of (margin float bits << 32 | entry id) over
+                                      //                the voxel's (block, voxel) entries, ~0 = none
   int64_t s_acc;
   uint32_t* fcnt;                     // [kMaxBatch] finished accumulate blocks per frame (self-resetting)
-  uint32_t* vlist;                    // [block][chunk] accumulator entries first touched by the block
+  uint32_t* vlist;                    // [block][chunk] the block's (block, voxel) entries (toroidal index)
   uint32_t* wlist;                    // [block][chunk] canvas words the scatter wrote (this set)
   int32_t* part;                      // [block][kPartW] partial records (this set)
   uint32_t* grid[kMaxBatch];          // canvas grids of this set's frame slots (all slots)
@@ -489,14 +493,15 @@ struct c3h_ctx {
   c3h::DevBuf<int32_t> rsd_types, grsd_trans;
   c3h::DevBuf<float> grsd_feat, vosch_feat;
   int64_t rsd_n = 0;                // centroids with valid radii / types
-  // voxeliser state (voxelize.hip): global hash table, slot / grid-word lists by epoch
-  // parity, counters; what the previous frame listed is cleared by the next frame
-  c3h::DevBuf<c3h::VoxSlot> vtab[2];
-  c3h::DevBuf<unsigned long long> vkeys[2];
-  c3h::DevBuf<uint32_t> vlists, vcnt;
+  // voxeliser state (voxelize.hip): toroidal accumulators, entry / grid-word lists by
+  // epoch parity, counters; the grid words the previous frame wrote are cleared by the next
+  c3h::DevBuf<ulonglong2> vacc;
+  c3h::DevBuf<unsigned long long> vmo;
+  c3h::DevBuf<uint32_t> vtpos, vlists, vlcnt, vcnt;
   c3h::DevBuf<int32_t> vpart;
-  uint64_t vtsize = 0, vlcap = 0;
-  uint64_t vocc_hint = 0;  // voxels of the last frame: sizes the next frame's table
+  int vtb[3] = {7, 7, 7};           // toroidal dims (log2 per axis); they only grow
+  int64_t vtor = 0;                 // cells of the allocated accumulators (0: none)
+  uint64_t vlcap = 0;
   int vpar = 0, vblk_cap = 0;
   int vblk_prev = 0;                // accum blocks of the previous frame (its lists to clear)
   bool vgrid_tracked = false;       // grid buffer is zero outside the previous frame's list
@@ -639,7 +644,8 @@ struct c3h_ctx {
   int pb_prev_nf = 0, pb_prev_total = 0;
   std::vector<int> pb_prev_blk0;
   c3h::DevBuf<ulonglong2> pb_acc;
-  c3h::DevBuf<uint32_t> pb_accM, pb_vlist, pb_fcnt;
+  c3h::DevBuf<unsigned long long> pb_accMO;
+  c3h::DevBuf<uint32_t> pb_vlist, pb_fcnt;
   int64_t pb_acc_vox = 0;
   int pb_acc_slots = 0;
   c3h::DevBuf<float> pb_stage;

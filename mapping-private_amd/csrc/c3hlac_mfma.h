@@ -81,9 +81,17 @@ __host__ __device__ inline int mf_wave_stride(int pb) { return kMfSlots * mf_slo
 __host__ __device__ inline int mf_const_bytes(int pb) { return mf_r256(128 + 3 * pb); }
 // 3 x 256 channel-byte tables | 128 B | 3 constant planes (0x00, 0x01, 0xff) | per-wave
 // regions: 3 layer slots of 12 planes, the centre mask
+// 981 epilogue (round 5): every accumulator value is staged in the wave's idle plane
+// slots at (k, row c, column n) -- stage index k * 144 + ((c >> 2) * 12 + n) * 4 + (c & 3),
+// the 12 zero-order sums at 14 * 144 + c -- and the row is gathered bin by bin through a
+// per-workgroup source table (981 u16 after the wave regions)
+constexpr int kMfStage = 14 * 144 + 12;  // floats per wave
+constexpr int kMfSrcBytes = 2048;
+static_assert(kMfSlots == 3, "the 981 staging needs the three layer slots (>= 10,752 bytes)");
 __host__ __device__ inline size_t mf_lds_bytes(int pb) {
-  return 3072 + (size_t)mf_const_bytes(pb) + (size_t)kMfWaves * mf_wave_stride(pb);
+  return 3072 + (size_t)mf_const_bytes(pb) + (size_t)kMfWaves * mf_wave_stride(pb) + kMfSrcBytes;
 }
+static_assert(4 * kMfStage <= 3 * 3584, "stage fits the layer slots of the smallest plane (288 B)");
 
 // channel plane of (type t: 0 colour LUT / 1 binary, reference channel c in 0..5): the
 // planes hold per colour col the bytes {sin, cos, beta, 1 - beta} (4 col + s)
@@ -236,6 +244,76 @@ struct MfRow2 {
 #ifndef C3H_MF_PREFETCH
 #define C3H_MF_PREFETCH 1  // two-step layers: each plane row's reads issued one row ahead
 #endif
+#ifndef C3H_MF_ASHIFT
+#define C3H_MF_ASHIFT 1  // two-step layers: the dx shifts on the centre operand (round 5)
+#endif
+
+// Two-step layers with the x shifts moved to the centre operand (round 5).  An offset
+// (dx, R) pairs the centre at position v with the neighbour at v + dx + R; written over
+// K = v + dx, that is A_s[K] = Xm(K + s) with s = -dx against the UNSHIFTED neighbour row
+// B[K] = Y(K + R).  The three dx of a row then share one B fragment, and only the masked
+// centre row is shifted: per K step two 4-dword v_alignbyte sets (A_{+1}, A_{-1}) instead
+// of two per neighbour row, and the centre mask is applied once, to the 10 dwords a lane
+// group's positions and their +-1 bytes span (mk: the tile's mask words, once per tile).
+// Each A_s still visits every centre exactly once: centres lie at K positions 1 ..
+// (ly - 1) PW + lx <= 118 of 0 .. 127, so A_{+1} (positions 1 .. 128) and A_{-1} (-1 ..
+// 126) cover them, and the positions a shift moves in or out (-1, 0, 127, 128) are
+// never centres: every A_s has the same row sums (the epilogue's rs) and
+// sum (A'+128)(B'+128) over K is the exact sum over centres, whatever B holds elsewhere.
+template <int R>
+__device__ __forceinline__ void mf_layer_ksteps2s(const uint8_t* pp, const uint8_t* pc, const uint32_t (&mk)[10],
+                                                  int pw16, int h4, mf_v4i (&acc)[kMfK]) {
+  const int o = 32 * h4;
+  MfRow2<0, -1, 1> c0;   // dz = 0, dy = 0: bytes -16 .. +48 around the lane group's 32
+  MfRow2<-R, 0, 0> cm;   // dz = 0, dy = -1 (k = 9 + dx + 1)
+  c0.issue(pc + o);
+  cm.issue(pc + o - pw16);
+  c0.pin();
+  // masked centre words am[j] = bytes 32 h + 4 (j - 1) .. + 3 (c0.w index j + 3: B0 = -1)
+  uint32_t am[10];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) am[j] = (c0.w[j + 3] & mk[j]) | (0x80808080u & ~mk[j]);
+  mf_v4i A[3][2];  // [s + 1][ks]: A_s of K step ks
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = 4 * ks + i + 1;
+      A[1][ks][i] = (int)am[j];
+      A[2][ks][i] = (int)__builtin_amdgcn_alignbyte(am[j + 1], am[j], 1);  // s = +1
+      A[0][ks][i] = (int)__builtin_amdgcn_alignbyte(am[j], am[j - 1], 3);  // s = -1
+    }
+  // offset k of a row with dx = -1, 0, +1 uses A_{+1}, A_0, A_{-1}
+#define C3H_MF3(BF, K0, KS)                                                                              \
+  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) {                                                     \
+    const mf_v4i b = ks ? BF.template frag<0, 1>() : BF.template frag<0, 0>();                          \
+    acc[K0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[2][ks], b, acc[K0], 0, 0, 0);                     \
+    acc[K0 + KS] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1][ks], b, acc[K0 + KS], 0, 0, 0);          \
+    acc[K0 + 2 * KS] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0][ks], b, acc[K0 + 2 * KS], 0, 0, 0);  \
+  }
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    acc[13] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1][ks], A[1][ks], acc[13], 0, 0, 0);  // own channels
+    // (-1, 0, 0): the unshifted dz = 0 row against A_{+1}
+    acc[12] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[2][ks], ks ? c0.template frag<0, 1>() : c0.template frag<0, 0>(),
+                                                   acc[12], 0, 0, 0);
+  }
+  MfRow2<-R, 0, 0> rm;  // dz = -1, dy = -1: k = 3 (dx + 1)
+  rm.issue(pp + o - pw16);
+  cm.pin();
+  C3H_MF3(cm, 9, 1)
+  MfRow2<0, 0, 0> r0;  // dz = -1, dy = 0: k = 3 (dx + 1) + 1
+  r0.issue(pp + o);
+  rm.pin();
+  C3H_MF3(rm, 0, 3)
+  MfRow2<R, 0, 0> rp;  // dz = -1, dy = +1: k = 3 (dx + 1) + 2
+  rp.issue(pp + o + pw16);
+  r0.pin();
+  C3H_MF3(r0, 1, 3)
+  rp.pin();
+  C3H_MF3(rp, 2, 3)
+#undef C3H_MF3
+}
 template <int R>
 __device__ __forceinline__ void mf_layer_ksteps2(const uint8_t* pp, const uint8_t* pc, const mf_u4 (&mk)[2],
                                                  int pw16, int h4, mf_v4i (&acc)[kMfK]) {
@@ -456,6 +534,26 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
   for (int i = threadIdx.x; i < 3 * PBM / 4; i += kBlock)
     reinterpret_cast<uint32_t*>(cplanes)[i] = i < PBM / 4 ? 0u : (i < 2 * PBM / 4 ? 0x01010101u : 0xffffffffu);
   uint8_t* wl = reinterpret_cast<uint8_t*>(smem + 768) + mf_const_bytes(PBM) + (size_t)wave * mf_wave_stride(PBM);
+  uint16_t* s_src = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(smem + 768) + mf_const_bytes(PBM) +
+                                                (size_t)kMfWaves * mf_wave_stride(PBM));
+  const bool staged = !a.atomic && a.variant == 981;
+  if (staged) {  // bin -> stage index (c3h bin_of's inverse; every bin written once)
+    auto sidx = [](int k, int c, int n) { return k * 144 + ((c >> 2) * 12 + n) * 4 + (c & 3); };
+    for (int e = threadIdx.x; e < 14 * 2 * 36; e += kBlock) {
+      const int k = e / 72, t = (e / 36) & 1, cc = (e / 6) % 6, nn = e % 6;
+      const int c = mf_plane(t, cc), n = mf_plane(t, nn);
+      if (k < 13) {
+        s_src[495 * t + bin981(k, cc, nn)] = (uint16_t)sidx(k, c, n);
+      } else {
+        const int b = bin_of(t, 13, nn, cc);
+        if (b >= 0) s_src[b] = (uint16_t)sidx(13, c, n);
+      }
+    }
+    for (int e = threadIdx.x; e < 12; e += kBlock) {
+      const int t = e / 6, cc = e % 6;
+      s_src[495 * t + cc] = (uint16_t)(14 * 144 + mf_plane(t, cc));
+    }
+  }
   __syncthreads();
   const int nwork = (int)ftf[2 + (a.epoch & 1)];
   if (2 * nwork < a.ntiles) return;  // sparse frame: the dot4 tile body takes it
@@ -490,12 +588,13 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
     if (!C3H_MF_SHAPE_CACHE || shape != shape_prev) {
       shape_prev = shape;
       // centre mask of the K positions PW + 4 j + b: rows 1..ly, columns 1..lx
-      for (int j = lane; j < 16 * nks; j += 64) {
+      // (one word more on each side: the shifted centre rows of mf_layer_ksteps2s read them)
+      for (int j = lane - 1; j < 16 * nks + 1; j += 64) {
         uint32_t m = 0;
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
           const int p = PW + 4 * j + b, row = p / PW, col = p - row * PW;
-          m |= (row <= ly && col >= 1 && col <= lx ? 0xffu : 0u) << (8 * b);
+          m |= (row >= 1 && row <= ly && col >= 1 && col <= lx ? 0xffu : 0u) << (8 * b);
         }
         *reinterpret_cast<uint32_t*>(mask + off0 + PW + 4 * j) = m;
       }
@@ -545,11 +644,16 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
     };
     // 12 channel planes of layer L: per voxel and colour one table read gives the 4 channel
     // bytes, a 4 x 4 byte transpose packs them per channel (4 voxels per dword)
-    auto store_layer = [&](int L, const uint32_t (&w)[LOAD][4]) {
+    // PBC: the plane stride as a compile-time constant (two-step tiles: 288 bytes, planes
+    // 4..11 16 bytes further), so the 12 plane stores take immediate offsets; 0 = runtime
+    auto store_layer_t = [&](int L, const uint32_t (&w)[LOAD][4], auto pbc) {
 #if C3H_MF_EXP & 2
       return;
 #endif
-      uint8_t* slot = wl + (L % kMfSlots) * SS;
+      constexpr int PBC = decltype(pbc)::value;
+      const int PBv = PBC ? PBC : PB, gapv = PBC ? C3H_MF_GAP : gap;
+      const int SSv = PBC ? mf_slot_stride(PBC) : SS;
+      uint8_t* slot = wl + (L % kMfSlots) * SSv;
 #pragma unroll
       for (int i = 0; i < LOAD; ++i) {
         if (it_dst[i] < 0) continue;
@@ -570,9 +674,13 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
           const uint32_t o[4] = {__builtin_amdgcn_perm(u2, u0, 0x05040100u), __builtin_amdgcn_perm(u2, u0, 0x07060302u),
                                  __builtin_amdgcn_perm(u3, u1, 0x05040100u), __builtin_amdgcn_perm(u3, u1, 0x07060302u)};
 #pragma unroll
-          for (int s2 = 0; s2 < 4; ++s2) *reinterpret_cast<uint32_t*>(dst + (4 * col + s2) * PB + (col ? gap : 0)) = o[s2];
+          for (int s2 = 0; s2 < 4; ++s2) *reinterpret_cast<uint32_t*>(dst + (4 * col + s2) * PBv + (col ? gapv : 0)) = o[s2];
         }
       }
+    };
+    auto store_layer = [&](int L, const uint32_t (&w)[LOAD][4]) {
+      if (two && PB == 288) store_layer_t(L, w, std::integral_constant<int, 288>{});
+      else store_layer_t(L, w, std::integral_constant<int, 0>{});
     };
     mf_v4i acc[kMfK];
 #pragma unroll
@@ -590,10 +698,16 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
     const uint8_t* pmask = realk ? mask + korg : cplanes + 2 * PBM + korg;
     const int pw16 = PW & ~15;
     mf_u4 mk2[2] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};  // two-step layers: the mask, once per tile
+    uint32_t mk10[10];  // C3H_MF_ASHIFT: the mask words of bytes 32 h - 4 .. 32 h + 36
     if (nks == 2) {
       mf_compiler_fence();  // the mask plane was written above by this wave
-      mk2[0] = *reinterpret_cast<const mf_u4*>(__builtin_assume_aligned(pmask + 32 * h4k, 16));
-      mk2[1] = *reinterpret_cast<const mf_u4*>(__builtin_assume_aligned(pmask + 32 * h4k + 16, 16));
+      if (C3H_MF_ASHIFT) {
+#pragma unroll
+        for (int j = 0; j < 10; ++j) mk10[j] = *reinterpret_cast<const uint32_t*>(pmask + 32 * h4k + 4 * (j - 1));
+      } else {
+        mk2[0] = *reinterpret_cast<const mf_u4*>(__builtin_assume_aligned(pmask + 32 * h4k, 16));
+        mk2[1] = *reinterpret_cast<const mf_u4*>(__builtin_assume_aligned(pmask + 32 * h4k + 16, 16));
+      }
     }
     for (int z = 0; z < lz; ++z) {
       mf_compiler_fence();  // same-wave LDS accesses complete in order; keep the compiler's too
@@ -602,7 +716,8 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
       const uint8_t* pc = realk ? wl + (((z + 1) % kMfSlots) * SS + pn) : cpad;  // dz = 0
 #if !(C3H_MF_EXP & 1)
       if (two) {  // S <= 10 tiles: pitch 12
-        if (C3H_MF_U32) mf_layer_ksteps2u<12>(pp, pc, mk2, pw16, h4k, acc);
+        if (C3H_MF_ASHIFT) mf_layer_ksteps2s<12>(pp, pc, mk10, pw16, h4k, acc);
+        else if (C3H_MF_U32) mf_layer_ksteps2u<12>(pp, pc, mk2, pw16, h4k, acc);
         else mf_layer_ksteps2<12>(pp, pc, mk2, pw16, h4k, acc);
       } else {
         switch (PW & 15) {
@@ -649,7 +764,48 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
       continue;
     }
 #endif
-    if (a.atomic || F == 981) {
+    if (staged) {
+      // every value once, no per-bin branches: v = C + 128 (rs + cs) + 128^2 pos, times the
+      // bin's normalisation (same-type products: type 0 -> kNorm1, type 1 -> 1; the
+      // zero-order sums: kNorm0 / 1), as a float4 per lane and k; then the row is gathered
+      float* sf = reinterpret_cast<float*>(wl);
+      mf_compiler_fence();
+      const bool slot = real && h4 < 3;
+      float* sl = sf + (h4 * 12 + n) * 4;
+      uint32_t base[4];
+      float nrm[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        base[r] = 128u * rs[r] + k2;
+        nrm[r] = mf_type(4 * h4 + r) ? 1.0f : kNorm1;
+      }
+#pragma unroll
+      for (int k = 0; k < kMfK; ++k) {
+        const uint32_t cs = 128u * (uint32_t)__shfl(acc[k][3], 48 + n, 64);
+        if (slot) {
+          float4 v;
+          v.x = (float)((uint32_t)acc[k][0] + base[0] + cs) * nrm[0];
+          v.y = (float)((uint32_t)acc[k][1] + base[1] + cs) * nrm[1];
+          v.z = (float)((uint32_t)acc[k][2] + base[2] + cs) * nrm[2];
+          v.w = (float)((uint32_t)acc[k][3] + base[3] + cs) * nrm[3];
+          *reinterpret_cast<float4*>(sl + 144 * k) = v;
+        }
+      }
+      if (n == 15 && h4 < 3) {  // zero order: the channel sums rs + 128 pos
+        float4 v;
+        v.x = (float)(rs[0] + 128u * pos) * (mf_type(4 * h4) ? 1.0f : kNorm0);
+        v.y = (float)(rs[1] + 128u * pos) * (mf_type(4 * h4 + 1) ? 1.0f : kNorm0);
+        v.z = (float)(rs[2] + 128u * pos) * (mf_type(4 * h4 + 2) ? 1.0f : kNorm0);
+        v.w = (float)(rs[3] + 128u * pos) * (mf_type(4 * h4 + 3) ? 1.0f : kNorm0);
+        *reinterpret_cast<float4*>(sf + 14 * 144 + 4 * h4) = v;
+      }
+      __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's values are in LDS
+      __builtin_amdgcn_wave_barrier();
+      float* out = ffeat + h * F;
+#pragma unroll 4
+      for (int i = lane; i < 981; i += 64) out[i] = sf[s_src[i]];
+      mf_compiler_fence();  // the next tile's planes overwrite sf after these reads
+    } else if (a.atomic || F == 981) {
       float* out = ffeat + h * F;
       unsigned long long* hacc = a.atomic ? facc + h * 981 : nullptr;
       // 981 rows are staged in the wave's (now idle) plane slots and stored coalesced: a

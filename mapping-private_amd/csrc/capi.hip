@@ -698,10 +698,10 @@ void c3h_destroy(c3h_ctx* ctx) {
   release(ctx->grsd_trans);
   release(ctx->grsd_feat);
   release(ctx->vosch_feat);
-  release(ctx->vtab[0]);
-  release(ctx->vtab[1]);
-  release(ctx->vkeys[0]);
-  release(ctx->vkeys[1]);
+  release(ctx->vacc);
+  release(ctx->vmo);
+  release(ctx->vtpos);
+  release(ctx->vlcnt);
   release(ctx->vlists);
   release(ctx->vcnt);
   release(ctx->vpart);
@@ -748,7 +748,7 @@ void c3h_destroy(c3h_ctx* ctx) {
   release(ctx->pb_xcnt);
   release(ctx->pb_moved);
   release(ctx->pb_acc);
-  release(ctx->pb_accM);
+  release(ctx->pb_accMO);
   release(ctx->pb_fcnt);
   release(ctx->pb_vlist);
   release(ctx->pb_stage);
@@ -818,45 +818,33 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
       d_pts = reinterpret_cast<const float4*>(ctx->pts.p);
     }
   }
-  // the global table: 2x the points (load <= 1/2).  C3H_VOX_ADAPTIVE=1 sizes it at ~4x the
-  // voxels expected instead (the last frame's count; 256k slots for a 1M-point Kinect frame
-  // of 58k voxels instead of 2M): measured 2 us slower per frame (profiles/r4/vox_ab/) --
-  // the flush's device-scope atomics serialise per cache line, and a denser table puts more
-  // voxels on each line.  A frame that fills the table (kGProbe probes without room) runs
-  // again on a table twice the size; the table only grows.  Slot lists and partial
-  // records: one segment of the block's points per block
+  // toroidal accumulators: 2^vtb cells per axis (they only grow: a frame whose extent
+  // exceeds them runs again on dims that fit it, from all-zero accumulators); entry lists
+  // and partial records: one segment of the block's points per block
   uint64_t pcap = 512;
   while (pcap < (uint64_t)n) pcap <<= 1;
-#ifndef C3H_VOX_ADAPTIVE
-#define C3H_VOX_ADAPTIVE 0  // diagnostics: 1 = the table at ~4x the expected voxels
-#endif
-  const uint64_t hint = C3H_VOX_ADAPTIVE ? (ctx->vocc_hint ? ctx->vocc_hint : (uint64_t)n / 4) : 2 * pcap;
-  uint64_t ts_want = 4096;
-  while (ts_want < 4 * hint && ts_want < 2 * pcap) ts_want <<= 1;
   const int nblk = (int)c3h::vox_blocks(n);
   c3h::VoxArgs a{};
   uint32_t* hc = ctx->h_small;
   for (int attempt = 0;; ++attempt) {
-    if (ctx->vtsize < ts_want || !ctx->vcnt.p || ctx->vblk_cap < nblk) {  // (re)allocation: all-empty state
-      const uint64_t ts = std::max<uint64_t>(ts_want, ctx->vtsize);
-      ctx->vtsize = 0;
-      const int bcap = (int)std::max<int64_t>(c3h::vox_blocks((int64_t)pcap), ctx->vblk_cap);
-      ENSURE(ctx->vtab[0], ts);
-      ENSURE(ctx->vtab[1], ts);
-      ENSURE(ctx->vkeys[0], ts);
-      ENSURE(ctx->vkeys[1], ts);
-      ENSURE(ctx->vlists, 4 * (size_t)bcap * c3h::vox_positions(1));
-      ENSURE(ctx->vpart, 2 * (size_t)bcap * c3h::vox_part_words());
+    const int64_t tor = (int64_t)1 << (ctx->vtb[0] + ctx->vtb[1] + ctx->vtb[2]);
+    if (ctx->vtor != tor || !ctx->vcnt.p) {  // (re)allocation: all-zero accumulators
+      ctx->vtor = 0;
+      ENSURE(ctx->vacc, (size_t)tor);
+      ENSURE(ctx->vmo, (size_t)tor);
+      ENSURE(ctx->vtpos, (size_t)tor);
       ENSURE(ctx->vcnt, c3h::kVcWords);
-      HIPCHK(hipMemsetAsync(ctx->vpart.p, 0, ctx->vpart.n * 4, ctx->stream));
-      for (int t = 0; t < 2; ++t) {  // empty slots: key ~0, sums 0, margin ~0
-        HIPCHK(hipMemset2DAsync(&ctx->vtab[t].p[0].key, sizeof(c3h::VoxSlot), 0xff, 8, ts, ctx->stream));
-        HIPCHK(hipMemsetAsync(ctx->vkeys[t].p, 0xff, ts * 8, ctx->stream));
-        HIPCHK(hipMemset2DAsync(&ctx->vtab[t].p[0].a, sizeof(c3h::VoxSlot), 0, 16, ts, ctx->stream));
-        HIPCHK(hipMemset2DAsync(&ctx->vtab[t].p[0].margin, sizeof(c3h::VoxSlot), 0xff, 8, ts, ctx->stream));
-      }
+      HIPCHK(hipMemsetAsync(ctx->vacc.p, 0, (size_t)tor * 16, ctx->stream));
+      HIPCHK(hipMemsetAsync(ctx->vmo.p, 0xff, (size_t)tor * 8, ctx->stream));
       HIPCHK(hipMemsetAsync(ctx->vcnt.p, 0, c3h::kVcWords * 4, ctx->stream));
-      ctx->vtsize = ts;
+      ctx->vtor = tor;
+    }
+    if (ctx->vblk_cap < nblk || !ctx->vlists.p) {  // lists: the previous frame's grid words are lost
+      const int bcap = (int)std::max<int64_t>(c3h::vox_blocks((int64_t)pcap), ctx->vblk_cap);
+      ENSURE(ctx->vlists, 4 * (size_t)bcap * c3h::vox_positions(1));
+      ENSURE(ctx->vlcnt, (size_t)bcap * c3h::vox_positions(1));
+      ENSURE(ctx->vpart, 2 * (size_t)bcap * c3h::vox_part_words());
+      HIPCHK(hipMemsetAsync(ctx->vpart.p, 0, ctx->vpart.n * 4, ctx->stream));
       ctx->vlcap = (uint64_t)bcap * (uint64_t)c3h::vox_positions(1);
       ctx->vblk_cap = bcap;
       ctx->vblk_prev = 0;
@@ -873,13 +861,13 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
     a.z_limit = z_limit;
     a.inv = gi.inv_leaf;
     a.leaf = leaf;
-    a.tab = ctx->vtab[ctx->vpar].p;
-    a.tab_prev = ctx->vtab[ctx->vpar ^ 1].p;
-    a.keys = ctx->vkeys[ctx->vpar].p;
-    a.keys_prev = ctx->vkeys[ctx->vpar ^ 1].p;
-    a.tmask = ctx->vtsize - 1;
+    a.acc = ctx->vacc.p;
+    a.mo = ctx->vmo.p;
+    a.tpos = ctx->vtpos.p;
+    for (int ax = 0; ax < 3; ++ax) a.tb[ax] = ctx->vtb[ax];
     a.lists = ctx->vlists.p;
     a.lcap = ctx->vlcap;
+    a.lcnt = ctx->vlcnt.p;
     a.part = ctx->vpart.p;
     a.nblk = nblk;
     a.nblk_prev = ctx->vblk_prev;
@@ -888,7 +876,6 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
     a.grid = ctx->grid.p;
     a.grid_cap = (int64_t)ctx->grid.n;
     a.par = ctx->vpar;
-    a.clear_tables = 1;
     a.clear_grid = clear_grid ? 1 : 0;
     {
       Timed t(ctx, 0);
@@ -896,18 +883,27 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
     }
     HIPCHK(hipMemcpyAsync(hc, ctx->vcnt.p, c3h::kVcWords * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    if (!(hc[c3h::kVcErr] & c3h::kVcErrFull) || (hc[c3h::kVcErr] & c3h::kVcErrRange)) break;
-    if (attempt >= 8 || ctx->vtsize >= ((uint64_t)1 << 28)) {
-      // the failed attempt's keys and sums are still in the tables: the next call must
-      // start from all-empty ones (re-allocation path: memsets, untracked grid)
-      ctx->vtsize = 0;
-      ctx->vgrid_tracked = false;
-      return fail(ctx, C3H_ERR_NOMEM, "c3h_voxelize: internal: voxel table still full");
+    // the previous frame's words are cleared now (its list is spent): nothing is tracked
+    // until this frame's scatter has written its own list
+    ctx->vblk_prev = 0;
+    if (!(hc[c3h::kVcErr] & c3h::kVcErrWrap) || (hc[c3h::kVcErr] & c3h::kVcErrRange)) break;
+    // the extent exceeds the toroidal dims: dims that fit it, all-zero accumulators (the
+    // wrapped sums are discarded with the old buffers), and the frame again
+    int tb[3], sum = 0;
+    for (int ax = 0; ax < 3; ++ax) {
+      const int64_t dv = (int64_t)(int32_t)hc[c3h::kVcMax + ax] - (int32_t)hc[c3h::kVcMin + ax] + 1;
+      tb[ax] = ctx->vtb[ax];
+      while (((int64_t)1 << tb[ax]) < dv) ++tb[ax];
+      sum += tb[ax];
     }
-    ts_want = 2 * ctx->vtsize;  // the frame again, from all-empty tables twice the size
-    ctx->vtsize = 0;
+    if (attempt >= 2 || sum > 31) {
+      ctx->vtor = 0;  // the next call starts from fresh accumulators
+      return fail(ctx, C3H_ERR_RANGE, "c3h_voxelize: frame extent beyond 2^31 voxels of accumulators");
+    }
+    for (int ax = 0; ax < 3; ++ax) ctx->vtb[ax] = tb[ax];
+    ctx->vgrid_tracked = true;  // the grid holds no word of this frame (its scatter wrote none)
   }
-  // from here the tables hold this frame's entries (listed under parity a.par)
+  // from here the lists hold this frame's entries (parity a.par)
   ctx->vpar ^= 1;
   ctx->vblk_prev = nblk;
   if (hc[c3h::kVcErr] & c3h::kVcErrRange) {
@@ -952,7 +948,6 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
   ctx->vgrid_tracked = true;
   ctx->vargs = a;
   ctx->vns = hc[c3h::kVcSlots + a.par];
-  ctx->vocc_hint = ctx->vns;
   gi.n_occ = ctx->vns;
   ctx->info = gi;
   ctx->grid_ptr = ctx->grid.p;
@@ -965,6 +960,20 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
   if (info) *info = gi;
   return C3H_OK;
 }
+
+#ifdef C3H_DIAG
+// diagnostics builds only (not in the C-ABI header): accumulator cells left dirty
+int c3h_diag_vox_dirty(c3h_ctx* ctx, uint32_t* out257) {
+  if (!ctx || !out257 || !ctx->vtor) return C3H_ERR_ARG;
+  HIPCHK(hipSetDevice(ctx->device));
+  ENSURE(ctx->scratch, 257);
+  HIPCHK(hipMemsetAsync(ctx->scratch.p, 0, 257 * 4, ctx->stream));
+  HIPCHK(c3h::launch_vox_dirty(ctx->vacc.p, ctx->vmo.p, ctx->vtor, ctx->scratch.p, ctx->stream));
+  HIPCHK(hipMemcpyAsync(out257, ctx->scratch.p, 257 * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return C3H_OK;
+}
+#endif
 
 int c3h_get_grid_info(c3h_ctx* ctx, c3h_grid_info* info) {
   if (!ctx || !info) return C3H_ERR_ARG;
@@ -2398,7 +2407,7 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
   std::vector<c3h_frame_info> fi((size_t)nframes);
   std::vector<char> redo((size_t)nframes, 1);
   int nm = 0;
-  bool exact_any = false, exact_used = false;  // the batches ran the exact pass + fixup
+  std::vector<char> exact_ran((size_t)nframes, 0);  // per frame: its batch ran the exact pass + fixup
   // canvas subdivisions: a frame with one subdivision where the canvas has several takes the
   // single-frame path (computeC3HLAC's hist_num == 1 rule puts every voxel in histogram 0)
   bool canvas_multi = false;
@@ -2431,10 +2440,10 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
     if (tvox > ((int64_t)1 << 31)) return fail(ctx, C3H_ERR_RANGE, "c3h_run_point_frames: canvas too large");
     if (ctx->pb_acc_vox != tvox || ctx->pb_acc_slots < B) {
       ENSURE(ctx->pb_acc, (size_t)B * tvox);
-      ENSURE(ctx->pb_accM, (size_t)B * tvox);
+      ENSURE(ctx->pb_accMO, (size_t)B * tvox);
       ENSURE(ctx->pb_fcnt, (size_t)c3h::kMaxBatch);
       HIPCHK(hipMemsetAsync(ctx->pb_acc.p, 0, (size_t)B * tvox * 16, ctx->stream));
-      HIPCHK(hipMemsetAsync(ctx->pb_accM.p, 0xff, (size_t)B * tvox * 4, ctx->stream));
+      HIPCHK(hipMemsetAsync(ctx->pb_accMO.p, 0xff, (size_t)B * tvox * 8, ctx->stream));
       HIPCHK(hipMemsetAsync(ctx->pb_fcnt.p, 0, (size_t)c3h::kMaxBatch * 4, ctx->stream));
       ctx->pb_acc_vox = tvox;
       ctx->pb_acc_slots = B;
@@ -2541,7 +2550,7 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
       va.inv_s = p->subdiv > 0 ? (float)(1.0 / p->subdiv) : 0.0f;
       for (int a = 0; a < 3; ++a) va.tb[a] = tb[a];
       va.acc = ctx->pb_acc.p;
-      va.accM = ctx->pb_accM.p;
+      va.accMO = ctx->pb_accMO.p;
       va.s_acc = tvox;
       va.fcnt = ctx->pb_fcnt.p;
       va.vlist = ctx->pb_vlist.p;
@@ -2618,7 +2627,7 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
         fx.epoch = cl.epoch;
         fresh.fix = true;
       }
-      exact_any = exact_any || exact;
+      if (exact) std::fill(exact_ran.begin() + f0, exact_ran.begin() + f0 + nb, (char)1);
       // tables / stamp resets the capture enqueued precede the stamps (first batches only)
       if (va.stamp && vs != ctx->stream && c->cap_h2d != h2d0) {
         HIPCHK(hipEventRecord(ctx->pb_vox_ev, ctx->stream));
@@ -2651,7 +2660,6 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
       return rc;
     }
     std::vector<c3h::VoxFrameRec> recs((size_t)nframes);
-    exact_used = exact_any;
     HIPCHK(hipMemcpyAsync(recs.data(), ctx->pb_info.p, recs.size() * sizeof(c3h::VoxFrameRec), hipMemcpyDeviceToHost,
                           ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -2671,7 +2679,7 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
       o.status = 0;
       const bool hist1_mismatch = p->subdiv > 0 && canvas_multi && one;
       const bool empty_sub = p->subdiv > 0 && (r.sb[0] == 0 || r.sb[1] == 0 || r.sb[2] == 0);
-      redo[i] = (r.err || (r.flagged && !exact_used) || r.n_valid == 0 || hist1_mismatch || empty_sub) ? 1 : 0;
+      redo[i] = (r.err || (r.flagged && !exact_ran[i]) || r.n_valid == 0 || hist1_mismatch || empty_sub) ? 1 : 0;
     }
   }
   for (int i = 0; i < nframes; ++i) {
@@ -2769,12 +2777,19 @@ int c3h_remove_overlap(int32_t M, int32_t rank, const int32_t range[3], c3h_det*
 // score (that score never decreases: the replay kernel's rule)
 int c3h_replay_scores(int32_t M, int32_t rank, const int32_t range[3], int32_t rotate, const int32_t subdiv_b[3],
                       const double* scores, c3h_det* lists) {
+  return c3h_replay_scores_floor(M, rank, range, rotate, subdiv_b, scores, lists, nullptr);
+}
+
+// the same, recording each row's entry floor: before the first position of row (mode, m,
+// z, y), the model's rank-th score (row_floor layout: per searched mode, M x ze x ye)
+int c3h_replay_scores_floor(int32_t M, int32_t rank, const int32_t range[3], int32_t rotate,
+                            const int32_t subdiv_b[3], const double* scores, c3h_det* lists, double* row_floor) {
   if (M < 1 || rank < 1 || !range || !subdiv_b || !scores || !lists) return C3H_ERR_ARG;
   const int r1 = range[0], r2 = range[1], r3 = range[2];
   if (r1 < 1 || r2 < 1 || r3 < 1) return C3H_ERR_ARG;
   int modes[6];
   const int nm = mode_schedule(r1, r2, r3, rotate, modes);
-  int64_t off = 0;
+  int64_t off = 0, roff = 0;
   int searched = 0;
   for (int i = 0; i < nm; ++i) {
     int xr, yr, zr;
@@ -2785,7 +2800,9 @@ int c3h_replay_scores(int32_t M, int32_t rank, const int32_t range[3], int32_t r
     for (int m = 0; m < M; ++m) {
       c3h_det* L = lists + (size_t)m * rank;
       const double* sc = scores + off + (int64_t)m * P;
+      double* fl = row_floor ? row_floor + roff + (int64_t)m * ze * ye : nullptr;
       for (int64_t p = 0; p < P; ++p) {
+        if (fl && p % xe == 0) fl[p / xe] = L[rank - 1].score;
         const double cs = sc[p];
         if (!(cs > L[rank - 1].score)) continue;
         const int x = (int)(p % xe), y = (int)((p / xe) % ye), z = (int)(p / ((int64_t)xe * ye));
@@ -2800,6 +2817,7 @@ int c3h_replay_scores(int32_t M, int32_t rank, const int32_t range[3], int32_t r
       }
     }
     off += P * M;
+    roff += (int64_t)M * ze * ye;
     ++searched;
   }
   return searched;

@@ -4,26 +4,29 @@
 // VoxelGrid::filter, semantics restated in SURVEY.md App. B) and limitPoint
 // (color_voxel_recognition/test/detect_object.cpp:68-87).
 //
-// Hot path: two launches, no host round trip between them.
-//   vox_accum   one workgroup per 2,048 consecutive points (a depth camera's pixel order
+// Hot path: two launches, no hash table, no returning atomic (round 5).
+//   vox_accum   one workgroup per 4,096 consecutive points (a depth camera's pixel order
 //               is spatially coherent: a voxel is hit by runs of neighbouring pixels):
-//               coalesced 16-B loads; per point an LDS hash insert of the absolute cell
-//               with LDS atomics for count | r, b | g (u64 each) and the point's distance
-//               to the cell boundary (min).  Each (workgroup, voxel) then leaves one
-//               global hash insert and two global atomics on one 32-B slot; the new slots
-//               go to the workgroup's own segment of the frame's slot list, and bounds /
-//               counts to its partial record (no same-address atomics across workgroups:
-//               they serialise at the memory side).  The same launch clears what the
-//               previous frame left: its grid words and its hash-table slots (listed by
-//               it).  Two tables alternate by frame parity, so the clear of one never
-//               races the inserts into the other; the grid buffer stays all-zero outside
-//               the voxels a frame writes, without a 4 B/voxel memset per frame.
-//   vox_scatter every block reduces the partial records (bounds, totals), then converts
-//               its segment's voxels: cell - min_b -> linear index (PCL's
-//               (floor(p * inv) - min_b) . divb_mul), the canonical colour mean
-//               kOcc | r<<16 | g<<8 | b with r = (int)(float(sum_r) * (1 / float(count)))
-//               (Eigen 3.0's scalar quotient, see pcl_colour_word), the grid word, and the
-//               safety test below.
+//               coalesced 16-B loads; the cell's toroidal index t (VoxArgs); runs of equal
+//               t in each 16-lane row merged by a DPP segmented scan; one LDS hash insert
+//               per run (count | r, b | g sums, the closest point's distance to a cell face).
+//               Flush: each (workgroup, voxel) pair becomes one list entry of the
+//               workgroup's segment (plain store) and three fire-and-forget atomics: two
+//               64-bit adds into acc[t] and a 64-bit min of (margin << 32 | entry id) into
+//               mo[t].  Nothing waits on a round trip (round 4's hash claim -- a returning
+//               64-bit CAS followed by the adds on its slot -- cost ~14 us of a 36-44 us
+//               frame, profiles/r4/vox_ab/).  The launch also clears the grid words the
+//               previous frame wrote (listed by it) and writes bounds / counts to its own
+//               partial record (no same-address atomics across workgroups).
+//   vox_scatter every block reduces the partial records (bounds, totals), then visits its
+//               segment: the entry whose id is the low half of mo[t] owns the voxel (one
+//               per voxel, the min of its entries), converts it -- linear index (cell -
+//               min_b) . divb_mul from t (modular offsets, exact while the extent fits the
+//               toroidal dims), the canonical colour mean kOcc | r<<16 | g<<8 | b with
+//               r = (int)(float(sum_r) * (1 / float(count))) (Eigen 3.0's scalar quotient,
+//               see pcl_colour_word), the centroid safety test below -- and returns
+//               acc[t] / mo[t] to zero / ~0; the other entries of the voxel skip it (they
+//               read the owner's id, or ~0 once it has reset mo[t]: neither is theirs).
 // Integer sums are exact and order-independent, so the grid is deterministic.
 //
 // Centroids.  C3-HLAC takes a voxel's subdivision (floor(c / voxel_size)) and neighbour
@@ -34,7 +37,7 @@
 // rounding of a cell boundary; vox_scatter flags a voxel when its closest point's margin
 // is below (count + 4) * 2^-22 * (|cell| + 1) cells (4x the error bound of the mean, the
 // multiply and the divide).  Only then (and for c3h_get_downsampled) the exact pass runs:
-// points are bucketed per voxel (counting sort over the slot list), each bucket sorted by
+// points are bucketed per voxel (counting sort over the owning entries), each bucket sorted by
 // point index and summed sequentially in fp32 -- bit-identical to the oracle -- and voxels
 // whose centroid cells differ from their own cell are recorded (c3h_extract corrects
 // their C3-HLAC contribution, c3hlac.hip offcell_delta_kernel).
@@ -47,8 +50,8 @@ namespace c3h {
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr unsigned long long kNoKey = ~0ull;
 constexpr uint32_t kNoMargin = 0xffffffffu;  // above every float's bits: "no point yet"
+constexpr uint32_t kNoT = 0xffffffffu;       // no toroidal index / no grid word
 #ifndef C3H_VOX_CHUNK
 #define C3H_VOX_CHUNK 4096
 #endif
@@ -59,21 +62,14 @@ constexpr int kVB = C3H_VOX_THREADS;
 constexpr int kVoxChunk = C3H_VOX_CHUNK;      // points per workgroup (16 per thread; 4096 / 2048 slots measured
                                               // 40.9 us per 1M-point frame vs 41.9 at 2048 / 1024, 51 at 1024)
 constexpr int kVoxPer = kVoxChunk / kVB;
-constexpr int kVoxRound = kVoxPer;             // loads in flight per thread (one round)
 #ifndef C3H_VOX_SLOTS
 #define C3H_VOX_SLOTS 2048
 #endif
-#ifndef C3H_VOX_DIAG_FLUSH
-#define C3H_VOX_DIAG_FLUSH 0  // diagnostics builds only: 1 = flush atomics at workgroup scope (wrong
-                              // across XCDs: times L2-local atomics), 2 = no global flush at all,
-                              // 3 = no LDS hash either, 4 = the flush's CAS only, 5 = its adds
-                              // only (at the first probe slot, no claim)
-#endif
-#ifndef C3H_VOX_SPEC_ADD
-#define C3H_VOX_SPEC_ADD 0  // diagnostics: 1 = the flush's sums issued with its claim (measured neutral)
-#endif
 #ifndef C3H_VOX_MERGE
 #define C3H_VOX_MERGE 1  // the run merge (0: every point updates the LDS table itself)
+#endif
+#ifndef C3H_VOX_ATOM_SCOPE
+#define C3H_VOX_ATOM_SCOPE __HIP_MEMORY_SCOPE_AGENT
 #endif
 constexpr int kLSlots = C3H_VOX_SLOTS;        // LDS hash slots per workgroup
 constexpr int kLProbe = 48;                   // LDS probes before a point goes straight to the global table
@@ -81,7 +77,6 @@ constexpr int kCellBias = 1 << 20;
 // point margins (cells) at or above this are not recorded per voxel: the scatter's bound
 // is below it except for very dense far voxels, which it then flags conservatively
 constexpr uint32_t kMarginFlush = 0x3c800000u;  // 1/64
-static_assert(sizeof(VoxSlot) == 32, "one 32-B slot per voxel");
 
 // PCL VoxelGrid's colour of a voxel (the reference's PCL 1.0 on Eigen 3.0): the channel
 // sums divided by the point count, which Eigen 3.0 evaluates as sum * (1 / n) in float,
@@ -106,71 +101,8 @@ __device__ __forceinline__ T wave_reduce(T v, Op op) {
   return v;
 }
 
-__device__ __forceinline__ unsigned long long pack_cell(int x, int y, int z) {
-  return (unsigned long long)(uint32_t)(x + kCellBias) |
-         ((unsigned long long)(uint32_t)(y + kCellBias) << 21) |
-         ((unsigned long long)(uint32_t)(z + kCellBias) << 42);
-}
-
-__device__ __forceinline__ void unpack_cell(unsigned long long k, int& x, int& y, int& z) {
-  x = (int)(k & 0x1fffff) - kCellBias;
-  y = (int)((k >> 21) & 0x1fffff) - kCellBias;
-  z = (int)((k >> 42) & 0x1fffff) - kCellBias;
-}
-
-__device__ __forceinline__ uint32_t mix64(unsigned long long k) {
-  k ^= k >> 33;
-  k *= 0xff51afd7ed558ccdull;
-  k ^= k >> 33;
-  k *= 0xc4ceb9fe1a85ec53ull;
-  k ^= k >> 33;
-  return (uint32_t)k;
-}
-
-#ifndef C3H_VOX_SOA
-#define C3H_VOX_SOA 1  // keys in their own array: the claims and the sums' atomics hit different lines
-#endif
-__device__ __forceinline__ unsigned long long& vkey(const VoxArgs& a, uint64_t h) {
-  return C3H_VOX_SOA ? a.keys[h] : a.tab[h].key;
-}
-__device__ __forceinline__ unsigned long long& vkey_prev(const VoxArgs& a, uint64_t h) {
-  return C3H_VOX_SOA ? a.keys_prev[h] : a.tab_prev[h].key;
-}
-
-// global table insert: returns the slot (or -1 when kGProbe probes found no room: the host
-// runs the frame again on a table twice the size); *fresh = this call inserted the key
-constexpr uint64_t kGProbe = 64;  // global probes before the table counts as full (load <= 1/4 by sizing)
-__device__ __forceinline__ int64_t global_slot(const VoxArgs& a, unsigned long long key, bool* fresh) {
-  uint64_t h = mix64(key) & a.tmask;
-  for (uint64_t probes = 0; probes < kGProbe && probes <= a.tmask; ++probes) {
-    const unsigned long long prev = atomicCAS(&vkey(a, h), kNoKey, key);
-    if (prev == kNoKey) {
-      *fresh = true;
-      return (int64_t)h;
-    }
-    if (prev == key) {
-      *fresh = false;
-      return (int64_t)h;
-    }
-    h = (h + 1) & a.tmask;
-  }
-  return -1;
-}
-
-// existing key -> slot (the key must be in the table)
-__device__ __forceinline__ int64_t find_slot(const VoxArgs& a, unsigned long long key) {
-  uint64_t h = mix64(key) & a.tmask;
-  for (uint64_t probes = 0; probes <= a.tmask; ++probes) {
-    const unsigned long long k = vkey(a, h);
-    if (k == key) return (int64_t)h;
-    if (k == kNoKey) return -1;
-    h = (h + 1) & a.tmask;
-  }
-  return -1;
-}
-
-__device__ __forceinline__ bool point_cell(const VoxArgs& a, const float4& p, int c[3], float* margin) {
-  const float f[3] = {p.x * a.inv, p.y * a.inv, p.z * a.inv};
+__device__ __forceinline__ bool point_cell(float inv, const float4& p, int c[3], float* margin) {
+  const float f[3] = {p.x * inv, p.y * inv, p.z * inv};
   float m = 1.0f;
   bool ok = true;
 #pragma unroll
@@ -184,76 +116,25 @@ __device__ __forceinline__ bool point_cell(const VoxArgs& a, const float4& p, in
   return ok;
 }
 
-// per accum block: {min xyz, max xyz, valid points, new slots, error} at part[par][b]
+// toroidal index of an absolute cell (two's complement masks: cell mod 2^tb per axis)
+__device__ __forceinline__ uint32_t tor_index(const int tb[3], const int c[3]) {
+  return ((uint32_t)c[0] & ((1u << tb[0]) - 1)) | (((uint32_t)c[1] & ((1u << tb[1]) - 1)) << tb[0]) |
+         (((uint32_t)c[2] & ((1u << tb[2]) - 1)) << (tb[0] + tb[1]));
+}
+// offsets of a toroidal index from min_b (exact while the extent fits 2^tb per axis)
+__device__ __forceinline__ void tor_offsets(const int tb[3], uint32_t t, const int mn[3], uint32_t o[3]) {
+  const uint32_t mx = (1u << tb[0]) - 1, my = (1u << tb[1]) - 1, mz = (1u << tb[2]) - 1;
+  o[0] = ((t & mx) - (uint32_t)mn[0]) & mx;
+  o[1] = (((t >> tb[0]) & my) - (uint32_t)mn[1]) & my;
+  o[2] = (((t >> (tb[0] + tb[1])) & mz) - (uint32_t)mn[2]) & mz;
+}
+
+// per accum block: {min xyz, max xyz, valid points, list entries, error} at part[par][b]
 constexpr int kPartW = 12;
 enum { kPMin = 0, kPMax = 3, kPValid = 6, kPNew = 7, kPErr = 8 };
 
 __device__ __forceinline__ const int32_t* part_of(const VoxArgs& a, int par) {
   return a.part + (size_t)par * a.nblk_cap * kPartW;
-}
-
-// the previous frame's grid words and its table's slots (its segments b, b + nblk, ...).
-// The first segment's list is loaded at the start of the accumulate (speculatively, all
-// kVoxChunk entries: no wait for its count) and cleared at its end, after the flush: the
-// clear is off the workgroup's dependency chain (this frame uses the other table; the
-// scatter, a later launch, writes the grid)
-constexpr int kClrPer = kVoxChunk / kVB;
-struct VoxClear {
-  int nn = 0;
-  uint32_t sl[kClrPer], tl[kClrPer];
-};
-__device__ __forceinline__ void vox_clear_issue(const VoxArgs& a, VoxClear& c) {
-  const int pp = a.par ^ 1, b = blockIdx.x;
-  if (b >= a.nblk_prev) return;  // uniform
-  c.nn = part_of(a, pp)[(size_t)b * kPartW + kPNew];
-  const uint32_t* sl = a.lists + (size_t)pp * a.lcap + (size_t)b * kVoxChunk;
-  const uint32_t* tl = a.lists + (size_t)(2 + pp) * a.lcap + (size_t)b * kVoxChunk;
-#pragma unroll
-  for (int k = 0; k < kClrPer; ++k) {
-    c.sl[k] = sl[threadIdx.x + k * kVB];
-    c.tl[k] = tl[threadIdx.x + k * kVB];
-  }
-}
-__device__ __forceinline__ void vox_clear_finish(const VoxArgs& a, const VoxClear& c) {
-#pragma unroll
-  for (int k = 0; k < kClrPer; ++k) {
-    if ((int)(threadIdx.x + k * kVB) >= c.nn) continue;
-    if (a.clear_tables) {
-      VoxSlot& t = a.tab_prev[c.sl[k]];
-      *reinterpret_cast<ulonglong2*>(&t.key) = make_ulonglong2(kNoKey, 0ull);
-      if (C3H_VOX_SOA) vkey_prev(a, c.sl[k]) = kNoKey;
-      *reinterpret_cast<ulonglong2*>(&t.b) = make_ulonglong2(0ull, (unsigned long long)kNoMargin);
-    }
-    if (a.clear_grid) a.grid[c.tl[k]] = 0;
-  }
-}
-// the previous frame's segments beyond the first (more previous blocks than this launch's)
-__device__ __forceinline__ void vox_clear_prev(const VoxArgs& a, int b_first) {
-  const int pp = a.par ^ 1;
-  for (int b = b_first; b < a.nblk_prev; b += gridDim.x) {
-    const int nn = part_of(a, pp)[(size_t)b * kPartW + kPNew];
-    const uint32_t* sl = a.lists + (size_t)pp * a.lcap + (size_t)b * kVoxChunk;
-    const uint32_t* tl = a.lists + (size_t)(2 + pp) * a.lcap + (size_t)b * kVoxChunk;
-    for (int i = threadIdx.x; i < nn; i += kVB) {
-      if (a.clear_tables) {
-        VoxSlot& t = a.tab_prev[sl[i]];
-        *reinterpret_cast<ulonglong2*>(&t.key) = make_ulonglong2(kNoKey, 0ull);
-        if (C3H_VOX_SOA) vkey_prev(a, sl[i]) = kNoKey;
-        *reinterpret_cast<ulonglong2*>(&t.b) = make_ulonglong2(0ull, (unsigned long long)kNoMargin);
-      }
-      if (a.clear_grid) a.grid[tl[i]] = 0;
-    }
-  }
-}
-
-// the flush's slot claim (diagnostics: C3H_VOX_DIAG_FLUSH 1 at workgroup scope)
-__device__ __forceinline__ unsigned long long vox_cas(unsigned long long* p, unsigned long long cmp,
-                                                      unsigned long long val) {
-  if (C3H_VOX_DIAG_FLUSH == 1) {
-    __hip_atomic_compare_exchange_strong(p, &cmp, val, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return cmp;
-  }
-  return atomicCAS(p, cmp, val);
 }
 
 // DPP row_shr:o (within 16-lane rows); lanes without a source read 0
@@ -263,21 +144,14 @@ __device__ __forceinline__ uint32_t vrow_shr(uint32_t v) {
 }
 
 __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
-  __shared__ unsigned long long s_key[kLSlots];
-  __shared__ unsigned long long s_gb[kLSlots];  // b << 32 | g
-  __shared__ unsigned long long s_cr[kLSlots];  // count << 32 | r
+  __shared__ uint32_t s_key[kLSlots];
+  __shared__ unsigned long long s_A[kLSlots];  // count << 40 | sum r
+  __shared__ unsigned long long s_B[kLSlots];  // sum b << 32 | sum g
   __shared__ uint32_t s_m[kLSlots];
-  __shared__ uint32_t s_nnew;                   // global slots this workgroup inserted (its list segment)
+  __shared__ uint32_t s_nnew;                  // list entries of this workgroup
   __shared__ int s_red[kVB / 64][8];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int s = tid; s < kLSlots; s += kVB) {
-    s_key[s] = kNoKey;
-    s_gb[s] = 0;
-    s_cr[s] = 0;
-    s_m[s] = kNoMargin;
-  }
-  if (tid == 0) s_nnew = 0;
-  if (blockIdx.x == 0 && tid == 0) {  // totals of an empty frame (the scatter publishes the others)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, b = blockIdx.x;
+  if (b == 0 && tid == 0) {  // totals of an empty frame (the scatter publishes the others)
     for (int ax = 0; ax < 3; ++ax) {
       reinterpret_cast<int32_t*>(a.cnt)[kVcMin + ax] = INT_MAX;
       reinterpret_cast<int32_t*>(a.cnt)[kVcMax + ax] = INT_MIN;
@@ -286,12 +160,24 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
     a.cnt[kVcSlots + a.par] = 0;
     a.cnt[kVcFlag] = a.cnt[kVcErr] = a.cnt[kVcOver] = a.cnt[kVcOff] = 0;
   }
-  const int64_t base = blockIdx.x * (int64_t)kVoxChunk;
-  // the points' loads are in flight while the previous frame is cleared (one round)
-  static_assert(kVoxPer == kVoxRound, "one round of point loads");
-  float4 p[kVoxRound];
+  // the previous frame's grid words (its segments b, b + grid, ...), cleared while this
+  // block's point loads are in flight (this frame's scatter, a later launch, writes the grid)
+  if (a.clear_grid) {
+    const int pp = a.par ^ 1;
+    for (int pb = b; pb < a.nblk_prev; pb += gridDim.x) {
+      const int nn = part_of(a, pp)[(size_t)pb * kPartW + kPNew];
+      const uint32_t* tl = a.lists + (size_t)(2 + pp) * a.lcap + (size_t)pb * kVoxChunk;
+      for (int i = tid; i < nn; i += kVB) {
+        const uint32_t wi = tl[i];
+        if (wi != kNoT) a.grid[wi] = 0u;
+      }
+    }
+  }
+  if (b >= a.nblk) return;  // clearing only (an empty frame still runs one block)
+  const int64_t base = b * (int64_t)kVoxChunk;
+  float4 p[kVoxPer];
 #pragma unroll
-  for (int j = 0; j < kVoxRound; ++j) {
+  for (int j = 0; j < kVoxPer; ++j) {
     const int64_t i = base + j * kVB + tid;
     if (i < a.n) {  // streamed once: non-temporal
       const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.pts) + i);
@@ -300,38 +186,39 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
       p[j] = make_float4(NAN, NAN, NAN, 0.0f);
     }
   }
-  VoxClear clr;
-  vox_clear_issue(a, clr);
-  uint32_t* sl = a.lists + (size_t)a.par * a.lcap + (size_t)blockIdx.x * kVoxChunk;
+  for (int s = tid; s < kLSlots; s += kVB) {
+    s_key[s] = kNoT;
+    s_A[s] = 0;
+    s_B[s] = 0;
+    s_m[s] = kNoMargin;
+  }
+  if (tid == 0) s_nnew = 0;
   __syncthreads();
+  uint32_t* sl = a.lists + (size_t)a.par * a.lcap + (size_t)b * kVoxChunk;
+  const uint32_t q0 = (uint32_t)b * (uint32_t)kVoxChunk;
+  ulonglong2* __restrict__ acc = a.acc;
+  unsigned long long* __restrict__ mo = a.mo;
+  // one (workgroup, voxel) entry: fire-and-forget sums and the owner / margin min
+  auto add_entry = [&](uint32_t i, uint32_t t, unsigned long long va, unsigned long long vb, uint32_t m) {
+    sl[i] = t;
+    __hip_atomic_fetch_add(&acc[t].x, va, __ATOMIC_RELAXED, C3H_VOX_ATOM_SCOPE);
+    __hip_atomic_fetch_add(&acc[t].y, vb, __ATOMIC_RELAXED, C3H_VOX_ATOM_SCOPE);
+    __hip_atomic_fetch_min(mo + t, ((unsigned long long)m << 32) | (q0 + i), __ATOMIC_RELAXED, C3H_VOX_ATOM_SCOPE);
+  };
   int mn[3] = {INT_MAX, INT_MAX, INT_MAX}, mx[3] = {INT_MIN, INT_MIN, INT_MIN};
   int nv = 0;
-  int err = 0;  // kVcErrRange | kVcErrFull
-  auto add_global = [&](unsigned long long key, unsigned long long A, unsigned long long B, uint32_t m) {
-    bool fresh = false;
-    const int64_t s = global_slot(a, key, &fresh);
-    if (s < 0) {
-      err |= kVcErrFull;
-      return;
-    }
-    if (fresh) sl[atomicAdd(&s_nnew, 1u)] = (uint32_t)s;
-    atomicAdd(&a.tab[s].a, A);
-    atomicAdd(&a.tab[s].b, B);
-    if (m < kMarginFlush) atomicMin(&a.tab[s].margin, m);
-  };
+  int err = 0;  // kVcErrRange
   const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1);  // lanes <= this one
-  {
 #pragma unroll
-  for (int j = 0; j < kVoxRound; ++j) {
+  for (int j = 0; j < kVoxPer; ++j) {
     int c[3] = {0, 0, 0};
     float margin = 1.0f;
     bool valid = point_valid(p[j], a.z_limit);
-    if (valid && !point_cell(a, p[j], c, &margin)) {
+    if (valid && !point_cell(a.inv, p[j], c, &margin)) {
       err |= kVcErrRange;
       valid = false;
     }
-    unsigned long long key = kNoKey;
-    uint32_t w0 = 0, w1 = 0, mb = kNoMargin;
+    uint32_t t = kNoT, w0 = 0, w1 = 0, mb = kNoMargin;
     if (valid) {
       ++nv;
 #pragma unroll
@@ -339,19 +226,17 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
         mn[ax] = min(mn[ax], c[ax]);
         mx[ax] = max(mx[ax], c[ax]);
       }
-      key = pack_cell(c[0], c[1], c[2]);
+      t = tor_index(a.tb, c);
       const uint32_t rgb = __float_as_uint(p[j].w);
       w0 = ((rgb >> 16) & 0xffu) | (((rgb >> 8) & 0xffu) << 12) | (1u << 24);  // r | g << 12 | count << 24
       w1 = rgb & 0xffu;                                                         // b
       const uint32_t mbits = __float_as_uint(margin);
       mb = mbits < kMarginFlush ? mbits : kNoMargin;
     }
-    // a depth camera's neighbouring pixels hit one voxel in runs: inside each 16-lane row
-    // the runs are summed by a segmented DPP scan (as voxb_accum) and only a run's last
+    // runs of equal keys inside each 16-lane row: a lane starts a run when it is invalid,
+    // the row's first lane, or its key differs from the previous lane's; only a run's last
     // lane updates the LDS table (same-address LDS atomics serialise)
-    const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);
-    const bool head = !C3H_VOX_MERGE || !valid || (lane & 15) == 0 || vrow_shr<1>(klo) != klo ||
-                      vrow_shr<1>(khi) != khi;
+    const bool head = !C3H_VOX_MERGE || !valid || (lane & 15) == 0 || vrow_shr<1>(t) != t;
     const uint64_t hm = __ballot(head);
     const int o0 = lane - (63 - __clzll(hm & le));  // lanes before this one in its run
     uint32_t s0, s1, sm;
@@ -363,95 +248,43 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
     if (o0 >= 4) { w0 += s0; w1 += s1; mb = min(mb, sm); }
     s0 = vrow_shr<8>(w0); s1 = vrow_shr<8>(w1); sm = vrow_shr<8>(mb);
     if (o0 >= 8) { w0 += s0; w1 += s1; mb = min(mb, sm); }
-    const bool tail = C3H_VOX_DIAG_FLUSH < 3 && valid && ((lane & 15) == 15 || ((hm >> (lane + 1)) & 1));
+    const bool tail = valid && ((lane & 15) == 15 || ((hm >> (lane + 1)) & 1));
     if (!tail) continue;
     // the run's totals: count <= 16, channel sums <= 4080
-    const unsigned long long cr = ((unsigned long long)(w0 >> 24) << 32) | (w0 & 0xfffu);
-    const unsigned long long gb = ((unsigned long long)w1 << 32) | ((w0 >> 12) & 0xfffu);
-    uint32_t h = mix64(key) & (kLSlots - 1);
+    const unsigned long long A = ((unsigned long long)(w0 >> 24) << 40) | (w0 & 0xfffu);
+    const unsigned long long B = ((unsigned long long)w1 << 32) | ((w0 >> 12) & 0xfffu);
+    uint32_t h = (t * 0x9E3779B1u) >> (32 - __builtin_ctz(kLSlots));
     bool done = false;
     for (int probe = 0; probe < kLProbe; ++probe) {
-      const unsigned long long prev = atomicCAS(&s_key[h], kNoKey, key);
-      if (prev == kNoKey || prev == key) {
-        atomicAdd(&s_cr[h], cr);
-        atomicAdd(&s_gb[h], gb);
+      const uint32_t prev = atomicCAS(&s_key[h], kNoT, t);
+      if (prev == kNoT || prev == t) {
+        atomicAdd(&s_A[h], A);
+        atomicAdd(&s_B[h], B);
         if (mb != kNoMargin) atomicMin(&s_m[h], mb);
         done = true;
         break;
       }
       h = (h + 1) & (kLSlots - 1);
     }
-    if (!done) add_global(key, ((cr >> 32) << 40) | (cr & 0xffffffffull), gb, mb);  // LDS table full
+    if (!done) add_entry(atomicAdd(&s_nnew, 1u), t, A, B, mb);  // LDS table full: an entry of its own
   }
-  }
-  // flush: one global insert + two (three near a cell boundary) atomics per (workgroup, voxel);
-  // a thread's first probes are all issued before any result is used (round trips)
   __syncthreads();  // every point's LDS update is in
-  {
+  {  // flush: list positions by one LDS counter add per wave
     constexpr int kFl = (kLSlots + kVB - 1) / kVB;
-    unsigned long long key[kFl], prev[kFl];
-    uint64_t h[kFl];
-    // Speculative sums (C3H_VOX_SPEC_ADD): the two adds go to the key's home slot together
-    // with its claim, not after the claim's round trip; a claim that finds another key there
-    // (a collision, ~3 % of voxels at the table's load) takes the sums back out (64-bit
-    // wrap-around subtraction: exact) and adds them where the probe lands.  The scatter
-    // reads the sums only after this launch, so the intermediate state is never seen.
-    bool spec[kFl];
 #pragma unroll
     for (int k = 0; k < kFl; ++k) {
       const int s = tid + k * kVB;
-      key[k] = s < kLSlots && C3H_VOX_DIAG_FLUSH < 2 ? s_key[s] : kNoKey;
-      h[k] = mix64(key[k]) & a.tmask;
-      prev[k] = key[k] != kNoKey && C3H_VOX_DIAG_FLUSH != 5 ? vox_cas(&vkey(a, h[k]), kNoKey, key[k]) : kNoKey;
-      spec[k] = C3H_VOX_SPEC_ADD && C3H_VOX_DIAG_FLUSH == 0 && key[k] != kNoKey;
-      if (spec[k]) {
-        const unsigned long long cr = s_cr[s];
-        atomicAdd(&a.tab[h[k]].a, ((cr >> 32) << 40) | (cr & 0xffffffffull));
-        atomicAdd(&a.tab[h[k]].b, s_gb[s]);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < kFl; ++k) {
-      if (key[k] == kNoKey) continue;
-      const int s = tid + k * kVB;
-      const unsigned long long cr = s_cr[s];
-      const unsigned long long va = ((cr >> 32) << 40) | (cr & 0xffffffffull), vb = s_gb[s];
-      if (spec[k] && prev[k] != kNoKey && prev[k] != key[k]) {  // collision: undo at home
-        atomicAdd(&a.tab[h[k]].a, 0ull - va);
-        atomicAdd(&a.tab[h[k]].b, 0ull - vb);
-        spec[k] = false;
-      }
-      // collisions: linear probing as global_slot (the host sizes the table at >= 2x points)
-      uint64_t probes = 1;
-      while (prev[k] != kNoKey && prev[k] != key[k] && probes < kGProbe && probes <= a.tmask) {
-        h[k] = (h[k] + 1) & a.tmask;
-        prev[k] = vox_cas(&vkey(a, h[k]), kNoKey, key[k]);
-        ++probes;
-      }
-      if (prev[k] != kNoKey && prev[k] != key[k]) {
-        err |= kVcErrFull;
-        continue;
-      }
-      if (prev[k] == kNoKey) sl[atomicAdd(&s_nnew, 1u)] = (uint32_t)h[k];
-      if (C3H_VOX_DIAG_FLUSH == 4) continue;  // diagnostics: the claim only
-      if (spec[k]) {  // the sums are in already
-        if (s_m[s] < kMarginFlush) atomicMin(&a.tab[h[k]].margin, s_m[s]);
-        continue;
-      }
-      if (C3H_VOX_DIAG_FLUSH == 1) {
-        __hip_atomic_fetch_add(&a.tab[h[k]].a, ((cr >> 32) << 40) | (cr & 0xffffffffull), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_add(&a.tab[h[k]].b, s_gb[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      } else {
-        atomicAdd(&a.tab[h[k]].a, ((cr >> 32) << 40) | (cr & 0xffffffffull));
-        atomicAdd(&a.tab[h[k]].b, s_gb[s]);
-      }
-      if (s_m[s] < kMarginFlush) atomicMin(&a.tab[h[k]].margin, s_m[s]);
+      const uint32_t key = s < kLSlots ? s_key[s] : kNoT;
+      const bool have = key != kNoT;
+      const unsigned long long bm = __ballot(have);
+      if (!bm) continue;
+      uint32_t w0 = 0;
+      if (lane == 0) w0 = atomicAdd(&s_nnew, (uint32_t)__popcll(bm));
+      w0 = __shfl(w0, 0, 64);
+      if (have) add_entry(w0 + (uint32_t)__popcll(bm & ((1ull << lane) - 1)), key, s_A[s], s_B[s], s_m[s]);
     }
   }
-  vox_clear_finish(a, clr);
-  vox_clear_prev(a, blockIdx.x + gridDim.x);
-  // bounds, counts and the slot list go to this block's partial record: no same-address
+  // bounds, counts and the entry count go to this block's partial record: no same-address
   // atomics across blocks (they serialise at the memory side)
 #pragma unroll
   for (int ax = 0; ax < 3; ++ax) {
@@ -469,7 +302,7 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
     s_red[w][7] = e;
   }
   __syncthreads();
-  int32_t* pr = a.part + ((size_t)a.par * a.nblk_cap + blockIdx.x) * kPartW;
+  int32_t* pr = a.part + ((size_t)a.par * a.nblk_cap + b) * kPartW;
   if (tid < 8) {
     int v = s_red[0][tid];
     for (int i = 1; i < kVB / 64; ++i) {
@@ -493,7 +326,7 @@ __device__ VoxTotals vox_reduce(const VoxArgs& a, bool publish) {
   __shared__ int s_r[kBlock / 64][10];
   const int32_t* pt = part_of(a, a.par);
   int mn[3] = {INT_MAX, INT_MAX, INT_MAX}, mx[3] = {INT_MIN, INT_MIN, INT_MIN};
-  int nv = 0, nn = 0, er = 0;
+  int nv = 0, er = 0;
   for (int b = threadIdx.x; b < a.nblk; b += kBlock) {
     const int32_t* r = pt + (size_t)b * kPartW;
     if (r[kPValid]) {
@@ -503,7 +336,6 @@ __device__ VoxTotals vox_reduce(const VoxArgs& a, bool publish) {
       }
     }
     nv += r[kPValid];
-    nn += r[kPNew];
     er |= r[kPErr];
   }
   for (int ax = 0; ax < 3; ++ax) {
@@ -511,7 +343,6 @@ __device__ VoxTotals vox_reduce(const VoxArgs& a, bool publish) {
     mx[ax] = wave_reduce(mx[ax], [](int x, int y) { return max(x, y); });
   }
   nv = wave_reduce(nv, [](int x, int y) { return x + y; });
-  nn = wave_reduce(nn, [](int x, int y) { return x + y; });
   er = wave_reduce(er, [](int x, int y) { return x | y; });
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
@@ -520,7 +351,6 @@ __device__ VoxTotals vox_reduce(const VoxArgs& a, bool publish) {
       s_r[w][3 + ax] = mx[ax];
     }
     s_r[w][6] = nv;
-    s_r[w][7] = nn;
     s_r[w][8] = er;
   }
   __syncthreads();
@@ -536,10 +366,9 @@ __device__ VoxTotals vox_reduce(const VoxArgs& a, bool publish) {
     t.dv[ax] = hi - lo + 1;
     nvox *= t.dv[ax];
   }
-  int tv = 0, tn = 0, te = 0;
+  int tv = 0, te = 0;
   for (int i = 0; i < kBlock / 64; ++i) {
     tv += s_r[i][6];
-    tn += s_r[i][7];
     te |= s_r[i][8];
   }
   t.any = tv > 0;
@@ -552,7 +381,6 @@ __device__ VoxTotals vox_reduce(const VoxArgs& a, bool publish) {
     }
     a.cnt[kVcValid] = (uint32_t)tv;
     a.cnt[kVcValid + 1] = 0;
-    a.cnt[kVcSlots + a.par] = (uint32_t)tn;
     if (te) a.cnt[kVcErr] = (uint32_t)te;
   }
   return t;
@@ -562,62 +390,77 @@ __device__ __forceinline__ int seg_count(const VoxArgs& a, int b) {
   return part_of(a, a.par)[(size_t)b * kPartW + kPNew];
 }
 
-// one block per accum block: its listed voxels (the block's segment of the slot list).  The
-// first round of the segment's slots is loaded before the totals are reduced (neither
-// depends on the other): the reduction's round trip hides the slots' latency
+// one block per accum block: its segment's entries.  The first round of entries and their
+// owner words are loaded before the totals are reduced (neither depends on the other)
 __global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
   const int b = blockIdx.x;
   const int nn = seg_count(a, b);
   const size_t seg = (size_t)b * kVoxChunk;
   const uint32_t* sl = a.lists + (size_t)a.par * a.lcap + seg;
   uint32_t* tl = a.lists + (size_t)(2 + a.par) * a.lcap + seg;
-  constexpr int kPre = 2;  // slots per thread loaded ahead (a segment averages ~1.5 rounds)
-  uint32_t ps[kPre];
-  ulonglong2 pka[kPre], pbm[kPre];
+  uint32_t* lc = a.lcnt + seg;
+  const uint32_t q0 = (uint32_t)seg;
+  constexpr int kPre = 2;  // entries per thread loaded ahead
+  uint32_t pt[kPre];
+  unsigned long long pmo[kPre];
 #pragma unroll
   for (int k = 0; k < kPre; ++k) {
     const int i = threadIdx.x + k * kBlock;
-    ps[k] = i < nn ? sl[i] : 0u;
-    if (i < nn) {
-      pka[k] = *reinterpret_cast<const ulonglong2*>(&a.tab[ps[k]].key);
-      pka[k].x = vkey(a, ps[k]);
-      pbm[k] = *reinterpret_cast<const ulonglong2*>(&a.tab[ps[k]].b);
-    }
+    pt[k] = i < nn ? sl[i] : 0u;
+    pmo[k] = i < nn ? a.mo[pt[k]] : ~0ull;
   }
-  const VoxTotals t = vox_reduce(a, blockIdx.x == 0);
-  if (!t.any) return;
-  if (t.nvox > a.grid_cap || t.nvox > INT_MAX) {  // the host grows the grid and runs this again
+  const VoxTotals tot = vox_reduce(a, blockIdx.x == 0);
+  if (!tot.any) return;
+  // the extent beyond the toroidal dims (the host enlarges them and runs the frame again),
+  // or beyond the grid buffer (the host grows it and runs this again): nothing is written
+  bool wrap = false;
+  for (int ax = 0; ax < 3; ++ax) wrap = wrap || tot.dv[ax] > (1 << a.tb[ax]);
+  if (wrap) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.cnt + kVcErr, kVcErrWrap);
+    return;
+  }
+  if (tot.nvox > a.grid_cap || tot.nvox > INT_MAX) {
     if (blockIdx.x == 0 && threadIdx.x == 0) a.cnt[kVcOver] = 1;
     return;
   }
-  uint32_t flagged = 0;
-  auto convert = [&](int i, uint32_t s, const ulonglong2& ka, const ulonglong2& bm) {
-    int x, y, z;
-    unpack_cell(ka.x, x, y, z);
-    const int64_t idx = (x - t.mn[0]) + (int64_t)t.dv[0] * ((y - t.mn[1]) + (int64_t)t.dv[1] * (z - t.mn[2]));
-    const unsigned long long A = ka.y, B = bm.x;
-    const uint32_t count = (uint32_t)(A >> 40);
-    a.grid[idx] = pcl_colour_word(A & 0xffffffffffull, B & 0xffffffffull, B >> 32, count);
+  uint32_t flagged = 0, owned = 0;
+  auto visit = [&](int i, uint32_t t, unsigned long long m) {
+    const uint32_t q = q0 + (uint32_t)i;
+    if ((uint32_t)m != q) {  // another entry of the voxel owns it
+      tl[i] = kNoT;
+      lc[i] = 0u;
+      return;
+    }
+    ++owned;
+    const ulonglong2 v = a.acc[t];
+    a.acc[t] = make_ulonglong2(0ull, 0ull);
+    a.mo[t] = ~0ull;
+    a.tpos[t] = q;
+    uint32_t o[3];
+    tor_offsets(a.tb, t, tot.mn, o);
+    const int64_t idx = o[0] + (int64_t)tot.dv[0] * (o[1] + (int64_t)tot.dv[1] * o[2]);
+    const uint32_t count = (uint32_t)(v.x >> 40);
+    a.grid[idx] = pcl_colour_word(v.x & 0xffffffffffull, v.y & 0xffffffffull, v.y >> 32, count);
     tl[i] = (uint32_t)idx;
-    a.tab[s].pos = (uint32_t)(seg + i);
+    lc[i] = count;
     // margins >= kMarginFlush were not recorded: conservative when the bound exceeds it
-    const int cmag = max(max(abs(x), abs(y)), abs(z)) + 1;
+    const int cmag = max(max(abs(tot.mn[0] + (int)o[0]), abs(tot.mn[1] + (int)o[1])), abs(tot.mn[2] + (int)o[2])) + 1;
     const float eps = (float)(count + 4) * (float)cmag * 0x1p-22f;
-    if (__uint_as_float((uint32_t)bm.y) < eps || eps >= __uint_as_float(kMarginFlush)) ++flagged;
+    if (__uint_as_float((uint32_t)(m >> 32)) < eps || eps >= __uint_as_float(kMarginFlush)) ++flagged;
   };
 #pragma unroll
   for (int k = 0; k < kPre; ++k) {
     const int i = threadIdx.x + k * kBlock;
-    if (i < nn) convert(i, ps[k], pka[k], pbm[k]);
+    if (i < nn) visit(i, pt[k], pmo[k]);
   }
   for (int i = threadIdx.x + kPre * kBlock; i < nn; i += kBlock) {
-    const uint32_t s = sl[i];
-    ulonglong2 ka = *reinterpret_cast<const ulonglong2*>(&a.tab[s].key);
-    ka.x = vkey(a, s);
-    convert(i, s, ka, *reinterpret_cast<const ulonglong2*>(&a.tab[s].b));
+    const uint32_t t = sl[i];
+    visit(i, t, a.mo[t]);
   }
   flagged = wave_reduce(flagged, [](uint32_t u, uint32_t v) { return u + v; });
+  owned = wave_reduce(owned, [](uint32_t u, uint32_t v) { return u + v; });
   if ((threadIdx.x & 63) == 0 && flagged) atomicAdd(a.cnt + kVcFlag, flagged);
+  if ((threadIdx.x & 63) == 0 && owned) atomicAdd(a.cnt + kVcSlots + a.par, owned);
 }
 
 __device__ __forceinline__ bool vox_bounds(const VoxArgs& a, int mn[3], int dv[3], int64_t* nvox) {
@@ -633,14 +476,13 @@ __device__ __forceinline__ bool vox_bounds(const VoxArgs& a, int mn[3], int dv[3
 }
 
 // ---- exact centroids (flagged frames and c3h_get_downsampled) ----------------------
-// positions p = b * kVoxChunk + i of the segmented slot list; gaps (i >= the segment's
-// count) hold count 0
+// positions p = b * kVoxChunk + i of the segmented entry list; entries that do not own
+// their voxel and gaps (i >= the segment's count) hold count 0
 __global__ __launch_bounds__(kBlock) void vox_counts_kernel(VoxArgs a, uint32_t* __restrict__ counts) {
   const int64_t np = (int64_t)a.nblk * kVoxChunk;
-  const uint32_t* sl = a.lists + (size_t)a.par * a.lcap;
   for (int64_t q = blockIdx.x * (int64_t)kBlock + threadIdx.x; q < np; q += (int64_t)gridDim.x * kBlock) {
     const int b = (int)(q / kVoxChunk), i = (int)(q % kVoxChunk);
-    counts[q] = i < seg_count(a, b) ? (uint32_t)(a.tab[sl[q]].a >> 40) : 0u;
+    counts[q] = i < seg_count(a, b) ? a.lcnt[q] : 0u;
   }
 }
 
@@ -652,10 +494,8 @@ __global__ __launch_bounds__(kBlock) void vox_bucket_kernel(VoxArgs a, const uin
     if (!point_valid(p, a.z_limit)) continue;
     int c[3];
     float m;
-    if (!point_cell(a, p, c, &m)) continue;
-    const int64_t s = find_slot(a, pack_cell(c[0], c[1], c[2]));
-    if (s < 0) continue;
-    const uint32_t lp = a.tab[s].pos;
+    if (!point_cell(a.inv, p, c, &m)) continue;
+    const uint32_t lp = a.tpos[tor_index(a.tb, c)];
     bucket[off[lp] + atomicAdd(&cur[lp], 1u)] = (uint32_t)i;
   }
 }
@@ -699,25 +539,26 @@ __global__ __launch_bounds__(kBlock) void vox_centroid_kernel(VoxArgs a, const u
     const float c[3] = {__fmul_rn(sx, rn), __fmul_rn(sy, rn), __fmul_rn(sz, rn)};
     const uint32_t idx = tl[q];
     cent[q] = make_float4(c[0], c[1], c[2], __uint_as_float(a.grid[idx] & 0x00ffffffu));
-    int own[3];
-    unpack_cell(vkey(a, sl[q]), own[0], own[1], own[2]);
+    uint32_t o[3];
+    tor_offsets(a.tb, sl[q], mn, o);
     int nb[3], sb[3];
     bool moved = false;
 #pragma unroll
     for (int ax = 0; ax < 3; ++ax) {
+      const int own = mn[ax] + (int)o[ax];
       nb[ax] = (int)floorf(__fdiv_rn(c[ax], a.leaf));  // PCL 1.0 getNeighborCentroidIndices: floor(p / leaf)
       sb[ax] = nb[ax];                                  // c3_hlac.cpp:349-354: floor(p / voxel_size)
-      moved = moved || nb[ax] != own[ax] || sb[ax] != own[ax];
+      moved = moved || nb[ax] != own || sb[ax] != own;
     }
     if (moved) {
       const uint32_t k = atomicAdd(a.cnt + kVcOff, 1u);
-      int32_t* o = offcell + 8 * (int64_t)k;
-      o[0] = (int32_t)idx;
+      int32_t* oc = offcell + 8 * (int64_t)k;
+      oc[0] = (int32_t)idx;
       for (int ax = 0; ax < 3; ++ax) {
-        o[1 + ax] = nb[ax] - mn[ax];
-        o[4 + ax] = sb[ax] - mn[ax];
+        oc[1 + ax] = nb[ax] - mn[ax];
+        oc[4 + ax] = sb[ax] - mn[ax];
       }
-      o[7] = 0;
+      oc[7] = 0;
     }
   }
 }
@@ -859,7 +700,6 @@ constexpr int kBRound = kBPer < C3H_VB_ROUND ? kBPer : C3H_VB_ROUND;  // loads i
 static_assert(kBPer % kBRound == 0, "rounds");
 constexpr int kBSlots = C3H_VB_SLOTS;
 static_assert(kBChunk % kBT == 0 && (kBSlots & (kBSlots - 1)) == 0, "batch voxeliser shape");
-constexpr uint32_t kNoT = 0xffffffffu;
 #ifndef C3H_VB_DIAG
 #define C3H_VB_DIAG 0  // diagnostics builds only: 1 = no global flush, 2 = no LDS insert either
 #endif
@@ -896,7 +736,10 @@ __global__ __launch_bounds__(kBT) void voxb_accum_kernel(VoxBatchArgs a) {
     const int nn = pr[kPNew];
     uint32_t* g = a.grid[fp];
     const uint32_t* wl = a.wlist + (size_t)b * kBChunk;
-    for (int i = tid; i < nn; i += kBT) g[wl[i]] = 0u;
+    for (int i = tid; i < nn; i += kBT) {
+      const uint32_t wi = wl[i];
+      if (wi != kNoT) g[wi] = 0u;  // (entries that did not own their voxel wrote no word)
+    }
   }
   if (b >= a.total) return;  // clearing only
   const int f = vb_frame(a.blk0, a.nf, b);
@@ -906,7 +749,7 @@ __global__ __launch_bounds__(kBT) void voxb_accum_kernel(VoxBatchArgs a) {
   const uint32_t mx_ = (1u << a.tb[0]) - 1, my_ = (1u << a.tb[1]) - 1, mz_ = (1u << a.tb[2]) - 1;
   const int sy = a.tb[0], sz = a.tb[0] + a.tb[1];
   ulonglong2* __restrict__ acc = a.acc + f * a.s_acc;
-  uint32_t* __restrict__ Mg = a.accM + f * a.s_acc;
+  unsigned long long* __restrict__ MO = a.accMO + f * a.s_acc;
   uint32_t* __restrict__ vl = a.vlist + (size_t)b * kBChunk;
   for (int s = tid; s < kBSlots; s += kBT) {
     s_key[s] = kNoT;
@@ -919,14 +762,20 @@ __global__ __launch_bounds__(kBT) void voxb_accum_kernel(VoxBatchArgs a) {
   int mn[3] = {INT_MAX, INT_MAX, INT_MAX}, mx[3] = {INT_MIN, INT_MIN, INT_MIN};
   int nv = 0;
   bool err = false;
-  auto add_global = [&](uint32_t t, unsigned long long va, unsigned long long vb, uint32_t m) {
-    const unsigned long long old = atomicAdd(&acc[t].x, va);
-    if ((old >> 40) == 0) vl[atomicAdd(&s_nnew, 1u)] = t;
-    atomicAdd(&acc[t].y, vb);
-    if (m < kMarginFlush) atomicMin(Mg + t, m);
+  // one (block, voxel) entry: the block's list gets t, the accumulator the sums, and
+  // MO[t] the min of (margin << 32 | entry id) -- no returning atomic: the entry holding
+  // the min owns the voxel in the scatter (unique: entry ids are), every other entry of
+  // the voxel skips it there
+  const uint32_t q0 = (uint32_t)b * (uint32_t)kBChunk;
+  auto add_entry = [&](uint32_t i, uint32_t t, unsigned long long va, unsigned long long vb, uint32_t m) {
+    vl[i] = t;
+    __hip_atomic_fetch_add(&acc[t].x, va, __ATOMIC_RELAXED, C3H_VB_ATOM_SCOPE);
+    __hip_atomic_fetch_add(&acc[t].y, vb, __ATOMIC_RELAXED, C3H_VB_ATOM_SCOPE);
+    __hip_atomic_fetch_min(MO + t, ((unsigned long long)m << 32) | (q0 + i), __ATOMIC_RELAXED, C3H_VB_ATOM_SCOPE);
   };
-  VoxArgs q{};  // point_cell's quantisation parameters
-  q.inv = a.inv;
+  auto add_global = [&](uint32_t t, unsigned long long va, unsigned long long vb, uint32_t m) {
+    add_entry(atomicAdd(&s_nnew, 1u), t, va, vb, m);
+  };
   const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1);  // lanes <= this one
   for (int r0 = 0; r0 < kBPer; r0 += kBRound) {
   float4 p[kBRound];
@@ -945,7 +794,7 @@ __global__ __launch_bounds__(kBT) void voxb_accum_kernel(VoxBatchArgs a) {
     int c[3];
     float margin;
     bool valid = point_valid(p[j], a.z_limit);
-    if (valid && !point_cell(q, p[j], c, &margin)) {
+    if (valid && !point_cell(a.inv, p[j], c, &margin)) {
       err = true;
       valid = false;
     }
@@ -1002,26 +851,23 @@ __global__ __launch_bounds__(kBT) void voxb_accum_kernel(VoxBatchArgs a) {
   }
   }
   __syncthreads();
-  // flush: a thread's slots' returning atomics are all issued before any result is used
-  // (they are round trips to the memory side; one after the other they kept blocks resident)
+  // flush: every (block, voxel) entry is listed and its sums go out as non-returning
+  // atomics (fire and forget: nothing waits for a round trip; round 4's returning add,
+  // which detected the first touch, kept blocks resident until it came back).  List
+  // positions: one LDS counter add per wave
   if (C3H_VB_DIAG == 0) {
     constexpr int kFl = (kBSlots + kBT - 1) / kBT;
-    uint32_t key[kFl];
-    unsigned long long old[kFl];
 #pragma unroll
     for (int k = 0; k < kFl; ++k) {
       const int s = tid + k * kBT;
-      key[k] = s < kBSlots ? s_key[s] : kNoT;
-      old[k] = key[k] != kNoT ? __hip_atomic_fetch_add(&acc[key[k]].x, s_A[s], __ATOMIC_RELAXED, C3H_VB_ATOM_SCOPE)
-                              : 1ull << 40;
-    }
-#pragma unroll
-    for (int k = 0; k < kFl; ++k) {
-      const int s = tid + k * kBT;
-      if (key[k] == kNoT) continue;
-      __hip_atomic_fetch_add(&acc[key[k]].y, s_B[s], __ATOMIC_RELAXED, C3H_VB_ATOM_SCOPE);
-      if (s_m[s] < kMarginFlush) __hip_atomic_fetch_min(Mg + key[k], s_m[s], __ATOMIC_RELAXED, C3H_VB_ATOM_SCOPE);
-      if ((old[k] >> 40) == 0) vl[atomicAdd(&s_nnew, 1u)] = key[k];
+      const uint32_t key = s < kBSlots ? s_key[s] : kNoT;
+      const bool have = key != kNoT;
+      const unsigned long long bm = __ballot(have);
+      if (!bm) continue;
+      uint32_t w0 = 0;
+      if (lane == 0) w0 = atomicAdd(&s_nnew, (uint32_t)__popcll(bm));
+      w0 = __shfl(w0, 0, 64);
+      if (have) add_entry(w0 + (uint32_t)__popcll(bm & ((1ull << lane) - 1)), key, s_A[s], s_B[s], s_m[s]);
     }
   }
 #pragma unroll
@@ -1125,7 +971,7 @@ __global__ __launch_bounds__(kBlock) void voxb_reduce_kernel(VoxBatchArgs a) {
   }
   a.lim[4 * f + 3] = 0;
   rec.n_valid = (uint32_t)tv;
-  rec.n_occ = (uint32_t)tn;
+  rec.n_occ = 0;  // the scatter counts the voxels (one owning entry each; tn counts entries)
   rec.flagged = 0;  // the scatter adds its flags
   rec.err = (err ? 1u : 0u) | (over ? 2u : 0u);
   rec.moved = 0;
@@ -1149,8 +995,9 @@ __global__ __launch_bounds__(kBlock) void voxb_scatter_kernel(VoxBatchArgs a) {
   const uint32_t* vl = a.vlist + (size_t)b * kBChunk;
   uint32_t* wl = a.wlist + (size_t)b * kBChunk;
   ulonglong2* __restrict__ acc = a.acc + f * a.s_acc;
-  uint32_t* __restrict__ Mg = a.accM + f * a.s_acc;
+  unsigned long long* __restrict__ MO = a.accMO + f * a.s_acc;
   uint32_t* __restrict__ grid = a.grid[f];
+  const uint32_t q0 = (uint32_t)b * (uint32_t)kBChunk;
   // the tick's tile stamps (occupancy_bits_body's rule: a centre voxel of subdivision
   // t = mx[x] + ns0 (my[y] + ns1 mz[z]) stamps t; the first stamper lists it)
   const int16_t* __restrict__ ax = a.axmap;
@@ -1164,16 +1011,26 @@ __global__ __launch_bounds__(kBlock) void voxb_scatter_kernel(VoxBatchArgs a) {
     for (int i = tid; i < (a.ntiles + 31) / 32; i += kBlock) vb_stamped[i] = 0u;
     __syncthreads();
   }
-  uint32_t flagged = 0;
+  uint32_t flagged = 0, owned = 0;
   for (int i0 = 0; i0 < nseg; i0 += kBlock) {  // wave-uniform trip count (the stamp ballots)
     const int i = i0 + tid;
     int tile = -1;
+    bool own = false;
+    uint32_t t = 0;
+    unsigned long long mo = 0;
     if (i < nseg) {
-      const uint32_t t = vl[i];
+      t = vl[i];
+      mo = MO[t];
+      own = (uint32_t)mo == q0 + (uint32_t)i;  // this entry owns the voxel (the min of its entries)
+      if (!own) wl[i] = kNoT;                 // another entry writes (and later clears) the word
+    }
+    if (own) {
+      ++owned;
       const ulonglong2 v = acc[t];
-      const uint32_t m = Mg[t];
+      const uint32_t m = (uint32_t)(mo >> 32);
+      // every entry of the voxel has read MO[t] or reads ~0 after this (not its id either)
       acc[t] = make_ulonglong2(0ull, 0ull);
-      if (m != kNoMargin) Mg[t] = kNoMargin;  // only the rare near-face voxels changed it
+      MO[t] = ~0ull;
       // offsets from min_b: the toroidal coordinates minus min_b, modulo 2^tb
       const uint32_t cx = ((t & mx_) - (uint32_t)lo[0]) & mx_;
       const uint32_t cy = (((t >> sy) & my_) - (uint32_t)lo[1]) & my_;
@@ -1226,7 +1083,9 @@ __global__ __launch_bounds__(kBlock) void voxb_scatter_kernel(VoxBatchArgs a) {
     }
   }
   flagged = wave_reduce(flagged, [](uint32_t u, uint32_t v) { return u + v; });
+  owned = wave_reduce(owned, [](uint32_t u, uint32_t v) { return u + v; });
   if ((tid & 63) == 0 && flagged) atomicAdd(&a.info[f].flagged, flagged);
+  if ((tid & 63) == 0 && owned) atomicAdd(&a.info[f].n_occ, owned);
 }
 
 // ---- exact centroids of the flagged voxels (round 4) ---------------------------------
@@ -1259,15 +1118,13 @@ __global__ __launch_bounds__(kBT) void voxb_bucket_kernel(VoxBatchArgs a) {
   const int64_t n = a.n[f];
   const uint32_t mx_ = (1u << a.tb[0]) - 1, my_ = (1u << a.tb[1]) - 1, mz_ = (1u << a.tb[2]) - 1;
   const int sy = a.tb[0], sz = a.tb[0] + a.tb[1];
-  VoxArgs q{};
-  q.inv = a.inv;
   for (int j = 0; j < kBPer; ++j) {
     const int64_t i = base + (int64_t)j * kBT + tid;
     if (i >= n) break;
     const float4 p = pts[i];
     int c[3];
     float margin;
-    if (!point_valid(p, a.z_limit) || !point_cell(q, p, c, &margin)) continue;
+    if (!point_valid(p, a.z_limit) || !point_cell(a.inv, p, c, &margin)) continue;
     const uint32_t t = ((uint32_t)c[0] & mx_) | (((uint32_t)c[1] & my_) << sy) | (((uint32_t)c[2] & mz_) << sz);
     uint32_t h = (t * 0x9E3779B1u) >> (32 - __builtin_ctz(kVbFlagSlots));
     for (;;) {
@@ -1331,6 +1188,15 @@ __global__ __launch_bounds__(kBlock) void voxb_exact_kernel(VoxBatchArgs a) {
       moved = moved || bc[ax] != own[ax];
     }
     if (!moved) continue;
+    // a centroid cell past the canvas (a frame whose extent fills an axis, a boundary voxel
+    // whose centroid rounds up past it): the fixup's canvas maps have no entry there (its
+    // centre subdivision would be dropped), while the reference may still count the voxel
+    // in the last subdivision -- the frame takes the single-frame path.  (Below the canvas,
+    // bc = -1, the reference's tmp < 0 is no centre either: the fixup agrees.)
+    if (bc[0] >= Cx || bc[1] >= Cy || bc[2] >= a.C[2]) {
+      atomicOr(&rec.err, 8u);
+      continue;
+    }
     if (a.subdiv > 0) {  // computeC3HLAC's subdivision of the centroid (c3_hlac.cpp:349-362)
       bool centre = true, past = false;
       for (int ax = 0; ax < 3; ++ax) {
@@ -1379,6 +1245,30 @@ hipError_t launch_voxelize(const VoxArgs& a, hipStream_t s) {
   if (a.nblk > 0) vox_scatter_kernel<<<(unsigned)a.nblk, kBlock, 0, s>>>(a);
   return hipGetLastError();
 }
+
+#ifdef C3H_DIAG
+// diagnostics: accumulator cells not back at zero / ~0 after a frame (out[0] = count,
+// out[1 + 4 k ..] = t, acc.x lo, acc.x hi, mo lo of the first 64)
+__global__ void vox_dirty_kernel(const ulonglong2* acc, const unsigned long long* mo, int64_t tor, uint32_t* out) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < tor; t += (int64_t)gridDim.x * blockDim.x) {
+    const ulonglong2 v = acc[t];
+    if (v.x | v.y || mo[t] != ~0ull) {
+      const uint32_t k = atomicAdd(out, 1u);
+      if (k < 64) {
+        out[1 + 4 * k] = (uint32_t)t;
+        out[2 + 4 * k] = (uint32_t)v.x;
+        out[3 + 4 * k] = (uint32_t)(v.x >> 32);
+        out[4 + 4 * k] = (uint32_t)mo[t];
+      }
+    }
+  }
+}
+hipError_t launch_vox_dirty(const ulonglong2* acc, const unsigned long long* mo, int64_t tor, uint32_t* out,
+                            hipStream_t s) {
+  vox_dirty_kernel<<<2048, kBlock, 0, s>>>(acc, mo, tor, out);
+  return hipGetLastError();
+}
+#endif
 
 hipError_t launch_vox_scatter(const VoxArgs& a, hipStream_t s) {
   if (a.nblk > 0) vox_scatter_kernel<<<(unsigned)a.nblk, kBlock, 0, s>>>(a);

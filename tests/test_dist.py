@@ -253,3 +253,121 @@ def test_merge_slab_scores_equals_whole_scene_replay(ranges, world):
     for f in ("x", "y", "z", "mode"):
         np.testing.assert_array_equal(lists[f], ref[f])
     np.testing.assert_allclose(lists["score"], ref["score"], rtol=1e-12)
+
+
+def _random_scene_parts(rng, grid, subdiv, ranges, M, world, rotate=True):
+    """Whole-scene score arrays of a random scene (smooth field + noise, gated holes, a few
+    sharp peaks next to slab boundaries: a peak of one slab suppresses the other slab's top
+    positions through checkOverlap, so low positions of that slab enter the lists) and every
+    rank's owned blocks of them."""
+    from c3hlac.dist import _mode_geoms, mode_ranges, mode_schedule, owned_blocks, scene_subdivisions, slab_extent
+    sbg = scene_subdivisions(grid, subdiv)
+    full = []
+    for _, xe, ye, ze in _mode_geoms(sbg, ranges, rotate):
+        z, y, x = np.meshgrid(np.arange(ze), np.arange(ye), np.arange(xe), indexing="ij")
+        a = []
+        for m in range(M):
+            f = 0.3 + 0.1 * np.sin(x * rng.random() + y * rng.random() + z * rng.random())
+            f = f + 0.01 * rng.random(f.shape)
+            f[rng.random(f.shape) < 0.2] = -1.0
+            for _ in range(3):  # peaks
+                f[rng.integers(ze), rng.integers(ye), rng.integers(xe)] = 0.6 + 0.1 * rng.random()
+            a.append(f)
+        full.append(np.stack(a).reshape(-1))
+    scores = np.concatenate(full)
+    zr_max = max(mode_ranges(md, ranges)[2] for md in mode_schedule(ranges, rotate))
+    locals_ = []
+    for r in range(world):
+        ext = slab_extent(grid[2], subdiv, zr_max, r, world)
+        if ext is None:
+            locals_.append(None)
+            continue
+        p0, p1 = ext[0], ext[1]
+        blocks, o = [], 0
+        for _, xe, ye, ze in _mode_geoms(sbg, ranges, rotate):
+            blk = scores[o:o + M * ze * ye * xe].reshape(M, ze, ye, xe)
+            blocks.append(np.ascontiguousarray(blk[:, p0:max(p0, min(p1, ze))]))
+            o += M * ze * ye * xe
+        locals_.append((p0, blocks))
+    return sbg, scores, locals_
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_candidate_merge_equals_dense_replay(seed):
+    """The z-slab candidate merge: slabs send only positions above
+    their own local rank-th score plus per-row bounds of the rest, unresolved rows are
+    fetched whole; the lists equal the dense replay over every score (c3h_replay_scores),
+    on random scenes with peaks that make low positions enter across slab boundaries."""
+    from c3hlac import replay_scores
+    from c3hlac._capi import DET_DTYPE
+    from c3hlac.dist import merge_slab_candidates
+    rng = np.random.default_rng(seed)
+    ranges = [(2, 2, 2), (1, 2, 3), (3, 1, 1), (2, 3, 2)][seed % 4]
+    world = [2, 3, 5, 8][seed % 4]
+    M, srank = 3, [2, 4, 6][seed % 3]
+    grid = (70, 60, 90)
+    sbg, scores, locals_ = _random_scene_parts(rng, grid, 5, ranges, M, world)
+    ref = replay_scores(scores, sbg, ranges, np.zeros((M, srank), DET_DTYPE))
+    got, st = merge_slab_candidates(locals_, grid, 5, ranges, M, srank)
+    assert np.array_equal(got, ref)
+    dense = scores.size * 8
+    assert sum(st["bytes_per_rank"]) < dense  # less than every score once
+
+
+def test_candidate_merge_needs_row_rounds():
+    """A scene built so the first guess fails: slab 1's own top positions all overlap a peak
+    of slab 0 reaching into its planes, so its (unsent) low positions enter the lists; the
+    row bounds expose them and the rows are fetched."""
+    from c3hlac import replay_scores
+    from c3hlac._capi import DET_DTYPE
+    from c3hlac.dist import merge_slab_candidates, _mode_geoms, scene_subdivisions
+    ranges, M, srank, world, grid, S = (2, 2, 2), 1, 3, 2, (40, 40, 40), 5
+    sbg = scene_subdivisions(grid, S)
+    (_, xe, ye, ze), = _mode_geoms(sbg, ranges, False)
+    a = np.full((ze, ye, xe), 0.05)  # a[z, y, x]
+    a[3, 3, 3] = 0.99            # slab 0 (planes 0..3): a peak in its last plane
+    # slab 1's four best positions, mutually apart (checkOverlap: more than the box range
+    # in x or y) but each overlapping the peak's box: its local lists hold three of them
+    # (local rank-3 score 0.9), the whole scene's drops them all
+    a[4, 1, 1] = a[4, 1, 4] = a[4, 4, 1] = a[4, 4, 4] = 0.9
+    a[6, 6, 6] = 0.2             # below slab 1's local rank-th score, yet enters the lists
+    scores = a.reshape(-1).copy()
+    locals_ = [(0, [a[None, 0:4].copy()]), (4, [a[None, 4:7].copy()])]
+    ref = replay_scores(scores, sbg, ranges, np.zeros((M, srank), DET_DTYPE), rotate=False)
+    got, st = merge_slab_candidates(locals_, grid, S, ranges, M, srank, rotate=False)
+    assert np.array_equal(got, ref)
+    assert st["row_rounds"] >= 1
+    assert any(int(e["z"]) == 6 for e in ref[0])  # the low position is in the lists
+
+
+def _cand_worker(rank, world, port, seed, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from c3hlac.dist import gather_slab_scores
+    rng = np.random.default_rng(seed)
+    sbg, scores, locals_ = _random_scene_parts(rng, (70, 60, 90), 5, (1, 2, 3), 3, world)
+    st = {}
+    out = gather_slab_scores(locals_[rank], (70, 60, 90), 5, (1, 2, 3), 3, 4, dist, stats=st)
+    q.put((rank, out.tobytes(), st["row_rounds"]))
+    dist.destroy_process_group()
+
+
+def test_gloo_candidate_merge_world_three():
+    """The candidate merge over gloo at world size 3 (size exchange, candidates, row
+    rounds): every rank's lists equal the dense replay."""
+    from c3hlac import replay_scores
+    from c3hlac._capi import DET_DTYPE
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cand_worker, args=(r, 3, port, 5, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sbg, scores, _ = _random_scene_parts(np.random.default_rng(5), (70, 60, 90), 5, (1, 2, 3), 3, 3)
+    ref = replay_scores(scores, sbg, (1, 2, 3), np.zeros((3, 4), DET_DTYPE))
+    for rank, raw, _ in res:
+        assert np.array_equal(np.frombuffer(raw, DET_DTYPE).reshape(3, 4), ref)

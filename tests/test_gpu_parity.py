@@ -209,18 +209,20 @@ def test_multipoint_voxel_colour_mean(ctx):
 
 
 def test_voxel_table_regrows(ctx):
-    """The single-frame voxeliser sizes its hash table from the previous frame's voxel count
-    (round 4): a small frame followed by 400k scattered points (~400k voxels) fills it, and
-    the frame runs again on larger tables -- the grid, colours and downsampled cloud are the
-    oracle's, and a small frame after it is exact too."""
+    """The single-frame voxeliser accumulates into toroidal arrays of 2^tb cells per axis
+    sized by the frames so far (round 5; 128^3 at first): a frame whose extent exceeds them
+    on any axis runs again on dims that fit it.  Small, large (400k scattered points), long
+    (300 cells in x, then 270 in y and 160 in z) and small frames again: the grid, colours
+    and downsampled cloud are the oracle's after every change of dims."""
     rng = np.random.default_rng(11)
 
     def cloud(n, span):
-        xyz = (rng.random((n, 3)) * span).astype(np.float32)
+        xyz = (rng.random((n, 3)) * np.asarray(span, np.float64)).astype(np.float32)
         col = rng.integers(0, 256, (n, 3))
         return np.concatenate([xyz, synth.pack_rgb(col[:, 0], col[:, 1], col[:, 2])[:, None]], 1).astype(np.float32)
 
-    for pts in (cloud(2000, 0.05), cloud(400_000, 1.0), cloud(3000, 0.08)):
+    for pts in (cloud(2000, 0.05), cloud(400_000, 1.0), cloud(3000, 0.08), cloud(50_000, (3.0, 0.2, 0.2)),
+                cloud(60_000, (0.2, 2.7, 1.6)), cloud(1500, 0.04)):
         gi = ctx.voxelize(pts, 0.01)
         g, layout, cl = po.voxelize(pts, 0.01)
         assert list(gi.div_b) == list(g.div_b) and gi.n_occ == (layout >= 0).sum()

@@ -181,6 +181,61 @@ def test_mixed_geometries_in_one_batch(ctx, bases):
     ctx.set_batch(32)
 
 
+def test_centroid_rounding_past_a_full_canvas(ctx):
+    """A frame whose extent fills the canvas (32^3 at leaf 0.01) with a voxel in the last
+    x cell whose three points' fp32 centroid rounds up onto the face x = 32 * leaf: the
+    reference counts it in subdivision 5 of 6 ((32 - 0) % 6 != 0, c3_hlac.cpp:349-362), the
+    batch's canvas maps have no cell 32, so the frame must leave the batch (status 1) and
+    give the single-frame path's records; a control frame without that voxel stays batched."""
+    import torch
+    dev = torch.device("cuda", 0)
+    f32 = np.float32
+    leaf = f32(0.01)
+    rng = np.random.default_rng(5)
+    xyz = (rng.integers(0, 32, (4000, 3)) + rng.random((4000, 3)) * 0.8 + 0.1).astype(f32) * leaf
+    special = np.array([31, 10, 12])
+    cells = np.floor(xyz * (f32(1) / leaf)).astype(int)
+    xyz = xyz[~(cells == special).all(1)]
+    corners = np.array([[0.5, 0.5, 0.5], [31.5, 31.5, 31.5]], f32) * leaf  # extent 0..31 on every axis
+    x_face = f32(0.31999996)  # 3 points: fp32 sum * fl(1/3) = 0.32 -> floor(c / leaf) = 32
+    pts3 = np.array([[x_face, (10.5 * leaf), (12.5 * leaf)]] * 3, f32)
+    col = rng.integers(0, 256, (len(xyz) + 5, 3))
+    rgb = synth.pack_rgb(col[:, 0], col[:, 1], col[:, 2])
+
+    def cloud(with_special):
+        p = np.concatenate([xyz, corners] + ([pts3] if with_special else []), 0)
+        return np.ascontiguousarray(np.concatenate([p, rgb[:len(p), None]], 1), f32)
+
+    frames = [cloud(True), cloud(False)]
+    g, layout, cl = po.voxelize(frames[0], float(leaf))
+    assert list(g.div_b) == [32, 32, 32] and list(g.min_b) == [0, 0, 0]
+    occ = np.flatnonzero(layout >= 0)
+    k = occ[np.flatnonzero(occ == special[0] + 32 * (special[1] + 32 * special[2]))[0]]
+    assert int(np.floor(cl[layout[k], 0] / leaf)) == 32  # the case under test is there
+    axis_t, var, axis_q = synth.random_bases(117, 24, 2, 6, seed=41)
+    ctx.search_setup(axis_t, var, axis_q)
+    ctx.set_rank(1)
+    ctx.set_batch(8)
+    devf = [torch.from_numpy(f).to(dev) for f in frames]
+    torch.cuda.synchronize()
+    d_out = torch.zeros((2, 6), dtype=torch.int64, device=dev)
+    _, info = ctx.run_point_frames(devf, float(leaf), (32, 32, 32), 117, THR, 6, BOX, 0, True, d_out)
+    got = d_out.cpu().numpy().view(c3hlac.DET_DTYPE).reshape(2, 2)
+    assert list(info["status"]) == [1, 0], info
+    for i in range(2):
+        ctx.voxelize(devf[i], float(leaf))
+        ctx.extract(117, THR, 6)
+        ctx.set_rank(1)
+        ref, _ = ctx.search(BOX, 0)
+        assert np.array_equal(got[i], ref[:, 0]), (i, got[i], ref[:, 0])
+    # the single-frame path on the special frame against the oracle's exact features
+    ctx.voxelize(devf[0], float(leaf))
+    ctx.extract(117, THR, 6)
+    fe, _, _ = po.c3hlac(g, layout, cl, 117, THR, float(leaf), 6, exact=True)
+    assert np.array_equal(ctx.features(), fe)
+    ctx.set_batch(32)
+
+
 def test_points_in_256_canvas_overlap_and_repeat(ctx):
     """256^3 canvases (C3-HLAC-117 + 3 models): the batch scatter stamps the tick's tiles
     (no occupancy stream), the voxeliser runs on its own stream beside the tick.  Two calls

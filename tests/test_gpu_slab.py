@@ -80,3 +80,42 @@ def test_slabs_rank_above_one_kinect_256(ctx, srank, world, ranges):
     scores, lists = merge_slab_scores(parts, (d[0], d[1], d[2]), 10, ranges, srank)
     assert np.array_equal(scores, whole_scores)
     assert np.array_equal(lists, np.ascontiguousarray(whole))
+    # the candidate merge (what gather_slab_scores sends over the collective) gives the same
+    from c3hlac.dist import merge_slab_candidates
+    cand, st = merge_slab_candidates(parts, (d[0], d[1], d[2]), 10, ranges, 10, srank)
+    assert np.array_equal(cand, np.ascontiguousarray(whole))
+    assert sum(st["bytes_per_rank"]) < scores.size * 8
+
+
+def test_slab_merge_rank4_dense_512_eight_slabs(ctx, record_property):
+    """512^3 (random dense words: no ties), C3-HLAC-981, M = 10 x r = 20,
+    rank 4, 8 slabs on this GPU one after another.  Dense merge (every owned score) and the
+    candidate merge give the whole-scene search's lists bit for bit; the candidate payload
+    and both merges' host times are recorded (json in the test's stdout)."""
+    import json
+    import time
+    from c3hlac.dist import merge_slab_candidates, merge_slab_scores, slab_scores
+    G, S, world, srank, ranges = 512, 10, 8, 4, (2, 2, 2)
+    words = synth.random_words(G, 0.5, seed=61, colour_max=255).reshape(G, G, G)
+    axis_t, var, axis_q = synth.random_bases(981, 100, 10, 20, seed=62)
+    ctx.search_setup(axis_t, var, axis_q)
+    ctx.set_grid(np.ascontiguousarray(words).reshape(-1), (G, G, G))
+    ctx.extract(981, THR, S)
+    ctx.set_rank(srank)
+    whole, _ = ctx.search(ranges, 100)
+    whole = np.ascontiguousarray(whole)
+    assert (whole["score"] > 0).all()
+    parts = [slab_scores(ctx, words, 981, THR, S, ranges, 100, r, world) for r in range(world)]
+    t0 = time.perf_counter()
+    scores, dense_lists = merge_slab_scores(parts, (G, G, G), S, ranges, srank)
+    t1 = time.perf_counter()
+    cand, st = merge_slab_candidates(parts, (G, G, G), S, ranges, 10, srank)
+    t2 = time.perf_counter()
+    assert np.array_equal(dense_lists, whole)
+    assert np.array_equal(cand, whole)
+    rec = {"dense_bytes_per_rank_max": max(sum(b.size for b in p[1]) * 8 for p in parts),
+           "candidate_bytes_per_rank": st["bytes_per_rank"], "row_rounds": st["row_rounds"],
+           "dense_merge_s": t1 - t0, "candidate_merge_s": t2 - t1}
+    print("slab_merge_512:", json.dumps(rec))
+    record_property("slab_merge_512", rec)
+    assert max(st["bytes_per_rank"]) * 4 < rec["dense_bytes_per_rank_max"]
