@@ -154,7 +154,12 @@ def load(path=None):
             "libc3hlac_mi355x.so not found at %s: build it with `make -C mapping-private_amd` "
             "(or __graft_entry__.build()); there is no CPU fallback" % p)
     lib = C.CDLL(str(p))
+    # a diagnostics override (C3HLAC_LIB: an older build in an A/B) may lack newer entry
+    # points; the product library must export every one
+    lenient = path is None and "C3HLAC_LIB" in os.environ
     for name, (res, args) in _SIGS.items():
+        if lenient and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

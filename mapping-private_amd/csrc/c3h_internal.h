@@ -125,6 +125,9 @@ struct VoxArgs {
   int clear_grid;           // clear the grid words the previous frame listed
 };
 hipError_t launch_voxelize(const VoxArgs& a, hipStream_t s);
+// f16 feature rows -> f32 rows when *flag (device-side check: no host sync)
+hipError_t launch_feat16_to_f32(const _Float16* f16, int f16s, const uint32_t* flag, int64_t H, int F, float* out,
+                                hipStream_t s);
 #ifdef C3H_DIAG
 hipError_t launch_vox_dirty(const ulonglong2* acc, const unsigned long long* mo, int64_t tor, uint32_t* out,
                             hipStream_t s);
@@ -282,6 +285,11 @@ struct C3Launch {
   long long* prof;  // diagnostics (C3H_PROF)
   int debug;
   uint32_t* dense = nullptr;  // stand-alone large grids: the density probe's verdict word
+  // fp16 search precision on large grids: the dense MFMA body writes the feature rows as
+  // f16 (row stride f16s halves) and sets *feat16_flag; the f32 rows are then not written
+  _Float16* feat16 = nullptr;
+  uint32_t* feat16_flag = nullptr;
+  int f16s = 0;
 };
 
 int64_t c3hlac_grid(const C3Launch& a);  // persistent grid of the tile kernel
@@ -417,9 +425,13 @@ struct SparseCompress {
   int64_t s_feat, s_G, s_rows, s_nrows;  // per-frame strides
   const _Float16* PT16 = nullptr;         // fp16 search precision: f16 axis, 128 x Fp16
   int Fp16 = 0;
+  const _Float16* feat16 = nullptr;       // f16 feature rows (stride f16s) when *feat16_flag
+  const uint32_t* feat16_flag = nullptr;
+  int f16s = 0;
 };
 bool compress_rows_ok(int F, int Dpad);
 constexpr int64_t kBoxsumRows = 65536;  // subdivisions from which the search precomputes box sums
+constexpr int64_t kCompressMfmaRows = 65536;  // ... and compresses on the matrix cores
 hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc, hipStream_t s);
 int64_t sparse_score_blocks(const SparseSearch& a);
 
@@ -568,6 +580,10 @@ struct c3h_ctx {
   c3h::DevBuf<_Float16> axis_pt16;  // 128 x Fp16 f16 copy (column-major) for the fp16 compress
   int Fp16 = 0;
   bool prec16 = false;              // c3h_set_search_precision: fp16 matrix-core compress
+  c3h::DevBuf<_Float16> feat16;     // f16 feature rows of the last large dense extract (prec16)
+  c3h::DevBuf<uint32_t> feat16_flag;
+  bool feat16_pending = false;      // the last extract may have written f16 rows only
+  int feat16_s = 0;                 // their row stride (halves)
   int score_engine = 0;             // c3h_set_score_engine: 0 auto, 1 VALU, 2 matrix cores
   c3h::DevBuf<_Float16> qt16;       // f16 basis for the fp16 matrix-core projection
   int Kq16 = 0;

@@ -586,6 +586,9 @@ C3Args build_c3_args(const C3Launch& l) {
   a.lut = l.lut;
   a.feat = l.feat;
   a.exist = l.exist;
+  a.feat16 = l.feat16;
+  a.feat16_flag = l.feat16_flag;
+  a.f16s = l.f16s;
   a.acc64 = l.acc64;
   a.tf = l.tf;
   a.flags = l.tf + 4;
@@ -605,6 +608,23 @@ C3Args build_c3_args(const C3Launch& l) {
   c.tgrid = (int)c3hlac_grid(l);
   c.nframes = l.nframes;
   return c;
+}
+
+__global__ __launch_bounds__(kBlock) void feat16_to_f32_kernel(const _Float16* __restrict__ f16, int f16s,
+                                                                const uint32_t* __restrict__ flag, int64_t H, int F,
+                                                                float* __restrict__ out) {
+  if (!*flag) return;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < H * F; i += (int64_t)gridDim.x * kBlock) {
+    const int64_t h = i / F;
+    out[i] = (float)f16[h * f16s + (i - h * F)];
+  }
+}
+
+hipError_t launch_feat16_to_f32(const _Float16* f16, int f16s, const uint32_t* flag, int64_t H, int F, float* out,
+                                hipStream_t s) {
+  const int64_t g = std::min<int64_t>((H * F + kBlock - 1) / kBlock, 8192);
+  if (g > 0) feat16_to_f32_kernel<<<(unsigned)g, kBlock, 0, s>>>(f16, f16s, flag, H, F, out);
+  return hipGetLastError();
 }
 
 // dense-tile MFMA kernel: tiles up to 16 x 16 per layer, resident persistent grid

@@ -634,6 +634,9 @@ struct KArgs {
   int mfma;         // the dense-tile MFMA kernel runs beside (c3hlac_mfma.h): frames with
                     // >= half of their tiles non-empty are left to it
   int mf_pb;        // its largest channel-plane size (mf_plane_bytes of the largest tile)
+  _Float16* feat16;     // C3Launch::feat16 (nullable), its row stride, the frame's flag
+  uint32_t* feat16_flag;
+  int f16s;
   int debug;  // diagnostics only (C3H_C3_DEBUG): 1 stop after the loads, 2 after compaction,
              // 3 skip the tile kernel
 };

@@ -801,9 +801,20 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
       }
       __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's values are in LDS
       __builtin_amdgcn_wave_barrier();
-      float* out = ffeat + h * F;
+      if (a.feat16) {  // fp16 search precision: the row as f16 pairs (half the bytes)
+        uint32_t* out2 = reinterpret_cast<uint32_t*>(a.feat16 + h * a.f16s);
+#pragma unroll 2
+        for (int i = lane; i < 491; i += 64) {
+          const _Float16 lo = (_Float16)sf[s_src[2 * i]];
+          const _Float16 hi = 2 * i + 1 < 981 ? (_Float16)sf[s_src[2 * i + 1]] : (_Float16)0.0f;
+          out2[i] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+        }
+        if (wid == 0 && lane == 0) *a.feat16_flag = 1u;
+      } else {
+        float* out = ffeat + h * F;
 #pragma unroll 4
-      for (int i = lane; i < 981; i += 64) out[i] = sf[s_src[i]];
+        for (int i = lane; i < 981; i += 64) out[i] = sf[s_src[i]];
+      }
       mf_compiler_fence();  // the next tile's planes overwrite sf after these reads
     } else if (a.atomic || F == 981) {
       float* out = ffeat + h * F;

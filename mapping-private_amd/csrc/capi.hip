@@ -356,6 +356,16 @@ int sync_host_lists(c3h_ctx* ctx) {
 #endif
 constexpr int kSparseScores = C3H_SPARSE_SCORES;
 
+// The f32 feature rows of the last extract when it wrote them as f16 (fp16 search precision
+// on a large dense grid): converted on the device if the MFMA body set the flag.
+int feat_rows_f32(c3h_ctx* ctx) {
+  if (!ctx->feat16_pending) return C3H_OK;
+  HIPCHK(c3h::launch_feat16_to_f32(ctx->feat16.p, ctx->feat16_s, ctx->feat16_flag.p, ctx->hist_num, ctx->feat_dim,
+                                   ctx->feat.p, ctx->stream));
+  ctx->feat16_pending = false;
+  return C3H_OK;
+}
+
 int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int32_t rotate,
                   c3h_det* const* d_outs, int clean) {
   if (!ctx->have_feat) return fail(ctx, C3H_ERR_STATE, "c3h_search: no features (call c3h_extract)");
@@ -409,6 +419,8 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
                         c3h::compress_rows_ok(ctx->F, ctx->Dpad);
   if (ctx->capture && !sparse_g) return 0;  // not pipelinable: the caller falls back
   if (!ctx->g_valid && !sparse_g) {  // dense compress of every frame of the extract
+    int rc = feat_rows_f32(ctx);
+    if (rc != C3H_OK) return rc;
     Timed t(ctx, 2, nf);
     for (int f = 0; f < nf; ++f)
       HIPCHK(c3h::launch_compress(ctx->feat.p + (size_t)f * H * ctx->F, H, ctx->F, ctx->axis_pt.p, ctx->D,
@@ -541,6 +553,16 @@ int search_frames(c3h_ctx* ctx, int nf, const int32_t range[3], int32_t thr, int
       if (ctx->prec16 && ctx->Fp16 > 0) {
         sc.PT16 = ctx->axis_pt16.p;
         sc.Fp16 = ctx->Fp16;
+      }
+      if (ctx->feat16_pending) {
+        if (sc.PT16 && H >= c3h::kCompressMfmaRows && nf == 1) {  // the f16 compress reads the f16 rows
+          sc.feat16 = ctx->feat16.p;
+          sc.feat16_flag = ctx->feat16_flag.p;
+          sc.f16s = ctx->feat16_s;
+        } else {
+          int rc = feat_rows_f32(ctx);
+          if (rc != C3H_OK) return rc;
+        }
       }
       ctx->g_valid = true;
       ctx->g_sparse = true;
@@ -1309,6 +1331,19 @@ int extract_frames(c3h_ctx* ctx, const uint32_t* const* grids, int nf, const c3h
     l.feat = ctx->feat.p;
     l.exist = ctx->exist.p;
     l.acc64 = ctx->acc64.p;
+    // fp16 search precision on a large grid: the dense MFMA body writes f16 rows (the f16
+    // compress reads them; every f32 reader converts them first, feat_rows_f32)
+    ctx->feat16_pending = false;
+    if (ctx->prec16 && nf == 1 && !ctx->capture && !atomic && F == 981 && hist_num >= c3h::kCompressMfmaRows) {
+      ctx->feat16_s = F + (F & 1);
+      ENSURE(ctx->feat16, (size_t)hist_num * ctx->feat16_s);
+      ENSURE(ctx->feat16_flag, 1);
+      HIPCHK(hipMemsetAsync(ctx->feat16_flag.p, 0, 4, ctx->stream));
+      l.feat16 = ctx->feat16.p;
+      l.feat16_flag = ctx->feat16_flag.p;
+      l.f16s = ctx->feat16_s;
+      ctx->feat16_pending = true;
+    }
     l.axmap = ctx->axmap.p;
     {  // closed-form y / z maps (uniform subdivisions from an offset): the occupancy stream
        // computes a row's segment with two scalar multiplies instead of two LDS lookups
@@ -1597,6 +1632,7 @@ int c3h_extract_grsd(c3h_ctx* ctx, const c3h_grsd_params* p, int32_t subdiv_out[
   int64_t H = 0;
   int rc = grsd_frames(ctx, p, sb, &H);
   if (rc != C3H_OK) return rc;
+  ctx->feat16_pending = false;
   ENSURE(ctx->feat, (size_t)std::max<int64_t>(H, 1) * 20);
   ENSURE(ctx->exist, (size_t)std::max<int64_t>(H, 1));
   if (H > 0) {
@@ -1678,6 +1714,7 @@ int c3h_set_features(c3h_ctx* ctx, const float* feat, const int32_t subdiv_b[3],
   HIPCHK(hipSetDevice(ctx->device));
   const int64_t H = (int64_t)subdiv_b[0] * subdiv_b[1] * subdiv_b[2];
   if (H > 0 && !feat) return C3H_ERR_ARG;
+  ctx->feat16_pending = false;  // the caller's rows replace the extract's
   ctx->have_feat = false;
   ctx->g_valid = false;
   ctx->rows_valid = false;
@@ -1737,6 +1774,10 @@ int c3h_get_features(c3h_ctx* ctx, float* out, int on_device) {
   if (!ctx->have_feat) return fail(ctx, C3H_ERR_STATE, "no features");
   HIPCHK(hipSetDevice(ctx->device));
   const size_t n = (size_t)ctx->hist_num * ctx->feat_dim;
+  {
+    int rc = feat_rows_f32(ctx);
+    if (rc != C3H_OK) return rc;
+  }
   if (n && ctx->feat_sparse) return masked_readback(ctx, ctx->feat.p, ctx->feat_dim, out, on_device);
   if (n) HIPCHK(hipMemcpyAsync(out, ctx->feat.p, n * 4, on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));

@@ -933,7 +933,7 @@ __global__ __launch_bounds__(64) void replay_kernel(const double* __restrict__ s
 
 // subdivision counts from which the stand-alone search compresses on the matrix cores
 // (512^3 at S = 10: 140,608; the bench's 256^3 frames, 17,576, keep the fused VALU launch)
-constexpr int64_t kCompressMfmaRows = 65536;
+// kCompressMfmaRows (c3h_internal.h): the matrix-core compresses from this many rows
 
 bool compress_rows_ok(int F, int Dpad) {
   (void)F;
@@ -1010,7 +1010,8 @@ hipError_t launch_sparse_search(const SparseSearch& a, const SparseCompress* sc,
   const unsigned nf = (unsigned)a.nframes;
   if (sc) {  // compress (non-empty rows) and gate in one launch
     const CompressRows cr{sc->feat, sc->PT, sc->fmax, sc->G, sc->rows, sc->nrows, sc->F, sc->D, sc->Dpad,
-                          sc->fmax_len, sc->s_feat, sc->s_G, sc->s_rows, sc->s_nrows, sc->H};
+                          sc->fmax_len, sc->s_feat, sc->s_G, sc->s_rows, sc->s_nrows, sc->H,
+                          sc->PT16 ? sc->feat16 : nullptr, sc->feat16_flag, sc->f16s};
     if (sc->H >= kCompressMfmaRows) {  // large grids: the f32 matrix-core compress, then the gate
       // persistent: every workgroup resident (row blocks b, b + grid, ...), so no partial
       // last round of workgroups

@@ -30,6 +30,9 @@ struct CompressRows {
   int F, D, Dpad, fmax_len;
   int64_t s_feat, s_G, s_rows, s_nrows;  // per-frame strides (frame = launch y / z index)
   int64_t H = 0;  // subdivisions per frame: a list of all H rows is read as rows 0..H-1 in order
+  const _Float16* feat16 = nullptr;  // f16 rows (stride f16s) instead of feat when *feat16_flag
+  const uint32_t* feat16_flag = nullptr;
+  int f16s = 0;
 };
 
 __device__ __forceinline__ void compress_rows_body(const CompressRows& cr, int bid, int nblk, int64_t f,
@@ -270,6 +273,7 @@ __device__ __forceinline__ void compress_f16_body(const CompressRows& cr, const 
   _Float16* As = smem;               // [128 rows][kCFS]
   _Float16* Bs = smem + 128 * kCFS;  // [128 columns][kCFS]
   const bool ident = n == cr.H;
+  const _Float16* __restrict__ f16 = (cr.feat16 && *cr.feat16_flag) ? cr.feat16 : nullptr;  // uniform
   for (int r0 = bid * kMR; r0 < n; r0 += nblk * kMR) {
     // every subdivision listed (dense frame): the list is a permutation of 0..H-1, so row
     // block r0 covers subdivisions r0.. in memory order instead (contiguous feature rows)
@@ -282,7 +286,10 @@ __device__ __forceinline__ void compress_f16_body(const CompressRows& cr, const 
 #pragma unroll
       for (int j = 0; j < kCFRows; ++j) {
         const int h = __builtin_amdgcn_readlane(hrow, j);
-        areg[j] = (h >= 0 && k < F) ? __builtin_nontemporal_load(feat + (int64_t)h * F + k) : 0.0f;
+        if (f16)
+          areg[j] = (h >= 0 && k < F) ? (float)__builtin_nontemporal_load(f16 + (int64_t)h * cr.f16s + k) : 0.0f;
+        else
+          areg[j] = (h >= 0 && k < F) ? __builtin_nontemporal_load(feat + (int64_t)h * F + k) : 0.0f;
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {

@@ -68,6 +68,25 @@ constexpr int kVoxPer = kVoxChunk / kVB;
 #ifndef C3H_VOX_MERGE
 #define C3H_VOX_MERGE 1  // the run merge (0: every point updates the LDS table itself)
 #endif
+#ifndef C3H_VOX_RMW
+#define C3H_VOX_RMW 2  // the accumulators' plain accesses: 2 = device-scope (coherent) loads and
+                       // stores; 0 = default cache policy, 1 = the owner's read and clear as atomic
+                       // exchanges (diagnostics)
+#endif
+// Loads and stores of the accumulators outside the atomics.  The atomics of one launch land
+// coherently for the whole device; a default-policy load in a later launch could be served
+// from a line an XCD's L2 still holds from an earlier launch (round 5: small frames after a
+// large one read sums their owner XCD had cached before other XCDs' clears and adds).
+template <class T>
+__device__ __forceinline__ T ld_coh(const T* p) {
+  if (C3H_VOX_RMW == 2) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return *p;
+}
+template <class T>
+__device__ __forceinline__ void st_coh(T* p, T v) {
+  if (C3H_VOX_RMW == 2) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
 #ifndef C3H_VOX_ATOM_SCOPE
 #define C3H_VOX_ATOM_SCOPE __HIP_MEMORY_SCOPE_AGENT
 #endif
@@ -407,7 +426,7 @@ __global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
   for (int k = 0; k < kPre; ++k) {
     const int i = threadIdx.x + k * kBlock;
     pt[k] = i < nn ? sl[i] : 0u;
-    pmo[k] = i < nn ? a.mo[pt[k]] : ~0ull;
+    pmo[k] = i < nn ? ld_coh(&a.mo[pt[k]]) : ~0ull;
   }
   const VoxTotals tot = vox_reduce(a, blockIdx.x == 0);
   if (!tot.any) return;
@@ -432,9 +451,20 @@ __global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
       return;
     }
     ++owned;
-    const ulonglong2 v = a.acc[t];
-    a.acc[t] = make_ulonglong2(0ull, 0ull);
-    a.mo[t] = ~0ull;
+#if C3H_VOX_RMW == 1
+    // diagnostics: the owner's read-and-clear as device-scope atomic exchanges
+    ulonglong2 v;
+    v.x = __hip_atomic_exchange(&a.acc[t].x, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    v.y = __hip_atomic_exchange(&a.acc[t].y, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_exchange(&a.mo[t], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    ulonglong2 v;
+    v.x = ld_coh(&a.acc[t].x);
+    v.y = ld_coh(&a.acc[t].y);
+    st_coh(&a.acc[t].x, 0ull);
+    st_coh(&a.acc[t].y, 0ull);
+    st_coh(&a.mo[t], ~0ull);
+#endif
     a.tpos[t] = q;
     uint32_t o[3];
     tor_offsets(a.tb, t, tot.mn, o);
@@ -455,7 +485,7 @@ __global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
   }
   for (int i = threadIdx.x + kPre * kBlock; i < nn; i += kBlock) {
     const uint32_t t = sl[i];
-    visit(i, t, a.mo[t]);
+    visit(i, t, ld_coh(&a.mo[t]));
   }
   flagged = wave_reduce(flagged, [](uint32_t u, uint32_t v) { return u + v; });
   owned = wave_reduce(owned, [](uint32_t u, uint32_t v) { return u + v; });
@@ -1020,17 +1050,20 @@ __global__ __launch_bounds__(kBlock) void voxb_scatter_kernel(VoxBatchArgs a) {
     unsigned long long mo = 0;
     if (i < nseg) {
       t = vl[i];
-      mo = MO[t];
+      mo = ld_coh(&MO[t]);
       own = (uint32_t)mo == q0 + (uint32_t)i;  // this entry owns the voxel (the min of its entries)
       if (!own) wl[i] = kNoT;                 // another entry writes (and later clears) the word
     }
     if (own) {
       ++owned;
-      const ulonglong2 v = acc[t];
+      ulonglong2 v;
+      v.x = ld_coh(&acc[t].x);
+      v.y = ld_coh(&acc[t].y);
       const uint32_t m = (uint32_t)(mo >> 32);
       // every entry of the voxel has read MO[t] or reads ~0 after this (not its id either)
-      acc[t] = make_ulonglong2(0ull, 0ull);
-      MO[t] = ~0ull;
+      st_coh(&acc[t].x, 0ull);
+      st_coh(&acc[t].y, 0ull);
+      st_coh(&MO[t], ~0ull);
       // offsets from min_b: the toroidal coordinates minus min_b, modulo 2^tb
       const uint32_t cx = ((t & mx_) - (uint32_t)lo[0]) & mx_;
       const uint32_t cy = (((t >> sy) & my_) - (uint32_t)lo[1]) & my_;

@@ -231,3 +231,38 @@ def test_dense512_random_search_vs_oracle(ctx, dense512):
         _check_records(l16, scd, P, F16_RTOL, "dense512 f16")
     finally:
         ctx.set_search_precision(False)
+
+
+def test_dense512_fp16_feature_rows(ctx, dense512):
+    """fp16 search precision set before the extract (BASELINE configs[4]: "fp16 features";
+    VERDICT r4 item 4): the dense MFMA body writes the 981-feature rows as f16 (half the
+    bytes; the f16 compress reads them).  The rows are the f32 rows rounded to nearest f16,
+    bit for bit (features() converts them); scores within the fp16 tolerance of the float64
+    oracle; a search at f32 precision on the same extract converts the rows first."""
+    G, S, M, D, R, BOX = 512, 10, 10, 100, 20, (2, 2, 2)
+    ctx.set_grid(dense512.reshape(-1), (G,) * 3, leaf=0.01)
+    sb, H = ctx.extract(981, THR, S)
+    fe = ctx.features()
+    ex = ctx.exist()
+    axis_t, var, axis_q = synth.random_bases(981, D, M, R, seed=5120)
+    ctx.search_setup(axis_t, var, axis_q)
+    _, _, scd = po.search(sb, fe, ex, synth.whiten(axis_t, var), axis_q, BOX, 1, 100, dbl=True, want_scores=True)
+    P = _set_pdims(sb, BOX)
+    ctx.set_search_precision(True)
+    try:
+        ctx.extract(981, THR, S)
+        ctx.set_rank(1)
+        l16, _ = ctx.search(BOX, 100)
+        s16 = ctx.scores()
+        np.testing.assert_allclose(s16, scd, rtol=F16_RTOL)
+        _check_records(l16, scd, P, F16_RTOL, "dense512 f16 rows")
+        f16 = ctx.features()
+        assert np.array_equal(f16, fe.astype(np.float16).astype(np.float32))
+        assert np.array_equal(ctx.exist(), ex)
+        ctx.extract(981, THR, S)
+        ctx.set_search_precision(False)  # f32 search on f16 rows: converted on the device
+        ctx.set_rank(1)
+        ctx.search(BOX, 100)
+        np.testing.assert_allclose(ctx.scores(), scd, rtol=F16_RTOL)
+    finally:
+        ctx.set_search_precision(False)

@@ -1,18 +1,21 @@
 #!/bin/bash
-# round 5, session b: voxelisers without returning atomics (single-frame: toroidal
-# accumulators + owner min; batched: owner min instead of the first-touch add), the staged
-# 981 epilogue of the dense MFMA body, the slab candidate merge -- the whole GPU suite, then
-# interleaved A/Bs against the round-4 kernels (lib/variants/r4*.so, built from HEAD~):
-# single-frame voxeliser (tools/vox_bench.py), config 5 (tools/config5.py), the batched
-# voxeliser (points_bench with and without the voxeliser / tick overlap), kernel traces
+# round 5, session b: the dirty-accumulator diagnostics (plain / exchange / coherent
+# accesses), the whole GPU suite on the product build, then interleaved A/Bs against the
+# round-4 kernels (lib/variants/r4*.so, built from the round-4 sources): single-frame
+# voxeliser (tools/vox_bench.py), config 5 (tools/config5.py), the batched voxeliser
+# (points_bench with and without the voxeliser / tick overlap), kernel traces
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r5b
 mkdir -p $O
-export C3H_REQUIRE_GPU=1
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
-  -s > $O/tests.log 2>&1 || exit 1
 V=$R/mapping-private_amd/lib/variants
+for v in diag diag_rmw diag_ald; do
+  C3HLAC_LIB=$V/$v.so timeout -k 10 300 python3 tools/vox_dirty.py > $O/dirty_$v.jsonl 2> $O/dirty_$v.err || exit 1
+done
+export C3H_REQUIRE_GPU=1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+  -s > $O/tests.log 2>&1
+rc=$?; echo "tests rc=$rc" >> $O/rc.txt; [ $rc -ge 124 ] && exit $rc
 for rep in 1 2; do
   for v in default r4; do
     if [ $v = default ]; then unset C3HLAC_LIB; else export C3HLAC_LIB=$V/$v.so; fi

@@ -8,11 +8,12 @@ from pathlib import Path
 import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
-sys.path[:0] = [str(ROOT / "mapping-private_amd")]
+sys.path[:0] = [str(ROOT / "mapping-private_amd"), str(ROOT / "oracle")]
 
 
 def main():
     import c3hlac
+    import pyoracle as po
     from c3hlac import synth
     rng = np.random.default_rng(11)
 
@@ -28,10 +29,14 @@ def main():
                           ("sparse400k", cloud(400_000, 1.0)), ("sparse100k", cloud(100_000, 1.0)),
                           ("sparse400k_b", cloud(400_000, 1.0)), ("small2", cloud(3000, 0.08))):
             gi = ctx.voxelize(pts, 0.01)
+            g, layout, cl = po.voxelize(pts, 0.01)
+            w = ctx.grid()
+            occ = layout >= 0
+            bad = int((w[occ] != ((1 << 24) | cl[layout[occ], 3].view(np.uint32))).sum())
             out = np.zeros(257, np.uint32)
             rc = f(ctx.h, out.ctypes.data)
             ent = out[1:1 + 4 * min(int(out[0]), 16)].reshape(-1, 4).tolist()
-            print(json.dumps({"frame": name, "n_occ": int(gi.n_occ), "rc": rc, "dirty": int(out[0]),
+            print(json.dumps({"frame": name, "n_occ": int(gi.n_occ), "rc": rc, "dirty": int(out[0]), "bad_words": bad,
                               "first": ent}), flush=True)
 
 
