@@ -442,6 +442,8 @@ def main():
         if "points_in" in result:
             result["points_in"]["cpu_baseline"] = cpu_baseline_points(synth, args.cpu_seconds)
     if rank == 0:
+        from c3hlac import _capi
+        result["build"] = _capi.build_provenance()
         print(json.dumps(result))
     ctx.close()
     if dist:

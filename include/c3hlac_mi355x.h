@@ -80,6 +80,9 @@ typedef struct {
 } c3h_det;
 
 int c3h_version(void);
+/* build provenance (no reference counterpart): "src=<sha256 of the library's sources,
+ * concatenated in sorted path order> arch=<gfx> host=<build host> built=<UTC time>" */
+const char* c3h_build_info(void);
 
 /* context (one device, one stream) */
 int c3h_create(int hip_device, c3h_ctx** out);

@@ -61,6 +61,7 @@ _SIGS = {
     "c3h_set_stream": (C.c_int, [_P, _P]),
     "c3h_synchronize": (C.c_int, [_P]),
     "c3h_last_error": (C.c_char_p, [_P]),
+    "c3h_build_info": (C.c_char_p, []),
     "c3h_voxelize": (C.c_int, [_P, _P, C.c_int64, C.c_int, C.c_float, C.c_float, C.POINTER(GridInfo)]),
     "c3h_voxelize_pointcloud2": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                             C.POINTER(C.c_int32), C.c_int32, C.c_int, C.c_float, C.c_float,
@@ -202,3 +203,24 @@ def ptr(a):
 
 def i32x3(v):
     return (C.c_int32 * 3)(*[int(x) for x in v])
+
+
+def build_provenance():
+    """Which build the process loaded: the library's c3h_build_info() (sha256 of the sources
+    it was compiled from, build host and time) beside the same hash of the sources in this
+    tree (the Makefile's HASHSRC: csrc/*.hip, csrc/*.h, ../include/c3hlac_mi355x.h, sorted
+    by path string, contents concatenated)."""
+    import hashlib
+    lib = load()
+    info = dict(kv.split("=", 1) for kv in lib.c3h_build_info().decode().split())
+    pkg = Path(__file__).resolve().parents[1]
+    names = sorted(["csrc/" + p.name for p in (pkg / "csrc").glob("*.hip")]
+                   + ["csrc/" + p.name for p in (pkg / "csrc").glob("*.h")]
+                   + ["../include/c3hlac_mi355x.h"])
+    h = hashlib.sha256()
+    for n in names:
+        h.update((pkg / n).read_bytes())
+    tree = h.hexdigest()
+    return {"lib": os.path.relpath(os.path.realpath(lib._name), pkg.parent), "lib_src_sha256": info.get("src"),
+            "tree_src_sha256": tree, "lib_matches_tree": info.get("src") == tree,
+            "built_on": info.get("host"), "built_at": info.get("built"), "arch": info.get("arch")}

@@ -69,14 +69,10 @@ constexpr int kVoxPer = kVoxChunk / kVB;
 #define C3H_VOX_MERGE 1  // the run merge (0: every point updates the LDS table itself)
 #endif
 #ifndef C3H_VOX_RMW
-#define C3H_VOX_RMW 2  // the accumulators' plain accesses: 2 = device-scope (coherent) loads and
-                       // stores; 0 = default cache policy, 1 = the owner's read and clear as atomic
-                       // exchanges (diagnostics)
+#define C3H_VOX_RMW 0  // the accumulators' plain accesses in the scatters: 0 = default cache
+                       // policy (the adds are a previous launch's); diagnostics: 1 = the owner's
+                       // read and clear as atomic exchanges, 2 = device-scope loads and stores
 #endif
-// Loads and stores of the accumulators outside the atomics.  The atomics of one launch land
-// coherently for the whole device; a default-policy load in a later launch could be served
-// from a line an XCD's L2 still holds from an earlier launch (round 5: small frames after a
-// large one read sums their owner XCD had cached before other XCDs' clears and adds).
 template <class T>
 __device__ __forceinline__ T ld_coh(const T* p) {
   if (C3H_VOX_RMW == 2) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -86,6 +82,23 @@ template <class T>
 __device__ __forceinline__ void st_coh(T* p, T v) {
   if (C3H_VOX_RMW == 2) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else *p = v;
+}
+// the owner's read and clear of a voxel's sums (one 16-B load and store by default)
+__device__ __forceinline__ ulonglong2 take_acc(ulonglong2* p) {
+  ulonglong2 v;
+  if (C3H_VOX_RMW == 1) {
+    v.x = __hip_atomic_exchange(&p->x, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    v.y = __hip_atomic_exchange(&p->y, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (C3H_VOX_RMW == 2) {
+    v.x = ld_coh(&p->x);
+    v.y = ld_coh(&p->y);
+    st_coh(&p->x, 0ull);
+    st_coh(&p->y, 0ull);
+  } else {
+    v = *p;
+    *p = make_ulonglong2(0ull, 0ull);
+  }
+  return v;
 }
 #ifndef C3H_VOX_ATOM_SCOPE
 #define C3H_VOX_ATOM_SCOPE __HIP_MEMORY_SCOPE_AGENT
@@ -254,8 +267,12 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
     }
     // runs of equal keys inside each 16-lane row: a lane starts a run when it is invalid,
     // the row's first lane, or its key differs from the previous lane's; only a run's last
-    // lane updates the LDS table (same-address LDS atomics serialise)
-    const bool head = !C3H_VOX_MERGE || !valid || (lane & 15) == 0 || vrow_shr<1>(t) != t;
+    // lane updates the LDS table (same-address LDS atomics serialise).  The DPP read runs
+    // with every lane active: under a short-circuit mask a lane whose source lane is off
+    // reads 0 and would join a run of key 0 (round 5 bug: cell 0's voxel took its
+    // neighbour lane's point)
+    const uint32_t tp = vrow_shr<1>(t);
+    const bool head = !C3H_VOX_MERGE || !valid || (lane & 15) == 0 || tp != t;
     const uint64_t hm = __ballot(head);
     const int o0 = lane - (63 - __clzll(hm & le));  // lanes before this one in its run
     uint32_t s0, s1, sm;
@@ -451,20 +468,8 @@ __global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
       return;
     }
     ++owned;
-#if C3H_VOX_RMW == 1
-    // diagnostics: the owner's read-and-clear as device-scope atomic exchanges
-    ulonglong2 v;
-    v.x = __hip_atomic_exchange(&a.acc[t].x, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    v.y = __hip_atomic_exchange(&a.acc[t].y, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_exchange(&a.mo[t], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-    ulonglong2 v;
-    v.x = ld_coh(&a.acc[t].x);
-    v.y = ld_coh(&a.acc[t].y);
-    st_coh(&a.acc[t].x, 0ull);
-    st_coh(&a.acc[t].y, 0ull);
+    const ulonglong2 v = take_acc(&a.acc[t]);
     st_coh(&a.mo[t], ~0ull);
-#endif
     a.tpos[t] = q;
     uint32_t o[3];
     tor_offsets(a.tb, t, tot.mn, o);
@@ -1056,13 +1061,9 @@ __global__ __launch_bounds__(kBlock) void voxb_scatter_kernel(VoxBatchArgs a) {
     }
     if (own) {
       ++owned;
-      ulonglong2 v;
-      v.x = ld_coh(&acc[t].x);
-      v.y = ld_coh(&acc[t].y);
+      const ulonglong2 v = take_acc(&acc[t]);
       const uint32_t m = (uint32_t)(mo >> 32);
       // every entry of the voxel has read MO[t] or reads ~0 after this (not its id either)
-      st_coh(&acc[t].x, 0ull);
-      st_coh(&acc[t].y, 0ull);
       st_coh(&MO[t], ~0ull);
       // offsets from min_b: the toroidal coordinates minus min_b, modulo 2^tb
       const uint32_t cx = ((t & mx_) - (uint32_t)lo[0]) & mx_;

@@ -87,3 +87,12 @@ def test_read_axis_transform():
     assert q.shape == (20, 100)
     np.testing.assert_array_equal(q[0], axis[:, 0])
     np.testing.assert_allclose(q[5], axis[:, 5] * np.sqrt(var[5]) / np.sqrt(var[0]), rtol=1e-6)
+
+
+def test_build_provenance_record():
+    # c3h_build_info: the sha256 of the sources the library was built from; bench.py reports
+    # it beside the tree's own hash (no GPU call)
+    from c3hlac import _capi
+    b = _capi.build_provenance()
+    assert len(b["lib_src_sha256"]) == 64 and len(b["tree_src_sha256"]) == 64
+    assert b["arch"] == "gfx950" and b["built_at"]

@@ -1,6 +1,5 @@
 #!/bin/bash
-# round 5, session b: the dirty-accumulator diagnostics (plain / exchange / coherent
-# accesses), the whole GPU suite on the product build, then interleaved A/Bs against the
+# round 5, session b: the bad-voxel check, the whole GPU suite on the product build, then interleaved A/Bs against the
 # round-4 kernels (lib/variants/r4*.so, built from the round-4 sources): single-frame
 # voxeliser (tools/vox_bench.py), config 5 (tools/config5.py), the batched voxeliser
 # (points_bench with and without the voxeliser / tick overlap), kernel traces
@@ -9,13 +8,20 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r5b
 mkdir -p $O
 V=$R/mapping-private_amd/lib/variants
-for v in diag diag_rmw diag_ald; do
-  C3HLAC_LIB=$V/$v.so timeout -k 10 300 python3 tools/vox_dirty.py > $O/dirty_$v.jsonl 2> $O/dirty_$v.err || exit 1
-done
+STAGE=${1:-all}
+if [ $STAGE = tests ] || [ $STAGE = all ]; then
+timeout -k 10 200 python3 tools/vox_bad.py > $O/vox_bad.jsonl 2> $O/vox_bad.err || exit 1
 export C3H_REQUIRE_GPU=1
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider \
   -s > $O/tests.log 2>&1
 rc=$?; echo "tests rc=$rc" >> $O/rc.txt; [ $rc -ge 124 ] && exit $rc
+fi
+[ $STAGE = tests ] && exit 0
+if [ $STAGE = pmc ]; then
+  tools/pmc_points.sh r5b/pmc256 256 256 || exit 6
+  C5ARGS=--fp16 tools/pmc_config5.sh r5b_fp16 || exit 6
+  exit 0
+fi
 for rep in 1 2; do
   for v in default r4; do
     if [ $v = default ]; then unset C3HLAC_LIB; else export C3HLAC_LIB=$V/$v.so; fi
