@@ -804,8 +804,8 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
       if (a.feat16) {  // fp16 search precision: the row as f16 pairs (half the bytes)
         uint32_t* out2 = reinterpret_cast<uint32_t*>(a.feat16 + h * a.f16s);
 #pragma unroll 2
-        for (int i = lane; i < 491; i += 64) {
-          const _Float16 lo = (_Float16)sf[s_src[2 * i]];
+        for (int i = lane; i < (a.f16s >> 1); i += 64) {  // the padding to f16s as zeros
+          const _Float16 lo = 2 * i < 981 ? (_Float16)sf[s_src[2 * i]] : (_Float16)0.0f;
           const _Float16 hi = 2 * i + 1 < 981 ? (_Float16)sf[s_src[2 * i + 1]] : (_Float16)0.0f;
           out2[i] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
         }

@@ -1335,7 +1335,7 @@ int extract_frames(c3h_ctx* ctx, const uint32_t* const* grids, int nf, const c3h
     // compress reads them; every f32 reader converts them first, feat_rows_f32)
     ctx->feat16_pending = false;
     if (ctx->prec16 && nf == 1 && !ctx->capture && !atomic && F == 981 && hist_num >= c3h::kCompressMfmaRows) {
-      ctx->feat16_s = F + (F & 1);
+      ctx->feat16_s = (F + 7) & ~7;  // 16-B aligned rows (the compress loads 8 halves per lane)
       ENSURE(ctx->feat16, (size_t)hist_num * ctx->feat16_s);
       ENSURE(ctx->feat16_flag, 1);
       HIPCHK(hipMemsetAsync(ctx->feat16_flag.p, 0, 4, ctx->stream));

@@ -196,7 +196,10 @@ __global__ __launch_bounds__(kBlock, 3) void compress_f32c_kernel(CompressRows c
 
 __global__ __launch_bounds__(kBlock, 3) void compress_f16_kernel(CompressRows cr, const _Float16* PT16, int Fp16) {
   __shared__ __attribute__((aligned(16))) _Float16 cf_smem[kCFLds / 2];
-  compress_f16_body(cr, PT16, Fp16, blockIdx.x, gridDim.x, blockIdx.y, cf_smem);
+  if (cr.feat16 && *cr.feat16_flag)  // uniform: the extract wrote f16 rows
+    compress_f16_body<true>(cr, PT16, Fp16, blockIdx.x, gridDim.x, blockIdx.y, cf_smem);
+  else
+    compress_f16_body<false>(cr, PT16, Fp16, blockIdx.x, gridDim.x, blockIdx.y, cf_smem);
 }
 
 __global__ __launch_bounds__(kBlock) void boxsum_kernel(SparseSearch a) {

@@ -260,6 +260,11 @@ constexpr int kCFS = kCFK + 8;       // LDS row stride in halves (144 B: conflic
 constexpr int kCFRows = kMR / 4;     // rows of one wave's loads (= the wave's 32 A rows)
 constexpr int kCFLds = 2 * 128 * kCFS * 2;  // A (128 rows) + B (128 columns), bytes
 
+typedef unsigned mf_u32x4 __attribute__((ext_vector_type(4)));
+// kF16In: the rows are the C3 epilogue's f16 rows (c3h_set_search_precision before the
+// extract): a lane loads 16 B = 8 halves of a row, so one wave-wide load covers 8 rows'
+// 128-B chunk slices (2-B loads per lane ran the compress at 0.54 ms instead of 0.17)
+template <bool kF16In>
 __device__ __forceinline__ void compress_f16_body(const CompressRows& cr, const _Float16* __restrict__ PT16,
                                                   int Fp16, int bid, int nblk, int64_t f, _Float16* smem) {
   const float* __restrict__ feat = cr.feat + f * cr.s_feat;
@@ -273,23 +278,33 @@ __device__ __forceinline__ void compress_f16_body(const CompressRows& cr, const 
   _Float16* As = smem;               // [128 rows][kCFS]
   _Float16* Bs = smem + 128 * kCFS;  // [128 columns][kCFS]
   const bool ident = n == cr.H;
-  const _Float16* __restrict__ f16 = (cr.feat16 && *cr.feat16_flag) ? cr.feat16 : nullptr;  // uniform
+  const _Float16* __restrict__ f16 = cr.feat16;
+  const int f16s = cr.f16s;  // a multiple of 8 halves (16-B aligned rows, zero padding)
   for (int r0 = bid * kMR; r0 < n; r0 += nblk * kMR) {
     // every subdivision listed (dense frame): the list is a permutation of 0..H-1, so row
     // block r0 covers subdivisions r0.. in memory order instead (contiguous feature rows)
     const int myrow = r0 + wave * 32 + (lane & 31);
     const int hrow = myrow < n ? (ident ? myrow : rows[myrow]) : -1;  // lane j: the wave's row j
-    float areg[kCFRows];
+    float areg[kF16In ? 1 : kCFRows];
+    mf_u32x4 a16[kF16In ? kCFRows / 8 : 1];
     uint4 breg[4];
     auto fetch = [&](int c) {
-      const int k = c * kCFK + lane;
+      if (kF16In) {
+        const int kq = c * kCFK + (lane & 7) * 8;
 #pragma unroll
-      for (int j = 0; j < kCFRows; ++j) {
-        const int h = __builtin_amdgcn_readlane(hrow, j);
-        if (f16)
-          areg[j] = (h >= 0 && k < F) ? (float)__builtin_nontemporal_load(f16 + (int64_t)h * cr.f16s + k) : 0.0f;
-        else
+        for (int j = 0; j < kCFRows / 8; ++j) {
+          const int h = __shfl(hrow, j * 8 + (lane >> 3), 64);
+          a16[j] = (h >= 0 && kq < f16s)
+                       ? __builtin_nontemporal_load(reinterpret_cast<const mf_u32x4*>(f16 + (int64_t)h * f16s + kq))
+                       : mf_u32x4{0u, 0u, 0u, 0u};
+        }
+      } else {
+        const int k = c * kCFK + lane;
+#pragma unroll
+        for (int j = 0; j < kCFRows; ++j) {
+          const int h = __builtin_amdgcn_readlane(hrow, j);
           areg[j] = (h >= 0 && k < F) ? __builtin_nontemporal_load(feat + (int64_t)h * F + k) : 0.0f;
+        }
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -298,15 +313,40 @@ __device__ __forceinline__ void compress_f16_body(const CompressRows& cr, const 
       }
     };
     auto stage = [&](int c) {
-      const int k = c * kCFK + lane;
-      float mx = 1.0f;
-      const bool norm = k < fmax_len;  // setData max-normalisation (search.cpp:563-570)
-      if (norm) mx = fmax[k];
+      if (kF16In) {
+        const int kq = c * kCFK + (lane & 7) * 8;
+        float mx[8];
 #pragma unroll
-      for (int j = 0; j < kCFRows; ++j) {
-        float v = areg[j];
-        if (norm) v = mx == 0.0f ? 0.0f : (v == mx ? 1.0f : __fdiv_rn(v, mx));
-        As[(wave * 32 + j) * kCFS + lane] = (_Float16)v;
+        for (int e = 0; e < 8; ++e) mx[e] = kq + e < fmax_len ? fmax[kq + e] : -1.0f;  // -1: not normalised
+#pragma unroll
+        for (int j = 0; j < kCFRows / 8; ++j) {
+          mf_u32x4 o;
+#pragma unroll
+          for (int e2 = 0; e2 < 4; ++e2) {
+            const uint32_t w = a16[j][e2];
+            float v[2] = {(float)__builtin_bit_cast(_Float16, (uint16_t)(w & 0xffffu)),
+                          (float)__builtin_bit_cast(_Float16, (uint16_t)(w >> 16))};
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {  // setData max-normalisation (search.cpp:563-570)
+              const float m = mx[2 * e2 + u];
+              if (m >= 0.0f) v[u] = m == 0.0f ? 0.0f : (v[u] == m ? 1.0f : __fdiv_rn(v[u], m));
+            }
+            o[e2] = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)v[0]) |
+                    ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)v[1]) << 16);
+          }
+          *reinterpret_cast<mf_u32x4*>(As + (wave * 32 + j * 8 + (lane >> 3)) * kCFS + (lane & 7) * 8) = o;
+        }
+      } else {
+        const int k = c * kCFK + lane;
+        float mx = 1.0f;
+        const bool norm = k < fmax_len;  // setData max-normalisation (search.cpp:563-570)
+        if (norm) mx = fmax[k];
+#pragma unroll
+        for (int j = 0; j < kCFRows; ++j) {
+          float v = areg[j];
+          if (norm) v = mx == 0.0f ? 0.0f : (v == mx ? 1.0f : __fdiv_rn(v, mx));
+          As[(wave * 32 + j) * kCFS + lane] = (_Float16)v;
+        }
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {

@@ -100,6 +100,12 @@ __device__ __forceinline__ ulonglong2 take_acc(ulonglong2* p) {
   }
   return v;
 }
+#ifndef C3H_VOX_DIAG_NOFLUSH
+#define C3H_VOX_DIAG_NOFLUSH 0
+#endif
+#ifndef C3H_VOX_DIAG_NOCNT
+#define C3H_VOX_DIAG_NOCNT 0
+#endif
 #ifndef C3H_VOX_ATOM_SCOPE
 #define C3H_VOX_ATOM_SCOPE __HIP_MEMORY_SCOPE_AGENT
 #endif
@@ -194,7 +200,8 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
   }
   // the previous frame's grid words (its segments b, b + grid, ...), cleared while this
   // block's point loads are in flight (this frame's scatter, a later launch, writes the grid)
-  if (a.clear_grid) {
+  auto clear_prev = [&]() {
+    if (!a.clear_grid) return;
     const int pp = a.par ^ 1;
     for (int pb = b; pb < a.nblk_prev; pb += gridDim.x) {
       const int nn = part_of(a, pp)[(size_t)pb * kPartW + kPNew];
@@ -204,8 +211,11 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
         if (wi != kNoT) a.grid[wi] = 0u;
       }
     }
+  };
+  if (b >= a.nblk) {  // clearing only (an empty frame still runs one block)
+    clear_prev();
+    return;
   }
-  if (b >= a.nblk) return;  // clearing only (an empty frame still runs one block)
   const int64_t base = b * (int64_t)kVoxChunk;
   float4 p[kVoxPer];
 #pragma unroll
@@ -218,6 +228,7 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
       p[j] = make_float4(NAN, NAN, NAN, 0.0f);
     }
   }
+  clear_prev();
   for (int s = tid; s < kLSlots; s += kVB) {
     s_key[s] = kNoT;
     s_A[s] = 0;
@@ -233,6 +244,7 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
   // one (workgroup, voxel) entry: fire-and-forget sums and the owner / margin min
   auto add_entry = [&](uint32_t i, uint32_t t, unsigned long long va, unsigned long long vb, uint32_t m) {
     sl[i] = t;
+    if (C3H_VOX_DIAG_NOFLUSH) return;  // diagnostics: the skeleton without the global sums
     __hip_atomic_fetch_add(&acc[t].x, va, __ATOMIC_RELAXED, C3H_VOX_ATOM_SCOPE);
     __hip_atomic_fetch_add(&acc[t].y, vb, __ATOMIC_RELAXED, C3H_VOX_ATOM_SCOPE);
     __hip_atomic_fetch_min(mo + t, ((unsigned long long)m << 32) | (q0 + i), __ATOMIC_RELAXED, C3H_VOX_ATOM_SCOPE);
@@ -439,11 +451,13 @@ __global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
   constexpr int kPre = 2;  // entries per thread loaded ahead
   uint32_t pt[kPre];
   unsigned long long pmo[kPre];
+  ulonglong2 pacc[kPre];  // the sums, loaded with the owner word (read-only until the owner takes them)
 #pragma unroll
   for (int k = 0; k < kPre; ++k) {
     const int i = threadIdx.x + k * kBlock;
     pt[k] = i < nn ? sl[i] : 0u;
     pmo[k] = i < nn ? ld_coh(&a.mo[pt[k]]) : ~0ull;
+    pacc[k] = i < nn && C3H_VOX_RMW == 0 ? a.acc[pt[k]] : make_ulonglong2(0ull, 0ull);
   }
   const VoxTotals tot = vox_reduce(a, blockIdx.x == 0);
   if (!tot.any) return;
@@ -460,7 +474,7 @@ __global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
     return;
   }
   uint32_t flagged = 0, owned = 0;
-  auto visit = [&](int i, uint32_t t, unsigned long long m) {
+  auto visit = [&](int i, uint32_t t, unsigned long long m, const ulonglong2* pre) {
     const uint32_t q = q0 + (uint32_t)i;
     if ((uint32_t)m != q) {  // another entry of the voxel owns it
       tl[i] = kNoT;
@@ -468,7 +482,13 @@ __global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
       return;
     }
     ++owned;
-    const ulonglong2 v = take_acc(&a.acc[t]);
+    ulonglong2 v;
+    if (pre) {  // prefetched: every add is a previous launch's; clear with one 16-B store
+      v = *pre;
+      a.acc[t] = make_ulonglong2(0ull, 0ull);
+    } else {
+      v = take_acc(&a.acc[t]);
+    }
     st_coh(&a.mo[t], ~0ull);
     a.tpos[t] = q;
     uint32_t o[3];
@@ -486,16 +506,27 @@ __global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
 #pragma unroll
   for (int k = 0; k < kPre; ++k) {
     const int i = threadIdx.x + k * kBlock;
-    if (i < nn) visit(i, pt[k], pmo[k]);
+    if (i < nn) visit(i, pt[k], pmo[k], C3H_VOX_RMW == 0 ? &pacc[k] : nullptr);
   }
   for (int i = threadIdx.x + kPre * kBlock; i < nn; i += kBlock) {
     const uint32_t t = sl[i];
-    visit(i, t, ld_coh(&a.mo[t]));
+    visit(i, t, ld_coh(&a.mo[t]), nullptr);
   }
+  // one count add per block (same-address adds serialise at the memory side)
+  __shared__ uint32_t s_cnt[2][kBlock / 64];
   flagged = wave_reduce(flagged, [](uint32_t u, uint32_t v) { return u + v; });
   owned = wave_reduce(owned, [](uint32_t u, uint32_t v) { return u + v; });
-  if ((threadIdx.x & 63) == 0 && flagged) atomicAdd(a.cnt + kVcFlag, flagged);
-  if ((threadIdx.x & 63) == 0 && owned) atomicAdd(a.cnt + kVcSlots + a.par, owned);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s_cnt[0][w] = flagged;
+    s_cnt[1][w] = owned;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 && !C3H_VOX_DIAG_NOCNT) {
+    uint32_t v = 0;
+    for (int i = 0; i < kBlock / 64; ++i) v += s_cnt[threadIdx.x][i];
+    if (v) atomicAdd(a.cnt + (threadIdx.x == 0 ? kVcFlag : kVcSlots + a.par), v);
+  }
 }
 
 __device__ __forceinline__ bool vox_bounds(const VoxArgs& a, int mn[3], int dv[3], int64_t* nvox) {
