@@ -62,6 +62,12 @@ __global__ __launch_bounds__(256) void flush_kernel(unsigned long long* acc, uns
   }
 }
 
+// same-address returning adds: `per_block` lanes of every workgroup add 1 to one counter
+// (the voxeliser's per-brick list index) and store what they got
+__global__ __launch_bounds__(256) void same_addr_kernel(unsigned* ctr, unsigned* out, int per_block) {
+  if ((int)threadIdx.x < per_block) out[blockIdx.x * per_block + threadIdx.x] = atomicAdd(ctr, 1u);
+}
+
 int main() {
   const int tb = 24;  // 2^24 cells: the 256^3 frame's toroidal table
   const size_t cells = (size_t)1 << tb;
@@ -101,6 +107,22 @@ int main() {
       first = false;
     }
   }
+  }
+  for (int blocks : {245, 490}) {
+    for (int per : {12, 40}) {
+      float best = 1e9f;
+      for (int rep = 0; rep < 6; ++rep) {
+        CHK(hipMemset(mo, 0, 4));
+        CHK(hipEventRecord(e0));
+        same_addr_kernel<<<blocks, 256>>>(reinterpret_cast<unsigned*>(mo), reinterpret_cast<unsigned*>(acc), per);
+        CHK(hipEventRecord(e1));
+        CHK(hipEventSynchronize(e1));
+        float ms;
+        CHK(hipEventElapsedTime(&ms, e0, e1));
+        if (rep > 0 && ms < best) best = ms;
+      }
+      printf(", \"same_addr_%dx%d_us\": %.2f", blocks, per, best * 1e3);
+    }
   }
   printf("}\n");
   CHK(hipFree(acc));
