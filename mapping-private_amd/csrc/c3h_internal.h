@@ -94,53 +94,41 @@ enum {
   kVcErr = 11,    // kVcErrRange | kVcErrWrap
   kVcOver = 12,   // grid buffer too small (scatter not run)
   kVcOff = 13,    // off-cell voxels recorded by the exact pass
-  kVcBricks = 14, // bricks of the frame (vox_plan)
-  kVcPos = 15,    // list positions of the frame (vox_plan)
   kVcWords = 16
 };
 constexpr uint32_t kVcErrRange = 1;  // cell coordinates beyond +-2^20
 constexpr uint32_t kVcErrWrap = 4;   // the frame's extent exceeds the toroidal accumulator (the
                                      // frame runs again on larger dims; the scatter wrote nothing)
-// Single-frame voxeliser state (round 5: ownership by brick, no per-voxel global atomics).
-// Cells are bricked 8 x 8 x 8 on a toroidal index: cell (x, y, z) -> t = (x mod 2^tb0) |
-// (y mod 2^tb1) << tb0 | (z mod 2^tb2) << (tb0 + tb1), brick = t's coordinates >> 3, so a
-// frame whose extent fits 2^tb per axis maps its voxels one-to-one without a hash table.
-// vox_bin groups each block's points by brick (LDS), vox_plan lists the frame's bricks and
-// each brick's (bin block, range) pairs, vox_emit forms every voxel's sums in the one
-// workgroup that owns its brick and writes them with plain stores.
+// Single-frame voxeliser state.  The accumulators are toroidal: voxel (x, y, z) sums at
+// t = (x mod 2^tb0) | (y mod 2^tb1) << tb0 | (z mod 2^tb2) << (tb0 + tb1), so a frame whose
+// extent fits 2^tb per axis maps its voxels one-to-one without a hash table.  Every
+// (accumulate block, voxel) pair is one list entry; its sums go out as non-returning
+// atomics, and the entry with the min (margin << 32 | entry id) owns the voxel in the
+// scatter, which converts it and returns the accumulator to zero.
 struct VoxArgs {
   const float4* pts;
   int64_t n;
   float z_limit, inv, leaf;
-  uint32_t* tpos;             // [2^(tb0+tb1+tb2)] list position of each occupied cell (written by vox_emit)
+  ulonglong2* acc;          // [2^(tb0+tb1+tb2)] {count << 40 | sum r, sum b << 32 | sum g}, 0 between frames
+  unsigned long long* mo;   // [same] min over the voxel's entries of (margin bits << 32 | entry id), ~0 between frames
+  uint32_t* tpos;           // [same] list position of the voxel's owning entry (written by the scatter)
   int tb[3];
-  unsigned long long* bpc;    // [tor >> 9] per brick: (pairs << 32 | points) of this frame, 0 between frames
-  uint32_t* bidx;             // [tor >> 9] brick -> its index in blist (this frame's bricks only)
-  unsigned long long* stage;  // [nblk_cap * 4096] point records, each bin block's grouped by brick
-  uint4* ptab;                // [nblk_cap * 4096] per bin block: {brick, start | count << 16, pair rank, 0}
-  uint2* plist;               // [nblk_cap * 4096] the frame's pairs by brick: {bin block, start | count << 16}
-  uint32_t* blist;            // [nblk_cap * 4096 + 1] the frame's bricks
-  uint32_t* pbase;            // [same] first pair of brick i (pbase[nbricks] = pairs)
-  uint32_t* bpos;             // [same] first list position of brick i (bpos[nbricks] = positions)
-  uint32_t* lists;            // [cells parity 0 | parity 1 | grid words parity 0 | parity 1] x lcap
-  uint64_t lcap;              //   by list position (a brick's voxels at bpos[i] ..; gaps: kNoT)
-  uint32_t* lcnt;             // [lcap] point count of the voxel at each position (0: gap)
-  int32_t* part;              // per bin block: bounds, counts, pairs (vox_part_words() ints)
-  int nblk, nblk_cap;         // bin blocks of this frame, capacity
-  int64_t npos, npos_prev;    // list positions of this frame (known after the call) / the previous frame's
-  uint32_t* cnt;              // kVcWords counters (totals published by vox_plan)
-  uint32_t* wgtot;            // [vox_emit_blocks()][2] owned, flagged voxels per emit workgroup
-  uint32_t* grid;             // packed grid buffer (capacity grid_cap words)
+  uint32_t* lists;          // [entries parity 0 | entries parity 1 | grid words parity 0 | parity 1] x lcap,
+  uint64_t lcap;            //   each a segment of vox_positions(1) per accum block
+  uint32_t* lcnt;           // [lcap] this frame's owning entries' point counts (0: not owning)
+  int32_t* part;            // per parity, per accum block: bounds, counts (vox_part_words() ints)
+  int nblk, nblk_prev, nblk_cap;  // accum blocks of this / the previous frame, capacity
+  uint32_t* cnt;            // kVcWords counters (totals published by the scatter)
+  uint32_t* grid;           // packed grid buffer (capacity grid_cap words)
   int64_t grid_cap;
-  int par;                    // epoch parity of this frame
-  int clear_grid;             // clear the grid words the previous frame listed
+  int par;                  // epoch parity of this frame
+  int clear_grid;           // clear the grid words the previous frame listed
 };
 hipError_t launch_voxelize(const VoxArgs& a, hipStream_t s);
 // f16 feature rows -> f32 rows when *flag (device-side check: no host sync)
 hipError_t launch_feat16_to_f32(const _Float16* f16, int f16s, const uint32_t* flag, int64_t H, int F, float* out,
                                 hipStream_t s);
-hipError_t launch_vox_emit(const VoxArgs& a, hipStream_t s);
-int vox_emit_blocks();
+hipError_t launch_vox_scatter(const VoxArgs& a, hipStream_t s);
 int64_t vox_blocks(int64_t n);
 int64_t vox_positions(int64_t n);
 int vox_part_words();
@@ -515,16 +503,15 @@ struct c3h_ctx {
   int64_t rsd_n = 0;                // centroids with valid radii / types
   // voxeliser state (voxelize.hip): toroidal accumulators, entry / grid-word lists by
   // epoch parity, counters; the grid words the previous frame wrote are cleared by the next
-  c3h::DevBuf<unsigned long long> vbpc, vstage;
-  c3h::DevBuf<uint4> vptab;
-  c3h::DevBuf<uint2> vplist;
-  c3h::DevBuf<uint32_t> vtpos, vbidx, vblist, vpbase, vbpos, vlists, vlcnt, vcnt;
+  c3h::DevBuf<ulonglong2> vacc;
+  c3h::DevBuf<unsigned long long> vmo;
+  c3h::DevBuf<uint32_t> vtpos, vlists, vlcnt, vcnt;
   c3h::DevBuf<int32_t> vpart;
   int vtb[3] = {7, 7, 7};           // toroidal dims (log2 per axis); they only grow
-  int64_t vtor = 0;                 // cells of the allocated toroidal tables (0: none)
+  int64_t vtor = 0;                 // cells of the allocated accumulators (0: none)
   uint64_t vlcap = 0;
   int vpar = 0, vblk_cap = 0;
-  int64_t vnpos_prev = 0;           // list positions of the previous frame (its grid words to clear)
+  int vblk_prev = 0;                // accum blocks of the previous frame (its lists to clear)
   bool vgrid_tracked = false;       // grid buffer is zero outside the previous frame's list
   c3h::VoxArgs vargs{};             // the last voxelize (exact centroid pass, downsampled)
   int64_t vns = 0;                  // voxels of the last voxelize
@@ -538,7 +525,7 @@ struct c3h_ctx {
   c3h::DevBuf<uint32_t> scratch;    // minmax / counters
   c3h::DevBuf<uint32_t> tmp_u32;    // leaf-layout block sums
   c3h::DevBuf<int32_t> tmp_i32;     // leaf layout for host copies
-  uint32_t* h_small = nullptr;      // pinned host scratch (kVcWords + 2 x vox_emit_blocks() words)
+  uint32_t* h_small = nullptr;      // pinned host scratch (64 words)
   bool table_valid = false;         // hash table matches the grid (voxelize path)
 
   // features

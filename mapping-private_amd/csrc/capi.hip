@@ -674,9 +674,7 @@ int c3h_create(int hip_device, c3h_ctx** out) {
     return bail(C3H_ERR_HIP);
   ctx->stream = ctx->own_stream;
 
-  // pinned host scratch: counters + the voxeliser's per-workgroup totals (one D2H per frame)
-  if (hipHostMalloc(&ctx->h_small, (c3h::kVcWords + 2 * c3h::vox_emit_blocks()) * sizeof(uint32_t)) != hipSuccess)
-    return bail(C3H_ERR_HIP);
+  if (hipHostMalloc(&ctx->h_small, 64 * sizeof(uint32_t)) != hipSuccess) return bail(C3H_ERR_HIP);
   if (ensure(ctx, ctx->scratch, 64) != C3H_OK) return bail(C3H_ERR_NOMEM);
   if (ensure(ctx, ctx->lut, 3 * 256) != C3H_OK) return bail(C3H_ERR_NOMEM);
   uint32_t lut[3 * 256];
@@ -722,14 +720,8 @@ void c3h_destroy(c3h_ctx* ctx) {
   release(ctx->grsd_trans);
   release(ctx->grsd_feat);
   release(ctx->vosch_feat);
-  release(ctx->vbpc);
-  release(ctx->vstage);
-  release(ctx->vptab);
-  release(ctx->vplist);
-  release(ctx->vbidx);
-  release(ctx->vblist);
-  release(ctx->vpbase);
-  release(ctx->vbpos);
+  release(ctx->vacc);
+  release(ctx->vmo);
   release(ctx->vtpos);
   release(ctx->vlcnt);
   release(ctx->vlists);
@@ -848,9 +840,9 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
       d_pts = reinterpret_cast<const float4*>(ctx->pts.p);
     }
   }
-  // toroidal tables: 2^vtb cells per axis (they only grow: a frame whose extent exceeds
-  // them runs again on dims that fit it, from all-zero brick counters); stages, pair tables
-  // and lists: 4,096 positions per bin block
+  // toroidal accumulators: 2^vtb cells per axis (they only grow: a frame whose extent
+  // exceeds them runs again on dims that fit it, from all-zero accumulators); entry lists
+  // and partial records: one segment of the block's points per block
   uint64_t pcap = 512;
   while (pcap < (uint64_t)n) pcap <<= 1;
   const int nblk = (int)c3h::vox_blocks(n);
@@ -858,64 +850,51 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
   uint32_t* hc = ctx->h_small;
   for (int attempt = 0;; ++attempt) {
     const int64_t tor = (int64_t)1 << (ctx->vtb[0] + ctx->vtb[1] + ctx->vtb[2]);
-    if (ctx->vtor != tor || !ctx->vcnt.p) {  // (re)allocation: all-zero brick counters
+    if (ctx->vtor != tor || !ctx->vcnt.p) {  // (re)allocation: all-zero accumulators
       ctx->vtor = 0;
+      ENSURE(ctx->vacc, (size_t)tor);
+      ENSURE(ctx->vmo, (size_t)tor);
       ENSURE(ctx->vtpos, (size_t)tor);
-      ENSURE(ctx->vbpc, (size_t)(tor >> 9));
-      ENSURE(ctx->vbidx, (size_t)(tor >> 9));
-      ENSURE(ctx->vcnt, c3h::kVcWords + 2 * (size_t)c3h::vox_emit_blocks());  // counters | per-emit-block totals
-      HIPCHK(hipMemsetAsync(ctx->vbpc.p, 0, (size_t)(tor >> 9) * 8, ctx->stream));
+      ENSURE(ctx->vcnt, c3h::kVcWords);
+      HIPCHK(hipMemsetAsync(ctx->vacc.p, 0, (size_t)tor * 16, ctx->stream));
+      HIPCHK(hipMemsetAsync(ctx->vmo.p, 0xff, (size_t)tor * 8, ctx->stream));
       HIPCHK(hipMemsetAsync(ctx->vcnt.p, 0, c3h::kVcWords * 4, ctx->stream));
       ctx->vtor = tor;
     }
     if (ctx->vblk_cap < nblk || !ctx->vlists.p) {  // lists: the previous frame's grid words are lost
       const int bcap = (int)std::max<int64_t>(c3h::vox_blocks((int64_t)pcap), ctx->vblk_cap);
-      const size_t npc = (size_t)bcap * c3h::vox_positions(1);
-      ENSURE(ctx->vlists, 4 * npc);
-      ENSURE(ctx->vlcnt, npc);
-      ENSURE(ctx->vstage, npc);
-      ENSURE(ctx->vptab, npc);
-      ENSURE(ctx->vplist, npc);
-      ENSURE(ctx->vblist, npc + 1);
-      ENSURE(ctx->vpbase, npc + 1);
-      ENSURE(ctx->vbpos, npc + 1);
-      ENSURE(ctx->vpart, (size_t)bcap * c3h::vox_part_words());
+      ENSURE(ctx->vlists, 4 * (size_t)bcap * c3h::vox_positions(1));
+      ENSURE(ctx->vlcnt, (size_t)bcap * c3h::vox_positions(1));
+      ENSURE(ctx->vpart, 2 * (size_t)bcap * c3h::vox_part_words());
       HIPCHK(hipMemsetAsync(ctx->vpart.p, 0, ctx->vpart.n * 4, ctx->stream));
-      ctx->vlcap = (uint64_t)npc;
+      ctx->vlcap = (uint64_t)bcap * (uint64_t)c3h::vox_positions(1);
       ctx->vblk_cap = bcap;
-      ctx->vnpos_prev = 0;
+      ctx->vblk_prev = 0;
       ctx->vgrid_tracked = false;
     }
-    // the previous frame's grid words are cleared through its list only when its emit
+    // the previous frame's grid words are cleared through its list only when its scatter
     // completed (tracked); otherwise the whole buffer is zeroed once
     const bool clear_grid = ctx->vgrid_tracked && ctx->grid.n;
     if (!ctx->vgrid_tracked && ctx->grid.n) HIPCHK(hipMemsetAsync(ctx->grid.p, 0, ctx->grid.n * 4, ctx->stream));
-    ctx->vgrid_tracked = false;  // until this frame's emit completes
+    ctx->vgrid_tracked = false;  // until this frame's scatter completes
     a = c3h::VoxArgs{};
     a.pts = d_pts;
     a.n = n;
     a.z_limit = z_limit;
     a.inv = gi.inv_leaf;
     a.leaf = leaf;
+    a.acc = ctx->vacc.p;
+    a.mo = ctx->vmo.p;
     a.tpos = ctx->vtpos.p;
     for (int ax = 0; ax < 3; ++ax) a.tb[ax] = ctx->vtb[ax];
-    a.bpc = ctx->vbpc.p;
-    a.bidx = ctx->vbidx.p;
-    a.stage = ctx->vstage.p;
-    a.ptab = ctx->vptab.p;
-    a.plist = ctx->vplist.p;
-    a.blist = ctx->vblist.p;
-    a.pbase = ctx->vpbase.p;
-    a.bpos = ctx->vbpos.p;
     a.lists = ctx->vlists.p;
     a.lcap = ctx->vlcap;
     a.lcnt = ctx->vlcnt.p;
     a.part = ctx->vpart.p;
     a.nblk = nblk;
+    a.nblk_prev = ctx->vblk_prev;
     a.nblk_cap = ctx->vblk_cap;
-    a.npos_prev = clear_grid ? ctx->vnpos_prev : 0;
     a.cnt = ctx->vcnt.p;
-    a.wgtot = ctx->vcnt.p + c3h::kVcWords;
     a.grid = ctx->grid.p;
     a.grid_cap = (int64_t)ctx->grid.n;
     a.par = ctx->vpar;
@@ -924,18 +903,14 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
       Timed t(ctx, 0);
       HIPCHK(c3h::launch_voxelize(a, ctx->stream));
     }
-    HIPCHK(hipMemcpyAsync(hc, ctx->vcnt.p, ctx->vcnt.n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(hc, ctx->vcnt.p, c3h::kVcWords * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     // the previous frame's words are cleared now (its list is spent): nothing is tracked
-    // until this frame's emit has written its own list
-    ctx->vnpos_prev = 0;
-    if (hc[c3h::kVcErr] & c3h::kVcErrRange) {
-      ctx->vtor = 0;  // the bin blocks' brick counts stay behind: fresh tables next call
-      break;
-    }
-    if (!(hc[c3h::kVcErr] & c3h::kVcErrWrap)) break;
-    // the extent exceeds the toroidal dims: dims that fit it, zero brick counters (the
-    // wrapped counts are discarded with the old tables), and the frame again
+    // until this frame's scatter has written its own list
+    ctx->vblk_prev = 0;
+    if (!(hc[c3h::kVcErr] & c3h::kVcErrWrap) || (hc[c3h::kVcErr] & c3h::kVcErrRange)) break;
+    // the extent exceeds the toroidal dims: dims that fit it, all-zero accumulators (the
+    // wrapped sums are discarded with the old buffers), and the frame again
     int tb[3], sum = 0;
     for (int ax = 0; ax < 3; ++ax) {
       const int64_t dv = (int64_t)(int32_t)hc[c3h::kVcMax + ax] - (int32_t)hc[c3h::kVcMin + ax] + 1;
@@ -943,15 +918,16 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
       while (((int64_t)1 << tb[ax]) < dv) ++tb[ax];
       sum += tb[ax];
     }
-    ctx->vtor = 0;  // the next attempt (or call) starts from fresh tables
     if (attempt >= 2 || sum > 31) {
+      ctx->vtor = 0;  // the next call starts from fresh accumulators
       return fail(ctx, C3H_ERR_RANGE, "c3h_voxelize: frame extent beyond 2^31 voxels of accumulators");
     }
     for (int ax = 0; ax < 3; ++ax) ctx->vtb[ax] = tb[ax];
-    ctx->vgrid_tracked = true;  // the grid holds no word of this frame (its emit wrote none)
+    ctx->vgrid_tracked = true;  // the grid holds no word of this frame (its scatter wrote none)
   }
-  // from here the lists hold this frame's voxels (parity a.par)
+  // from here the lists hold this frame's entries (parity a.par)
   ctx->vpar ^= 1;
+  ctx->vblk_prev = nblk;
   if (hc[c3h::kVcErr] & c3h::kVcErrRange) {
     return fail(ctx, C3H_ERR_RANGE, "c3h_voxelize: leaf size too small (cell coordinates beyond +-2^20)");
   }
@@ -977,7 +953,7 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
   if (nvox > 2147483647LL) {
     return fail(ctx, C3H_ERR_RANGE, "c3h_voxelize: leaf size too small for int32 voxel indices");
   }
-  if (hc[c3h::kVcOver]) {  // the grid buffer grows (zeroed) and vox_emit runs again
+  if (hc[c3h::kVcOver]) {  // the grid buffer grows (zeroed) and the scatter runs again
     ENSURE(ctx->grid, (size_t)nvox);
     HIPCHK(hipMemsetAsync(ctx->grid.p, 0, ctx->grid.n * 4, ctx->stream));
     a.grid = ctx->grid.p;
@@ -985,29 +961,21 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
     HIPCHK(hipMemsetAsync(ctx->vcnt.p + c3h::kVcOver, 0, 4, ctx->stream));
     {
       Timed t(ctx, 0);
-      HIPCHK(c3h::launch_vox_emit(a, ctx->stream));
+      HIPCHK(c3h::launch_vox_scatter(a, ctx->stream));
     }
-    HIPCHK(hipMemcpyAsync(hc, ctx->vcnt.p, ctx->vcnt.n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(hc, ctx->vcnt.p, c3h::kVcWords * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     if (hc[c3h::kVcOver]) return fail(ctx, C3H_ERR_HIP, "c3h_voxelize: internal: grid still too small");
   }
-  // voxels and flagged voxels: the emit workgroups' counts (no same-address atomics)
-  int64_t owned = 0, flagged = 0;
-  for (int i = 0; i < c3h::vox_emit_blocks(); ++i) {
-    owned += hc[c3h::kVcWords + 2 * i];
-    flagged += hc[c3h::kVcWords + 2 * i + 1];
-  }
   ctx->vgrid_tracked = true;
-  a.npos = hc[c3h::kVcPos];
-  ctx->vnpos_prev = a.npos;
   ctx->vargs = a;
-  ctx->vns = owned;
+  ctx->vns = hc[c3h::kVcSlots + a.par];
   gi.n_occ = ctx->vns;
   ctx->info = gi;
   ctx->grid_ptr = ctx->grid.p;
   ctx->have_grid = true;
   ctx->table_valid = true;
-  if (flagged) {  // centroids may leave their cells: the exact pass decides
+  if (hc[c3h::kVcFlag]) {  // centroids may leave their cells: the exact pass decides
     int rc = exact_centroids(ctx);
     if (rc != C3H_OK) return rc;
   }

@@ -4,28 +4,29 @@
 // VoxelGrid::filter, semantics restated in SURVEY.md App. B) and limitPoint
 // (color_voxel_recognition/test/detect_object.cpp:68-87).
 //
-// Hot path (round 5): ownership by brick -- every voxel's sums are formed in exactly one
-// workgroup and stored with plain writes; no per-(workgroup, voxel) global atomic.  Cells
-// are grouped in 8 x 8 x 8 bricks of the toroidal index (VoxArgs).  Three launches:
-//   vox_bin    one workgroup per 4,096 consecutive points (a depth camera's pixel order is
-//              spatially coherent): coalesced 16-B loads, cell / brick / 8-B record per
-//              point; runs of equal bricks in each 16-lane row (DPP) take one LDS counter
-//              add per run, which ranks the run's points inside the block's brick group;
-//              an LDS scan lays the groups out and the records are stored grouped by brick.
-//              One global atomic per (block, brick) pair (the brick's pair and point
-//              counts, ~25 per block on a Kinect frame instead of ~380 x 3 per-voxel
-//              atomics: 64-bit device atomics run at ~22 G/s chip-wide whatever their
-//              scope or table size, tools/atomic_bench.hip, profiles/r5/).  Also clears
-//              the grid words the previous frame listed.
-//   vox_plan   one workgroup: bounds and totals from the blocks' partial records, the
-//              frame's brick list, every pair filed under its brick, list positions.
-//   vox_emit   persistent workgroups over the bricks: a brick's records summed in LDS by
-//              in-brick index (runs merged by DPP first), then every occupied cell is one
-//              voxel -- linear index (cell - min_b) from its toroidal coordinates (modular
-//              offsets, exact while the extent fits the dims), the canonical colour mean
-//              kOcc | r<<16 | g<<8 | b with r = (int)(float(sum_r) * (1 / float(count)))
-//              (Eigen 3.0's scalar quotient, see pcl_colour_word), the centroid safety
-//              test below; the brick's counters return to zero for the next frame.
+// Hot path: two launches, no hash table, no returning atomic (round 5).
+//   vox_accum   one workgroup per 4,096 consecutive points (a depth camera's pixel order
+//               is spatially coherent: a voxel is hit by runs of neighbouring pixels):
+//               coalesced 16-B loads; the cell's toroidal index t (VoxArgs); runs of equal
+//               t in each 16-lane row merged by a DPP segmented scan; one LDS hash insert
+//               per run (count | r, b | g sums, the closest point's distance to a cell face).
+//               Flush: each (workgroup, voxel) pair becomes one list entry of the
+//               workgroup's segment (plain store) and three fire-and-forget atomics: two
+//               64-bit adds into acc[t] and a 64-bit min of (margin << 32 | entry id) into
+//               mo[t].  Nothing waits on a round trip (round 4's hash claim -- a returning
+//               64-bit CAS followed by the adds on its slot -- cost ~14 us of a 36-44 us
+//               frame, profiles/r4/vox_ab/).  The launch also clears the grid words the
+//               previous frame wrote (listed by it) and writes bounds / counts to its own
+//               partial record (no same-address atomics across workgroups).
+//   vox_scatter every block reduces the partial records (bounds, totals), then visits its
+//               segment: the entry whose id is the low half of mo[t] owns the voxel (one
+//               per voxel, the min of its entries), converts it -- linear index (cell -
+//               min_b) . divb_mul from t (modular offsets, exact while the extent fits the
+//               toroidal dims), the canonical colour mean kOcc | r<<16 | g<<8 | b with
+//               r = (int)(float(sum_r) * (1 / float(count))) (Eigen 3.0's scalar quotient,
+//               see pcl_colour_word), the centroid safety test below -- and returns
+//               acc[t] / mo[t] to zero / ~0; the other entries of the voxel skip it (they
+//               read the owner's id, or ~0 once it has reset mo[t]: neither is theirs).
 // Integer sums are exact and order-independent, so the grid is deterministic.
 //
 // Centroids.  C3-HLAC takes a voxel's subdivision (floor(c / voxel_size)) and neighbour
@@ -33,10 +34,10 @@
 // float centroid c = (fp32 sequential sum of its points in input order) * (1 / count), as
 // PCL 1.0's VoxelGrid on Eigen 3.0 computes it (pinned by the reference's shape_data
 // feature files, tests/test_shape_fixtures.py).  That can leave the voxel's own cell only when c lies within the sum's
-// rounding of a cell boundary; vox_emit flags a voxel when its closest point's margin
+// rounding of a cell boundary; vox_scatter flags a voxel when its closest point's margin
 // is below (count + 4) * 2^-22 * (|cell| + 1) cells (4x the error bound of the mean, the
 // multiply and the divide).  Only then (and for c3h_get_downsampled) the exact pass runs:
-// points are bucketed per voxel (counting sort over the list positions), each bucket sorted by
+// points are bucketed per voxel (counting sort over the owning entries), each bucket sorted by
 // point index and summed sequentially in fp32 -- bit-identical to the oracle -- and voxels
 // whose centroid cells differ from their own cell are recorded (c3h_extract corrects
 // their C3-HLAC contribution, c3hlac.hip offcell_delta_kernel).
@@ -55,12 +56,18 @@ constexpr uint32_t kNoT = 0xffffffffu;       // no toroidal index / no grid word
 #define C3H_VOX_CHUNK 4096
 #endif
 #ifndef C3H_VOX_THREADS
-#define C3H_VOX_THREADS 1024  // bin workgroup: 16 waves (4 per SIMD) over one LDS brick table
+#define C3H_VOX_THREADS 1024  // accumulate workgroup: 16 waves (4 per SIMD) over one LDS table
 #endif
 constexpr int kVB = C3H_VOX_THREADS;
 constexpr int kVoxChunk = C3H_VOX_CHUNK;      // points per workgroup (16 per thread; 4096 / 2048 slots measured
                                               // 40.9 us per 1M-point frame vs 41.9 at 2048 / 1024, 51 at 1024)
 constexpr int kVoxPer = kVoxChunk / kVB;
+#ifndef C3H_VOX_SLOTS
+#define C3H_VOX_SLOTS 2048
+#endif
+#ifndef C3H_VOX_MERGE
+#define C3H_VOX_MERGE 1  // the run merge (0: every point updates the LDS table itself)
+#endif
 #ifndef C3H_VOX_RMW
 #define C3H_VOX_RMW 0  // the accumulators' plain accesses in the scatters: 0 = default cache
                        // policy (the adds are a previous launch's); diagnostics: 1 = the owner's
@@ -93,9 +100,16 @@ __device__ __forceinline__ ulonglong2 take_acc(ulonglong2* p) {
   }
   return v;
 }
+#ifndef C3H_VOX_DIAG_NOFLUSH
+#define C3H_VOX_DIAG_NOFLUSH 0
+#endif
+#ifndef C3H_VOX_DIAG_NOCNT
+#define C3H_VOX_DIAG_NOCNT 0
+#endif
 #ifndef C3H_VOX_ATOM_SCOPE
 #define C3H_VOX_ATOM_SCOPE __HIP_MEMORY_SCOPE_AGENT
 #endif
+constexpr int kLSlots = C3H_VOX_SLOTS;        // LDS hash slots per workgroup
 constexpr int kLProbe = 48;                   // LDS probes before a point goes straight to the global table
 constexpr int kCellBias = 1 << 20;
 // point margins (cells) at or above this are not recorded per voxel: the scatter's bound
@@ -153,9 +167,13 @@ __device__ __forceinline__ void tor_offsets(const int tb[3], uint32_t t, const i
   o[2] = (((t >> (tb[0] + tb[1])) & mz) - (uint32_t)mn[2]) & mz;
 }
 
-// per bin block: {min xyz, max xyz, valid points, pairs, error} at part[b]
+// per accum block: {min xyz, max xyz, valid points, list entries, error} at part[par][b]
 constexpr int kPartW = 12;
 enum { kPMin = 0, kPMax = 3, kPValid = 6, kPNew = 7, kPErr = 8 };
+
+__device__ __forceinline__ const int32_t* part_of(const VoxArgs& a, int par) {
+  return a.part + (size_t)par * a.nblk_cap * kPartW;
+}
 
 // DPP row_shr:o (within 16-lane rows); lanes without a source read 0
 template <int O>
@@ -163,82 +181,35 @@ __device__ __forceinline__ uint32_t vrow_shr(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 | O, 0xf, 0xf, true);
 }
 
-// ---- single-frame voxeliser: ownership by brick -------------------------------------
-// A brick is 8 x 8 x 8 cells of the toroidal index; brick id = the cell's toroidal
-// coordinates >> 3 (tb - 3 bits per axis), in-brick index ib = the low 3 bits per axis.
-constexpr int kBrickBits = 9;
-constexpr int kBrickCells = 1 << kBrickBits;
-constexpr int kEmitBlocks = 1024;  // vox_emit workgroups (persistent over the frame's bricks)
-constexpr uint32_t kNoM16 = 0xffffu;  // a record's margin: none below kMarginFlush
-
-__device__ __forceinline__ void brick_of(const int tb[3], const int c[3], uint32_t* bk, uint32_t* ib) {
-  const uint32_t x = (uint32_t)c[0] & ((1u << tb[0]) - 1), y = (uint32_t)c[1] & ((1u << tb[1]) - 1),
-                 z = (uint32_t)c[2] & ((1u << tb[2]) - 1);
-  *bk = (x >> 3) | ((y >> 3) << (tb[0] - 3)) | ((z >> 3) << (tb[0] + tb[1] - 6));
-  *ib = (x & 7u) | ((y & 7u) << 3) | ((z & 7u) << 6);
-}
-// the toroidal cell index of (brick, in-brick index)
-__device__ __forceinline__ uint32_t brick_cell(const int tb[3], uint32_t bk, uint32_t ib) {
-  const uint32_t bx = bk & ((1u << (tb[0] - 3)) - 1), by = (bk >> (tb[0] - 3)) & ((1u << (tb[1] - 3)) - 1),
-                 bz = bk >> (tb[0] + tb[1] - 6);
-  const uint32_t x = (bx << 3) | (ib & 7u), y = (by << 3) | ((ib >> 3) & 7u), z = (bz << 3) | (ib >> 6);
-  return x | (y << tb[0]) | (z << (tb[0] + tb[1]));
-}
-
-// block-wide exclusive scan (kT threads, one value each); *total = the block's sum
-template <int kT>
-__device__ __forceinline__ uint32_t excl_scan(uint32_t v, uint32_t* lds, uint32_t* total) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) lds[wid] = x;
-  __syncthreads();
-  uint32_t wbase = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < kT / 64; ++w) {
-    const uint32_t s = lds[w];
-    if (w < wid) wbase += s;
-    tot += s;
-  }
-  *total = tot;
-  __syncthreads();
-  return wbase + x - v;
-}
-
-// vox_bin: one workgroup per 4,096 consecutive points.  Each point's cell, brick and a
-// 64-bit record {rgb | ib << 24 | margin16 << 33}; runs of equal bricks in each 16-lane
-// row (a depth camera's neighbouring pixels) take one LDS counter add per run, which also
-// ranks the run's points in the block's brick group; the groups are laid out by an LDS
-// scan and every record is stored at its group position (plain coalesced stores).  Each
-// (block, brick) pair then takes ONE global atomic (the brick's pair and point counts) and
-// is listed in the block's pair table.  The previous frame's grid words are cleared here.
-__global__ __launch_bounds__(kVB) void vox_bin_kernel(VoxArgs a) {
-  __shared__ uint32_t s_key[kVoxChunk];  // brick per slot (kNoT: free)
-  __shared__ uint32_t s_cnt[kVoxChunk];  // points per slot, then the slot's group start
-  __shared__ uint32_t s_scan[kVB / 64];
+__global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
+  __shared__ uint32_t s_key[kLSlots];
+  __shared__ unsigned long long s_A[kLSlots];  // count << 40 | sum r
+  __shared__ unsigned long long s_B[kLSlots];  // sum b << 32 | sum g
+  __shared__ uint32_t s_m[kLSlots];
+  __shared__ uint32_t s_nnew;                  // list entries of this workgroup
   __shared__ int s_red[kVB / 64][8];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, b = blockIdx.x;
-  if (b == 0 && tid == 0) {  // totals of an empty frame (vox_plan publishes the others)
+  if (b == 0 && tid == 0) {  // totals of an empty frame (the scatter publishes the others)
     for (int ax = 0; ax < 3; ++ax) {
       reinterpret_cast<int32_t*>(a.cnt)[kVcMin + ax] = INT_MAX;
       reinterpret_cast<int32_t*>(a.cnt)[kVcMax + ax] = INT_MIN;
     }
     a.cnt[kVcValid] = a.cnt[kVcValid + 1] = 0;
+    a.cnt[kVcSlots + a.par] = 0;
     a.cnt[kVcFlag] = a.cnt[kVcErr] = a.cnt[kVcOver] = a.cnt[kVcOff] = 0;
-    a.cnt[kVcBricks] = a.cnt[kVcPos] = 0;
   }
-  // the previous frame's grid words (its list positions b, b + grid, ...), cleared while
-  // this block's point loads are in flight (this frame's vox_emit, a later launch, writes)
+  // the previous frame's grid words (its segments b, b + grid, ...), cleared while this
+  // block's point loads are in flight (this frame's scatter, a later launch, writes the grid)
   auto clear_prev = [&]() {
     if (!a.clear_grid) return;
-    const uint32_t* tl = a.lists + (size_t)(2 + (a.par ^ 1)) * a.lcap;
-    for (int64_t q = (int64_t)b * kVB + tid; q < a.npos_prev; q += (int64_t)gridDim.x * kVB) {
-      const uint32_t wi = tl[q];
-      if (wi != kNoT) a.grid[wi] = 0u;
+    const int pp = a.par ^ 1;
+    for (int pb = b; pb < a.nblk_prev; pb += gridDim.x) {
+      const int nn = part_of(a, pp)[(size_t)pb * kPartW + kPNew];
+      const uint32_t* tl = a.lists + (size_t)(2 + pp) * a.lcap + (size_t)pb * kVoxChunk;
+      for (int i = tid; i < nn; i += kVB) {
+        const uint32_t wi = tl[i];
+        if (wi != kNoT) a.grid[wi] = 0u;
+      }
     }
   };
   if (b >= a.nblk) {  // clearing only (an empty frame still runs one block)
@@ -258,16 +229,30 @@ __global__ __launch_bounds__(kVB) void vox_bin_kernel(VoxArgs a) {
     }
   }
   clear_prev();
-  for (int s = tid; s < kVoxChunk; s += kVB) {
+  for (int s = tid; s < kLSlots; s += kVB) {
     s_key[s] = kNoT;
-    s_cnt[s] = 0;
+    s_A[s] = 0;
+    s_B[s] = 0;
+    s_m[s] = kNoMargin;
   }
+  if (tid == 0) s_nnew = 0;
   __syncthreads();
+  uint32_t* sl = a.lists + (size_t)a.par * a.lcap + (size_t)b * kVoxChunk;
+  const uint32_t q0 = (uint32_t)b * (uint32_t)kVoxChunk;
+  ulonglong2* __restrict__ acc = a.acc;
+  unsigned long long* __restrict__ mo = a.mo;
+  // one (workgroup, voxel) entry: fire-and-forget sums and the owner / margin min
+  auto add_entry = [&](uint32_t i, uint32_t t, unsigned long long va, unsigned long long vb, uint32_t m) {
+    sl[i] = t;
+    if (C3H_VOX_DIAG_NOFLUSH) return;  // diagnostics: the skeleton without the global sums
+    __hip_atomic_fetch_add(&acc[t].x, va, __ATOMIC_RELAXED, C3H_VOX_ATOM_SCOPE);
+    __hip_atomic_fetch_add(&acc[t].y, vb, __ATOMIC_RELAXED, C3H_VOX_ATOM_SCOPE);
+    __hip_atomic_fetch_min(mo + t, ((unsigned long long)m << 32) | (q0 + i), __ATOMIC_RELAXED, C3H_VOX_ATOM_SCOPE);
+  };
   int mn[3] = {INT_MAX, INT_MAX, INT_MAX}, mx[3] = {INT_MIN, INT_MIN, INT_MIN};
-  int nv = 0, err = 0;
+  int nv = 0;
+  int err = 0;  // kVcErrRange
   const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1);  // lanes <= this one
-  uint32_t pslot[kVoxPer], prank[kVoxPer];
-  unsigned long long prec[kVoxPer];
 #pragma unroll
   for (int j = 0; j < kVoxPer; ++j) {
     int c[3] = {0, 0, 0};
@@ -277,8 +262,7 @@ __global__ __launch_bounds__(kVB) void vox_bin_kernel(VoxArgs a) {
       err |= kVcErrRange;
       valid = false;
     }
-    uint32_t bk = kNoT, ib = 0;
-    prec[j] = 0;
+    uint32_t t = kNoT, w0 = 0, w1 = 0, mb = kNoMargin;
     if (valid) {
       ++nv;
 #pragma unroll
@@ -286,67 +270,70 @@ __global__ __launch_bounds__(kVB) void vox_bin_kernel(VoxArgs a) {
         mn[ax] = min(mn[ax], c[ax]);
         mx[ax] = max(mx[ax], c[ax]);
       }
-      brick_of(a.tb, c, &bk, &ib);
-      // a margin below kMarginFlush, truncated to its upper 16 bits (rounds it down:
-      // the flag test stays conservative); kNoM16 otherwise
+      t = tor_index(a.tb, c);
+      const uint32_t rgb = __float_as_uint(p[j].w);
+      w0 = ((rgb >> 16) & 0xffu) | (((rgb >> 8) & 0xffu) << 12) | (1u << 24);  // r | g << 12 | count << 24
+      w1 = rgb & 0xffu;                                                         // b
       const uint32_t mbits = __float_as_uint(margin);
-      const uint32_t m16 = mbits < kMarginFlush ? (mbits >> 16) : kNoM16;
-      prec[j] = (unsigned long long)(__float_as_uint(p[j].w) & 0xffffffu) | ((unsigned long long)ib << 24) |
-                ((unsigned long long)m16 << 33);
+      mb = mbits < kMarginFlush ? mbits : kNoMargin;
     }
-    // runs of equal bricks in each 16-lane row (every lane active for the DPP read)
-    const uint32_t bp = vrow_shr<1>(bk);
-    const bool head = !valid || (lane & 15) == 0 || bp != bk;
+    // runs of equal keys inside each 16-lane row: a lane starts a run when it is invalid,
+    // the row's first lane, or its key differs from the previous lane's; only a run's last
+    // lane updates the LDS table (same-address LDS atomics serialise).  The DPP read runs
+    // with every lane active: under a short-circuit mask a lane whose source lane is off
+    // reads 0 and would join a run of key 0 (round 5 bug: cell 0's voxel took its
+    // neighbour lane's point)
+    const uint32_t tp = vrow_shr<1>(t);
+    const bool head = !C3H_VOX_MERGE || !valid || (lane & 15) == 0 || tp != t;
     const uint64_t hm = __ballot(head);
     const int o0 = lane - (63 - __clzll(hm & le));  // lanes before this one in its run
-    const uint64_t above = hm & ~le;
-    const int tail = min(above ? (int)__builtin_ctzll(above) - 1 : 63, lane | 15);
-    uint32_t h = 0, rb = 0;
-    if (valid && tail == lane) {
-      h = (bk * 0x9E3779B1u) >> (32 - __builtin_ctz(kVoxChunk));
-      for (int probe = 0; probe < kVoxChunk; ++probe) {  // <= 4,096 bricks per block: a free slot exists
-        const uint32_t prev = atomicCAS(&s_key[h], kNoT, bk);
-        if (prev == kNoT || prev == bk) break;
-        h = (h + 1) & (kVoxChunk - 1);
+    uint32_t s0, s1, sm;
+    s0 = vrow_shr<1>(w0); s1 = vrow_shr<1>(w1); sm = vrow_shr<1>(mb);
+    if (o0 >= 1) { w0 += s0; w1 += s1; mb = min(mb, sm); }
+    s0 = vrow_shr<2>(w0); s1 = vrow_shr<2>(w1); sm = vrow_shr<2>(mb);
+    if (o0 >= 2) { w0 += s0; w1 += s1; mb = min(mb, sm); }
+    s0 = vrow_shr<4>(w0); s1 = vrow_shr<4>(w1); sm = vrow_shr<4>(mb);
+    if (o0 >= 4) { w0 += s0; w1 += s1; mb = min(mb, sm); }
+    s0 = vrow_shr<8>(w0); s1 = vrow_shr<8>(w1); sm = vrow_shr<8>(mb);
+    if (o0 >= 8) { w0 += s0; w1 += s1; mb = min(mb, sm); }
+    const bool tail = valid && ((lane & 15) == 15 || ((hm >> (lane + 1)) & 1));
+    if (!tail) continue;
+    // the run's totals: count <= 16, channel sums <= 4080
+    const unsigned long long A = ((unsigned long long)(w0 >> 24) << 40) | (w0 & 0xfffu);
+    const unsigned long long B = ((unsigned long long)w1 << 32) | ((w0 >> 12) & 0xfffu);
+    uint32_t h = (t * 0x9E3779B1u) >> (32 - __builtin_ctz(kLSlots));
+    bool done = false;
+    for (int probe = 0; probe < kLProbe; ++probe) {
+      const uint32_t prev = atomicCAS(&s_key[h], kNoT, t);
+      if (prev == kNoT || prev == t) {
+        atomicAdd(&s_A[h], A);
+        atomicAdd(&s_B[h], B);
+        if (mb != kNoMargin) atomicMin(&s_m[h], mb);
+        done = true;
+        break;
       }
-      rb = atomicAdd(&s_cnt[h], (uint32_t)(o0 + 1));
+      h = (h + 1) & (kLSlots - 1);
     }
-    pslot[j] = (uint32_t)__shfl((int)h, tail, 64);
-    prank[j] = (uint32_t)__shfl((int)rb, tail, 64) + (uint32_t)o0;
-    if (!valid) pslot[j] = kNoT;
+    if (!done) add_entry(atomicAdd(&s_nnew, 1u), t, A, B, mb);  // LDS table full: an entry of its own
   }
-  __syncthreads();  // every group count is in
-  // group starts (slot order) and the pair table: 4 slots per thread
-  constexpr int kSpt = kVoxChunk / kVB;
-  uint32_t cnts[kSpt], used = 0, sum = 0;
+  __syncthreads();  // every point's LDS update is in
+  {  // flush: list positions by one LDS counter add per wave
+    constexpr int kFl = (kLSlots + kVB - 1) / kVB;
 #pragma unroll
-  for (int k = 0; k < kSpt; ++k) {
-    cnts[k] = s_cnt[tid * kSpt + k];
-    used += cnts[k] ? 1u : 0u;
-    sum += cnts[k];
+    for (int k = 0; k < kFl; ++k) {
+      const int s = tid + k * kVB;
+      const uint32_t key = s < kLSlots ? s_key[s] : kNoT;
+      const bool have = key != kNoT;
+      const unsigned long long bm = __ballot(have);
+      if (!bm) continue;
+      uint32_t w0 = 0;
+      if (lane == 0) w0 = atomicAdd(&s_nnew, (uint32_t)__popcll(bm));
+      w0 = __shfl(w0, 0, 64);
+      if (have) add_entry(w0 + (uint32_t)__popcll(bm & ((1ull << lane) - 1)), key, s_A[s], s_B[s], s_m[s]);
+    }
   }
-  uint32_t npairs, ntot;
-  uint32_t pidx = excl_scan<kVB>(used, s_scan, &npairs);
-  uint32_t start = excl_scan<kVB>(sum, s_scan, &ntot);
-  uint4* pt = a.ptab + (size_t)b * kVoxChunk;
-#pragma unroll
-  for (int k = 0; k < kSpt; ++k) {
-    if (!cnts[k]) continue;
-    const uint32_t bk = s_key[tid * kSpt + k];
-    s_cnt[tid * kSpt + k] = start;
-    // one global atomic per (block, brick): the brick's pair count (high half) and points
-    const unsigned long long old =
-        __hip_atomic_fetch_add(&a.bpc[bk], (1ull << 32) | cnts[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    pt[pidx] = make_uint4(bk, start | (cnts[k] << 16), (uint32_t)(old >> 32), 0u);
-    start += cnts[k];
-    ++pidx;
-  }
-  __syncthreads();  // group starts in s_cnt
-  unsigned long long* st = a.stage + (size_t)b * kVoxChunk;
-#pragma unroll
-  for (int j = 0; j < kVoxPer; ++j)
-    if (pslot[j] != kNoT) st[s_cnt[pslot[j]] + prank[j]] = prec[j];
-  // bounds, counts and pairs go to this block's partial record
+  // bounds, counts and the entry count go to this block's partial record: no same-address
+  // atomics across blocks (they serialise at the memory side)
 #pragma unroll
   for (int ax = 0; ax < 3; ++ax) {
     mn[ax] = wave_reduce(mn[ax], [](int x, int y) { return min(x, y); });
@@ -363,7 +350,7 @@ __global__ __launch_bounds__(kVB) void vox_bin_kernel(VoxArgs a) {
     s_red[w][7] = e;
   }
   __syncthreads();
-  int32_t* pr = a.part + (size_t)b * kPartW;
+  int32_t* pr = a.part + ((size_t)a.par * a.nblk_cap + b) * kPartW;
   if (tid < 8) {
     int v = s_red[0][tid];
     for (int i = 1; i < kVB / 64; ++i) {
@@ -372,27 +359,24 @@ __global__ __launch_bounds__(kVB) void vox_bin_kernel(VoxArgs a) {
     }
     pr[tid < 7 ? tid : kPErr] = v;
   }
-  if (tid == 8) pr[kPNew] = (int)npairs;
+  if (tid == 8) pr[kPNew] = (int)s_nnew;
 }
 
-// vox_plan: one workgroup.  Reduces the bin blocks' records (bounds, totals), lists the
-// frame's bricks (the pairs of pair rank 0, in block order), and files every pair under
-// its brick: plist[pbase[i] + pair rank].  Brick i's voxels get list positions bpos[i] ..
-// bpos[i] + min(512, its points).  Publishes the totals; flags an extent beyond the
-// toroidal dims (kVcErrWrap: nothing else runs, the host enlarges them) or beyond the
-// grid buffer (kVcOver: vox_emit does not run, the host grows the buffer and reruns it).
-constexpr int kPlanT = 1024;
-__global__ __launch_bounds__(kPlanT) void vox_plan_kernel(VoxArgs a) {
-  __shared__ uint32_t s_pstart[kVoxChunk + 1];  // pair prefix over bin blocks (<= 4,096 blocks)
-  __shared__ uint32_t s_scan[kPlanT / 64];
-  __shared__ int s_r[kPlanT / 64][10];
-  __shared__ int s_stop;
-  const int tid = threadIdx.x;
-  // 1. bounds and totals
+// every block reduces the accum blocks' partial records (a few KB, from L2); block 0
+// publishes the totals for the host and the later kernels
+struct VoxTotals {
+  int mn[3], dv[3];
+  int64_t nvox;
+  bool any;
+};
+
+__device__ VoxTotals vox_reduce(const VoxArgs& a, bool publish) {
+  __shared__ int s_r[kBlock / 64][10];
+  const int32_t* pt = part_of(a, a.par);
   int mn[3] = {INT_MAX, INT_MAX, INT_MAX}, mx[3] = {INT_MIN, INT_MIN, INT_MIN};
   int nv = 0, er = 0;
-  for (int b = tid; b < a.nblk; b += kPlanT) {
-    const int32_t* r = a.part + (size_t)b * kPartW;
+  for (int b = threadIdx.x; b < a.nblk; b += kBlock) {
+    const int32_t* r = pt + (size_t)b * kPartW;
     if (r[kPValid]) {
       for (int ax = 0; ax < 3; ++ax) {
         mn[ax] = min(mn[ax], r[kPMin + ax]);
@@ -408,244 +392,140 @@ __global__ __launch_bounds__(kPlanT) void vox_plan_kernel(VoxArgs a) {
   }
   nv = wave_reduce(nv, [](int x, int y) { return x + y; });
   er = wave_reduce(er, [](int x, int y) { return x | y; });
-  if ((tid & 63) == 0) {
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
     for (int ax = 0; ax < 3; ++ax) {
-      s_r[tid >> 6][ax] = mn[ax];
-      s_r[tid >> 6][3 + ax] = mx[ax];
+      s_r[w][ax] = mn[ax];
+      s_r[w][3 + ax] = mx[ax];
     }
-    s_r[tid >> 6][6] = nv;
-    s_r[tid >> 6][8] = er;
+    s_r[w][6] = nv;
+    s_r[w][8] = er;
   }
   __syncthreads();
-  if (tid == 0) {
-    int lo[3], hi[3], tv = 0, te = 0;
-    for (int ax = 0; ax < 3; ++ax) {
-      lo[ax] = s_r[0][ax];
-      hi[ax] = s_r[0][3 + ax];
+  VoxTotals t;
+  int64_t nvox = 1;
+  for (int ax = 0; ax < 3; ++ax) {
+    int lo = s_r[0][ax], hi = s_r[0][3 + ax];
+    for (int i = 1; i < kBlock / 64; ++i) {
+      lo = min(lo, s_r[i][ax]);
+      hi = max(hi, s_r[i][3 + ax]);
     }
-    for (int i = 0; i < kPlanT / 64; ++i) {
-      for (int ax = 0; ax < 3; ++ax) {
-        lo[ax] = min(lo[ax], s_r[i][ax]);
-        hi[ax] = max(hi[ax], s_r[i][3 + ax]);
-      }
-      tv += s_r[i][6];
-      te |= s_r[i][8];
-    }
+    t.mn[ax] = lo;
+    t.dv[ax] = hi - lo + 1;
+    nvox *= t.dv[ax];
+  }
+  int tv = 0, te = 0;
+  for (int i = 0; i < kBlock / 64; ++i) {
+    tv += s_r[i][6];
+    te |= s_r[i][8];
+  }
+  t.any = tv > 0;
+  t.nvox = t.any ? nvox : 0;
+  if (publish && threadIdx.x == 0) {
     int32_t* ci = reinterpret_cast<int32_t*>(a.cnt);
-    int64_t nvox = 1;
-    bool wrap = false;
     for (int ax = 0; ax < 3; ++ax) {
-      ci[kVcMin + ax] = lo[ax];
-      ci[kVcMax + ax] = hi[ax];
-      const int64_t dv = (int64_t)hi[ax] - lo[ax] + 1;
-      nvox *= dv;
-      wrap = wrap || dv > (1ll << a.tb[ax]);
+      ci[kVcMin + ax] = t.mn[ax];
+      ci[kVcMax + ax] = t.mn[ax] + t.dv[ax] - 1;
     }
     a.cnt[kVcValid] = (uint32_t)tv;
     a.cnt[kVcValid + 1] = 0;
-    uint32_t e = (uint32_t)te;
-    if (tv > 0 && wrap) e |= kVcErrWrap;
-    a.cnt[kVcErr] = e;
-    if (tv > 0 && !wrap && (nvox > a.grid_cap || nvox > INT_MAX)) a.cnt[kVcOver] = 1;
-    s_stop = tv == 0 || wrap || (e & kVcErrRange);
+    if (te) a.cnt[kVcErr] = (uint32_t)te;
   }
-  __syncthreads();
-  if (s_stop) return;
-  // 2. pair prefix over blocks
-  uint32_t tot;
-  {
-    constexpr int kPer = kVoxChunk / kPlanT;
-    uint32_t v[kPer], sum = 0;
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int b = tid * kPer + k;
-      v[k] = b < a.nblk ? (uint32_t)a.part[(size_t)b * kPartW + kPNew] : 0u;
-      sum += v[k];
-    }
-    uint32_t s0 = excl_scan<kPlanT>(sum, s_scan, &tot);
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      s_pstart[tid * kPer + k] = s0;
-      s0 += v[k];
-    }
-    if (tid == 0) s_pstart[kVoxChunk] = tot;
-  }
-  __syncthreads();
-  auto pair_at = [&](uint32_t g, int* blk) {  // the g-th pair of the frame (block order)
-    int lo = 0, hi = a.nblk;                   // largest b with s_pstart[b] <= g
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (s_pstart[mid] <= g) lo = mid; else hi = mid;
-    }
-    *blk = lo;
-    return a.ptab[(size_t)lo * kVoxChunk + (g - s_pstart[lo])];
-  };
-  // 3. the frame's bricks: pairs of rank 0, in pair order
-  uint32_t nb = 0;
-  for (uint32_t g0 = 0; g0 < tot; g0 += kPlanT) {
-    const uint32_t g = g0 + tid;
-    int blk = 0;
-    uint4 pr = make_uint4(0, 0, 1, 0);
-    if (g < tot) pr = pair_at(g, &blk);
-    const uint32_t first = (g < tot && pr.z == 0) ? 1u : 0u;
-    uint32_t nfirst;
-    const uint32_t r = excl_scan<kPlanT>(first, s_scan, &nfirst);
-    if (first) {
-      a.blist[nb + r] = pr.x;
-      a.bidx[pr.x] = nb + r;
-    }
-    nb += nfirst;
-  }
-  __syncthreads();  // blist / bidx visible to the workgroup
-  // 4. per brick: first pair and first list position
-  uint32_t pacc = 0, qacc = 0;
-  for (uint32_t i0 = 0; i0 < nb; i0 += kPlanT) {
-    const uint32_t i = i0 + tid;
-    unsigned long long v = 0;
-    if (i < nb) v = a.bpc[a.blist[i]];
-    const uint32_t np = (uint32_t)(v >> 32), cap = min((uint32_t)kBrickCells, (uint32_t)v);
-    uint32_t tp, tq;
-    const uint32_t sp = excl_scan<kPlanT>(np, s_scan, &tp);
-    const uint32_t sq = excl_scan<kPlanT>(cap, s_scan, &tq);
-    if (i < nb) {
-      a.pbase[i] = pacc + sp;
-      a.bpos[i] = qacc + sq;
-    }
-    pacc += tp;
-    qacc += tq;
-  }
-  if (tid == 0) {
-    a.pbase[nb] = pacc;
-    a.bpos[nb] = qacc;
-    a.cnt[kVcBricks] = nb;
-    a.cnt[kVcPos] = qacc;
-  }
-  __syncthreads();  // pbase visible
-  // 5. every pair under its brick
-  for (uint32_t g = tid; g < tot; g += kPlanT) {
-    int blk = 0;
-    const uint4 pr = pair_at(g, &blk);
-    a.plist[a.pbase[a.bidx[pr.x]] + pr.z] = make_uint2((uint32_t)blk, pr.y);
-  }
+  return t;
 }
 
-// vox_emit: persistent workgroups over the frame's bricks; a brick's records (all its
-// pairs' ranges of the bin blocks' stages) are summed in LDS (runs of equal cells in each
-// 16-lane row merged first), then every occupied cell becomes one voxel: the packed grid
-// word, its list position (cell, grid word, count; tpos), the centroid safety flag.  The
-// brick's counter returns to zero for the next frame.  No global atomics.
-constexpr int kEmitT = 256;
-__global__ __launch_bounds__(kEmitT) void vox_emit_kernel(VoxArgs a) {
-  __shared__ uint32_t s_c[kBrickCells], s_r[kBrickCells], s_g[kBrickCells], s_b[kBrickCells], s_m[kBrickCells];
-  __shared__ uint32_t s_scan[kEmitT / 64];
-  const int tid = threadIdx.x, lane = tid & 63;
-  uint32_t owned = 0, flagged = 0;
-  const bool run = !(a.cnt[kVcErr] & (kVcErrWrap | kVcErrRange)) && !a.cnt[kVcOver] && a.cnt[kVcValid] > 0;
-  const uint32_t nb = run ? a.cnt[kVcBricks] : 0u;
-  const int32_t* ci = reinterpret_cast<const int32_t*>(a.cnt);
-  int mn[3], dv[3];
-  for (int ax = 0; ax < 3; ++ax) {
-    mn[ax] = ci[kVcMin + ax];
-    dv[ax] = ci[kVcMax + ax] - mn[ax] + 1;
-  }
-  uint32_t* sl = a.lists + (size_t)a.par * a.lcap;
-  uint32_t* tl = a.lists + (size_t)(2 + a.par) * a.lcap;
-  const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1);
-  for (uint32_t i = blockIdx.x; i < nb; i += gridDim.x) {
-    for (int s = tid; s < kBrickCells; s += kEmitT) {
-      s_c[s] = s_r[s] = s_g[s] = s_b[s] = 0u;
-      s_m[s] = kNoM16;
-    }
-    __syncthreads();
-    const uint32_t bk = a.blist[i];
-    const uint32_t p0 = a.pbase[i], p1 = a.pbase[i + 1];
-    for (uint32_t pp = p0; pp < p1; ++pp) {  // uniform: the brick's pairs
-      const uint2 pe = a.plist[pp];
-      const unsigned long long* rec = a.stage + (size_t)pe.x * kVoxChunk + (pe.y & 0xffffu);
-      const int cnt = (int)(pe.y >> 16);
-      for (int j0 = 0; j0 < cnt; j0 += kEmitT) {  // uniform trip count: every lane reaches the DPP
-        const int j = j0 + tid;
-        const bool valid = j < cnt;
-        const unsigned long long r = valid ? rec[j] : 0ull;
-        const uint32_t ib = valid ? (uint32_t)(r >> 24) & (kBrickCells - 1) : kNoT;
-        uint32_t w0 = valid ? (((uint32_t)(r >> 16) & 0xffu) | ((((uint32_t)r >> 8) & 0xffu) << 12) | (1u << 24)) : 0u;
-        uint32_t w1 = valid ? (uint32_t)r & 0xffu : 0u;
-        uint32_t mb = valid ? (uint32_t)(r >> 33) & 0xffffu : kNoM16;
-        const uint32_t ip = vrow_shr<1>(ib);
-        const bool head = !valid || (lane & 15) == 0 || ip != ib;
-        const uint64_t hm = __ballot(head);
-        const int o0 = lane - (63 - __clzll(hm & le));
-        uint32_t s0, s1, sm;
-        s0 = vrow_shr<1>(w0); s1 = vrow_shr<1>(w1); sm = vrow_shr<1>(mb);
-        if (o0 >= 1) { w0 += s0; w1 += s1; mb = min(mb, sm); }
-        s0 = vrow_shr<2>(w0); s1 = vrow_shr<2>(w1); sm = vrow_shr<2>(mb);
-        if (o0 >= 2) { w0 += s0; w1 += s1; mb = min(mb, sm); }
-        s0 = vrow_shr<4>(w0); s1 = vrow_shr<4>(w1); sm = vrow_shr<4>(mb);
-        if (o0 >= 4) { w0 += s0; w1 += s1; mb = min(mb, sm); }
-        s0 = vrow_shr<8>(w0); s1 = vrow_shr<8>(w1); sm = vrow_shr<8>(mb);
-        if (o0 >= 8) { w0 += s0; w1 += s1; mb = min(mb, sm); }
-        const bool tail = valid && ((lane & 15) == 15 || ((hm >> (lane + 1)) & 1));
-        if (tail) {  // the run's totals: count <= 16, channel sums <= 4080
-          atomicAdd(&s_c[ib], w0 >> 24);
-          atomicAdd(&s_r[ib], w0 & 0xfffu);
-          atomicAdd(&s_g[ib], (w0 >> 12) & 0xfffu);
-          atomicAdd(&s_b[ib], w1);
-          if (mb != kNoM16) atomicMin(&s_m[ib], mb);
-        }
-      }
-    }
-    __syncthreads();
-    // the brick's voxels in cell order: list positions bpos[i] + rank
-    constexpr int kSpt = kBrickCells / kEmitT;
-    uint32_t occ = 0;
+__device__ __forceinline__ int seg_count(const VoxArgs& a, int b) {
+  return part_of(a, a.par)[(size_t)b * kPartW + kPNew];
+}
+
+// one block per accum block: its segment's entries.  The first round of entries and their
+// owner words are loaded before the totals are reduced (neither depends on the other)
+__global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
+  const int b = blockIdx.x;
+  const int nn = seg_count(a, b);
+  const size_t seg = (size_t)b * kVoxChunk;
+  const uint32_t* sl = a.lists + (size_t)a.par * a.lcap + seg;
+  uint32_t* tl = a.lists + (size_t)(2 + a.par) * a.lcap + seg;
+  uint32_t* lc = a.lcnt + seg;
+  const uint32_t q0 = (uint32_t)seg;
+  constexpr int kPre = 2;  // entries per thread loaded ahead
+  uint32_t pt[kPre];
+  unsigned long long pmo[kPre];
+  ulonglong2 pacc[kPre];  // the sums, loaded with the owner word (read-only until the owner takes them)
 #pragma unroll
-    for (int k = 0; k < kSpt; ++k) occ += s_c[tid * kSpt + k] ? 1u : 0u;
-    uint32_t nvox;
-    uint32_t rank = excl_scan<kEmitT>(occ, s_scan, &nvox);
-    const uint32_t q0 = a.bpos[i], cap = a.bpos[i + 1] - q0;
-#pragma unroll
-    for (int k = 0; k < kSpt; ++k) {
-      const int s = tid * kSpt + k;
-      const uint32_t count = s_c[s];
-      if (!count) continue;
-      const uint32_t q = q0 + rank++;
-      const uint32_t t = brick_cell(a.tb, bk, (uint32_t)s);
-      uint32_t o[3];
-      tor_offsets(a.tb, t, mn, o);
-      const int64_t idx = o[0] + (int64_t)dv[0] * (o[1] + (int64_t)dv[1] * o[2]);
-      a.grid[idx] = pcl_colour_word(s_r[s], s_g[s], s_b[s], count);
-      sl[q] = t;
-      tl[q] = (uint32_t)idx;
-      a.lcnt[q] = count;
-      a.tpos[t] = q;
-      ++owned;
-      // margins >= kMarginFlush were not recorded: conservative when the bound exceeds it
-      const int cmag = max(max(abs(mn[0] + (int)o[0]), abs(mn[1] + (int)o[1])), abs(mn[2] + (int)o[2])) + 1;
-      const float eps = (float)(count + 4) * (float)cmag * 0x1p-22f;
-      const uint32_t m16 = s_m[s];
-      if ((m16 != kNoM16 && __uint_as_float(m16 << 16) < eps) || eps >= __uint_as_float(kMarginFlush)) ++flagged;
-    }
-    for (uint32_t g = nvox + tid; g < cap; g += kEmitT) {  // the brick's unused positions
-      tl[q0 + g] = kNoT;
-      a.lcnt[q0 + g] = 0u;
-    }
-    if (tid == 0) a.bpc[bk] = 0ull;  // the next frame's counters
-    __syncthreads();                 // before the next brick's LDS clear
+  for (int k = 0; k < kPre; ++k) {
+    const int i = threadIdx.x + k * kBlock;
+    pt[k] = i < nn ? sl[i] : 0u;
+    pmo[k] = i < nn ? ld_coh(&a.mo[pt[k]]) : ~0ull;
+    pacc[k] = i < nn && C3H_VOX_RMW == 0 ? a.acc[pt[k]] : make_ulonglong2(0ull, 0ull);
   }
-  owned = wave_reduce(owned, [](uint32_t u, uint32_t v) { return u + v; });
+  const VoxTotals tot = vox_reduce(a, blockIdx.x == 0);
+  if (!tot.any) return;
+  // the extent beyond the toroidal dims (the host enlarges them and runs the frame again),
+  // or beyond the grid buffer (the host grows it and runs this again): nothing is written
+  bool wrap = false;
+  for (int ax = 0; ax < 3; ++ax) wrap = wrap || tot.dv[ax] > (1 << a.tb[ax]);
+  if (wrap) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.cnt + kVcErr, kVcErrWrap);
+    return;
+  }
+  if (tot.nvox > a.grid_cap || tot.nvox > INT_MAX) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.cnt[kVcOver] = 1;
+    return;
+  }
+  uint32_t flagged = 0, owned = 0;
+  auto visit = [&](int i, uint32_t t, unsigned long long m, const ulonglong2* pre) {
+    const uint32_t q = q0 + (uint32_t)i;
+    if ((uint32_t)m != q) {  // another entry of the voxel owns it
+      tl[i] = kNoT;
+      lc[i] = 0u;
+      return;
+    }
+    ++owned;
+    ulonglong2 v;
+    if (pre) {  // prefetched: every add is a previous launch's; clear with one 16-B store
+      v = *pre;
+      a.acc[t] = make_ulonglong2(0ull, 0ull);
+    } else {
+      v = take_acc(&a.acc[t]);
+    }
+    st_coh(&a.mo[t], ~0ull);
+    a.tpos[t] = q;
+    uint32_t o[3];
+    tor_offsets(a.tb, t, tot.mn, o);
+    const int64_t idx = o[0] + (int64_t)tot.dv[0] * (o[1] + (int64_t)tot.dv[1] * o[2]);
+    const uint32_t count = (uint32_t)(v.x >> 40);
+    a.grid[idx] = pcl_colour_word(v.x & 0xffffffffffull, v.y & 0xffffffffull, v.y >> 32, count);
+    tl[i] = (uint32_t)idx;
+    lc[i] = count;
+    // margins >= kMarginFlush were not recorded: conservative when the bound exceeds it
+    const int cmag = max(max(abs(tot.mn[0] + (int)o[0]), abs(tot.mn[1] + (int)o[1])), abs(tot.mn[2] + (int)o[2])) + 1;
+    const float eps = (float)(count + 4) * (float)cmag * 0x1p-22f;
+    if (__uint_as_float((uint32_t)(m >> 32)) < eps || eps >= __uint_as_float(kMarginFlush)) ++flagged;
+  };
+#pragma unroll
+  for (int k = 0; k < kPre; ++k) {
+    const int i = threadIdx.x + k * kBlock;
+    if (i < nn) visit(i, pt[k], pmo[k], C3H_VOX_RMW == 0 ? &pacc[k] : nullptr);
+  }
+  for (int i = threadIdx.x + kPre * kBlock; i < nn; i += kBlock) {
+    const uint32_t t = sl[i];
+    visit(i, t, ld_coh(&a.mo[t]), nullptr);
+  }
+  // one count add per block (same-address adds serialise at the memory side)
+  __shared__ uint32_t s_cnt[2][kBlock / 64];
   flagged = wave_reduce(flagged, [](uint32_t u, uint32_t v) { return u + v; });
-  if (lane == 0) s_scan[tid >> 6] = owned;
+  owned = wave_reduce(owned, [](uint32_t u, uint32_t v) { return u + v; });
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s_cnt[0][w] = flagged;
+    s_cnt[1][w] = owned;
+  }
   __syncthreads();
-  uint32_t ow = 0;
-  for (int k = 0; k < kEmitT / 64; ++k) ow += s_scan[k];
-  __syncthreads();
-  if (lane == 0) s_scan[tid >> 6] = flagged;
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t fl = 0;
-    for (int k = 0; k < kEmitT / 64; ++k) fl += s_scan[k];
-    a.wgtot[2 * blockIdx.x] = ow;
-    a.wgtot[2 * blockIdx.x + 1] = fl;
+  if (threadIdx.x < 2 && !C3H_VOX_DIAG_NOCNT) {
+    uint32_t v = 0;
+    for (int i = 0; i < kBlock / 64; ++i) v += s_cnt[threadIdx.x][i];
+    if (v) atomicAdd(a.cnt + (threadIdx.x == 0 ? kVcFlag : kVcSlots + a.par), v);
   }
 }
 
@@ -662,10 +542,14 @@ __device__ __forceinline__ bool vox_bounds(const VoxArgs& a, int mn[3], int dv[3
 }
 
 // ---- exact centroids (flagged frames and c3h_get_downsampled) ----------------------
-// list positions q < npos: a voxel's point count, 0 at the gaps of each brick's range
+// positions p = b * kVoxChunk + i of the segmented entry list; entries that do not own
+// their voxel and gaps (i >= the segment's count) hold count 0
 __global__ __launch_bounds__(kBlock) void vox_counts_kernel(VoxArgs a, uint32_t* __restrict__ counts) {
-  for (int64_t q = blockIdx.x * (int64_t)kBlock + threadIdx.x; q < a.npos; q += (int64_t)gridDim.x * kBlock)
-    counts[q] = a.lcnt[q];
+  const int64_t np = (int64_t)a.nblk * kVoxChunk;
+  for (int64_t q = blockIdx.x * (int64_t)kBlock + threadIdx.x; q < np; q += (int64_t)gridDim.x * kBlock) {
+    const int b = (int)(q / kVoxChunk), i = (int)(q % kVoxChunk);
+    counts[q] = i < seg_count(a, b) ? a.lcnt[q] : 0u;
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void vox_bucket_kernel(VoxArgs a, const uint32_t* __restrict__ off,
@@ -693,7 +577,7 @@ __global__ __launch_bounds__(kBlock) void vox_centroid_kernel(VoxArgs a, const u
   int mn[3], dv[3];
   int64_t nvox;
   vox_bounds(a, mn, dv, &nvox);
-  const int64_t np = a.npos;
+  const int64_t np = (int64_t)a.nblk * kVoxChunk;
   const uint32_t* sl = a.lists + (size_t)a.par * a.lcap;
   const uint32_t* tl = a.lists + (size_t)(2 + a.par) * a.lcap;
   for (int64_t q = blockIdx.x * (int64_t)kBlock + threadIdx.x; q < np; q += (int64_t)gridDim.x * kBlock) {
@@ -749,7 +633,7 @@ __global__ __launch_bounds__(kBlock) void vox_downsampled_kernel(VoxArgs a, cons
                                                                  const uint32_t* __restrict__ counts,
                                                                  const int32_t* __restrict__ leaf,
                                                                  float4* __restrict__ out) {
-  const int64_t np = a.npos;
+  const int64_t np = (int64_t)a.nblk * kVoxChunk;
   const uint32_t* tl = a.lists + (size_t)(2 + a.par) * a.lcap;
   for (int64_t q = blockIdx.x * (int64_t)kBlock + threadIdx.x; q < np; q += (int64_t)gridDim.x * kBlock)
     if (counts[q]) out[leaf[tl[q]]] = cent[q];
@@ -1421,20 +1305,17 @@ int64_t scan_blocks(int64_t n) { return (n + kScanBlock - 1) / kScanBlock; }
 int64_t leaf_layout_blocks(int64_t nvox) { return scan_blocks(nvox); }
 
 hipError_t launch_voxelize(const VoxArgs& a, hipStream_t s) {
-  // at least one bin block: it also clears the previous frame and resets the totals
-  vox_bin_kernel<<<(unsigned)std::max(a.nblk, 1), kVB, 0, s>>>(a);
-  if (a.nblk > 0) {
-    vox_plan_kernel<<<1, kPlanT, 0, s>>>(a);
-    vox_emit_kernel<<<kEmitBlocks, kEmitT, 0, s>>>(a);
-  }
+  // at least one accum block: it also clears the previous frame and resets the totals
+  vox_accum_kernel<<<(unsigned)std::max(a.nblk, 1), kVB, 0, s>>>(a);
+  if (a.nblk > 0) vox_scatter_kernel<<<(unsigned)a.nblk, kBlock, 0, s>>>(a);
   return hipGetLastError();
 }
 
-hipError_t launch_vox_emit(const VoxArgs& a, hipStream_t s) {
-  if (a.nblk > 0) vox_emit_kernel<<<kEmitBlocks, kEmitT, 0, s>>>(a);
+
+hipError_t launch_vox_scatter(const VoxArgs& a, hipStream_t s) {
+  if (a.nblk > 0) vox_scatter_kernel<<<(unsigned)a.nblk, kBlock, 0, s>>>(a);
   return hipGetLastError();
 }
-int vox_emit_blocks() { return kEmitBlocks; }
 
 int64_t vox_blocks(int64_t n) { return (n + kVoxChunk - 1) / kVoxChunk; }
 int64_t vox_positions(int64_t n) { return vox_blocks(n) * kVoxChunk; }
@@ -1443,7 +1324,7 @@ int vox_part_words() { return kPartW; }
 hipError_t launch_vox_centroids(const VoxArgs& a, uint32_t* counts, uint32_t* offs, uint32_t* cur,
                                 uint32_t* block_sums, uint32_t* bucket, float4* cent, int32_t* offcell,
                                 hipStream_t s) {
-  const int64_t np = a.npos;
+  const int64_t np = (int64_t)a.nblk * kVoxChunk;
   if (np <= 0) return hipSuccess;
   vox_counts_kernel<<<grid_for(np), kBlock, 0, s>>>(a, counts);
   const int64_t nb = scan_blocks(np);
@@ -1459,7 +1340,7 @@ hipError_t launch_vox_centroids(const VoxArgs& a, uint32_t* counts, uint32_t* of
 
 hipError_t launch_vox_downsampled(const VoxArgs& a, const float4* cent, const uint32_t* counts, const int32_t* leaf,
                                   float* out, hipStream_t s) {
-  const int64_t np = a.npos;
+  const int64_t np = (int64_t)a.nblk * kVoxChunk;
   if (np <= 0) return hipSuccess;
   vox_downsampled_kernel<<<grid_for(np), kBlock, 0, s>>>(a, cent, counts, leaf, reinterpret_cast<float4*>(out));
   return hipGetLastError();
