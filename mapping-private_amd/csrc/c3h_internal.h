@@ -102,15 +102,15 @@ constexpr uint32_t kVcErrWrap = 4;   // the frame's extent exceeds the toroidal 
 // Single-frame voxeliser state.  The accumulators are toroidal: voxel (x, y, z) sums at
 // t = (x mod 2^tb0) | (y mod 2^tb1) << tb0 | (z mod 2^tb2) << (tb0 + tb1), so a frame whose
 // extent fits 2^tb per axis maps its voxels one-to-one without a hash table.  Every
-// (accumulate block, voxel) pair is one list entry; its sums go out as non-returning
-// atomics, and the entry with the min (margin << 32 | entry id) owns the voxel in the
-// scatter, which converts it and returns the accumulator to zero.
+// (accumulate block, voxel) pair adds its sums (the first toucher, seen by its returning
+// add, lists the voxel); the scatter converts each listed voxel and returns its
+// accumulator to zero.
 struct VoxArgs {
   const float4* pts;
   int64_t n;
   float z_limit, inv, leaf;
   ulonglong2* acc;          // [2^(tb0+tb1+tb2)] {count << 40 | sum r, sum b << 32 | sum g}, 0 between frames
-  unsigned long long* mo;   // [same] min over the voxel's entries of (margin bits << 32 | entry id), ~0 between frames
+  uint32_t* mg;             // [same] min near-face margin (float bits) of the voxel's points, ~0 between frames
   uint32_t* tpos;           // [same] list position of the voxel's owning entry (written by the scatter)
   int tb[3];
   uint32_t* lists;          // [entries parity 0 | entries parity 1 | grid words parity 0 | parity 1] x lcap,
@@ -193,8 +193,7 @@ struct VoxBatchArgs {
   int subdiv, off[3];
   float inv_s;
   ulonglong2* acc;                    // [frame][2^(tb0+tb1+tb2)] {count << 40 | sum r, sum b << 32 | sum g}
-  unsigned long long* accMO;          //                min of (margin float bits << 32 | entry id) over
-                                      //                the voxel's (block, voxel) entries, ~0 = none
+  uint32_t* accM;                     //                min boundary margin (float bits), ~0 = none
   int64_t s_acc;
   uint32_t* fcnt;                     // [kMaxBatch] finished accumulate blocks per frame (self-resetting)
   uint32_t* vlist;                    // [block][chunk] the block's (block, voxel) entries (toroidal index)
@@ -504,7 +503,7 @@ struct c3h_ctx {
   // voxeliser state (voxelize.hip): toroidal accumulators, entry / grid-word lists by
   // epoch parity, counters; the grid words the previous frame wrote are cleared by the next
   c3h::DevBuf<ulonglong2> vacc;
-  c3h::DevBuf<unsigned long long> vmo;
+  c3h::DevBuf<uint32_t> vmg;
   c3h::DevBuf<uint32_t> vtpos, vlists, vlcnt, vcnt;
   c3h::DevBuf<int32_t> vpart;
   int vtb[3] = {7, 7, 7};           // toroidal dims (log2 per axis); they only grow
@@ -656,8 +655,7 @@ struct c3h_ctx {
   int pb_prev_nf = 0, pb_prev_total = 0;
   std::vector<int> pb_prev_blk0;
   c3h::DevBuf<ulonglong2> pb_acc;
-  c3h::DevBuf<unsigned long long> pb_accMO;
-  c3h::DevBuf<uint32_t> pb_vlist, pb_fcnt;
+  c3h::DevBuf<uint32_t> pb_accM, pb_vlist, pb_fcnt;
   int64_t pb_acc_vox = 0;
   int pb_acc_slots = 0;
   c3h::DevBuf<float> pb_stage;

@@ -721,7 +721,7 @@ void c3h_destroy(c3h_ctx* ctx) {
   release(ctx->grsd_feat);
   release(ctx->vosch_feat);
   release(ctx->vacc);
-  release(ctx->vmo);
+  release(ctx->vmg);
   release(ctx->vtpos);
   release(ctx->vlcnt);
   release(ctx->vlists);
@@ -770,7 +770,7 @@ void c3h_destroy(c3h_ctx* ctx) {
   release(ctx->pb_xcnt);
   release(ctx->pb_moved);
   release(ctx->pb_acc);
-  release(ctx->pb_accMO);
+  release(ctx->pb_accM);
   release(ctx->pb_fcnt);
   release(ctx->pb_vlist);
   release(ctx->pb_stage);
@@ -853,11 +853,11 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
     if (ctx->vtor != tor || !ctx->vcnt.p) {  // (re)allocation: all-zero accumulators
       ctx->vtor = 0;
       ENSURE(ctx->vacc, (size_t)tor);
-      ENSURE(ctx->vmo, (size_t)tor);
+      ENSURE(ctx->vmg, (size_t)tor);
       ENSURE(ctx->vtpos, (size_t)tor);
       ENSURE(ctx->vcnt, c3h::kVcWords);
       HIPCHK(hipMemsetAsync(ctx->vacc.p, 0, (size_t)tor * 16, ctx->stream));
-      HIPCHK(hipMemsetAsync(ctx->vmo.p, 0xff, (size_t)tor * 8, ctx->stream));
+      HIPCHK(hipMemsetAsync(ctx->vmg.p, 0xff, (size_t)tor * 4, ctx->stream));
       HIPCHK(hipMemsetAsync(ctx->vcnt.p, 0, c3h::kVcWords * 4, ctx->stream));
       ctx->vtor = tor;
     }
@@ -884,7 +884,7 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
     a.inv = gi.inv_leaf;
     a.leaf = leaf;
     a.acc = ctx->vacc.p;
-    a.mo = ctx->vmo.p;
+    a.mg = ctx->vmg.p;
     a.tpos = ctx->vtpos.p;
     for (int ax = 0; ax < 3; ++ax) a.tb[ax] = ctx->vtb[ax];
     a.lists = ctx->vlists.p;
@@ -2468,10 +2468,10 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
     if (tvox > ((int64_t)1 << 31)) return fail(ctx, C3H_ERR_RANGE, "c3h_run_point_frames: canvas too large");
     if (ctx->pb_acc_vox != tvox || ctx->pb_acc_slots < B) {
       ENSURE(ctx->pb_acc, (size_t)B * tvox);
-      ENSURE(ctx->pb_accMO, (size_t)B * tvox);
+      ENSURE(ctx->pb_accM, (size_t)B * tvox);
       ENSURE(ctx->pb_fcnt, (size_t)c3h::kMaxBatch);
       HIPCHK(hipMemsetAsync(ctx->pb_acc.p, 0, (size_t)B * tvox * 16, ctx->stream));
-      HIPCHK(hipMemsetAsync(ctx->pb_accMO.p, 0xff, (size_t)B * tvox * 8, ctx->stream));
+      HIPCHK(hipMemsetAsync(ctx->pb_accM.p, 0xff, (size_t)B * tvox * 4, ctx->stream));
       HIPCHK(hipMemsetAsync(ctx->pb_fcnt.p, 0, (size_t)c3h::kMaxBatch * 4, ctx->stream));
       ctx->pb_acc_vox = tvox;
       ctx->pb_acc_slots = B;
@@ -2578,7 +2578,7 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
       va.inv_s = p->subdiv > 0 ? (float)(1.0 / p->subdiv) : 0.0f;
       for (int a = 0; a < 3; ++a) va.tb[a] = tb[a];
       va.acc = ctx->pb_acc.p;
-      va.accMO = ctx->pb_accMO.p;
+      va.accM = ctx->pb_accM.p;
       va.s_acc = tvox;
       va.fcnt = ctx->pb_fcnt.p;
       va.vlist = ctx->pb_vlist.p;

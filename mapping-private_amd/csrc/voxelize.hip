@@ -4,29 +4,31 @@
 // VoxelGrid::filter, semantics restated in SURVEY.md App. B) and limitPoint
 // (color_voxel_recognition/test/detect_object.cpp:68-87).
 //
-// Hot path: two launches, no hash table, no returning atomic (round 5).
+// Hot path: two launches, no hash table.
 //   vox_accum   one workgroup per 4,096 consecutive points (a depth camera's pixel order
 //               is spatially coherent: a voxel is hit by runs of neighbouring pixels):
 //               coalesced 16-B loads; the cell's toroidal index t (VoxArgs); runs of equal
 //               t in each 16-lane row merged by a DPP segmented scan; one LDS hash insert
 //               per run (count | r, b | g sums, the closest point's distance to a cell face).
-//               Flush: each (workgroup, voxel) pair becomes one list entry of the
-//               workgroup's segment (plain store) and three fire-and-forget atomics: two
-//               64-bit adds into acc[t] and a 64-bit min of (margin << 32 | entry id) into
-//               mo[t].  Nothing waits on a round trip (round 4's hash claim -- a returning
-//               64-bit CAS followed by the adds on its slot -- cost ~14 us of a 36-44 us
-//               frame, profiles/r4/vox_ab/).  The launch also clears the grid words the
-//               previous frame wrote (listed by it) and writes bounds / counts to its own
-//               partial record (no same-address atomics across workgroups).
-//   vox_scatter every block reduces the partial records (bounds, totals), then visits its
-//               segment: the entry whose id is the low half of mo[t] owns the voxel (one
-//               per voxel, the min of its entries), converts it -- linear index (cell -
-//               min_b) . divb_mul from t (modular offsets, exact while the extent fits the
-//               toroidal dims), the canonical colour mean kOcc | r<<16 | g<<8 | b with
-//               r = (int)(float(sum_r) * (1 / float(count))) (Eigen 3.0's scalar quotient,
-//               see pcl_colour_word), the centroid safety test below -- and returns
-//               acc[t] / mo[t] to zero / ~0; the other entries of the voxel skip it (they
-//               read the owner's id, or ~0 once it has reset mo[t]: neither is theirs).
+//               Flush, per (workgroup, voxel): two 64-bit adds into acc[t] (the first one
+//               returning: the workgroup that sees count 0 is the voxel's first toucher and
+//               lists it in its segment) and, only for points near a cell face, a min into
+//               mg[t].  64-bit device atomics run at ~22 G/s chip-wide whatever their scope
+//               or table size (tools/atomic_bench.hip, profiles/r5/), so the flush is priced
+//               by their count: round 4's global hash claim (a returning CAS + two adds)
+//               and round 5's owner word (a third atomic on every pair) both cost more.
+//               The launch also clears the grid words the previous frame wrote (listed by
+//               it) and writes bounds / counts to its own partial record.
+//   vox_scatter every block reduces the partial records (bounds, totals), then converts
+//               its segment's voxels -- linear index (cell - min_b) from t (modular
+//               offsets, exact while the extent fits the toroidal dims), the canonical
+//               colour mean kOcc | r<<16 | g<<8 | b with r = (int)(float(sum_r) * (1 /
+//               float(count))) (Eigen 3.0's scalar quotient, see pcl_colour_word), the
+//               centroid safety test below -- and returns acc[t] / mg[t] to zero / ~0.
+//               The sums are loaded with the list entries, before the bounds reduction.
+// A brick-partitioned variant with no per-voxel global atomic (one atomic per (workgroup,
+// 8^3-cell brick) pair, a planning launch and a per-brick emit) was built and measured at
+// 76 us per 1M-point frame against this design's 32 (profiles/r5/vox_brick/).
 // Integer sums are exact and order-independent, so the grid is deterministic.
 //
 // Centroids.  C3-HLAC takes a voxel's subdivision (floor(c / voxel_size)) and neighbour
@@ -68,43 +70,15 @@ constexpr int kVoxPer = kVoxChunk / kVB;
 #ifndef C3H_VOX_MERGE
 #define C3H_VOX_MERGE 1  // the run merge (0: every point updates the LDS table itself)
 #endif
-#ifndef C3H_VOX_RMW
-#define C3H_VOX_RMW 0  // the accumulators' plain accesses in the scatters: 0 = default cache
-                       // policy (the adds are a previous launch's); diagnostics: 1 = the owner's
-                       // read and clear as atomic exchanges, 2 = device-scope loads and stores
-#endif
-template <class T>
-__device__ __forceinline__ T ld_coh(const T* p) {
-  if (C3H_VOX_RMW == 2) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return *p;
-}
-template <class T>
-__device__ __forceinline__ void st_coh(T* p, T v) {
-  if (C3H_VOX_RMW == 2) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
-}
-// the owner's read and clear of a voxel's sums (one 16-B load and store by default)
+// the owner's read and clear of a voxel's sums (one 16-B load and store; the adds are a
+// previous launch's)
 __device__ __forceinline__ ulonglong2 take_acc(ulonglong2* p) {
-  ulonglong2 v;
-  if (C3H_VOX_RMW == 1) {
-    v.x = __hip_atomic_exchange(&p->x, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    v.y = __hip_atomic_exchange(&p->y, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else if (C3H_VOX_RMW == 2) {
-    v.x = ld_coh(&p->x);
-    v.y = ld_coh(&p->y);
-    st_coh(&p->x, 0ull);
-    st_coh(&p->y, 0ull);
-  } else {
-    v = *p;
-    *p = make_ulonglong2(0ull, 0ull);
-  }
+  const ulonglong2 v = *p;
+  *p = make_ulonglong2(0ull, 0ull);
   return v;
 }
 #ifndef C3H_VOX_DIAG_NOFLUSH
 #define C3H_VOX_DIAG_NOFLUSH 0
-#endif
-#ifndef C3H_VOX_DIAG_NOCNT
-#define C3H_VOX_DIAG_NOCNT 0
 #endif
 #ifndef C3H_VOX_ATOM_SCOPE
 #define C3H_VOX_ATOM_SCOPE __HIP_MEMORY_SCOPE_AGENT
@@ -238,16 +212,15 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
   if (tid == 0) s_nnew = 0;
   __syncthreads();
   uint32_t* sl = a.lists + (size_t)a.par * a.lcap + (size_t)b * kVoxChunk;
-  const uint32_t q0 = (uint32_t)b * (uint32_t)kVoxChunk;
   ulonglong2* __restrict__ acc = a.acc;
-  unsigned long long* __restrict__ mo = a.mo;
-  // one (workgroup, voxel) entry: fire-and-forget sums and the owner / margin min
-  auto add_entry = [&](uint32_t i, uint32_t t, unsigned long long va, unsigned long long vb, uint32_t m) {
-    sl[i] = t;
-    if (C3H_VOX_DIAG_NOFLUSH) return;  // diagnostics: the skeleton without the global sums
-    __hip_atomic_fetch_add(&acc[t].x, va, __ATOMIC_RELAXED, C3H_VOX_ATOM_SCOPE);
+  uint32_t* __restrict__ mg = a.mg;
+  // a (workgroup, voxel) pair that missed the LDS table: the first toucher (its returning
+  // add saw count 0) lists the voxel; the margin goes to mg only when near a face
+  auto add_global = [&](uint32_t t, unsigned long long va, unsigned long long vb, uint32_t m) {
+    const unsigned long long old = __hip_atomic_fetch_add(&acc[t].x, va, __ATOMIC_RELAXED, C3H_VOX_ATOM_SCOPE);
+    if ((old >> 40) == 0) sl[atomicAdd(&s_nnew, 1u)] = t;
     __hip_atomic_fetch_add(&acc[t].y, vb, __ATOMIC_RELAXED, C3H_VOX_ATOM_SCOPE);
-    __hip_atomic_fetch_min(mo + t, ((unsigned long long)m << 32) | (q0 + i), __ATOMIC_RELAXED, C3H_VOX_ATOM_SCOPE);
+    if (m != kNoMargin) __hip_atomic_fetch_min(mg + t, m, __ATOMIC_RELAXED, C3H_VOX_ATOM_SCOPE);
   };
   int mn[3] = {INT_MAX, INT_MAX, INT_MAX}, mx[3] = {INT_MIN, INT_MIN, INT_MIN};
   int nv = 0;
@@ -314,22 +287,32 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
       }
       h = (h + 1) & (kLSlots - 1);
     }
-    if (!done) add_entry(atomicAdd(&s_nnew, 1u), t, A, B, mb);  // LDS table full: an entry of its own
+    if (!done) add_global(t, A, B, mb);  // LDS table full: straight to the global sums
   }
   __syncthreads();  // every point's LDS update is in
-  {  // flush: list positions by one LDS counter add per wave
+  // flush: per (workgroup, voxel) two adds and, near a face only, the margin min (~2 global
+  // atomics per pair: 64-bit device atomics run at ~22 G/s chip-wide, tools/atomic_bench.hip,
+  // so their count sets the flush's cost).  The returning add detects the voxel's first
+  // toucher, which lists it (one list entry per voxel); a thread's returning adds are all
+  // issued before any result is used
+  if (!C3H_VOX_DIAG_NOFLUSH) {
     constexpr int kFl = (kLSlots + kVB - 1) / kVB;
+    uint32_t key[kFl];
+    unsigned long long old[kFl];
 #pragma unroll
     for (int k = 0; k < kFl; ++k) {
       const int s = tid + k * kVB;
-      const uint32_t key = s < kLSlots ? s_key[s] : kNoT;
-      const bool have = key != kNoT;
-      const unsigned long long bm = __ballot(have);
-      if (!bm) continue;
-      uint32_t w0 = 0;
-      if (lane == 0) w0 = atomicAdd(&s_nnew, (uint32_t)__popcll(bm));
-      w0 = __shfl(w0, 0, 64);
-      if (have) add_entry(w0 + (uint32_t)__popcll(bm & ((1ull << lane) - 1)), key, s_A[s], s_B[s], s_m[s]);
+      key[k] = s < kLSlots ? s_key[s] : kNoT;
+      old[k] = key[k] != kNoT ? __hip_atomic_fetch_add(&acc[key[k]].x, s_A[s], __ATOMIC_RELAXED, C3H_VOX_ATOM_SCOPE)
+                              : 1ull << 40;
+    }
+#pragma unroll
+    for (int k = 0; k < kFl; ++k) {
+      const int s = tid + k * kVB;
+      if (key[k] == kNoT) continue;
+      __hip_atomic_fetch_add(&acc[key[k]].y, s_B[s], __ATOMIC_RELAXED, C3H_VOX_ATOM_SCOPE);
+      if (s_m[s] != kNoMargin) __hip_atomic_fetch_min(mg + key[k], s_m[s], __ATOMIC_RELAXED, C3H_VOX_ATOM_SCOPE);
+      if ((old[k] >> 40) == 0) sl[atomicAdd(&s_nnew, 1u)] = key[k];
     }
   }
   // bounds, counts and the entry count go to this block's partial record: no same-address
@@ -450,14 +433,12 @@ __global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
   const uint32_t q0 = (uint32_t)seg;
   constexpr int kPre = 2;  // entries per thread loaded ahead
   uint32_t pt[kPre];
-  unsigned long long pmo[kPre];
-  ulonglong2 pacc[kPre];  // the sums, loaded with the owner word (read-only until the owner takes them)
+  ulonglong2 pacc[kPre];  // the sums (the accumulate launch's adds are all in)
 #pragma unroll
   for (int k = 0; k < kPre; ++k) {
     const int i = threadIdx.x + k * kBlock;
     pt[k] = i < nn ? sl[i] : 0u;
-    pmo[k] = i < nn ? ld_coh(&a.mo[pt[k]]) : ~0ull;
-    pacc[k] = i < nn && C3H_VOX_RMW == 0 ? a.acc[pt[k]] : make_ulonglong2(0ull, 0ull);
+    pacc[k] = i < nn ? a.acc[pt[k]] : make_ulonglong2(0ull, 0ull);
   }
   const VoxTotals tot = vox_reduce(a, blockIdx.x == 0);
   if (!tot.any) return;
@@ -474,22 +455,12 @@ __global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
     return;
   }
   uint32_t flagged = 0, owned = 0;
-  auto visit = [&](int i, uint32_t t, unsigned long long m, const ulonglong2* pre) {
+  auto visit = [&](int i, uint32_t t, ulonglong2 v) {  // every listed voxel is listed once
     const uint32_t q = q0 + (uint32_t)i;
-    if ((uint32_t)m != q) {  // another entry of the voxel owns it
-      tl[i] = kNoT;
-      lc[i] = 0u;
-      return;
-    }
     ++owned;
-    ulonglong2 v;
-    if (pre) {  // prefetched: every add is a previous launch's; clear with one 16-B store
-      v = *pre;
-      a.acc[t] = make_ulonglong2(0ull, 0ull);
-    } else {
-      v = take_acc(&a.acc[t]);
-    }
-    st_coh(&a.mo[t], ~0ull);
+    a.acc[t] = make_ulonglong2(0ull, 0ull);
+    const uint32_t m = a.mg[t];
+    if (m != kNoMargin) a.mg[t] = kNoMargin;  // only the near-face voxels changed it
     a.tpos[t] = q;
     uint32_t o[3];
     tor_offsets(a.tb, t, tot.mn, o);
@@ -501,16 +472,16 @@ __global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
     // margins >= kMarginFlush were not recorded: conservative when the bound exceeds it
     const int cmag = max(max(abs(tot.mn[0] + (int)o[0]), abs(tot.mn[1] + (int)o[1])), abs(tot.mn[2] + (int)o[2])) + 1;
     const float eps = (float)(count + 4) * (float)cmag * 0x1p-22f;
-    if (__uint_as_float((uint32_t)(m >> 32)) < eps || eps >= __uint_as_float(kMarginFlush)) ++flagged;
+    if (__uint_as_float(m) < eps || eps >= __uint_as_float(kMarginFlush)) ++flagged;
   };
 #pragma unroll
   for (int k = 0; k < kPre; ++k) {
     const int i = threadIdx.x + k * kBlock;
-    if (i < nn) visit(i, pt[k], pmo[k], C3H_VOX_RMW == 0 ? &pacc[k] : nullptr);
+    if (i < nn) visit(i, pt[k], pacc[k]);
   }
   for (int i = threadIdx.x + kPre * kBlock; i < nn; i += kBlock) {
     const uint32_t t = sl[i];
-    visit(i, t, ld_coh(&a.mo[t]), nullptr);
+    visit(i, t, a.acc[t]);
   }
   // one count add per block (same-address adds serialise at the memory side)
   __shared__ uint32_t s_cnt[2][kBlock / 64];
@@ -522,7 +493,7 @@ __global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
     s_cnt[1][w] = owned;
   }
   __syncthreads();
-  if (threadIdx.x < 2 && !C3H_VOX_DIAG_NOCNT) {
+  if (threadIdx.x < 2) {
     uint32_t v = 0;
     for (int i = 0; i < kBlock / 64; ++i) v += s_cnt[threadIdx.x][i];
     if (v) atomicAdd(a.cnt + (threadIdx.x == 0 ? kVcFlag : kVcSlots + a.par), v);
@@ -802,10 +773,7 @@ __global__ __launch_bounds__(kBT) void voxb_accum_kernel(VoxBatchArgs a) {
     const int nn = pr[kPNew];
     uint32_t* g = a.grid[fp];
     const uint32_t* wl = a.wlist + (size_t)b * kBChunk;
-    for (int i = tid; i < nn; i += kBT) {
-      const uint32_t wi = wl[i];
-      if (wi != kNoT) g[wi] = 0u;  // (entries that did not own their voxel wrote no word)
-    }
+    for (int i = tid; i < nn; i += kBT) g[wl[i]] = 0u;
   }
   if (b >= a.total) return;  // clearing only
   const int f = vb_frame(a.blk0, a.nf, b);
@@ -815,7 +783,7 @@ __global__ __launch_bounds__(kBT) void voxb_accum_kernel(VoxBatchArgs a) {
   const uint32_t mx_ = (1u << a.tb[0]) - 1, my_ = (1u << a.tb[1]) - 1, mz_ = (1u << a.tb[2]) - 1;
   const int sy = a.tb[0], sz = a.tb[0] + a.tb[1];
   ulonglong2* __restrict__ acc = a.acc + f * a.s_acc;
-  unsigned long long* __restrict__ MO = a.accMO + f * a.s_acc;
+  uint32_t* __restrict__ Mg = a.accM + f * a.s_acc;
   uint32_t* __restrict__ vl = a.vlist + (size_t)b * kBChunk;
   for (int s = tid; s < kBSlots; s += kBT) {
     s_key[s] = kNoT;
@@ -828,19 +796,13 @@ __global__ __launch_bounds__(kBT) void voxb_accum_kernel(VoxBatchArgs a) {
   int mn[3] = {INT_MAX, INT_MAX, INT_MAX}, mx[3] = {INT_MIN, INT_MIN, INT_MIN};
   int nv = 0;
   bool err = false;
-  // one (block, voxel) entry: the block's list gets t, the accumulator the sums, and
-  // MO[t] the min of (margin << 32 | entry id) -- no returning atomic: the entry holding
-  // the min owns the voxel in the scatter (unique: entry ids are), every other entry of
-  // the voxel skips it there
-  const uint32_t q0 = (uint32_t)b * (uint32_t)kBChunk;
-  auto add_entry = [&](uint32_t i, uint32_t t, unsigned long long va, unsigned long long vb, uint32_t m) {
-    vl[i] = t;
-    __hip_atomic_fetch_add(&acc[t].x, va, __ATOMIC_RELAXED, C3H_VB_ATOM_SCOPE);
-    __hip_atomic_fetch_add(&acc[t].y, vb, __ATOMIC_RELAXED, C3H_VB_ATOM_SCOPE);
-    __hip_atomic_fetch_min(MO + t, ((unsigned long long)m << 32) | (q0 + i), __ATOMIC_RELAXED, C3H_VB_ATOM_SCOPE);
-  };
+  // a (block, voxel) pair that misses the LDS table: the first toucher (the returning add
+  // saw count 0) lists the voxel; its margin goes to Mg only when near a face
   auto add_global = [&](uint32_t t, unsigned long long va, unsigned long long vb, uint32_t m) {
-    add_entry(atomicAdd(&s_nnew, 1u), t, va, vb, m);
+    const unsigned long long old = __hip_atomic_fetch_add(&acc[t].x, va, __ATOMIC_RELAXED, C3H_VB_ATOM_SCOPE);
+    if ((old >> 40) == 0) vl[atomicAdd(&s_nnew, 1u)] = t;
+    __hip_atomic_fetch_add(&acc[t].y, vb, __ATOMIC_RELAXED, C3H_VB_ATOM_SCOPE);
+    if (m < kMarginFlush) __hip_atomic_fetch_min(Mg + t, m, __ATOMIC_RELAXED, C3H_VB_ATOM_SCOPE);
   };
   const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1);  // lanes <= this one
   for (int r0 = 0; r0 < kBPer; r0 += kBRound) {
@@ -917,23 +879,29 @@ __global__ __launch_bounds__(kBT) void voxb_accum_kernel(VoxBatchArgs a) {
   }
   }
   __syncthreads();
-  // flush: every (block, voxel) entry is listed and its sums go out as non-returning
-  // atomics (fire and forget: nothing waits for a round trip; round 4's returning add,
-  // which detected the first touch, kept blocks resident until it came back).  List
-  // positions: one LDS counter add per wave
+  // flush: per (block, voxel) two adds and, near a face only, the margin min (~2 global
+  // atomics per pair; round 5's owner word -- a third atomic, min(margin << 32 | entry id),
+  // every pair -- measured slower: 6.1 vs 5.6 us per 128^3 frame, profiles/r5/).  The
+  // returning add detects the voxel's first toucher, which lists it; a thread's slots'
+  // returning adds are all issued before any result is used
   if (C3H_VB_DIAG == 0) {
     constexpr int kFl = (kBSlots + kBT - 1) / kBT;
+    uint32_t key[kFl];
+    unsigned long long old[kFl];
 #pragma unroll
     for (int k = 0; k < kFl; ++k) {
       const int s = tid + k * kBT;
-      const uint32_t key = s < kBSlots ? s_key[s] : kNoT;
-      const bool have = key != kNoT;
-      const unsigned long long bm = __ballot(have);
-      if (!bm) continue;
-      uint32_t w0 = 0;
-      if (lane == 0) w0 = atomicAdd(&s_nnew, (uint32_t)__popcll(bm));
-      w0 = __shfl(w0, 0, 64);
-      if (have) add_entry(w0 + (uint32_t)__popcll(bm & ((1ull << lane) - 1)), key, s_A[s], s_B[s], s_m[s]);
+      key[k] = s < kBSlots ? s_key[s] : kNoT;
+      old[k] = key[k] != kNoT ? __hip_atomic_fetch_add(&acc[key[k]].x, s_A[s], __ATOMIC_RELAXED, C3H_VB_ATOM_SCOPE)
+                              : 1ull << 40;
+    }
+#pragma unroll
+    for (int k = 0; k < kFl; ++k) {
+      const int s = tid + k * kBT;
+      if (key[k] == kNoT) continue;
+      __hip_atomic_fetch_add(&acc[key[k]].y, s_B[s], __ATOMIC_RELAXED, C3H_VB_ATOM_SCOPE);
+      if (s_m[s] < kMarginFlush) __hip_atomic_fetch_min(Mg + key[k], s_m[s], __ATOMIC_RELAXED, C3H_VB_ATOM_SCOPE);
+      if ((old[k] >> 40) == 0) vl[atomicAdd(&s_nnew, 1u)] = key[k];
     }
   }
 #pragma unroll
@@ -1037,7 +1005,7 @@ __global__ __launch_bounds__(kBlock) void voxb_reduce_kernel(VoxBatchArgs a) {
   }
   a.lim[4 * f + 3] = 0;
   rec.n_valid = (uint32_t)tv;
-  rec.n_occ = 0;  // the scatter counts the voxels (one owning entry each; tn counts entries)
+  rec.n_occ = (uint32_t)tn;  // listed voxels (one entry per voxel: its first toucher)
   rec.flagged = 0;  // the scatter adds its flags
   rec.err = (err ? 1u : 0u) | (over ? 2u : 0u);
   rec.moved = 0;
@@ -1061,9 +1029,8 @@ __global__ __launch_bounds__(kBlock) void voxb_scatter_kernel(VoxBatchArgs a) {
   const uint32_t* vl = a.vlist + (size_t)b * kBChunk;
   uint32_t* wl = a.wlist + (size_t)b * kBChunk;
   ulonglong2* __restrict__ acc = a.acc + f * a.s_acc;
-  unsigned long long* __restrict__ MO = a.accMO + f * a.s_acc;
+  uint32_t* __restrict__ Mg = a.accM + f * a.s_acc;
   uint32_t* __restrict__ grid = a.grid[f];
-  const uint32_t q0 = (uint32_t)b * (uint32_t)kBChunk;
   // the tick's tile stamps (occupancy_bits_body's rule: a centre voxel of subdivision
   // t = mx[x] + ns0 (my[y] + ns1 mz[z]) stamps t; the first stamper lists it)
   const int16_t* __restrict__ ax = a.axmap;
@@ -1077,25 +1044,15 @@ __global__ __launch_bounds__(kBlock) void voxb_scatter_kernel(VoxBatchArgs a) {
     for (int i = tid; i < (a.ntiles + 31) / 32; i += kBlock) vb_stamped[i] = 0u;
     __syncthreads();
   }
-  uint32_t flagged = 0, owned = 0;
+  uint32_t flagged = 0;
   for (int i0 = 0; i0 < nseg; i0 += kBlock) {  // wave-uniform trip count (the stamp ballots)
     const int i = i0 + tid;
     int tile = -1;
-    bool own = false;
-    uint32_t t = 0;
-    unsigned long long mo = 0;
-    if (i < nseg) {
-      t = vl[i];
-      mo = ld_coh(&MO[t]);
-      own = (uint32_t)mo == q0 + (uint32_t)i;  // this entry owns the voxel (the min of its entries)
-      if (!own) wl[i] = kNoT;                 // another entry writes (and later clears) the word
-    }
-    if (own) {
-      ++owned;
+    if (i < nseg) {  // every listed voxel is listed once (by its first toucher)
+      const uint32_t t = vl[i];
       const ulonglong2 v = take_acc(&acc[t]);
-      const uint32_t m = (uint32_t)(mo >> 32);
-      // every entry of the voxel has read MO[t] or reads ~0 after this (not its id either)
-      st_coh(&MO[t], ~0ull);
+      const uint32_t m = Mg[t];
+      if (m != kNoMargin) Mg[t] = kNoMargin;  // only the rare near-face voxels changed it
       // offsets from min_b: the toroidal coordinates minus min_b, modulo 2^tb
       const uint32_t cx = ((t & mx_) - (uint32_t)lo[0]) & mx_;
       const uint32_t cy = (((t >> sy) & my_) - (uint32_t)lo[1]) & my_;
@@ -1148,9 +1105,7 @@ __global__ __launch_bounds__(kBlock) void voxb_scatter_kernel(VoxBatchArgs a) {
     }
   }
   flagged = wave_reduce(flagged, [](uint32_t u, uint32_t v) { return u + v; });
-  owned = wave_reduce(owned, [](uint32_t u, uint32_t v) { return u + v; });
   if ((tid & 63) == 0 && flagged) atomicAdd(&a.info[f].flagged, flagged);
-  if ((tid & 63) == 0 && owned) atomicAdd(&a.info[f].n_occ, owned);
 }
 
 // ---- exact centroids of the flagged voxels (round 4) ---------------------------------
