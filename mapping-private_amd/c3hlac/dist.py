@@ -445,10 +445,21 @@ def _initial_lists(M, search_rank, lists):
 
 def merge_slab_candidates(locals_, grid_xyz, subdiv, ranges, M, search_rank, rotate=True, lists=None):
     """The candidate merge in one process (every rank's local blocks at hand): the same
-    payloads and decisions as gather_slab_scores.  Returns (lists, stats)."""
+    payloads and decisions as gather_slab_scores.  Returns (lists, stats); stats times each
+    rank's sender side (its slab-local replay and phase-1 payload: in a distributed run the
+    ranks do this concurrently, so the max is the critical path) and the merge (the
+    candidates' replays and row rounds, done by every rank)."""
+    import time
     lists0 = _initial_lists(M, search_rank, lists)
-    senders = [_SlabSender(lc, grid_xyz, subdiv, ranges, M, search_rank, rotate, lists0) for lc in locals_]
-    mg = _CandMerge([sd.phase1() for sd in senders], grid_xyz, subdiv, ranges, M, search_rank, rotate, lists0)
+    senders, payloads, t_send = [], [], []
+    for lc in locals_:
+        t0 = time.perf_counter()
+        sd = _SlabSender(lc, grid_xyz, subdiv, ranges, M, search_rank, rotate, lists0)
+        payloads.append(sd.phase1())
+        t_send.append(time.perf_counter() - t0)
+        senders.append(sd)
+    t0 = time.perf_counter()
+    mg = _CandMerge(payloads, grid_xyz, subdiv, ranges, M, search_rank, rotate, lists0)
     while True:
         lists, rows = mg.replay()
         if len(rows) == 0:
@@ -459,7 +470,8 @@ def merge_slab_candidates(locals_, grid_xyz, subdiv, ranges, M, search_rank, rot
             pl = sd.rows(mine, mg)
             mg.sent_bytes[r] += pl.size * 8
             mg.fill(mine, pl)
-    return lists, {"bytes_per_rank": mg.sent_bytes, "row_rounds": mg.rounds}
+    return lists, {"bytes_per_rank": mg.sent_bytes, "row_rounds": mg.rounds, "sender_s_max": max(t_send, default=0.0),
+                   "merge_s": time.perf_counter() - t0}
 
 
 def gather_slab_scores(local, grid_xyz, subdiv, ranges, M, search_rank, dist, rotate=True, device="cpu",

@@ -115,7 +115,8 @@ def test_slab_merge_rank4_dense_512_eight_slabs(ctx, record_property):
     assert np.array_equal(cand, whole)
     rec = {"dense_bytes_per_rank_max": max(sum(b.size for b in p[1]) * 8 for p in parts),
            "candidate_bytes_per_rank": st["bytes_per_rank"], "row_rounds": st["row_rounds"],
-           "dense_merge_s": t1 - t0, "candidate_merge_s": t2 - t1}
+           "dense_merge_s": t1 - t0, "candidate_merge_s": t2 - t1,
+           "candidate_sender_s_max_rank": st["sender_s_max"], "candidate_merge_only_s": st["merge_s"]}
     print("slab_merge_512:", json.dumps(rec))
     record_property("slab_merge_512", rec)
     assert max(st["bytes_per_rank"]) * 4 < rec["dense_bytes_per_rank_max"]
