@@ -929,6 +929,9 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
   ctx->vpar ^= 1;
   ctx->vblk_prev = nblk;
   if (hc[c3h::kVcErr] & c3h::kVcErrRange) {
+    // the scatter may have stopped early (an extent beyond the dims): its sums stay behind,
+    // so the next call starts from fresh accumulators
+    ctx->vtor = 0;
     return fail(ctx, C3H_ERR_RANGE, "c3h_voxelize: leaf size too small (cell coordinates beyond +-2^20)");
   }
   uint64_t nvalid;

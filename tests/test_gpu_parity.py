@@ -697,3 +697,23 @@ def test_run_frames_pipelined_many_batches(ctx, batch):
     for i in range(len(words)):
         np.testing.assert_array_equal(got[i], ref[i], err_msg="frame %d" % i)
     ctx.set_batch(4)
+
+
+def test_voxelize_range_error_leaves_no_sums(ctx):
+    """A frame with cells beyond +-2^20 (C3H_ERR_RANGE; its valid points span more than the
+    accumulator dims too) fails, and the next frame's grid is the oracle's: the failed
+    frame's sums do not leak into it."""
+    rng = np.random.default_rng(17)
+    xyz = (rng.random((5000, 3)) * 2.0).astype(np.float32)
+    xyz[0] = (30.0, 0.5, 0.5)  # 3e6 cells at leaf 1e-5: beyond +-2^20
+    col = rng.integers(0, 256, (5000, 3))
+    bad = np.concatenate([xyz, synth.pack_rgb(col[:, 0], col[:, 1], col[:, 2])[:, None]], 1).astype(np.float32)
+    with pytest.raises(c3hlac._capi.C3HError):
+        ctx.voxelize(bad, 1e-5)
+    pts = synth.parity_cloud(3000, grid=16, leaf=0.01, seed=19)
+    ctx.voxelize(pts, 0.01)
+    g, layout, cl = po.voxelize(pts, 0.01)
+    occ = layout >= 0
+    words = ctx.grid()
+    assert np.array_equal(ctx.leaf_layout(), layout)
+    assert np.array_equal(words[occ], (1 << 24) | cl[layout[occ], 3].view(np.uint32)) and not words[~occ].any()
