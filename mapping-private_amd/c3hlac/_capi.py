@@ -212,7 +212,10 @@ def build_provenance():
     by path string, contents concatenated)."""
     import hashlib
     lib = load()
-    info = dict(kv.split("=", 1) for kv in lib.c3h_build_info().decode().split())
+    try:
+        info = dict(kv.split("=", 1) for kv in lib.c3h_build_info().decode().split())
+    except AttributeError:  # a diagnostics build (C3HLAC_LIB) without the provenance record
+        info = {}
     pkg = Path(__file__).resolve().parents[1]
     names = sorted(["csrc/" + p.name for p in (pkg / "csrc").glob("*.hip")]
                    + ["csrc/" + p.name for p in (pkg / "csrc").glob("*.h")]

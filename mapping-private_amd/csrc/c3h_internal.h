@@ -180,6 +180,7 @@ struct VoxMoved {
   uint32_t idx;     // canvas word index of the voxel's own cell
   int32_t base[3];  // canvas coordinates of its centroid's cell (floor(c / leaf) - min_b)
 };
+static_assert(sizeof(VoxMoved) == 16, "VoxMoved: 4 words (point_fixup_kernel's LDS layout)");
 struct VoxBatchArgs {
   int nf, total;                      // frames, accumulate blocks of this batch
   int prev_nf, prev_total;            // the previous batch on this buffer set (its words to clear)
@@ -243,8 +244,10 @@ struct PointFixup {
   uint32_t* tf;                       // per frame: [2] reserved | [2] work counters | stamps
   int64_t s_feat, s_h, s_tf;
   uint32_t epoch;
+  int lmax[3];                        // the largest tile (LDS of the recompute)
 };
 hipError_t launch_point_fixup(const PointFixup& a, hipStream_t s);
+bool point_fixup_fits(const int lmax[3]);  // the recompute's LDS (tile halo, list, operands) fits a CU
 hipError_t launch_vox_batch(const VoxBatchArgs& a, hipStream_t s);
 
 struct C3Launch {

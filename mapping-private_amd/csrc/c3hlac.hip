@@ -311,16 +311,19 @@ __global__ __launch_bounds__(64) void offcell_delta_kernel(OffcellArgs o) {
   offcell_contrib(o, w, sc, nb, 1);
 }
 
-// ---- off-cell fixup of points-in batches (round 4) --------------------------------------
+// ---- off-cell fixup of points-in batches (round 4; dot4 recompute, round 5) ------------
 // After the tile role of a batch: for every voxel the exact pass moved (its centroid cell is
 // not its own), the subdivisions of its own cell and of its centroid cell are recomputed
 // from the canvas: every occupied cell of the subdivision as a centre at its own cell, except
 // the moved voxels, which take their centroid cell as subdivision and neighbour base
-// (c3_hlac.cpp:349-377).  Exact u32 sums in LDS, normalised as the tile role does; the exist
-// gate is rewritten; a subdivision the tile role never saw is stamped and appended to the
-// row list the compress role reads.  One workgroup per (frame, job), jobs deduplicated.
-constexpr int kFixThreads = 256;
-
+// (c3_hlac.cpp:349-377).  The cell-centred part runs the tile body's exact dot4
+// formulation (halo in LDS, compacted centres with the moved ones left out, packed
+// operands, v_dot4_u32_u8); the moved voxels whose centroid lies in the subdivision add
+// their bins by LDS atomics (round 4 did every centre that way: ~1,000 LDS atomics per
+// centre on 981 shared bins, 179 us per 32-frame batch on the tick's stream).  Normalised as
+// the tile role does; the exist gate is rewritten; a subdivision the tile role never saw is
+// stamped and appended to the row list the compress role reads.  One workgroup per (frame,
+// job), jobs deduplicated.
 __device__ __forceinline__ int fix_centre_sub(const PointFixup& a, const int c[3], int* tile) {
   for (int ax = 0; ax < 3; ++ax)
     if (c[ax] < 0 || c[ax] >= a.C[ax]) return -1;
@@ -331,21 +334,20 @@ __device__ __forceinline__ int fix_centre_sub(const PointFixup& a, const int c[3
                                        a.sby * a.segs[3 * (2 * a.seg_stride + iz) + 2]);
 }
 
-// centre word w at neighbour base b (canvas coordinates; the frame's grid is [0, dv))
+// centre word w at neighbour base b (canvas coordinates; the frame's grid is [0, dv)) into
+// the 981-bin layout (117 is folded from it at the end, as the tile body does)
 __device__ void fix_contrib(const PointFixup& a, const uint32_t* __restrict__ grid, const uint32_t* lut,
                             uint32_t w, const int b[3], const int dv[3], uint32_t* hist) {
-  const bool v981 = a.variant == 981;
   int ca[6], be[6];
   channels(w, lut, a.thr, ca, be);
-  const int z0 = v981 ? 495 : 63, pc0 = v981 ? 969 : 105, au0 = v981 ? 474 : 42;
   for (int c = 0; c < 6; ++c) {
-    if (be[c]) atomicAdd(&hist[z0 + c], 1u);
+    if (be[c]) atomicAdd(&hist[495 + c], 1u);
     atomicAdd(&hist[c], (uint32_t)ca[c]);
-    for (int n = c; n < 6; ++n) atomicAdd(&hist[au0 + tri6(c, n)], (uint32_t)(ca[c] * ca[n]));
+    for (int n = c; n < 6; ++n) atomicAdd(&hist[474 + tri6(c, n)], (uint32_t)(ca[c] * ca[n]));
   }
   for (int c = 0; c < 4; ++c)
     for (int n = (c < 2 ? 2 : 4); n < 6; ++n)
-      if (be[c] && be[n]) atomicAdd(&hist[pc0 + (c < 2 ? 4 * c + (n - 2) : 8 + 2 * (c - 2) + (n - 4))], 1u);
+      if (be[c] && be[n]) atomicAdd(&hist[969 + (c < 2 ? 4 * c + (n - 2) : 8 + 2 * (c - 2) + (n - 4))], 1u);
   for (int k = 0; k < 13; ++k) {  // relative coordinates, c3_hlac.cpp:177-202
     const int rel[3] = {k < 9 ? k / 3 - 1 : (k < 12 ? k - 10 : -1), k < 9 ? k % 3 - 1 : (k < 12 ? -1 : 0),
                         k < 9 ? -1 : 0};
@@ -362,19 +364,35 @@ __device__ void fix_contrib(const PointFixup& a, const uint32_t* __restrict__ gr
     channels(nw, lut, a.thr, na, nbe);
     for (int c = 0; c < 6; ++c)
       for (int n = 0; n < 6; ++n) {
-        const int bn = v981 ? bin981(k, c, n) : 6 + 6 * c + n;
+        const int bn = bin981(k, c, n);
         atomicAdd(&hist[bn], (uint32_t)(ca[c] * na[n]));
-        if (be[c] && nbe[n]) atomicAdd(&hist[v981 ? 495 + bn : 63 + bn], 1u);
+        if (be[c] && nbe[n]) atomicAdd(&hist[495 + bn], 1u);
       }
   }
 }
 
-__global__ __launch_bounds__(kFixThreads) void point_fixup_kernel(PointFixup a) {
-  __shared__ uint32_t s_hist[981];
-  __shared__ uint32_t s_lut[256];
-  __shared__ VoxMoved s_mv[kVbMovedCap];
-  __shared__ int s_h[2 * kVbMovedCap], s_t[2 * kVbMovedCap];
-  const int f = blockIdx.y, tid = threadIdx.x;
+// dynamic LDS of point_fixup_kernel: lut | moved | jobs | misc | exclusion bits | halo | list | operands
+__host__ __device__ inline int fix_halo_words(const int lmax[3]) { return (lmax[0] + 2) * (lmax[1] + 2) * (lmax[2] + 1); }
+__host__ __device__ inline int fix_list_max(const int lmax[3]) { return lmax[0] * lmax[1] * lmax[2]; }
+__host__ __device__ inline size_t fix_lds_words(const int lmax[3]) {
+  return 256 + 4 * (size_t)kVbMovedCap + 4 * (size_t)kVbMovedCap + 4 + ((fix_list_max(lmax) + 127) / 128) * 4 +
+         ((fix_halo_words(lmax) + 3) & ~3) + ((fix_list_max(lmax) + 7) / 8) * 4 + (size_t)kGroups * kArrStride;
+}
+
+__global__ __launch_bounds__(kBlock) void point_fixup_kernel(PointFixup a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t fx_smem[];
+  uint32_t* s_lut = fx_smem;                                                     // 256
+  VoxMoved* s_mv = reinterpret_cast<VoxMoved*>(s_lut + 256);                     // kVbMovedCap x 4 words
+  int* s_h = reinterpret_cast<int*>(s_mv + kVbMovedCap);                         // 2 kVbMovedCap
+  int* s_t = s_h + 2 * kVbMovedCap;                                              // 2 kVbMovedCap
+  uint32_t* s_misc = reinterpret_cast<uint32_t*>(s_t + 2 * kVbMovedCap);         // 4
+  const int list_max = fix_list_max(a.lmax);
+  uint32_t* s_excl = s_misc + 4;                                                 // list_max bits
+  uint32_t* s_tile = s_excl + ((list_max + 127) / 128) * 4;                      // halo words
+  uint16_t* s_list = reinterpret_cast<uint16_t*>(s_tile + ((fix_halo_words(a.lmax) + 3) & ~3));
+  uint32_t* s_arr = s_tile + ((fix_halo_words(a.lmax) + 3) & ~3) + ((list_max + 7) / 8) * 4;
+  uint32_t* s_hist = s_arr;  // epilogue alias (981 words)
+  const int f = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   const VoxFrameRec& rec = a.info[f];
   const int nm = (int)min(a.xcnt[4 * f + 2], (uint32_t)kVbMovedCap);
   if (nm == 0 || rec.err) return;  // uniform
@@ -383,8 +401,8 @@ __global__ __launch_bounds__(kFixThreads) void point_fixup_kernel(PointFixup a) 
   const int Cx = a.C[0], Cy = a.C[1];
   const int dv[3] = {rec.max_b[0] - rec.min_b[0] + 1, rec.max_b[1] - rec.min_b[1] + 1,
                      rec.max_b[2] - rec.min_b[2] + 1};
-  for (int i = tid; i < 256; i += kFixThreads) s_lut[i] = a.lut[i];
-  for (int i = tid; i < nm; i += kFixThreads) {
+  for (int i = tid; i < 256; i += kBlock) s_lut[i] = a.lut[i];
+  for (int i = tid; i < nm; i += kBlock) {
     const VoxMoved m = a.moved[(size_t)f * kVbMovedCap + i];
     s_mv[i] = m;
     const int own[3] = {(int)(m.idx % (uint32_t)Cx), (int)((m.idx / (uint32_t)Cx) % (uint32_t)Cy),
@@ -400,49 +418,166 @@ __global__ __launch_bounds__(kFixThreads) void point_fixup_kernel(PointFixup a) 
   int32_t* fexist = a.exist + (int64_t)f * a.s_h;
   int32_t* frows = a.rows + (int64_t)f * a.s_h;
   uint32_t* ftf = a.tf + (int64_t)f * a.s_tf;
+  const int at = tid / 90, arem = tid - at * 90, ak = arem / 6, an = arem - ak * 6;
   for (int j = blockIdx.x; j < 2 * nm; j += gridDim.x) {
     const int h = s_h[j], tile = s_t[j];
     bool skip = h < 0;
     for (int k = 0; k < j && !skip; ++k) skip = s_h[k] == h;  // recomputed by job k
     if (skip) continue;  // uniform
-    for (int i = tid; i < 981; i += kFixThreads) s_hist[i] = 0u;
-    __syncthreads();
     const int sx = tile % a.ns0, sy = (tile / a.ns0) % a.ns1, sz = tile / (a.ns0 * a.ns1);
     const int x0 = a.segs[3 * sx], lx = a.segs[3 * sx + 1];
     const int y0 = a.segs[3 * (a.seg_stride + sy)], ly = a.segs[3 * (a.seg_stride + sy) + 1];
     const int z0 = a.segs[3 * (2 * a.seg_stride + sz)], lz = a.segs[3 * (2 * a.seg_stride + sz) + 1];
-    // the subdivision's centres at their own cells, the moved voxels excepted
-    for (int e = tid; e < lx * ly * lz; e += kFixThreads) {
-      const int c[3] = {x0 + e % lx, y0 + (e / lx) % ly, z0 + e / (lx * ly)};
-      const uint32_t idx = (uint32_t)c[0] + (uint32_t)Cx * ((uint32_t)c[1] + (uint32_t)Cy * (uint32_t)c[2]);
-      const uint32_t w = grid[idx];
-      if (!w) continue;
-      bool mv = false;
-      for (int i = 0; i < nm && !mv; ++i) mv = s_mv[i].idx == idx;
-      if (!mv) fix_contrib(a, grid, s_lut, w, c, dv, s_hist);
+    const int TX = lx + 2, TY = ly + 2, TXY = TX * TY, V = lx * ly * lz;
+    // the moved voxels whose own cell is a centre of this tile: left out of the cell-centred sum
+    for (int i = tid; i < (V + 31) / 32; i += kBlock) s_excl[i] = 0u;
+    if (tid == 0) s_misc[0] = 0;
+    __syncthreads();
+    for (int i = tid; i < nm; i += kBlock) {
+      const uint32_t idx = s_mv[i].idx;
+      const int cx = (int)(idx % (uint32_t)Cx) - x0, cy = (int)((idx / (uint32_t)Cx) % (uint32_t)Cy) - y0,
+                cz = (int)(idx / ((uint32_t)Cx * (uint32_t)Cy)) - z0;
+      if (cx >= 0 && cx < lx && cy >= 0 && cy < ly && cz >= 0 && cz < lz) {
+        const int v = cx + lx * (cy + ly * cz);
+        atomicOr(&s_excl[v >> 5], 1u << (v & 31));
+      }
     }
-    // the moved voxels whose centroid cell is in this subdivision
-    for (int i = tid; i < nm; i += kFixThreads)
+    // 1. halo (lx+2) x (ly+2) x (lz+1) from (x0-1, y0-1, z0-1); outside the canvas: empty
+    for (int e = tid; e < TXY * (lz + 1); e += kBlock) {
+      const int qq = e / TX, rr = e - qq * TX;
+      const int gx = x0 - 1 + rr, gy = y0 - 1 + qq % TY, gz = z0 - 1 + qq / TY;
+      s_tile[e] = ((unsigned)gx < (unsigned)Cx && (unsigned)gy < (unsigned)Cy && (unsigned)gz < (unsigned)a.C[2])
+                      ? grid[gx + (int64_t)Cx * (gy + (int64_t)Cy * gz)] : 0u;
+    }
+    __syncthreads();
+    // 2. occupied centres, the moved ones left out
+    for (int v0 = 0; v0 < V; v0 += kBlock) {
+      const int v = v0 + tid;
+      int ti = 0;
+      bool occ = false;
+      if (v < V) {
+        const int cx = v % lx, cy = (v / lx) % ly, cz = v / (lx * ly);
+        ti = (cx + 1) + (cy + 1) * TX + (cz + 1) * TXY;
+        occ = s_tile[ti] != 0 && !((s_excl[v >> 5] >> (v & 31)) & 1u);
+      }
+      const unsigned long long m = __ballot(occ);
+      if (m) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&s_misc[0], (uint32_t)__popcll(m));
+        base = __shfl(base, 0, 64);
+        if (occ) s_list[base + __popcll(m & ((1ull << lane) - 1))] = (uint16_t)ti;
+      }
+    }
+    __syncthreads();
+    const int nlist = (int)s_misc[0];
+    // 3-4. packed operands and exact dot4 accumulation (c3hlac_tile_body's steps 3-4)
+    uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
+    for (int c0 = 0; c0 < nlist; c0 += kChunk) {
+      for (int job = tid; job < kGroups * 15; job += kBlock) {
+        const int jg = job / 15, jk = job - jg * 15;
+        const int rdx = jk <= 8 ? jk / 3 - 1 : (jk <= 11 ? jk - 10 : -1);
+        const int rdy = jk <= 8 ? jk % 3 - 1 : (jk <= 11 ? -1 : 0);
+        const int rdz = jk <= 8 ? -1 : 0;
+        const int delta = jk < 13 ? rdx + rdy * TX + rdz * TXY : 0;
+        uint32_t w[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int li = c0 + jg * 4 + q;
+          w[q] = li < nlist ? s_tile[s_list[li] + delta] : 0u;
+        }
+        uint32_t nb[6] = {0, 0, 0, 0, 0, 0}, bb[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int sh = 8 * q;
+          const uint32_t occ = w[q] ? 1u : 0u;
+          const uint32_t m8 = occ ? 0xffu : 0u;
+          if (jk == 14) {  // the ones column: occupancy in every channel
+#pragma unroll
+            for (int n = 0; n < 6; ++n) {
+              nb[n] |= occ << sh;
+              bb[n] |= occ << sh;
+            }
+          } else {
+            const uint32_t r = (w[q] >> 16) & 0xffu, g = (w[q] >> 8) & 0xffu, bl = w[q] & 0xffu;
+            const uint32_t lr = s_lut[r], lg = s_lut[g], lb = s_lut[bl];
+            nb[0] |= (lr & m8) << sh;
+            nb[1] |= ((lr >> 8) & m8) << sh;
+            nb[2] |= (lg & m8) << sh;
+            nb[3] |= ((lg >> 8) & m8) << sh;
+            nb[4] |= (lb & m8) << sh;
+            nb[5] |= ((lb >> 8) & m8) << sh;
+            const uint32_t br = (int)r > a.thr[0], bgn = (int)g > a.thr[1], bbl = (int)bl > a.thr[2];
+            bb[0] |= (occ & br) << sh;
+            bb[1] |= (occ & (br ^ 1u)) << sh;
+            bb[2] |= (occ & bgn) << sh;
+            bb[3] |= (occ & (bgn ^ 1u)) << sh;
+            bb[4] |= (occ & bbl) << sh;
+            bb[5] |= (occ & (bbl ^ 1u)) << sh;
+          }
+        }
+        uint32_t* dst = s_arr + jg * kArrStride + jk * 6;
+#pragma unroll
+        for (int n = 0; n < 6; ++n) {
+          dst[n] = nb[n];
+          dst[90 + n] = bb[n];
+        }
+      }
+      __syncthreads();
+      if (tid < 180) {
+        const int ng = (min(nlist - c0, kChunk) + 3) >> 2;
+        const uint32_t* col = s_arr + at * 90 + ak * 6 + an;
+        const uint32_t* ctr = s_arr + at * 90 + 13 * 6;
+        for (int g = 0; g < ng; ++g) {
+          const uint32_t nv = col[g * kArrStride];
+#pragma unroll
+          for (int c = 0; c < 6; ++c) acc[c] = __builtin_amdgcn_udot4(ctr[g * kArrStride + c], nv, acc[c], false);
+        }
+      }
+      __syncthreads();
+    }
+    // 5. the cell-centred bins, then the moved voxels whose centroid lies here
+    for (int i = tid; i < 981; i += kBlock) s_hist[i] = 0u;
+    __syncthreads();
+    if (tid < 180) {
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const int bi = bin_of(at, ak, an, c);
+        if (bi >= 0) s_hist[bi] = acc[c];
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < nm; i += kBlock)
       if (s_h[2 * i + 1] == h) fix_contrib(a, grid, s_lut, grid[s_mv[i].idx], s_mv[i].base, dv, s_hist);
     __syncthreads();
     float* out = ffeat + (int64_t)h * a.variant;
-    for (int i = tid; i < a.variant; i += kFixThreads)
-      out[i] = (float)s_hist[i] * (a.variant == 981 ? norm981(i) : norm117(i));
+    if (a.variant == 981) {
+      for (int i = tid; i < 981; i += kBlock) out[i] = (float)s_hist[i] * norm981(i);
+    } else {
+      for (int i = tid; i < 117; i += kBlock) out[i] = (float)fold117(s_hist, i) * norm117(i);
+    }
     if (tid == 0) {
       fexist[h] = exist_from((float)s_hist[0], (float)s_hist[1]);
       // a subdivision the tile role did not see: stamp it and list its row for the compress
       if (atomicExch(&ftf[4 + tile], a.epoch) != a.epoch) frows[atomicAdd(&ftf[2 + (a.epoch & 1)], 1u)] = h;
     }
-    __syncthreads();  // s_hist is reused by the next job
+    __syncthreads();  // LDS is reused by the next job
   }
 }
 
 }  // namespace
 
+constexpr size_t kFixLdsMax = 160 * 1024;
+bool point_fixup_fits(const int lmax[3]) { return 4 * fix_lds_words(lmax) <= kFixLdsMax; }
+
 hipError_t launch_point_fixup(const PointFixup& a, hipStream_t s) {
   if (a.nf <= 0) return hipSuccess;
   // jobs per frame: 2 per moved voxel; frames without moved voxels exit at once
-  point_fixup_kernel<<<dim3(32, (unsigned)a.nf), kFixThreads, 0, s>>>(a);
+  const size_t lds = 4 * fix_lds_words(a.lmax);
+  if (lds > kFixLdsMax) return hipErrorInvalidValue;  // callers check point_fixup_fits first
+  if (lds > 65536)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&point_fixup_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  point_fixup_kernel<<<dim3(32, (unsigned)a.nf), kBlock, lds, s>>>(a);
   return hipGetLastError();
 }
 

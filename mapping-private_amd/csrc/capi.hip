@@ -2623,7 +2623,7 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
       // the exact pass + off-cell fixup: the tick's direct mode (a row list, one tile per
       // subdivision) on the canvas itself; otherwise flagged frames take the single-frame path
       const bool exact = kPointExact && cl.rows && cl.axmap && cl.gx == canvas[0] && cl.gy == canvas[1] &&
-                         cl.gz == canvas[2];
+                         cl.gz == canvas[2] && c3h::point_fixup_fits(cl.lmax);
       if (exact) {
         va.flags = c->pb_flags.p;
         va.bucket = c->pb_bucket.p;
@@ -2656,6 +2656,7 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
         fx.s_h = cl.s_h;
         fx.s_tf = cl.s_tf;
         fx.epoch = cl.epoch;
+        for (int a = 0; a < 3; ++a) fx.lmax[a] = cl.lmax[a];
         fresh.fix = true;
       }
       if (exact) std::fill(exact_ran.begin() + f0, exact_ran.begin() + f0 + nb, (char)1);

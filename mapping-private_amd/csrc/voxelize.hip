@@ -1160,13 +1160,19 @@ __global__ __launch_bounds__(kBT) void voxb_bucket_kernel(VoxBatchArgs a) {
   }
 }
 
-// voxb_exact: block f, a thread per flagged voxel: its points in input order (shell sort of
-// the bucket), the fp32 sequential sum times 1/n (PCL 1.0 on Eigen 3.0, as the single-frame
-// path and the oracle), the centroid cell floor(c / leaf); a voxel whose centroid cell is
-// not its own cell goes to the frame's moved list (the fixup after the tile role).  A
-// centroid cell past the frame's last subdivision (where the reference reads beyond its
-// histograms) sends the frame to the single-frame path.
+// voxb_exact: kExactSplit blocks per frame, a thread per flagged voxel: its points in input
+// order (an insertion sort of the bucket in the thread's LDS slice when it holds <= 32
+// points, a shell sort in place otherwise), the fp32 sequential sum times 1/n (PCL 1.0 on
+// Eigen 3.0, as the single-frame path and the oracle; the point loads issued 8 ahead of the
+// adds, which stay in order), the centroid cell floor(c / leaf); a voxel whose centroid
+// cell is not its own cell goes to the frame's moved list (the fixup after the tile role).
+// A centroid cell past the frame's last subdivision (where the reference reads beyond its
+// histograms) sends the frame to the single-frame path.  (Round 4 ran one block per frame
+// with the sort in global memory: 136 us per 32-frame batch on the voxeliser's stream.)
+constexpr int kExactSplit = 16;
+constexpr int kExactLds = 32;  // bucket entries per thread sorted in LDS
 __global__ __launch_bounds__(kBlock) void voxb_exact_kernel(VoxBatchArgs a) {
+  __shared__ uint32_t s_bk[kBlock * kExactLds];
   const int f = blockIdx.x, tid = threadIdx.x;
   VoxFrameRec& rec = a.info[f];
   const uint32_t nflag = a.xcnt[4 * f];
@@ -1176,26 +1182,47 @@ __global__ __launch_bounds__(kBlock) void voxb_exact_kernel(VoxBatchArgs a) {
   uint32_t* bks = a.bucket + (size_t)f * kVbBucketCap;
   const float4* __restrict__ pts = a.pts[f];
   const int Cx = a.C[0], Cy = a.C[1];
-  for (int r = tid; r < nrec; r += kBlock) {
+  uint32_t* mine = s_bk + tid;  // this thread's slice, strided by kBlock (bank-conflict free)
+  for (int r = blockIdx.y * kBlock + tid; r < nrec; r += kBlock * gridDim.y) {
     const VoxFlag e = fl[r];
     const int m = (int)e.count;
     uint32_t* bk = bks + e.off;
-    const int gaps[8] = {701, 301, 132, 57, 23, 10, 4, 1};
-    for (int gi = 0; gi < 8; ++gi) {
-      const int gap = gaps[gi];
-      for (int u = gap; u < m; ++u) {
+    const bool small = m <= kExactLds;
+    if (small) {
+      for (int u = 0; u < m; ++u) {  // insertion sort while loading
         const uint32_t t = bk[u];
         int v = u;
-        for (; v >= gap && bk[v - gap] > t; v -= gap) bk[v] = bk[v - gap];
-        bk[v] = t;
+        for (; v > 0 && mine[(v - 1) * kBlock] > t; --v) mine[v * kBlock] = mine[(v - 1) * kBlock];
+        mine[v * kBlock] = t;
+      }
+    } else {
+      const int gaps[8] = {701, 301, 132, 57, 23, 10, 4, 1};
+      for (int gi = 0; gi < 8; ++gi) {
+        const int gap = gaps[gi];
+        for (int u = gap; u < m; ++u) {
+          const uint32_t t = bk[u];
+          int v = u;
+          for (; v >= gap && bk[v - gap] > t; v -= gap) bk[v] = bk[v - gap];
+          bk[v] = t;
+        }
       }
     }
     float sx = 0.0f, sy = 0.0f, sz = 0.0f;
-    for (int u = 0; u < m; ++u) {
-      const float4 p = pts[bk[u]];
-      sx += p.x;
-      sy += p.y;
-      sz += p.z;
+    for (int u0 = 0; u0 < m; u0 += 8) {
+      float4 p[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int u = u0 + q;
+        p[q] = u < m ? pts[small ? mine[u * kBlock] : bk[u]] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (u0 + q < m) {
+          sx += p[q].x;
+          sy += p[q].y;
+          sz += p[q].z;
+        }
+      }
     }
     const float rn = __fdiv_rn(1.0f, (float)m);
     const float c[3] = {__fmul_rn(sx, rn), __fmul_rn(sy, rn), __fmul_rn(sz, rn)};
@@ -1250,7 +1277,7 @@ hipError_t launch_vox_batch(const VoxBatchArgs& a, hipStream_t s) {
     voxb_scatter_kernel<<<(unsigned)a.total, kBlock, a.stamp ? 4 * (size_t)((a.ntiles + 31) / 32) : 0, s>>>(a);
     if (a.flags) {
       voxb_bucket_kernel<<<(unsigned)a.total, kBT, 0, s>>>(a);
-      voxb_exact_kernel<<<(unsigned)a.nf, kBlock, 0, s>>>(a);
+      voxb_exact_kernel<<<dim3((unsigned)a.nf, kExactSplit), kBlock, 0, s>>>(a);
     }
   }
   return hipGetLastError();
