@@ -1109,10 +1109,13 @@ __global__ __launch_bounds__(kBlock) void voxb_scatter_kernel(VoxBatchArgs a) {
 }
 
 // ---- exact centroids of the flagged voxels (round 4) ---------------------------------
-// voxb_bucket: block b of the accumulate grid re-reads its frame's points (frames without
-// flagged voxels return at once) and files every point of a flagged voxel (an LDS hash of
-// the frame's flagged keys) into that voxel's bucket.
+// voxb_bucket: kBucketSplit blocks per block b of the accumulate grid re-read its points
+// (a quarter each, loaded together; frames without flagged voxels return at once) and file
+// every point of a flagged voxel (an LDS hash of the frame's flagged keys) into that
+// voxel's bucket.
 constexpr int kVbFlagSlots = 2 * kVbFlagCap;
+constexpr int kBucketSplit = 4;  // blocks per accumulate chunk (each re-reads a quarter of its points)
+static_assert(kBPer % kBucketSplit == 0, "bucket split");
 static_assert((kVbFlagSlots & (kVbFlagSlots - 1)) == 0, "flag hash");
 __global__ __launch_bounds__(kBT) void voxb_bucket_kernel(VoxBatchArgs a) {
   __shared__ uint32_t s_key[kVbFlagSlots];
@@ -1138,13 +1141,20 @@ __global__ __launch_bounds__(kBT) void voxb_bucket_kernel(VoxBatchArgs a) {
   const int64_t n = a.n[f];
   const uint32_t mx_ = (1u << a.tb[0]) - 1, my_ = (1u << a.tb[1]) - 1, mz_ = (1u << a.tb[2]) - 1;
   const int sy = a.tb[0], sz = a.tb[0] + a.tb[1];
-  for (int j = 0; j < kBPer; ++j) {
-    const int64_t i = base + (int64_t)j * kBT + tid;
-    if (i >= n) break;
-    const float4 p = pts[i];
+  // this block's share of the chunk: kBPer / kBucketSplit points per thread, loaded together
+  constexpr int kPer = kBPer / kBucketSplit;
+  float4 p[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int64_t i = base + (int64_t)(blockIdx.y * kPer + q) * kBT + tid;
+    p[q] = i < n ? pts[i] : make_float4(NAN, NAN, NAN, 0.0f);
+  }
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int64_t i = base + (int64_t)(blockIdx.y * kPer + q) * kBT + tid;
     int c[3];
     float margin;
-    if (!point_valid(p, a.z_limit) || !point_cell(a.inv, p, c, &margin)) continue;
+    if (!point_valid(p[q], a.z_limit) || !point_cell(a.inv, p[q], c, &margin)) continue;
     const uint32_t t = ((uint32_t)c[0] & mx_) | (((uint32_t)c[1] & my_) << sy) | (((uint32_t)c[2] & mz_) << sz);
     uint32_t h = (t * 0x9E3779B1u) >> (32 - __builtin_ctz(kVbFlagSlots));
     for (;;) {
@@ -1285,7 +1295,7 @@ hipError_t launch_vox_batch(const VoxBatchArgs& a, hipStream_t s) {
     voxb_reduce_kernel<<<(unsigned)a.nf, kBlock, 0, s>>>(a);
     voxb_scatter_kernel<<<(unsigned)a.total, kBlock, a.stamp ? 4 * (size_t)((a.ntiles + 31) / 32) : 0, s>>>(a);
     if (a.flags) {
-      voxb_bucket_kernel<<<(unsigned)a.total, kBT, 0, s>>>(a);
+      voxb_bucket_kernel<<<dim3((unsigned)a.total, kBucketSplit), kBT, 0, s>>>(a);
       voxb_exact_kernel<<<dim3((unsigned)a.nf, kExactSplit), kBlock, 0, s>>>(a);
     }
   }

@@ -9,7 +9,7 @@ mkdir -p $O
 V=$R/mapping-private_amd/lib/variants
 export C3H_REQUIRE_GPU=1
 timeout -k 10 700 python -u -m pytest tests/test_gpu_points.py tests/test_gpu_real_views.py tests/test_gpu_production.py \
-  tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1 || exit 1
+  tests/test_gpu_parity.py tests/test_gpu_shape_fixtures.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1 || exit 1
 for rep in 1 2; do
   for v in default prefix; do
     if [ $v = default ]; then unset C3HLAC_LIB; else export C3HLAC_LIB=$V/$v.so; fi

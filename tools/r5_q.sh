@@ -3,5 +3,5 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $R/gpurun_out/smoke_r5q.txt 2>&1 || exit 7
-tools/gpu_round.sh r5q || exit $?
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $R/gpurun_out/smoke_r5r.txt 2>&1 || exit 7
+tools/gpu_round.sh r5r || exit $?
