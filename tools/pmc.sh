@@ -11,7 +11,7 @@ W=5; K=20; B=64
 run() {  # name, counters...
   local name=$1; shift
   timeout -s KILL 240 rocprofv3 --pmc "$@" -d $R/gpurun_out/pmc_$TAG/$name -o run --output-format csv -- \
-    python3 $R/bench.py --steps $K --warmup $W --no-cpu-baseline --point-frames 0 > $R/gpurun_out/pmc_$TAG/$name.log 2>&1
+    python3 $R/bench.py --steps $K --warmup $W --no-cpu-baseline --point-frames 0 --single-frames 0 > $R/gpurun_out/pmc_$TAG/$name.log 2>&1
 }
 run fetch FETCH_SIZE && run write WRITE_SIZE && run sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY && run inst SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT
 rc=$?
