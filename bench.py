@@ -571,9 +571,11 @@ def single_frame_pass(local, torch, synth, c3hlac, rank, n_frames, n_scenes=4):
         ctx.timing(False)
     finally:
         ctx.close()
+    native = native_single_frame(scenes, axis_t, var, axis_q, n_frames)
     med = lambda a: float(np.median(a)) * 1e3  # noqa: E731
     kms = lambda *names: sum(kt[n][0] for n in names) / n_frames  # noqa: E731
     return {
+        "native": native,
         "ms_per_frame_end_to_end": med(e2e),
         "ms_per_frame_end_to_end_mean": float(np.mean(e2e)) * 1e3,
         "frames_per_s": 1e3 / med(e2e),
@@ -586,6 +588,39 @@ def single_frame_pass(local, torch, synth, c3hlac, rank, n_frames, n_scenes=4):
                 "host); medians; compare cpu_baseline.phases_s_per_frame (same scene shape, one core)"
                 % (n_frames, n_scenes),
     }
+
+
+def native_single_frame(scenes, axis_t, var, axis_q, n_frames):
+    """The same per-callback loop in C++ on the C-ABI alone (tools/single_frame_native.cpp,
+    built by the library's Makefile): the frames and bases go through a scratch file to a
+    child process with its own context, which prints its medians (steady_clock around each
+    call) as one JSON line.  None when the tool was not built."""
+    exe = ROOT / "mapping-private_amd" / "lib" / "single_frame_native"
+    if not exe.exists():
+        return None
+    import subprocess
+    import tempfile
+    M, r, Dq = axis_q.shape
+    with tempfile.TemporaryDirectory() as td:
+        f = Path(td) / "frames.bin"
+        with open(f, "wb") as fh:
+            fh.write(np.array([len(scenes), D, VARIANT, M, r, VARIANT, SUBDIV, 0], np.int32).tobytes())
+            fh.write(np.array([LEAF, EXIST_THR], np.float32).tobytes())
+            fh.write(np.array(list(THR) + list(BOX), np.int32).tobytes())
+            for a in (axis_t, var, axis_q):
+                fh.write(np.ascontiguousarray(a, dtype=np.float32).tobytes())
+            for sc in scenes:
+                sc = np.ascontiguousarray(sc, dtype=np.float32)
+                fh.write(np.int64(sc.shape[0]).tobytes())
+                fh.write(sc.tobytes())
+        p = subprocess.run([str(exe), str(f), str(n_frames)], capture_output=True, text=True, timeout=300)
+    if p.returncode != 0:
+        raise RuntimeError("single_frame_native failed (%d): %s" % (p.returncode, p.stderr[-2000:]))
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    res["frames_per_s"] = 1e3 / res["ms_per_frame_end_to_end"]
+    res["note"] = ("the same frames through tools/single_frame_native.cpp: C++ on the C-ABI, no Python "
+                   "(steady_clock medians, its own process and context)")
+    return res
 
 
 def real_views_pass(ctx, dev, torch, synth, c3hlac, reps=10):

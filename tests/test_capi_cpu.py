@@ -96,3 +96,13 @@ def test_build_provenance_record():
     b = _capi.build_provenance()
     assert len(b["lib_src_sha256"]) == 64 and len(b["tree_src_sha256"]) == 64
     assert b["arch"] == "gfx950" and b["built_at"]
+
+
+def test_single_frame_native_tool_links():
+    # the C++ per-callback loop (bench.py single_frame.native) is built beside the library and
+    # resolves every C-ABI symbol it uses at load time; without arguments it prints its usage
+    import subprocess
+    exe = ROOT / "mapping-private_amd" / "lib" / "single_frame_native"
+    assert exe.exists(), "make -C mapping-private_amd builds lib/single_frame_native"
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 1 and "usage" in p.stderr
