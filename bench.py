@@ -536,7 +536,9 @@ def single_frame_pass(local, torch, synth, c3hlac, rank, n_frames, n_scenes=4):
     c3h_voxelize -> c3h_extract -> c3h_search at configs[2]'s shape (256^3, C3-HLAC-117 S=10,
     117 -> 100, 10 models x r = 20, box 2^3, rank 1), detections back on the host.  Its own
     context on its own stream.  Two timed loops over the same frames:
-    - end_to_end: the three calls back to back, exactly what the callback does (the host
+    Each frame's lists start empty (c3h_clean_max, the callback's cleanData, in the C3 phase
+    as detect_object.cpp:168-170 times it).
+    - end_to_end: the calls back to back, exactly what the callback does (the host
       syncs are the API's own: voxelize returns the grid info, search the lists);
     - phases: the same with a device sync after extract, so the wall clock splits as the
       reference prints it (detect_object.cpp:182-186), plus the HIP-event kernel time of
@@ -552,6 +554,7 @@ def single_frame_pass(local, torch, synth, c3hlac, rank, n_frames, n_scenes=4):
             t0 = time.perf_counter()
             ctx.voxelize(scenes[i % n_scenes], LEAF)
             t1 = time.perf_counter()
+            ctx.clean_max()  # search_obj.cleanData() (detect_object.cpp:169): each frame's lists start empty
             ctx.extract(VARIANT, THR, SUBDIV)
             if sync_phases:
                 ctx.synchronize()
@@ -590,7 +593,7 @@ def single_frame_pass(local, torch, synth, c3hlac, rank, n_frames, n_scenes=4):
     }
 
 
-def native_single_frame(scenes, axis_t, var, axis_q, n_frames):
+def native_single_frame(scenes, axis_t, var, axis_q, n_frames, lists_out=None):
     """The same per-callback loop in C++ on the C-ABI alone (tools/single_frame_native.cpp,
     built by the library's Makefile): the frames and bases go through a scratch file to a
     child process with its own context, which prints its medians (steady_clock around each
@@ -613,7 +616,8 @@ def native_single_frame(scenes, axis_t, var, axis_q, n_frames):
                 sc = np.ascontiguousarray(sc, dtype=np.float32)
                 fh.write(np.int64(sc.shape[0]).tobytes())
                 fh.write(sc.tobytes())
-        p = subprocess.run([str(exe), str(f), str(n_frames)], capture_output=True, text=True, timeout=300)
+        cmd = [str(exe), str(f), str(n_frames)] + ([str(lists_out)] if lists_out else [])
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     if p.returncode != 0:
         raise RuntimeError("single_frame_native failed (%d): %s" % (p.returncode, p.stderr[-2000:]))
     res = json.loads(p.stdout.strip().splitlines()[-1])
