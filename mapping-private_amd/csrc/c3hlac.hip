@@ -195,8 +195,10 @@ __global__ __launch_bounds__(kBlock) void c3_occupancy_kernel(OccArgs oa) {
 #endif
 template <int LOAD>
 __global__ __launch_bounds__(kBlock, C3H_MF_MINB) void c3hlac_mfma_kernel(KArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t mf_tab[kMfStaticWords];
   extern __shared__ __attribute__((aligned(16))) uint32_t mf_smem[];
-  c3hlac_mfma_body<LOAD>(a, blockIdx.x * kMfWaves + (threadIdx.x >> 6), gridDim.x * kMfWaves, blockIdx.y, mf_smem);
+  c3hlac_mfma_body<LOAD>(a, blockIdx.x * kMfWaves + (threadIdx.x >> 6), gridDim.x * kMfWaves, blockIdx.y, mf_tab,
+                         mf_smem);
 }
 
 // multi-tile subdivisions: 64-bit exact partial sums -> features
@@ -817,11 +819,12 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
   c3hlac_tile_kernel<<<dim3((unsigned)c.tgrid, (unsigned)l.nframes), kBlock, c.tile_lds, s>>>(c.ka);
   if (mf) {  // both kernels read the frame's work count; each takes the frames of its kind
     const size_t lds = mf_lds_bytes(c.ka.mf_pb);
+    const size_t dyn = mf_dyn_lds_bytes(c.ka.mf_pb);
     const dim3 g((unsigned)mfma_grid(l, lds), (unsigned)l.nframes);
     if (mf_load_items(l.lmax[0], l.lmax[1]) <= 1)
-      c3hlac_mfma_kernel<1><<<g, kBlock, lds, s>>>(c.ka);
+      c3hlac_mfma_kernel<1><<<g, kBlock, dyn, s>>>(c.ka);
     else
-      c3hlac_mfma_kernel<kMfLoad><<<g, kBlock, lds, s>>>(c.ka);
+      c3hlac_mfma_kernel<kMfLoad><<<g, kBlock, dyn, s>>>(c.ka);
   }
   return hipGetLastError();
 }

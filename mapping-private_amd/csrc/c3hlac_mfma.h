@@ -48,7 +48,7 @@ constexpr int kMfLoad = 2;  // (row, dword) items per lane of a layer (<= 18 row
 #define C3H_MF_GAP 16  // diagnostics: 0 = the round-3 plane placement of the two-step layers
 #endif
 #ifndef C3H_MF_EXP
-#define C3H_MF_EXP 0  // diagnostics variants: 1 no K steps, 2 no conversion, 4 no bin epilogue
+#define C3H_MF_EXP 0  // diagnostics variants: 1 no K steps, 2 no conversion, 4 no bin epilogue, 8 no layer loads
 #endif
 
 __host__ __device__ inline int mf_pitch(int lx) { return (lx + 2 + 3) & ~3; }
@@ -91,6 +91,9 @@ static_assert(kMfSlots == 3, "the 981 staging needs the three layer slots (>= 10
 __host__ __device__ inline size_t mf_lds_bytes(int pb) {
   return 3072 + (size_t)mf_const_bytes(pb) + (size_t)kMfWaves * mf_wave_stride(pb) + kMfSrcBytes;
 }
+// the tables and the 128-byte gap are the kernel's static LDS; the rest is dynamic
+constexpr int kMfStaticWords = 800;
+__host__ __device__ inline size_t mf_dyn_lds_bytes(int pb) { return mf_lds_bytes(pb) - 4 * kMfStaticWords; }
 static_assert(4 * kMfStage <= 3 * 3584, "stage fits the layer slots of the smallest plane (288 B)");
 
 // channel plane of (type t: 0 colour LUT / 1 binary, reference channel c in 0..5): the
@@ -408,6 +411,9 @@ __device__ __forceinline__ void mf_layer_ksteps2(const uint8_t* pp, const uint8_
 #undef C3H_MF2
 }
 
+#ifndef C3H_MF_OCCMASK
+#define C3H_MF_OCCMASK 1  // layer conversion: empty voxels restored by a per-dword mask, not a per-read select
+#endif
 #ifndef C3H_MF_SHAPE_CACHE
 #define C3H_MF_SHAPE_CACHE 1  // the tile shape's mask and item map kept across same-shape tiles
 #endif
@@ -508,7 +514,8 @@ __device__ __forceinline__ int mf_chan(int p) { return 2 * (p >> 2) + (p & 1); }
 // wave wid of nw (all waves of this launch for frame fy); smem = mf_lds_bytes(a.mf_pb);
 // LOAD = grid-word items per lane of a layer (1 when every tile's layer fits one pass)
 template <int LOAD>
-__device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int nw, int fy_, uint32_t* smem) {
+__device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int nw, int fy_, uint32_t* s_tab,
+                                                 uint32_t* dyn) {
   const int64_t fy = fy_;
   const int wid = wid_;
   const uint32_t* __restrict__ fgrid = a.grids[fy];
@@ -521,7 +528,6 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int PBM = a.mf_pb;
   // channel-byte tables: T_col[v] = {sin, cos, beta, 1 - beta} ^ 0x80 (setColor LUT, thresholds)
-  uint32_t* s_tab = smem;
   for (int i = threadIdx.x; i < 768; i += kBlock) {
     const int col = i >> 8, v = i & 255;
     const uint32_t l = a.lut[v];
@@ -530,11 +536,14 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
     s_tab[i] = ((l & 0xffu) | (l & 0xff00u) | (be << 16) | ((be ^ 1u) << 24)) ^ 0x80808080u;
   }
   if (threadIdx.x == 0) s_tab[768] = 0x80808080u;  // an empty voxel (in the 128-byte gap)
-  uint8_t* cplanes = reinterpret_cast<uint8_t*>(smem + 768) + 128;  // zeros | ones | 0xff
+  // s_tab: the kernel's static array (3,200 bytes at LDS address 0, so each table read's
+  // address is its byte offset); dyn: the dynamic region right after it (byte 3,200)
+  uint8_t* const lds_x = reinterpret_cast<uint8_t*>(dyn) - 128;  // byte 3,072 (the layout's origin)
+  uint8_t* cplanes = lds_x + 128;  // zeros | ones | 0xff
   for (int i = threadIdx.x; i < 3 * PBM / 4; i += kBlock)
     reinterpret_cast<uint32_t*>(cplanes)[i] = i < PBM / 4 ? 0u : (i < 2 * PBM / 4 ? 0x01010101u : 0xffffffffu);
-  uint8_t* wl = reinterpret_cast<uint8_t*>(smem + 768) + mf_const_bytes(PBM) + (size_t)wave * mf_wave_stride(PBM);
-  uint16_t* s_src = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(smem + 768) + mf_const_bytes(PBM) +
+  uint8_t* wl = lds_x + mf_const_bytes(PBM) + (size_t)wave * mf_wave_stride(PBM);
+  uint16_t* s_src = reinterpret_cast<uint16_t*>(lds_x + mf_const_bytes(PBM) +
                                                 (size_t)kMfWaves * mf_wave_stride(PBM));
   const bool staged = !a.atomic && a.variant == 981;
   if (staged) {  // bin -> stage index (c3h bin_of's inverse; every bin written once)
@@ -626,6 +635,9 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
     }
     uint32_t wv[2][LOAD][4];
     auto load_layer = [&](int L, uint32_t (&w)[LOAD][4]) {
+#if C3H_MF_EXP & 8
+      if (L >= 4) return;  // diagnostics: layers 4.. convert stale words (no loads in the layer loop)
+#endif
       const int gz = z0 - 1 + L;
       const bool zin = (unsigned)gz < (unsigned)a.gz;
 #pragma unroll
@@ -659,11 +671,37 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
         if (it_dst[i] < 0) continue;
         // empty voxels read entry 768 (all channels 0, i.e. 0x80 each)
         uint32_t t[3][4];
+#if C3H_MF_OCCMASK
+        // every voxel reads its colour bytes' entries (an empty word reads entry 0); the empty
+        // voxels' bytes are put back to 0x80 per plane dword by the occupancy mask (byte j =
+        // 0xff when voxel j's word has its occupancy byte)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          // byte address of each colour's entry in one VALU (the byte select of SDWA)
+          uint32_t ar, ag, ab;
+          __asm__("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+                  : "=v"(ar) : "v"(w[i][j]));
+          __asm__("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+                  : "=v"(ag) : "v"(w[i][j]));
+          __asm__("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+                  : "=v"(ab) : "v"(w[i][j]));
+          const uint8_t* tb = reinterpret_cast<const uint8_t*>(s_tab);
+          t[0][j] = *reinterpret_cast<const uint32_t*>(tb + ar);
+          t[1][j] = *reinterpret_cast<const uint32_t*>(tb + 1024 + ag);
+          t[2][j] = *reinterpret_cast<const uint32_t*>(tb + 2048 + ab);
+        }
+        const uint32_t occ = __builtin_amdgcn_perm(w[i][1], w[i][0], 0x0c0c0703u) |
+                             __builtin_amdgcn_perm(w[i][3], w[i][2], 0x07030c0cu);  // 0x01 / 0x00 bytes
+        uint32_t occ8 = occ << 8;
+        __asm__("" : "+v"(occ8));  // x 255 as a shift and a subtract, not a v_mul_lo_u32
+        const uint32_t om = occ8 - occ;
+#else
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
           for (int col = 0; col < 3; ++col)
             t[col][j] = s_tab[w[i][j] ? col * 256 + ((w[i][j] >> (16 - 8 * col)) & 0xffu) : 768u];
+#endif
         uint8_t* dst = slot + it_dst[i];
 #pragma unroll
         for (int col = 0; col < 3; ++col) {
@@ -671,8 +709,12 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
           const uint32_t u1 = __builtin_amdgcn_perm(t[col][1], t[col][0], 0x07030602u);
           const uint32_t u2 = __builtin_amdgcn_perm(t[col][3], t[col][2], 0x05010400u);
           const uint32_t u3 = __builtin_amdgcn_perm(t[col][3], t[col][2], 0x07030602u);
-          const uint32_t o[4] = {__builtin_amdgcn_perm(u2, u0, 0x05040100u), __builtin_amdgcn_perm(u2, u0, 0x07060302u),
-                                 __builtin_amdgcn_perm(u3, u1, 0x05040100u), __builtin_amdgcn_perm(u3, u1, 0x07060302u)};
+          uint32_t o[4] = {__builtin_amdgcn_perm(u2, u0, 0x05040100u), __builtin_amdgcn_perm(u2, u0, 0x07060302u),
+                           __builtin_amdgcn_perm(u3, u1, 0x05040100u), __builtin_amdgcn_perm(u3, u1, 0x07060302u)};
+#if C3H_MF_OCCMASK
+#pragma unroll
+          for (int s2 = 0; s2 < 4; ++s2) o[s2] = (o[s2] & om) | (0x80808080u & ~om);
+#endif
 #pragma unroll
           for (int s2 = 0; s2 < 4; ++s2) *reinterpret_cast<uint32_t*>(dst + (4 * col + s2) * PBv + (col ? gapv : 0)) = o[s2];
         }
