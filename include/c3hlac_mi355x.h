@@ -222,7 +222,9 @@ int c3h_extract_vosch(c3h_ctx* ctx, const c3h_grsd_params* p, const int32_t thr[
 #define C3H_EXIST_GRSD 2
 int c3h_set_features(c3h_ctx* ctx, const float* feat, const int32_t subdiv_b[3], int32_t dim,
                      const int32_t* exist, int32_t exist_rule, int on_device);
-/* hist_num x variant floats of the last extract */
+/* hist_num x variant floats of the last extract.  After an extract at fp16 search precision
+ * on a large dense 981 grid (c3h_set_search_precision below) the rows are the f16 ones the
+ * C3 kernel wrote, widened: each value is the exact integer-derived feature rounded to f16. */
 int c3h_get_features(c3h_ctx* ctx, float* out, int on_device);
 /* exist_voxel_num of SearchC3HLAC::setC3HLAC
  * (color_voxel_recognition/include/color_voxel_recognition/search_c3_hlac.h:60-61) */
@@ -248,7 +250,11 @@ int c3h_search_setup(c3h_ctx* ctx, const float* axis_p, const float* var, int32_
  * position's box row -- scaled by a power of two, |Q f|/|f| is scale-free -- and the model
  * basis to f16; both accumulate in f32 on v_mfma_f32_32x32x16_f16.  Scores then agree with
  * the float64 oracle within 2e-3 relative (fp16 = 0, the default: fp32, 1e-5).  The VALU
- * kernels and the pipelined c3h_run_frames path always run in fp32. */
+ * kernels and the pipelined c3h_run_frames path always run in fp32.
+ * The setting also applies to c3h_extract: at fp16 a large dense C3-HLAC-981 extract (the
+ * matrix-core C3 kernel) writes its feature rows as f16 only.  Setting fp16 = 0 afterwards
+ * searches those rounded rows (widened to f32) until the next extract, so the 1e-5 bound of
+ * fp32 precision holds only for features extracted at fp16 = 0: re-extract after switching. */
 int c3h_set_search_precision(c3h_ctx* ctx, int32_t fp16);
 /* Engine of the single-frame search's projection step (SearchObjMulti::searchPart's
  * M x r x D products, search.cpp:915-968): 0 = automatic (default: the matrix cores for

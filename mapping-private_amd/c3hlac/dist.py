@@ -208,10 +208,12 @@ def slab_scores(ctx, words_zyx, variant, thr, subdiv, ranges, exist_threshold, r
     sbl, _ = ctx.extract(variant, thr, subdiv, (0, 0, zoff))
     prev_rank = getattr(ctx, "rank", None)
     ctx.set_rank(1)  # the fast path: only the scores are used
-    ctx.search(ranges, exist_threshold, rotate=rotate)
-    out = owned_blocks(ctx.scores(), sbl, p0, p1, (gx, gy, gz), subdiv, ranges, max(ctx.M, 1), rotate)
-    if prev_rank is not None and prev_rank != 1:
-        ctx.set_rank(prev_rank)  # the caller's setRank (fresh lists of that rank)
+    try:
+        ctx.search(ranges, exist_threshold, rotate=rotate)
+        out = owned_blocks(ctx.scores(), sbl, p0, p1, (gx, gy, gz), subdiv, ranges, max(ctx.M, 1), rotate)
+    finally:  # restored on errors too
+        if prev_rank is not None and prev_rank != 1:
+            ctx.set_rank(prev_rank)  # the caller's setRank (fresh lists of that rank)
     return out
 
 

@@ -99,6 +99,14 @@ enum {
 constexpr uint32_t kVcErrRange = 1;  // cell coordinates beyond +-2^20
 constexpr uint32_t kVcErrWrap = 4;   // the frame's extent exceeds the toroidal accumulator (the
                                      // frame runs again on larger dims; the scatter wrote nothing)
+// a listed voxel outside the frame's bounds, a point whose voxel has no owning entry of this
+// frame, or a voxel whose accumulated count differs from the points filed into its bucket:
+// the accumulators held sums the frame did not add.  Every such access is skipped (device-
+// side bound checks) and the call fails (round 6: the round-5 fault)
+constexpr uint32_t kVcErrBad = 8;
+// toroidal accumulator cells at most 2^kVoxTorMaxBits (24 B each: 1.6 GB); a frame whose
+// extent needs more is voxelised by sorting its points (launch_vox_sorted)
+constexpr int kVoxTorMaxBits = 26;
 // Single-frame voxeliser state.  The accumulators are toroidal: voxel (x, y, z) sums at
 // t = (x mod 2^tb0) | (y mod 2^tb1) << tb0 | (z mod 2^tb2) << (tb0 + tb1), so a frame whose
 // extent fits 2^tb per axis maps its voxels one-to-one without a hash table.  Every
@@ -123,8 +131,13 @@ struct VoxArgs {
   int64_t grid_cap;
   int par;                  // epoch parity of this frame
   int clear_grid;           // clear the grid words the previous frame listed
+  int blk0;                 // first accumulate block of this launch (chunked host input)
 };
 hipError_t launch_voxelize(const VoxArgs& a, hipStream_t s);
+// the accumulate pass over blocks [a.blk0, a.blk0 + nblocks) only (host frames copied in
+// chunks: each chunk's blocks start when its copy lands; the first launch (blk0 0) resets
+// the counters and clears the previous frame's words)
+hipError_t launch_vox_accum(const VoxArgs& a, int nblocks, hipStream_t s);
 // f16 feature rows -> f32 rows when *flag (device-side check: no host sync)
 hipError_t launch_feat16_to_f32(const _Float16* f16, int f16s, const uint32_t* flag, int64_t H, int F, float* out,
                                 hipStream_t s);
@@ -132,11 +145,25 @@ hipError_t launch_vox_scatter(const VoxArgs& a, hipStream_t s);
 int64_t vox_blocks(int64_t n);
 int64_t vox_positions(int64_t n);
 int vox_part_words();
+constexpr int kVoxPartNew = 7;  // a partial record's word holding its segment's entry count
 hipError_t launch_vox_centroids(const VoxArgs& a, uint32_t* counts, uint32_t* offs, uint32_t* cur,
                                 uint32_t* block_sums, uint32_t* bucket, float4* cent, int32_t* offcell,
                                 hipStream_t s);
 hipError_t launch_vox_downsampled(const VoxArgs& a, const float4* cent, const uint32_t* counts, const int32_t* leaf,
                                   float* out, hipStream_t s);
+hipError_t launch_vox_clear(const VoxArgs& a, hipStream_t s);
+// wide frames (extent beyond 2^kVoxTorMaxBits accumulator cells): the voxeliser by a stable
+// radix sort of (voxel index, point index) pairs.  mn / dv: the frame's bounds from the first
+// pass; nv: its valid points.  Writes the grid, the lists, counts, exact centroids and the
+// off-cell records (the state the exact pass would leave).  tmp_bytes query: tmp == nullptr.
+struct VoxSortBufs {
+  uint32_t *keys, *keys2, *idx, *idx2, *head, *block_sums;
+  int32_t* ord;
+  void* tmp;
+  size_t tmp_bytes;
+};
+hipError_t launch_vox_sorted(const VoxArgs& a, const int mn[3], const int dv[3], int64_t nv, VoxSortBufs& b,
+                             uint32_t* counts, float4* cent, int32_t* offcell, hipStream_t s);
 int64_t scan_blocks(int64_t n);
 hipError_t launch_leaf_layout(const uint32_t* grid, int64_t nvox, int32_t* leaf,
                               uint32_t* block_sums, int64_t nblocks, hipStream_t s);
@@ -288,6 +315,14 @@ struct C3Launch {
   _Float16* feat16 = nullptr;
   uint32_t* feat16_flag = nullptr;
   int f16s = 0;
+  // the grid of the last c3h_voxelize (round 6): its scatter listed every occupied voxel's
+  // grid index (segment b of vl_seg positions at vl_words + b * vl_seg, vl_counts[b *
+  // vl_count_stride] of them), so the tiles are stamped from that list and the occupancy
+  // stream over the whole grid is skipped; nullptr: stream the grid
+  const uint32_t* vl_words = nullptr;
+  const int32_t* vl_counts = nullptr;
+  int vl_nseg = 0, vl_seg = 0, vl_count_stride = 0;
+  int64_t max_work = 0;  // > 0: at most this many tiles can be listed (single frame)
 };
 
 int64_t c3hlac_grid(const C3Launch& a);  // persistent grid of the tile kernel
@@ -666,6 +701,10 @@ struct c3h_ctx {
   // the batched voxeliser runs on its own stream, one batch ahead of the tick that consumes
   // it (events: a batch's voxels are done / the tick that last read a buffer set is done)
   hipStream_t pb_vstream = nullptr;
+  // c3h_voxelize of host frames: the chunked H2D's stream, its start and per-chunk events
+  hipStream_t vcopy = nullptr;
+  hipEvent_t vcopy_start = nullptr;
+  std::vector<hipEvent_t> vcopy_ev;
   hipEvent_t pb_vox_ev = nullptr, pb_tick_ev[4] = {nullptr, nullptr, nullptr, nullptr};
 
   std::vector<PipeBatch> pipe;   // in flight, oldest first

@@ -189,6 +189,68 @@ __global__ __launch_bounds__(kBlock) void c3_occupancy_kernel(OccArgs oa) {
   }
 }
 
+// c3h_extract of the grid the last c3h_voxelize wrote (round 6): the
+// voxeliser's scatter listed every occupied voxel's grid index, so the tiles of the
+// occupied centre voxels (c3_occupancy_kernel's rule: word != 0, every axis map >= 0) are
+// stamped from that list -- ~4 B per occupied voxel instead of a 4 B/voxel stream of the
+// whole grid (67 MB at 256^3 for ~0.3 % occupancy).  One workgroup per list segment;
+// neighbouring entries mostly share a tile (the scatter lists them in point order), so a
+// lane skips its predecessor's tile, the rest go through the LDS set and its flush.
+__global__ __launch_bounds__(kBlock) void c3_list_stamp_kernel(OccArgs oa, const uint32_t* __restrict__ words,
+                                                               const int32_t* __restrict__ counts, int seg,
+                                                               int count_stride) {
+  const int gx = oa.gx, gy = oa.gy, gz = oa.gz;
+  const int ns0 = oa.ns0, ns1 = oa.ns1;
+  const uint32_t epoch = oa.epoch;
+  uint32_t* __restrict__ flags = oa.tf + 4;
+  uint32_t* __restrict__ cnt = oa.tf + 2 + (epoch & 1);
+  int32_t* __restrict__ work = oa.work;
+  __shared__ int s_set[kOccSet];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int16_t* mx = oa.axmap;
+  const int16_t* my = mx + gx;
+  const int16_t* mz = my + gy;
+  for (int i = tid; i < kOccSet; i += kBlock) s_set[i] = -1;
+  __syncthreads();
+  const int nn = counts[(size_t)blockIdx.x * count_stride];
+  const uint32_t* wl = words + (size_t)blockIdx.x * seg;
+  const uint32_t nvox = (uint32_t)gx * (uint32_t)gy * (uint32_t)gz;  // < 2^31 (host-checked)
+  for (int i0 = 0; i0 < nn; i0 += kBlock) {  // wave-uniform trip count (the neighbour shuffle)
+    const int i = i0 + tid;
+    int t = -1;
+    if (i < nn) {
+      const uint32_t v = wl[i];
+      if (v < nvox) {  // (kNoT entries: none on a completed voxelize)
+        const uint32_t row = v / (uint32_t)gx;
+        const int x = (int)(v - row * (uint32_t)gx);
+        const int y = (int)(row % (uint32_t)gy), z = (int)(row / (uint32_t)gy);
+        const int tx = mx[x], ty = my[y], tz = mz[z];
+        if (tx >= 0 && ty >= 0 && tz >= 0) t = tx + ns0 * (ty + ns1 * tz);
+      }
+    }
+    const int tp = __shfl_up(t, 1, 64);
+    if (t >= 0 && !(lane > 0 && tp == t)) set_insert(s_set, t, epoch, flags, cnt, work);
+  }
+  __syncthreads();
+  int ts[kOccSet / kBlock];
+  bool fresh[kOccSet / kBlock];
+#pragma unroll
+  for (int j = 0; j < kOccSet / kBlock; ++j) {  // all exchanges in flight together
+    ts[j] = s_set[tid + j * kBlock];
+    fresh[j] = ts[j] >= 0 && atomicExch(&flags[ts[j]], epoch) != epoch;
+  }
+#pragma unroll
+  for (int j = 0; j < kOccSet / kBlock; ++j) {
+    const unsigned long long m = __ballot(fresh[j]);
+    if (m) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(cnt, (uint32_t)__popcll(m));
+      base = __shfl(base, 0, 64);
+      if (fresh[j]) work[base + __popcll(m & ((1ull << lane) - 1))] = ts[j];
+    }
+  }
+}
+
 // dense frames: one tile per wave on the i8 matrix cores (c3hlac_mfma.h)
 #ifndef C3H_MF_MINB
 #define C3H_MF_MINB 3
@@ -765,7 +827,12 @@ hipError_t launch_feat16_to_f32(const _Float16* f16, int f16s, const uint32_t* f
 }
 
 // dense-tile MFMA kernel: tiles up to 16 x 16 per layer, resident persistent grid
-static bool mfma_ok(const C3Launch& l) { return l.lmax[0] <= 16 && l.lmax[1] <= 16 && l.debug == 0; }
+static bool mfma_ok(const C3Launch& l) {
+  // a frame takes the MFMA body when at least half its tiles are listed: with a bound on
+  // the listed tiles below that (the voxeliser's occupied-voxel count), no launch
+  if (l.max_work > 0 && 2 * l.max_work < l.ntiles) return false;
+  return l.lmax[0] <= 16 && l.lmax[1] <= 16 && l.debug == 0;
+}
 
 static int64_t mfma_grid(const C3Launch& l, size_t lds) {
   static thread_local size_t c_lds = 0;
@@ -799,11 +866,17 @@ hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
 #endif
   c.oa.contiguous = C3H_OCC_CONTIG && l.ntiles >= 65536 ? 1 : 0;  // large grids (config 5): contiguous chunk ranges
   const dim3 g1d((unsigned)c.g1, (unsigned)l.nframes);
-  if (l.dense && l.nframes == 1 && c.bits && mf) {  // config 5: skip the stream of a dense grid
+  if (l.vl_words && l.nframes == 1) {  // the voxeliser's list of occupied voxels
+    if (l.vl_nseg > 0)
+      c3_list_stamp_kernel<<<(unsigned)l.vl_nseg, kBlock, 0, s>>>(c.oa, l.vl_words, l.vl_counts, l.vl_seg,
+                                                                  l.vl_count_stride);
+  } else if (l.dense && l.nframes == 1 && c.bits && mf) {  // config 5: skip the stream of a dense grid
     dense_probe_kernel<<<64, kBlock, 0, s>>>(c.oa, l.dense);
     c.oa.dense = l.dense;
   }
-  if (c.bits) {
+  if (l.vl_words && l.nframes == 1) {
+    // stamped above
+  } else if (c.bits) {
     if (c.ax)
       c3_occupancy_bits_kernel<true><<<g1d, kBlock, c.occ_lds, s>>>(c.oa);
     else

@@ -646,6 +646,13 @@ int exact_centroids(c3h_ctx* ctx) {
                                    ctx->vbucket.p, ctx->vcent.p, ctx->voffcell.p, ctx->stream));
   HIPCHK(hipMemcpyAsync(ctx->h_small, ctx->vcnt.p, c3h::kVcWords * 4, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (ctx->h_small[c3h::kVcErr] & c3h::kVcErrBad) {
+    // counts that the frame's points do not fill (the bound checks skipped every such
+    // access): the accumulators held foreign sums, the next call re-zeroes them
+    ctx->vtor = 0;
+    ctx->table_valid = false;
+    return fail(ctx, C3H_ERR_HIP, "c3h_voxelize: internal: voxel counts differ from the frame's points");
+  }
   ctx->n_offcell = ctx->h_small[c3h::kVcOff];
   ctx->vcent_valid = true;
   return C3H_OK;
@@ -700,6 +707,12 @@ void c3h_destroy(c3h_ctx* ctx) {
     (void)hipStreamDestroy(ctx->pb_vstream);
   }
   if (ctx->pb_vox_ev) (void)hipEventDestroy(ctx->pb_vox_ev);
+  if (ctx->vcopy) {
+    (void)hipStreamSynchronize(ctx->vcopy);
+    (void)hipStreamDestroy(ctx->vcopy);
+  }
+  if (ctx->vcopy_start) (void)hipEventDestroy(ctx->vcopy_start);
+  for (hipEvent_t e : ctx->vcopy_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->pb_tick_ev)
     if (e) (void)hipEventDestroy(e);
   release(ctx->grid);
@@ -810,6 +823,16 @@ int c3h_synchronize(c3h_ctx* ctx) {
 
 const char* c3h_last_error(const c3h_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
+// c3h_voxelize of host frames: chunked copy + accumulate overlap (0: one copy, then the pass)
+#ifndef C3H_VOX_CHUNKED_COPY
+#define C3H_VOX_CHUNKED_COPY 1
+#endif
+constexpr bool kVoxChunkedCopy = C3H_VOX_CHUNKED_COPY;
+#ifndef C3H_VOX_COPY_CHUNK_BLOCKS
+#define C3H_VOX_COPY_CHUNK_BLOCKS 64  // accumulate blocks (of 4,096 points) per copied chunk
+#endif
+constexpr int kVoxCopyChunkBlocks = C3H_VOX_COPY_CHUNK_BLOCKS;
+
 int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, float leaf,
                  float z_limit, c3h_grid_info* info) {
   if (!ctx) return C3H_ERR_ARG;
@@ -831,12 +854,18 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
   gi.leaf = leaf;
   gi.inv_leaf = 1.0f / leaf;
   const float4* d_pts = nullptr;
+  // host frames of >= 2 chunks go over PCIe in chunks on a copy stream, and each chunk's
+  // accumulate blocks start as soon as it lands: the accumulate pass hides under the copy
+  // (a 1M-point frame: 4 chunks of 64 accumulate blocks)
+  const int64_t chunk_pts = (int64_t)kVoxCopyChunkBlocks * c3h::vox_positions(1);
+  const bool chunked = kVoxChunkedCopy && n > 0 && !on_device && n >= 2 * chunk_pts;
   if (n > 0) {
     if (on_device) {
       d_pts = reinterpret_cast<const float4*>(xyzrgb);
     } else {
       ENSURE(ctx->pts, (size_t)n * 4);
-      HIPCHK(hipMemcpyAsync(ctx->pts.p, xyzrgb, (size_t)n * 16, hipMemcpyHostToDevice, ctx->stream));
+      if (!chunked)
+        HIPCHK(hipMemcpyAsync(ctx->pts.p, xyzrgb, (size_t)n * 16, hipMemcpyHostToDevice, ctx->stream));
       d_pts = reinterpret_cast<const float4*>(ctx->pts.p);
     }
   }
@@ -848,6 +877,17 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
   const int nblk = (int)c3h::vox_blocks(n);
   c3h::VoxArgs a{};
   uint32_t* hc = ctx->h_small;
+  // Every exit between the first launch and a completed scatter leaves sums in the
+  // accumulators that no later frame may add onto: the next call then starts
+  // from freshly zeroed accumulators (vtor = 0 forces the reallocation branch's memsets)
+  struct AccGuard {
+    c3h_ctx* c;
+    bool armed;
+    ~AccGuard() {
+      if (armed) c->vtor = 0;
+    }
+  } acc_guard{ctx, false};
+  bool wide = false;  // the extent needs more than 2^kVoxTorMaxBits accumulator cells: sorted path
   for (int attempt = 0;; ++attempt) {
     const int64_t tor = (int64_t)1 << (ctx->vtb[0] + ctx->vtb[1] + ctx->vtb[2]);
     if (ctx->vtor != tor || !ctx->vcnt.p) {  // (re)allocation: all-zero accumulators
@@ -899,7 +939,33 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
     a.grid_cap = (int64_t)ctx->grid.n;
     a.par = ctx->vpar;
     a.clear_grid = clear_grid ? 1 : 0;
-    {
+    acc_guard.armed = true;
+    if (chunked && attempt == 0) {
+      const int nch = (int)((n + chunk_pts - 1) / chunk_pts);
+      if (!ctx->vcopy) HIPCHK(hipStreamCreateWithFlags(&ctx->vcopy, hipStreamNonBlocking));
+      if (!ctx->vcopy_start) HIPCHK(hipEventCreateWithFlags(&ctx->vcopy_start, hipEventDisableTiming));
+      while ((int)ctx->vcopy_ev.size() < nch) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ctx->vcopy_ev.push_back(e);
+      }
+      // the copies overwrite ctx->pts: after everything queued that may read it
+      HIPCHK(hipEventRecord(ctx->vcopy_start, ctx->stream));
+      HIPCHK(hipStreamWaitEvent(ctx->vcopy, ctx->vcopy_start, 0));
+      Timed t(ctx, 0);
+      for (int k = 0; k < nch; ++k) {
+        const int64_t off = k * chunk_pts, cnt = std::min<int64_t>(chunk_pts, n - off);
+        HIPCHK(hipMemcpyAsync(ctx->pts.p + 4 * off, xyzrgb + 4 * off, (size_t)cnt * 16, hipMemcpyHostToDevice,
+                              ctx->vcopy));
+        HIPCHK(hipEventRecord(ctx->vcopy_ev[k], ctx->vcopy));
+        HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->vcopy_ev[k], 0));
+        c3h::VoxArgs ak = a;
+        ak.blk0 = (int)(off / c3h::vox_positions(1));
+        ak.clear_grid = k == 0 ? a.clear_grid : 0;
+        HIPCHK(c3h::launch_vox_accum(ak, (int)c3h::vox_blocks(cnt), ctx->stream));
+      }
+      HIPCHK(c3h::launch_vox_scatter(a, ctx->stream));
+    } else {
       Timed t(ctx, 0);
       HIPCHK(c3h::launch_voxelize(a, ctx->stream));
     }
@@ -918,10 +984,12 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
       while (((int64_t)1 << tb[ax]) < dv) ++tb[ax];
       sum += tb[ax];
     }
-    if (attempt >= 2 || sum > 31) {
-      ctx->vtor = 0;  // the next call starts from fresh accumulators
-      return fail(ctx, C3H_ERR_RANGE, "c3h_voxelize: frame extent beyond 2^31 voxels of accumulators");
+    if (sum > c3h::kVoxTorMaxBits) {  // a wide frame: no accumulators of that size
+      wide = true;
+      break;
     }
+    if (attempt >= 2)  // cannot happen: the dims above fit the extent the first pass measured
+      return fail(ctx, C3H_ERR_HIP, "c3h_voxelize: internal: extent still beyond the accumulators");
     for (int ax = 0; ax < 3; ++ax) ctx->vtb[ax] = tb[ax];
     ctx->vgrid_tracked = true;  // the grid holds no word of this frame (its scatter wrote none)
   }
@@ -938,6 +1006,7 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
   memcpy(&nvalid, hc + c3h::kVcValid, 8);
   gi.n_valid = (int64_t)nvalid;
   if (nvalid == 0) {  // nothing scattered, and the previous frame's words are cleared
+    acc_guard.armed = false;  // no point added anything
     ctx->vgrid_tracked = true;
     ctx->info = gi;
     ctx->have_grid = true;
@@ -956,6 +1025,60 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
   if (nvox > 2147483647LL) {
     return fail(ctx, C3H_ERR_RANGE, "c3h_voxelize: leaf size too small for int32 voxel indices");
   }
+  if (wide) {
+    // the sorted path (voxelize.hip): first the accumulate pass's sums go back to zero
+    // through its first-touch lists, then the frame is voxelised from its points alone
+    HIPCHK(c3h::launch_vox_clear(a, ctx->stream));
+    acc_guard.armed = false;
+    const bool fresh = ctx->grid.n < (size_t)nvox;
+    ENSURE(ctx->grid, (size_t)nvox);
+    if (fresh) HIPCHK(hipMemsetAsync(ctx->grid.p, 0, ctx->grid.n * 4, ctx->stream));
+    a.grid = ctx->grid.p;
+    a.grid_cap = (int64_t)ctx->grid.n;
+    const int64_t np = (int64_t)nblk * c3h::vox_positions(1);
+    const size_t npts = (size_t)std::max<int64_t>(n, 1);
+    ENSURE(ctx->vcounts, (size_t)np);
+    ENSURE(ctx->vcent, (size_t)np);
+    ENSURE(ctx->voffs, (size_t)np);
+    ENSURE(ctx->voffcell, (size_t)std::max<uint64_t>(nvalid, 1) * 8);
+    ENSURE(ctx->vbucket, npts);
+    ENSURE(ctx->tmp_u32, (size_t)c3h::scan_blocks((int64_t)nvalid));
+    ENSURE(ctx->nkeys, npts);
+    ENSURE(ctx->nkeys2, npts);
+    ENSURE(ctx->nidx, npts);
+    ENSURE(ctx->nidx2, npts);
+    c3h::VoxSortBufs sb{ctx->nkeys.p, ctx->nkeys2.p, ctx->nidx.p, ctx->nidx2.p, ctx->vbucket.p, ctx->tmp_u32.p,
+                        reinterpret_cast<int32_t*>(ctx->voffs.p), nullptr, 0};
+    int mn[3], dv[3];
+    for (int ax = 0; ax < 3; ++ax) {
+      mn[ax] = gi.min_b[ax];
+      dv[ax] = gi.div_b[ax];
+    }
+    HIPCHK(c3h::launch_vox_sorted(a, mn, dv, (int64_t)nvalid, sb, ctx->vcounts.p, ctx->vcent.p, ctx->voffcell.p,
+                                  ctx->stream));
+    ENSURE(ctx->ntmp, std::max<size_t>(sb.tmp_bytes, 1));
+    sb.tmp = ctx->ntmp.p;
+    sb.tmp_bytes = ctx->ntmp.n;
+    {
+      Timed t(ctx, 0);
+      HIPCHK(c3h::launch_vox_sorted(a, mn, dv, (int64_t)nvalid, sb, ctx->vcounts.p, ctx->vcent.p, ctx->voffcell.p,
+                                    ctx->stream));
+    }
+    HIPCHK(hipMemcpyAsync(hc, ctx->vcnt.p, c3h::kVcWords * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->vgrid_tracked = true;
+    ctx->vargs = a;
+    ctx->vns = hc[c3h::kVcSlots + a.par];
+    gi.n_occ = ctx->vns;
+    ctx->info = gi;
+    ctx->grid_ptr = ctx->grid.p;
+    ctx->have_grid = true;
+    ctx->table_valid = true;
+    ctx->n_offcell = hc[c3h::kVcOff];
+    ctx->vcent_valid = true;  // the exact centroids are in (the pass the toroidal path defers)
+    if (info) *info = gi;
+    return C3H_OK;
+  }
   if (hc[c3h::kVcOver]) {  // the grid buffer grows (zeroed) and the scatter runs again
     ENSURE(ctx->grid, (size_t)nvox);
     HIPCHK(hipMemsetAsync(ctx->grid.p, 0, ctx->grid.n * 4, ctx->stream));
@@ -970,6 +1093,9 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
     HIPCHK(hipStreamSynchronize(ctx->stream));
     if (hc[c3h::kVcOver]) return fail(ctx, C3H_ERR_HIP, "c3h_voxelize: internal: grid still too small");
   }
+  if (hc[c3h::kVcErr] & c3h::kVcErrBad)  // (the guard re-zeroes the accumulators)
+    return fail(ctx, C3H_ERR_HIP, "c3h_voxelize: internal: a listed voxel outside the frame's bounds");
+  acc_guard.armed = false;  // the scatter returned every touched accumulator to zero
   ctx->vgrid_tracked = true;
   ctx->vargs = a;
   ctx->vns = hc[c3h::kVcSlots + a.par];
@@ -1171,6 +1297,12 @@ int c3h_set_grid(c3h_ctx* ctx, const uint32_t* words, const int32_t div_b[3],
 #define C3H_DENSE_PROBE 1
 #endif
 constexpr bool kDenseProbe = C3H_DENSE_PROBE;
+// the extract after a c3h_voxelize stamps its tiles from the voxeliser's list (round 6;
+// 0: stream the grid, as round 5)
+#ifndef C3H_VOX_LIST_STAMP
+#define C3H_VOX_LIST_STAMP 1
+#endif
+constexpr bool kVoxListStamp = C3H_VOX_LIST_STAMP;
 
 static bool extract_params_ok(const c3h_extract_params* p) {
   return (p->variant == 981 || p->variant == 117) && p->color_mode >= C3H_COLOR_C3_FLOAT &&
@@ -1383,7 +1515,22 @@ int extract_frames(c3h_ctx* ctx, const uint32_t* const* grids, int nf, const c3h
     l.debug = 0;
     l.prof = nullptr;
     l.dense = nullptr;
-    if (!ctx->capture && nf == 1 && ntiles >= 65536 && l.zero_empty && !atomic && kDenseProbe) {
+    // the grid of the last c3h_voxelize: its occupied voxels are listed (vox_scatter / the
+    // sorted path), so the tiles are stamped from the list instead of the 4 B/voxel stream
+    // (sparse frames: 16 B of list work per occupied voxel below the grid's 4 B per voxel)
+    const bool from_list = kVoxListStamp && !ctx->capture && nf == 1 && ctx->table_valid &&
+                           ctx->grid_ptr == ctx->grid.p && ctx->vargs.lists &&
+                           (int64_t)ctx->vns * 16 < (int64_t)div[0] * div[1] * div[2];
+    if (from_list) {
+      const c3h::VoxArgs& va = ctx->vargs;
+      l.vl_words = va.lists + (size_t)(2 + va.par) * va.lcap;
+      l.vl_counts = va.part + (size_t)va.par * va.nblk_cap * c3h::vox_part_words() + c3h::kVoxPartNew;
+      l.vl_count_stride = c3h::vox_part_words();
+      l.vl_seg = (int)c3h::vox_positions(1);
+      l.vl_nseg = va.nblk;
+      l.max_work = std::max<int64_t>(ctx->vns, 1);  // a tile per occupied voxel at most
+    }
+    if (!from_list && !ctx->capture && nf == 1 && ntiles >= 65536 && l.zero_empty && !atomic && kDenseProbe) {
       ENSURE(ctx->dense_flag, 1);
       l.dense = ctx->dense_flag.p;
     }

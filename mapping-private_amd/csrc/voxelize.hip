@@ -46,6 +46,8 @@
 #include <algorithm>
 #include <climits>
 
+#include <rocprim/device/device_radix_sort.hpp>
+
 #include "c3h_internal.h"
 
 namespace c3h {
@@ -144,6 +146,7 @@ __device__ __forceinline__ void tor_offsets(const int tb[3], uint32_t t, const i
 // per accum block: {min xyz, max xyz, valid points, list entries, error} at part[par][b]
 constexpr int kPartW = 12;
 enum { kPMin = 0, kPMax = 3, kPValid = 6, kPNew = 7, kPErr = 8 };
+static_assert(kPNew == kVoxPartNew, "the extract's list stamp reads the entry counts");
 
 __device__ __forceinline__ const int32_t* part_of(const VoxArgs& a, int par) {
   return a.part + (size_t)par * a.nblk_cap * kPartW;
@@ -162,7 +165,7 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
   __shared__ uint32_t s_m[kLSlots];
   __shared__ uint32_t s_nnew;                  // list entries of this workgroup
   __shared__ int s_red[kVB / 64][8];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, b = blockIdx.x + a.blk0;
   if (b == 0 && tid == 0) {  // totals of an empty frame (the scatter publishes the others)
     for (int ax = 0; ax < 3; ++ax) {
       reinterpret_cast<int32_t*>(a.cnt)[kVcMin + ax] = INT_MAX;
@@ -177,7 +180,7 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
   auto clear_prev = [&]() {
     if (!a.clear_grid) return;
     const int pp = a.par ^ 1;
-    for (int pb = b; pb < a.nblk_prev; pb += gridDim.x) {
+    for (int pb = blockIdx.x; pb < a.nblk_prev; pb += gridDim.x) {  // (a launch with blk0 0)
       const int nn = part_of(a, pp)[(size_t)pb * kPartW + kPNew];
       const uint32_t* tl = a.lists + (size_t)(2 + pp) * a.lcap + (size_t)pb * kVoxChunk;
       for (int i = tid; i < nn; i += kVB) {
@@ -454,16 +457,26 @@ __global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
     if (blockIdx.x == 0 && threadIdx.x == 0) a.cnt[kVcOver] = 1;
     return;
   }
-  uint32_t flagged = 0, owned = 0;
+  uint32_t flagged = 0, owned = 0, bad = 0;
   auto visit = [&](int i, uint32_t t, ulonglong2 v) {  // every listed voxel is listed once
     const uint32_t q = q0 + (uint32_t)i;
-    ++owned;
     a.acc[t] = make_ulonglong2(0ull, 0ull);
     const uint32_t m = a.mg[t];
     if (m != kNoMargin) a.mg[t] = kNoMargin;  // only the near-face voxels changed it
-    a.tpos[t] = q;
     uint32_t o[3];
     tor_offsets(a.tb, t, tot.mn, o);
+    // bound check: a listed key is a cell of this frame's points, so its offsets lie inside
+    // the frame's extent -- unless the accumulators held sums no point of this frame added
+    // (kVcErrBad: nothing written, the call fails)
+    if (o[0] >= (uint32_t)tot.dv[0] || o[1] >= (uint32_t)tot.dv[1] || o[2] >= (uint32_t)tot.dv[2] ||
+        (v.x >> 40) == 0) {
+      tl[i] = kNoT;
+      lc[i] = 0u;
+      ++bad;
+      return;
+    }
+    ++owned;
+    a.tpos[t] = q;
     const int64_t idx = o[0] + (int64_t)tot.dv[0] * (o[1] + (int64_t)tot.dv[1] * o[2]);
     const uint32_t count = (uint32_t)(v.x >> 40);
     a.grid[idx] = pcl_colour_word(v.x & 0xffffffffffull, v.y & 0xffffffffull, v.y >> 32, count);
@@ -487,10 +500,12 @@ __global__ __launch_bounds__(kBlock) void vox_scatter_kernel(VoxArgs a) {
   __shared__ uint32_t s_cnt[2][kBlock / 64];
   flagged = wave_reduce(flagged, [](uint32_t u, uint32_t v) { return u + v; });
   owned = wave_reduce(owned, [](uint32_t u, uint32_t v) { return u + v; });
+  bad = wave_reduce(bad, [](uint32_t u, uint32_t v) { return u | v; });
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
     s_cnt[0][w] = flagged;
     s_cnt[1][w] = owned;
+    if (bad) atomicOr(a.cnt + kVcErr, kVcErrBad);
   }
   __syncthreads();
   if (threadIdx.x < 2) {
@@ -523,18 +538,40 @@ __global__ __launch_bounds__(kBlock) void vox_counts_kernel(VoxArgs a, uint32_t*
   }
 }
 
+// Bound checks (round 6): the bucket of a voxel has exactly its accumulated count of slots.
+// A point whose voxel's owning entry is not this frame's (tpos stale: the voxel was never
+// listed) or whose bucket is already full (the count holds a point it does not own) is not
+// filed, and the centroid pass skips a bucket with an unfilled slot -- the round-5 fault: a
+// run-merge bug moved one point's count to cell 0's voxel, which left one slot of its bucket
+// unwritten, and on a fresh context that slot's uninitialised index was read as a point.
 __global__ __launch_bounds__(kBlock) void vox_bucket_kernel(VoxArgs a, const uint32_t* __restrict__ off,
+                                                            const uint32_t* __restrict__ counts,
                                                             uint32_t* __restrict__ cur,
                                                             uint32_t* __restrict__ bucket) {
+  const uint64_t np = (uint64_t)a.nblk * kVoxChunk;
+  const uint32_t* sl = a.lists + (size_t)a.par * a.lcap;
+  bool bad = false;
   for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * kBlock) {
     const float4 p = a.pts[i];
     if (!point_valid(p, a.z_limit)) continue;
     int c[3];
     float m;
     if (!point_cell(a.inv, p, c, &m)) continue;
-    const uint32_t lp = a.tpos[tor_index(a.tb, c)];
-    bucket[off[lp] + atomicAdd(&cur[lp], 1u)] = (uint32_t)i;
+    const uint32_t t = tor_index(a.tb, c);
+    const uint32_t lp = a.tpos[t];
+    // counts[lp] is 0 beyond the entry's segment count and for entries that own nothing
+    if (lp >= np || sl[lp] != t || counts[lp] == 0) {
+      bad = true;
+      continue;
+    }
+    const uint32_t slot = atomicAdd(&cur[lp], 1u);
+    if (slot >= counts[lp]) {
+      bad = true;
+      continue;
+    }
+    bucket[off[lp] + slot] = (uint32_t)i;
   }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(a.cnt + kVcErr, kVcErrBad);
 }
 
 // per voxel: its points in input order (shell sort of the bucket), the fp32 sequential
@@ -542,6 +579,7 @@ __global__ __launch_bounds__(kBlock) void vox_bucket_kernel(VoxArgs a, const uin
 // {linear index, neighbour-base cell xyz, subdivision cell xyz} relative to min_b
 __global__ __launch_bounds__(kBlock) void vox_centroid_kernel(VoxArgs a, const uint32_t* __restrict__ off,
                                                               const uint32_t* __restrict__ counts,
+                                                              const uint32_t* __restrict__ cur,
                                                               uint32_t* __restrict__ bucket,
                                                               float4* __restrict__ cent,
                                                               int32_t* __restrict__ offcell) {
@@ -554,6 +592,11 @@ __global__ __launch_bounds__(kBlock) void vox_centroid_kernel(VoxArgs a, const u
   for (int64_t q = blockIdx.x * (int64_t)kBlock + threadIdx.x; q < np; q += (int64_t)gridDim.x * kBlock) {
     const int m = (int)counts[q];
     if (m == 0) continue;
+    if (cur[q] != (uint32_t)m) {  // a slot not filed by this frame's points (vox_bucket_kernel)
+      atomicOr(a.cnt + kVcErr, kVcErrBad);
+      cent[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      continue;
+    }
     uint32_t* bk = bucket + off[q];
     const int gaps[8] = {701, 301, 132, 57, 23, 10, 4, 1};
     for (int gi = 0; gi < 8; ++gi) {
@@ -608,6 +651,124 @@ __global__ __launch_bounds__(kBlock) void vox_downsampled_kernel(VoxArgs a, cons
   const uint32_t* tl = a.lists + (size_t)(2 + a.par) * a.lcap;
   for (int64_t q = blockIdx.x * (int64_t)kBlock + threadIdx.x; q < np; q += (int64_t)gridDim.x * kBlock)
     if (counts[q]) out[leaf[tl[q]]] = cent[q];
+}
+
+// returns the accumulators a frame's accumulate pass touched to zero (a frame the scatter
+// did not convert: its extent wrapped the toroidal dims and it went to the sorted path).
+// Every non-zero record was first touched by one (block, voxel) pair, which listed it.
+__global__ __launch_bounds__(kBlock) void vox_clear_kernel(VoxArgs a) {
+  const int b = blockIdx.x;
+  const int nn = seg_count(a, b);
+  const uint32_t* sl = a.lists + (size_t)a.par * a.lcap + (size_t)b * kVoxChunk;
+  for (int i = threadIdx.x; i < nn; i += kBlock) {
+    const uint32_t t = sl[i];
+    a.acc[t] = make_ulonglong2(0ull, 0ull);
+    a.mg[t] = kNoMargin;
+  }
+}
+
+// ---- wide frames: the sorted path ---------------------------------------------------
+// A frame whose extent needs more than 2^kVoxTorMaxBits toroidal cells (24 B each) is
+// voxelised by sorting instead: its valid points' linear voxel indices (cell - min_b, known
+// from the first pass; < 2^31 by the host's check) as 32-bit keys, invalid points keyed
+// nvox (after every voxel), a stable radix sort of (key, point index) pairs, and one thread
+// per run of equal keys.  The stable sort keeps a voxel's points in input order, so the
+// thread sums them exactly as the oracle does (fp32 sequential xyz, integer colour), and
+// writes the grid word, the list entries, the exact centroid and the off-cell record: the
+// state vox_scatter + the exact pass leave.  Memory O(points) whatever the extent.
+__global__ __launch_bounds__(kBlock) void voxs_keys_kernel(VoxArgs a, int3 mn, int3 dv, uint32_t sentinel,
+                                                           uint32_t* __restrict__ keys, uint32_t* __restrict__ idx) {
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * kBlock) {
+    const float4 p = a.pts[i];
+    int c[3];
+    float m;
+    uint32_t k = sentinel;
+    if (point_valid(p, a.z_limit) && point_cell(a.inv, p, c, &m)) {
+      const uint32_t o0 = (uint32_t)(c[0] - mn.x), o1 = (uint32_t)(c[1] - mn.y), o2 = (uint32_t)(c[2] - mn.z);
+      if (o0 < (uint32_t)dv.x && o1 < (uint32_t)dv.y && o2 < (uint32_t)dv.z)  // bounds of the same points
+        k = o0 + (uint32_t)dv.x * (o1 + (uint32_t)dv.y * o2);
+    }
+    keys[i] = k;
+    idx[i] = (uint32_t)i;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void voxs_heads_kernel(const uint32_t* __restrict__ keys, int64_t nv,
+                                                            uint32_t* __restrict__ head) {
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kBlock)
+    head[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void voxs_emit_kernel(VoxArgs a, int3 mn, int3 dv, const uint32_t* __restrict__ keys,
+                                                           const uint32_t* __restrict__ idx,
+                                                           const uint32_t* __restrict__ head,
+                                                           const int32_t* __restrict__ ord, int64_t nv,
+                                                           uint32_t* __restrict__ counts, float4* __restrict__ cent,
+                                                           int32_t* __restrict__ offcell) {
+  uint32_t* sl = a.lists + (size_t)a.par * a.lcap;
+  uint32_t* tl = a.lists + (size_t)(2 + a.par) * a.lcap;
+  uint32_t nocc = 0;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kBlock) {
+    if (!head[i]) continue;
+    const uint32_t key = keys[i];
+    const uint32_t q = (uint32_t)ord[i];
+    unsigned long long sr = 0, sg = 0, sb = 0;
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f;
+    uint32_t cnt = 0;
+    for (int64_t j = i; j < nv && keys[j] == key; ++j, ++cnt) {
+      const float4 p = a.pts[idx[j]];
+      sx += p.x;
+      sy += p.y;
+      sz += p.z;
+      const uint32_t rgb = __float_as_uint(p.w);
+      sr += (rgb >> 16) & 0xffu;
+      sg += (rgb >> 8) & 0xffu;
+      sb += rgb & 0xffu;
+    }
+    const uint32_t word = pcl_colour_word(sr, sg, sb, cnt);
+    a.grid[key] = word;
+    sl[q] = key;
+    tl[q] = key;
+    a.lcnt[q] = cnt;
+    counts[q] = cnt;
+    ++nocc;
+    const float rn = __fdiv_rn(1.0f, (float)cnt);  // Eigen 3.0: centroid / n == centroid * (1 / n)
+    const float c[3] = {__fmul_rn(sx, rn), __fmul_rn(sy, rn), __fmul_rn(sz, rn)};
+    cent[q] = make_float4(c[0], c[1], c[2], __uint_as_float(word & 0x00ffffffu));
+    const int own[3] = {mn.x + (int)(key % (uint32_t)dv.x), mn.y + (int)(key / (uint32_t)dv.x % (uint32_t)dv.y),
+                        mn.z + (int)(key / (uint32_t)dv.x / (uint32_t)dv.y)};
+    const int mnv[3] = {mn.x, mn.y, mn.z};
+    int nb[3];
+    bool moved = false;
+#pragma unroll
+    for (int ax = 0; ax < 3; ++ax) {
+      nb[ax] = (int)floorf(__fdiv_rn(c[ax], a.leaf));  // as vox_centroid_kernel
+      moved = moved || nb[ax] != own[ax];
+    }
+    if (moved) {
+      const uint32_t k = atomicAdd(a.cnt + kVcOff, 1u);
+      int32_t* oc = offcell + 8 * (int64_t)k;
+      oc[0] = (int32_t)key;
+      for (int ax = 0; ax < 3; ++ax) {
+        oc[1 + ax] = nb[ax] - mnv[ax];
+        oc[4 + ax] = nb[ax] - mnv[ax];
+      }
+      oc[7] = 0;
+    }
+  }
+  nocc = wave_reduce(nocc, [](uint32_t u, uint32_t v) { return u + v; });
+  if ((threadIdx.x & 63) == 0 && nocc) atomicAdd(a.cnt + kVcSlots + a.par, nocc);
+}
+
+// the segment counts of the positions 0 .. nocc - 1 (list segments of kVoxChunk), for the
+// readers that walk the lists by segment (the next frame's grid clear, the counts pass)
+__global__ __launch_bounds__(kBlock) void voxs_parts_kernel(VoxArgs a) {
+  const int64_t nocc = a.cnt[kVcSlots + a.par];
+  int32_t* pr = a.part + (size_t)a.par * a.nblk_cap * kPartW;
+  for (int b = blockIdx.x * kBlock + threadIdx.x; b < a.nblk; b += gridDim.x * kBlock) {
+    const int64_t r = nocc - (int64_t)b * kVoxChunk;
+    pr[(size_t)b * kPartW + kPNew] = (int32_t)(r < 0 ? 0 : (r > kVoxChunk ? kVoxChunk : r));
+  }
 }
 
 // ---- exclusive scans (leaf layout, bucket offsets) --------------------------------
@@ -1313,6 +1474,11 @@ hipError_t launch_voxelize(const VoxArgs& a, hipStream_t s) {
 }
 
 
+hipError_t launch_vox_accum(const VoxArgs& a, int nblocks, hipStream_t s) {
+  if (nblocks > 0) vox_accum_kernel<<<(unsigned)nblocks, kVB, 0, s>>>(a);
+  return hipGetLastError();
+}
+
 hipError_t launch_vox_scatter(const VoxArgs& a, hipStream_t s) {
   if (a.nblk > 0) vox_scatter_kernel<<<(unsigned)a.nblk, kBlock, 0, s>>>(a);
   return hipGetLastError();
@@ -1334,8 +1500,39 @@ hipError_t launch_vox_centroids(const VoxArgs& a, uint32_t* counts, uint32_t* of
   scan_write_kernel<false><<<(unsigned)nb, kBlock, 0, s>>>(counts, np, block_sums, reinterpret_cast<int32_t*>(offs));
   hipError_t e = hipMemsetAsync(cur, 0, (size_t)np * 4, s);
   if (e != hipSuccess) return e;
-  vox_bucket_kernel<<<grid_for(a.n, 8192), kBlock, 0, s>>>(a, offs, cur, bucket);
-  vox_centroid_kernel<<<grid_for(np), kBlock, 0, s>>>(a, offs, counts, bucket, cent, offcell);
+  vox_bucket_kernel<<<grid_for(a.n, 8192), kBlock, 0, s>>>(a, offs, counts, cur, bucket);
+  vox_centroid_kernel<<<grid_for(np), kBlock, 0, s>>>(a, offs, counts, cur, bucket, cent, offcell);
+  return hipGetLastError();
+}
+
+hipError_t launch_vox_clear(const VoxArgs& a, hipStream_t s) {
+  if (a.nblk > 0) vox_clear_kernel<<<(unsigned)a.nblk, kBlock, 0, s>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_vox_sorted(const VoxArgs& a, const int mn[3], const int dv[3], int64_t nv, VoxSortBufs& b,
+                             uint32_t* counts, float4* cent, int32_t* offcell, hipStream_t s) {
+  const int64_t nvox = (int64_t)dv[0] * dv[1] * dv[2];
+  int bits = 1;  // the keys' width: voxel indices and the sentinel nvox
+  while (bits < 32 && ((int64_t)1 << bits) <= nvox) ++bits;
+  const size_t n = (size_t)std::max<int64_t>(a.n, 1);
+  if (!b.tmp)  // size query
+    return rocprim::radix_sort_pairs(nullptr, b.tmp_bytes, b.keys, b.keys2, b.idx, b.idx2, n, 0, bits, s);
+  if (a.n <= 0 || nv <= 0) return hipSuccess;
+  const int3 m3 = make_int3(mn[0], mn[1], mn[2]), d3 = make_int3(dv[0], dv[1], dv[2]);
+  voxs_keys_kernel<<<grid_for(a.n, 8192), kBlock, 0, s>>>(a, m3, d3, (uint32_t)nvox, b.keys, b.idx);
+  hipError_t e = rocprim::radix_sort_pairs(b.tmp, b.tmp_bytes, b.keys, b.keys2, b.idx, b.idx2, (size_t)a.n, 0, bits, s);
+  if (e != hipSuccess) return e;
+  voxs_heads_kernel<<<grid_for(nv, 8192), kBlock, 0, s>>>(b.keys2, nv, b.head);
+  const int64_t nb = scan_blocks(nv);
+  scan_count_kernel<false><<<(unsigned)nb, kBlock, 0, s>>>(b.head, nv, b.block_sums);
+  scan_sums_kernel<<<1, kBlock, 0, s>>>(b.block_sums, nb);
+  scan_write_kernel<false><<<(unsigned)nb, kBlock, 0, s>>>(b.head, nv, b.block_sums, b.ord);
+  e = hipMemsetAsync(counts, 0, (size_t)a.nblk * kVoxChunk * 4, s);
+  if (e != hipSuccess) return e;
+  voxs_emit_kernel<<<grid_for(nv, 8192), kBlock, 0, s>>>(a, m3, d3, b.keys2, b.idx2, b.head, b.ord, nv, counts, cent,
+                                                          offcell);
+  voxs_parts_kernel<<<(unsigned)((a.nblk + kBlock - 1) / kBlock), kBlock, 0, s>>>(a);
   return hipGetLastError();
 }
 

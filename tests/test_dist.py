@@ -371,3 +371,32 @@ def test_gloo_candidate_merge_world_three():
     ref = replay_scores(scores, sbg, (1, 2, 3), np.zeros((3, 4), DET_DTYPE))
     for rank, raw, _ in res:
         assert np.array_equal(np.frombuffer(raw, DET_DTYPE).reshape(3, 4), ref)
+
+
+def test_slab_scores_restores_rank_on_error():
+    """slab_scores sets the context's rank to 1 for its search and gives the
+    caller's rank back when the search raises, too."""
+    from c3hlac import dist as cd
+
+    class Ctx:
+        rank, M = 4, 1
+        ranks = []
+
+        def set_grid(self, *a):
+            pass
+
+        def extract(self, *a):
+            return (6, 6, 6), 216
+
+        def set_rank(self, r):
+            self.rank = r
+            self.ranks.append(r)
+
+        def search(self, *a, **k):
+            raise RuntimeError("search failed")
+
+    c = Ctx()
+    words = np.zeros((64, 64, 64), np.uint32)
+    with pytest.raises(RuntimeError):
+        cd.slab_scores(c, words, 117, THR, 10, (2, 2, 2), 100, 0, 2)
+    assert c.rank == 4 and c.ranks == [1, 4]
