@@ -441,6 +441,7 @@ def main():
                                               scene_points(synth, rank, (f0 % nf) // 4), grids[(f0 % nf) // 4 * 4])
         if "points_in" in result:
             result["points_in"]["cpu_baseline"] = cpu_baseline_points(synth, args.cpu_seconds)
+            result["points_in"]["cpu_baseline_parallel"] = cpu_baseline_points_parallel(args.cpu_seconds)
     if rank == 0:
         from c3hlac import _capi
         result["build"] = _capi.build_provenance()
@@ -520,6 +521,27 @@ def points_pass(ctx, dev, rank, world, dist, torch, synth, c3hlac, n_total, n_ho
         "voxelize_batched_gpoints_per_s": (N_RAYS * kt["voxelize"][1] / (kt["voxelize"][0] / 1e3) / 1e9)
         if kt["voxelize"][0] else None,
     }
+    if world == 1:
+        # the shard one rank gets at N = 2, 4, 8 (frames 0, N, 2N, ... of this run), timed the
+        # same way on this GPU: the 1 -> 8 strong-scaling shape without an 8-GPU node
+        # (VERDICT r5 item 2); records must equal the full run's for the same frames
+        shard = {}
+        want = out[:len(mine)].cpu()
+        for n_w in (2, 4, 8):
+            sel = list(range(0, len(frames), n_w))
+            s_out = torch.zeros((len(sel), 3 * P_M), dtype=torch.int64, device=dev)
+            best = None
+            for _ in range(3):
+                el_s, _ = timed([frames[i] for i in sel], s_out, False)
+                best = el_s if best is None else min(best, el_s)
+            shard[str(len(sel))] = {"frames_per_s": len(sel) / best, "ms_per_call": best * 1e3,
+                                    "records_equal_full_run": bool(torch.equal(s_out.cpu(), want[sel]))}
+        res["shard_frames_per_s"] = {k: v["frames_per_s"] for k, v in shard.items()}
+        res["shard_over_full"] = {k: v["frames_per_s"] / res["frames_per_s_from_points"] for k, v in shard.items()}
+        res["shard"] = shard
+        res["shard_note"] = ("rank 0's shard of %d frames at N = 2, 4, 8 (every N-th frame), one c3h_run_point_frames "
+                             "call each on this GPU, best of 3; shard_over_full: per-frame rate against the %d-frame "
+                             "run" % (len(frames), len(frames)))
     if n_host > 0:  # H2D included: the frames start in pinned host memory
         hf = [f.cpu().pin_memory() for f in frames[:n_host]]
         hout = torch.zeros((len(hf), 3 * P_M), dtype=torch.int64, device=dev)
@@ -804,5 +826,49 @@ def cpu_baseline_points(synth, seconds):
     }
 
 
+def _cpu_points_worker(seconds, k):
+    """One core of cpu_baseline_points_parallel (a child process: numpy + the C oracle only)."""
+    from c3hlac import synth
+    import pyoracle as po
+    axis_t, var, axis_q = synth.random_bases(P_VARIANT, D, P_M, R, seed=synth.BASE_SEED + 31)
+    ap = synth.whiten(axis_t, var)
+    n, busy = 0, 0.0
+    t_start = time.perf_counter()
+    while n == 0 or time.perf_counter() - t_start < seconds:
+        pts = synth.kinect_scene(N_RAYS, grid=P_GRID, leaf=P_LEAF, seed=synth.BASE_SEED + 7000 + (k + n) % 16)
+        t0 = time.perf_counter()
+        g, layout, cloud = po.voxelize(pts, P_LEAF)
+        f, sb, _ = po.c3hlac(g, layout, cloud, P_VARIANT, THR, P_LEAF, SUBDIV)
+        po.search(sb, f, po.exist(f), ap, axis_q, BOX, RANK, EXIST_THR)
+        busy += time.perf_counter() - t0
+        n += 1
+    return {"frames": n, "busy_s": busy}
+
+
+def cpu_baseline_points_parallel(seconds, procs=None):
+    """configs[3]'s frame-parallel CPU upper bound: the
+    single-core loop of cpu_baseline_points in `procs` independent processes at once (frames
+    are independent: OpenMP over frames would do the same), each for `seconds`; frames/s is
+    the sum of the processes' rates.  Children are started as new interpreters (never a fork
+    of this GPU process's state) and touch no GPU."""
+    import subprocess
+    if procs is None:
+        procs = max(1, min(16, len(os.sched_getaffinity(0))))
+    env = dict(os.environ)
+    env["OMP_NUM_THREADS"] = "1"
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--cpu-points-worker", str(seconds)]
+    ps = [subprocess.Popen(cmd + [str(k)], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, env=env)
+          for k in range(procs)]
+    outs = [json.loads(p.communicate()[0].decode().strip().splitlines()[-1]) for p in ps]
+    rate = sum(o["frames"] / o["busy_s"] for o in outs)
+    return {"value": rate, "unit": "frames/s", "cores": procs, "kind": "port",
+            "sample": "%d processes x >= %.0f s of the single-core loop (voxelize + C3-HLAC-981 + search per 1M-point "
+                      "frame), %d frames in total; frames/s summed over the processes" %
+                      (procs, seconds, sum(o["frames"] for o in outs))}
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "--cpu-points-worker":
+        print(json.dumps(_cpu_points_worker(float(sys.argv[2]), int(sys.argv[3]))))
+        sys.exit(0)
     main()

@@ -633,6 +633,9 @@ __global__ __launch_bounds__(kBlock) void point_fixup_kernel(PointFixup a) {
 constexpr size_t kFixLdsMax = 160 * 1024;
 bool point_fixup_fits(const int lmax[3]) { return 4 * fix_lds_words(lmax) <= kFixLdsMax; }
 
+#ifndef C3H_FIX_BLOCKS
+#define C3H_FIX_BLOCKS 8
+#endif
 hipError_t launch_point_fixup(const PointFixup& a, hipStream_t s) {
   if (a.nf <= 0) return hipSuccess;
   // jobs per frame: 2 per moved voxel; frames without moved voxels exit at once
@@ -641,7 +644,11 @@ hipError_t launch_point_fixup(const PointFixup& a, hipStream_t s) {
   if (lds > 65536)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&point_fixup_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  point_fixup_kernel<<<dim3(32, (unsigned)a.nf), kBlock, lds, s>>>(a);
+  // 8 workgroups per frame (round 6; 32 until round 5): a frame's jobs (2 per moved voxel,
+  // ~2.4 per view on the reference's own Kinect views) loop over them, and the launch of a
+  // batch without moved voxels is 512 empty workgroups, not 2,048 that queue behind the
+  // voxeliser's 48 KB-LDS blocks for their own LDS (65-80 us on the tick's stream)
+  point_fixup_kernel<<<dim3(C3H_FIX_BLOCKS, (unsigned)a.nf), kBlock, lds, s>>>(a);
   return hipGetLastError();
 }
 

@@ -36,6 +36,7 @@ struct TickArgs {
   SparseSearch gq;                   // compress + gate role
   CompressRows cr;
   int g_ngate, g_ncomp;
+  int comp_mfma;                     // compress role on the matrix cores (compress_f32t_body)
   KArgs ka;                          // tile role
   int t_grid;
   OccArgs oa;                        // occupancy role
@@ -119,6 +120,7 @@ __device__ __forceinline__ void tick_roles(const TickArgs& t, uint32_t* tick_sme
     C3H_SETPRIO(C3H_TICK_PRIO_CG);
     role_frame(b, t.g_ngate + t.g_ncomp, t.xcd & 4, f, r);
     if (r < t.g_ngate) gate_body(t.gq, r, f);
+    else if (t.comp_mfma) compress_f32t_body(t.cr, r - t.g_ngate, t.g_ncomp, f, reinterpret_cast<float*>(tick_smem));
     else compress_rows_body(t.cr, r - t.g_ngate, t.g_ncomp, f, reinterpret_cast<float*>(tick_smem));
     return;
   }
@@ -252,8 +254,18 @@ hipError_t launch_tick(const TickParts& p, hipStream_t s) {
     t.cr = CompressRows{sc.feat, sc.PT, sc.fmax, sc.G, sc.rows, sc.nrows, sc.F, sc.D, sc.Dpad,
                         sc.fmax_len, sc.s_feat, sc.s_G, sc.s_rows, sc.s_nrows};
     t.g_ngate = (int)((a.pstart[a.nmodes] + kBlock - 1) / kBlock);
-    t.g_ncomp = (int)std::max<int64_t>(1, std::min<int64_t>((sc.H + kRR - 1) / kRR, env_int("C3H_TICK_COMP", 32)));
-    lds = std::max(lds, compress_rows_lds_bytes(sc.Dpad));
+    // the compress role on the matrix cores (round 6): 64-row blocks, D <= 128
+#ifndef C3H_TICK_COMP_MFMA
+#define C3H_TICK_COMP_MFMA 1
+#endif
+    t.comp_mfma = env_int("C3H_TICK_COMP_MFMA", C3H_TICK_COMP_MFMA) && sc.Dpad <= 128 ? 1 : 0;
+    if (t.comp_mfma) {
+      t.g_ncomp = (int)std::max<int64_t>(1, std::min<int64_t>((sc.H + kCR - 1) / kCR, env_int("C3H_TICK_COMP", 16)));
+      lds = std::max(lds, kTLds);
+    } else {
+      t.g_ncomp = (int)std::max<int64_t>(1, std::min<int64_t>((sc.H + kRR - 1) / kRR, env_int("C3H_TICK_COMP", 32)));
+      lds = std::max(lds, compress_rows_lds_bytes(sc.Dpad));
+    }
     t.n_cg = (t.g_ngate + t.g_ncomp) * a.nframes;
   }
   if (p.tile) {

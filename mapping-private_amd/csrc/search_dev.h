@@ -246,6 +246,101 @@ __device__ __forceinline__ void compress_f32c_body(const CompressRows& cr, int b
   }
 }
 
+// The tick's compress role on the matrix cores (round 6): compress_f32c_body's GEMM with k
+// in chunks of 32 (24.8 KB of LDS instead of 49: inside the tick's per-workgroup budget, so
+// the tick keeps its workgroups per CU), rows from the frame's non-empty row list.  The VALU
+// body (compress_rows_body) reads 3 LDS words per 8 FMAs and is LDS-bound; here a wave reads
+// 768 B per 4,096 FMAs.  k pairs run in ascending order on v_mfma_f32_32x32x2_f32: G is
+// bit-identical to the VALU body's (the same k-ordered fmaf chain per output).
+constexpr int kTK = 32;
+constexpr int kTAS = kTK + 1;
+constexpr size_t kTLds = sizeof(float) * ((size_t)kCR * kTAS + (size_t)kTK * 128);
+
+__device__ __forceinline__ void compress_f32t_body(const CompressRows& cr, int bid, int nblk, int64_t f,
+                                                   float* smem) {
+  const float* __restrict__ feat = cr.feat + f * cr.s_feat;
+  const float* __restrict__ fmax = cr.fmax;
+  float* __restrict__ G = cr.G + f * cr.s_G;
+  const int32_t* __restrict__ rows = cr.rows + f * cr.s_rows;
+  const int F = cr.F, D = cr.D, Dpad = cr.Dpad, fmax_len = cr.fmax_len;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rw = wave & 1, cw = wave >> 1;
+  const int half = lane >> 5, kl = lane & 31;
+  const int n = (int)cr.nrows[f * cr.s_nrows];
+  const int nch = (F + kTK - 1) / kTK;
+  float* As = smem;               // [kCR rows][kTAS]
+  float* Bs = smem + kCR * kTAS;  // [kTK][128]
+  for (int r0 = bid * kCR; r0 < n; r0 += nblk * kCR) {
+    const int myrow = r0 + wave * 16 + (lane & 15);
+    const int hrow = myrow < n ? rows[myrow] : -1;  // lane j < 16: this wave's load row j
+    float areg[8];
+    float4 breg[4];
+    auto fetch = [&](int c) {
+      const int k = c * kTK + kl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {  // rows 2 j (lanes 0-31) and 2 j + 1 (lanes 32-63)
+        const int h = __shfl(hrow, 2 * j + half, 64);
+        areg[j] = (h >= 0 && k < F) ? __builtin_nontemporal_load(feat + (int64_t)h * F + k) : 0.0f;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int pc = tid + kBlock * i, kk = c * kTK + (pc >> 5), col = 4 * (pc & 31);
+        breg[i] = (kk < F && col < Dpad) ? *reinterpret_cast<const float4*>(cr.PT + (int64_t)kk * Dpad + col)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    };
+    auto stage = [&](int c) {
+      const int k = c * kTK + kl;
+      float mx = 1.0f;
+      const bool norm = k < fmax_len;  // setData max-normalisation (search.cpp:563-570)
+      if (norm) mx = fmax[k];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = areg[j];
+        if (norm) v = mx == 0.0f ? 0.0f : (v == mx ? 1.0f : __fdiv_rn(v, mx));
+        As[(wave * 16 + 2 * j + half) * kTAS + kl] = v;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int pc = tid + kBlock * i;
+        *reinterpret_cast<float4*>(Bs + (pc >> 5) * 128 + 4 * (pc & 31)) = breg[i];
+      }
+    };
+    mf_f32x16 acc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[t][q] = 0.0f;
+    fetch(0);
+    const float* arow = As + (rw * 32 + kl) * kTAS + half;
+    const float* bcol = Bs + half * 128 + 64 * cw + kl;
+    for (int c = 0; c < nch; ++c) {
+      __syncthreads();  // every wave is done reading chunk c - 1
+      stage(c);
+      __syncthreads();
+      if (c + 1 < nch) fetch(c + 1);  // in flight while the matrix cores run
+#pragma unroll
+      for (int k = 0; k < kTK; k += 2) {
+        const float av = arow[k];
+        const float b0 = bcol[k * 128], b1 = bcol[k * 128 + 32];
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b0, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b1, acc[1], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int rr = r0 + rw * 32 + (q & 3) + 8 * (q >> 2) + 4 * half;
+      if (rr >= n) continue;
+      const int64_t hh = rows[rr];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int col = 64 * cw + 32 * t + kl;
+        if (col < D) G[hh * D + col] = acc[t][q];
+      }
+    }
+    __syncthreads();  // As / Bs are restaged by the next row block
+  }
+}
+
 // fp16 variant of the matrix-core compress (c3h_set_search_precision): the normalised
 // features are rounded to f16, the whitened axis is kept as f16 (PT16: 128 columns x
 // Fp16 = F rounded up to 16, column-major), products accumulate in f32 on

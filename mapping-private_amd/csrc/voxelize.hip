@@ -1278,55 +1278,68 @@ constexpr int kVbFlagSlots = 2 * kVbFlagCap;
 constexpr int kBucketSplit = 4;  // blocks per accumulate chunk (each re-reads a quarter of its points)
 static_assert(kBPer % kBucketSplit == 0, "bucket split");
 static_assert((kVbFlagSlots & (kVbFlagSlots - 1)) == 0, "flag hash");
-__global__ __launch_bounds__(kBT) void voxb_bucket_kernel(VoxBatchArgs a) {
+// A bounded grid (kBucketGrid blocks: one dispatch round) walks the (chunk, quarter) items:
+// frames without flagged voxels -- all of the synthetic points-in frames -- cost a counter
+// read per item instead of a dispatched 48 KB-LDS block each (round 6: 15.6k empty blocks
+// per 64-frame batch took ~20 us of the voxeliser's critical path)
+constexpr int kBucketGrid = 768;
+__global__ __launch_bounds__(kBT) void voxb_bucket_kernel(VoxBatchArgs a, int nitems) {
   __shared__ uint32_t s_key[kVbFlagSlots];
   __shared__ uint16_t s_rec[kVbFlagSlots];
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const int f = vb_frame(a.blk0, a.nf, b);
-  const uint32_t nflag = a.xcnt[4 * f];
-  if (nflag == 0 || a.info[f].err) return;  // uniform
-  const int nrec = (int)min(nflag, (uint32_t)kVbFlagCap);
-  VoxFlag* fl = a.flags + (size_t)f * kVbFlagCap;
-  uint32_t* bk = a.bucket + (size_t)f * kVbBucketCap;
-  for (int s = tid; s < kVbFlagSlots; s += kBT) s_key[s] = kNoT;
-  __syncthreads();
-  for (int r = tid; r < nrec; r += kBT) {
-    const uint32_t t = fl[r].t;
-    uint32_t h = (t * 0x9E3779B1u) >> (32 - __builtin_ctz(kVbFlagSlots));
-    while (atomicCAS(&s_key[h], kNoT, t) != kNoT) h = (h + 1) & (kVbFlagSlots - 1);
-    s_rec[h] = (uint16_t)r;
-  }
-  __syncthreads();
-  const int64_t base = (int64_t)(b - a.blk0[f]) * kBChunk;
-  const float4* __restrict__ pts = a.pts[f];
-  const int64_t n = a.n[f];
-  const uint32_t mx_ = (1u << a.tb[0]) - 1, my_ = (1u << a.tb[1]) - 1, mz_ = (1u << a.tb[2]) - 1;
-  const int sy = a.tb[0], sz = a.tb[0] + a.tb[1];
-  // this block's share of the chunk: kBPer / kBucketSplit points per thread, loaded together
-  constexpr int kPer = kBPer / kBucketSplit;
-  float4 p[kPer];
-#pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    const int64_t i = base + (int64_t)(blockIdx.y * kPer + q) * kBT + tid;
-    p[q] = i < n ? pts[i] : make_float4(NAN, NAN, NAN, 0.0f);
-  }
-#pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    const int64_t i = base + (int64_t)(blockIdx.y * kPer + q) * kBT + tid;
-    int c[3];
-    float margin;
-    if (!point_valid(p[q], a.z_limit) || !point_cell(a.inv, p[q], c, &margin)) continue;
-    const uint32_t t = ((uint32_t)c[0] & mx_) | (((uint32_t)c[1] & my_) << sy) | (((uint32_t)c[2] & mz_) << sz);
-    uint32_t h = (t * 0x9E3779B1u) >> (32 - __builtin_ctz(kVbFlagSlots));
-    for (;;) {
-      const uint32_t k = s_key[h];
-      if (k == kNoT) break;
-      if (k == t) {
-        VoxFlag& r = fl[s_rec[h]];
-        bk[r.off + atomicAdd(&r.cur, 1u)] = (uint32_t)i;
-        break;
+  const int tid = threadIdx.x;
+  int f_tab = -1;  // the frame whose flagged keys s_key holds
+  for (int w = blockIdx.x; w < nitems; w += gridDim.x) {  // uniform per block
+    const int b = w / kBucketSplit, qy = w - b * kBucketSplit;
+    const int f = vb_frame(a.blk0, a.nf, b);
+    const uint32_t nflag = a.xcnt[4 * f];
+    if (nflag == 0 || a.info[f].err) continue;  // uniform
+    const int nrec = (int)min(nflag, (uint32_t)kVbFlagCap);
+    VoxFlag* fl = a.flags + (size_t)f * kVbFlagCap;
+    uint32_t* bk = a.bucket + (size_t)f * kVbBucketCap;
+    if (f != f_tab) {
+      __syncthreads();  // the previous frame's lookups are done
+      for (int s = tid; s < kVbFlagSlots; s += kBT) s_key[s] = kNoT;
+      __syncthreads();
+      for (int r = tid; r < nrec; r += kBT) {
+        const uint32_t t = fl[r].t;
+        uint32_t h = (t * 0x9E3779B1u) >> (32 - __builtin_ctz(kVbFlagSlots));
+        while (atomicCAS(&s_key[h], kNoT, t) != kNoT) h = (h + 1) & (kVbFlagSlots - 1);
+        s_rec[h] = (uint16_t)r;
       }
-      h = (h + 1) & (kVbFlagSlots - 1);
+      __syncthreads();
+      f_tab = f;
+    }
+    const int64_t base = (int64_t)(b - a.blk0[f]) * kBChunk;
+    const float4* __restrict__ pts = a.pts[f];
+    const int64_t n = a.n[f];
+    const uint32_t mx_ = (1u << a.tb[0]) - 1, my_ = (1u << a.tb[1]) - 1, mz_ = (1u << a.tb[2]) - 1;
+    const int sy = a.tb[0], sz = a.tb[0] + a.tb[1];
+    // this item's share of the chunk: kBPer / kBucketSplit points per thread, loaded together
+    constexpr int kPer = kBPer / kBucketSplit;
+    float4 p[kPer];
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const int64_t i = base + (int64_t)(qy * kPer + q) * kBT + tid;
+      p[q] = i < n ? pts[i] : make_float4(NAN, NAN, NAN, 0.0f);
+    }
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const int64_t i = base + (int64_t)(qy * kPer + q) * kBT + tid;
+      int c[3];
+      float margin;
+      if (!point_valid(p[q], a.z_limit) || !point_cell(a.inv, p[q], c, &margin)) continue;
+      const uint32_t t = ((uint32_t)c[0] & mx_) | (((uint32_t)c[1] & my_) << sy) | (((uint32_t)c[2] & mz_) << sz);
+      uint32_t h = (t * 0x9E3779B1u) >> (32 - __builtin_ctz(kVbFlagSlots));
+      for (;;) {
+        const uint32_t k = s_key[h];
+        if (k == kNoT) break;
+        if (k == t) {
+          VoxFlag& r = fl[s_rec[h]];
+          bk[r.off + atomicAdd(&r.cur, 1u)] = (uint32_t)i;
+          break;
+        }
+        h = (h + 1) & (kVbFlagSlots - 1);
+      }
     }
   }
 }
@@ -1456,7 +1469,8 @@ hipError_t launch_vox_batch(const VoxBatchArgs& a, hipStream_t s) {
     voxb_reduce_kernel<<<(unsigned)a.nf, kBlock, 0, s>>>(a);
     voxb_scatter_kernel<<<(unsigned)a.total, kBlock, a.stamp ? 4 * (size_t)((a.ntiles + 31) / 32) : 0, s>>>(a);
     if (a.flags) {
-      voxb_bucket_kernel<<<dim3((unsigned)a.total, kBucketSplit), kBT, 0, s>>>(a);
+      const int items = a.total * kBucketSplit;
+      voxb_bucket_kernel<<<(unsigned)std::min(items, kBucketGrid), kBT, 0, s>>>(a, items);
       voxb_exact_kernel<<<dim3((unsigned)a.nf, kExactSplit), kBlock, 0, s>>>(a);
     }
   }
