@@ -322,7 +322,6 @@ struct C3Launch {
   const uint32_t* vl_words = nullptr;
   const int32_t* vl_counts = nullptr;
   int vl_nseg = 0, vl_seg = 0, vl_count_stride = 0;
-  int64_t max_work = 0;  // > 0: at most this many tiles can be listed (single frame)
 };
 
 int64_t c3hlac_grid(const C3Launch& a);  // persistent grid of the tile kernel

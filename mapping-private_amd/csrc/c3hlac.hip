@@ -834,12 +834,7 @@ hipError_t launch_feat16_to_f32(const _Float16* f16, int f16s, const uint32_t* f
 }
 
 // dense-tile MFMA kernel: tiles up to 16 x 16 per layer, resident persistent grid
-static bool mfma_ok(const C3Launch& l) {
-  // a frame takes the MFMA body when at least half its tiles are listed: with a bound on
-  // the listed tiles below that (the voxeliser's occupied-voxel count), no launch
-  if (l.max_work > 0 && 2 * l.max_work < l.ntiles) return false;
-  return l.lmax[0] <= 16 && l.lmax[1] <= 16 && l.debug == 0;
-}
+static bool mfma_ok(const C3Launch& l) { return l.lmax[0] <= 16 && l.lmax[1] <= 16 && l.debug == 0; }
 
 static int64_t mfma_grid(const C3Launch& l, size_t lds) {
   static thread_local size_t c_lds = 0;

@@ -529,6 +529,9 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
   const int32_t* __restrict__ fwork = a.work + fy * a.s_work;
   int32_t* frows = a.rows ? a.rows + fy * a.s_h : nullptr;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // a sparse frame (the dot4 tile body takes it): out before any table is built, so the
+  // launch on a sparse single frame costs its dispatch only
+  if (2 * (int)ftf[2 + (a.epoch & 1)] < a.ntiles) return;
   const int PBM = a.mf_pb;
   // channel-byte tables: T_col[v] = {sin, cos, beta, 1 - beta} ^ 0x80 (setColor LUT, thresholds)
   for (int i = threadIdx.x; i < 768; i += kBlock) {

@@ -825,7 +825,7 @@ const char* c3h_last_error(const c3h_ctx* ctx) { return ctx ? ctx->err.c_str() :
 
 // c3h_voxelize of host frames: chunked copy + accumulate overlap (0: one copy, then the pass)
 #ifndef C3H_VOX_CHUNKED_COPY
-#define C3H_VOX_CHUNKED_COPY 1
+#define C3H_VOX_CHUNKED_COPY 0  // measured round 6: the pageable chunk copies leave ~25 us gaps (0.45 -> 0.53 ms)
 #endif
 constexpr bool kVoxChunkedCopy = C3H_VOX_CHUNKED_COPY;
 #ifndef C3H_VOX_COPY_CHUNK_BLOCKS
@@ -1528,7 +1528,6 @@ int extract_frames(c3h_ctx* ctx, const uint32_t* const* grids, int nf, const c3h
       l.vl_count_stride = c3h::vox_part_words();
       l.vl_seg = (int)c3h::vox_positions(1);
       l.vl_nseg = va.nblk;
-      l.max_work = std::max<int64_t>(ctx->vns, 1);  // a tile per occupied voxel at most
     }
     if (!from_list && !ctx->capture && nf == 1 && ntiles >= 65536 && l.zero_empty && !atomic && kDenseProbe) {
       ENSURE(ctx->dense_flag, 1);
@@ -2821,14 +2820,21 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
         HIPCHK(c3h::launch_vox_batch(va, vs));
       }
       HIPCHK(hipEventRecord(ctx->pb_vox_ev, vs));
-      HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->pb_vox_ev, 0));
       c->pb_prev_nf = nb;
       c->pb_prev_total = va.total;
       c->pb_prev_blk0.assign(va.blk0, va.blk0 + nb + 1);
       fresh.stamped = va.stamp != 0;
+      // A stamped batch has no role in its own first tick (that tick runs the tile role of
+      // the batch before it, compress + gate and scoring of older ones), so the tick goes
+      // ahead of this batch's voxeliser and only the next tick waits for it (round 6: the
+      // batch's tile role then runs beside the next voxeliser instead of after it, one
+      // tick less per call after the last voxeliser).  An unstamped batch's first tick
+      // streams its canvases: it waits.
+      if (!fresh.stamped) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->pb_vox_ev, 0));
       rc = pipe_commit(ctx, fresh, k, rc);
       if (rc > 0) nm = rc;
       if (rc >= 0) HIPCHK(hipEventRecord(ctx->pb_tick_ev[ch & 3], ctx->stream));
+      if (fresh.stamped) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->pb_vox_ev, 0));
     }
     while (rc >= 0 && !ctx->pipe.empty()) {
       const int trc = pipe_tick(ctx, nullptr);
