@@ -829,8 +829,11 @@ __device__ __forceinline__ void c3hlac_tile_body(const KArgs& a, int bx, int fy_
     uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
     for (int c0 = 0; c0 < nlist; c0 += kChunk) {
       // 3. build packed operands for list entries [c0, c0+kChunk): job = (group, k);
-      //    branch-free so each job's LDS reads (list, tile, LUT) issue back to back
-      for (int job = tid; job < kGroups * 15; job += kBlock) {
+      //    branch-free so each job's LDS reads (list, tile, LUT) issue back to back.  Only
+      //    the chunk's groups: a surface tile holds a few dozen centres, and the dot4 pass
+      //    reads groups g < ng only (round 6: the 32 groups were all built before)
+      const int njobs = ((min(nlist - c0, kChunk) + 3) >> 2) * 15;
+      for (int job = tid; job < njobs; job += kBlock) {
         const int jg = job / 15, jk = job - jg * 15;
         // relative_coordinates (c3_hlac.cpp:180-201), arithmetically: k <= 8 -> (k/3-1, k%3-1, -1),
         // k = 9..11 -> (k-10, -1, 0), k = 12 -> (-1, 0, 0); 13, 14 = centre / ones columns

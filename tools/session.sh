@@ -20,6 +20,8 @@
 #                    (tools/single_frame_trace.py)          -> single/
 #   config5          BASELINE configs[4] stage times (tools/config5.py --fp16) -> config5.log
 #   real_views       the reference's 126 committed Kinect views (tools/real_views_bench.py) -> real_views.json
+#   tileprof         the dot4 tile body's phases on a points-in frame (tools/tile_prof.py; with
+#                    VARIANT=<a diagnostics build> the C3H_PROF phase lines) -> tile_prof.*
 # Variants: VARIANT=name selects lib/variants/name.so for the python steps (C3HLAC_LIB).
 set -o pipefail
 TAG=$1
@@ -58,6 +60,7 @@ for step in "$@"; do
             python3 $R/tools/single_frame_trace.py 40 > $O/single_block.json 2> $O/single.err || exit 20 ;;
     config5) timeout -k 10 300 python -u tools/config5.py --fp16 > $O/config5.log 2>&1 || exit 21 ;;
     real_views) timeout -k 10 300 python -u tools/real_views_bench.py tests/golden/kinect_views_126.npz > $O/real_views.json 2> $O/real_views.err || exit 22 ;;
+    tileprof) C3H_PROF=$O/tile_prof_phases.txt timeout -k 10 200 python -u tools/tile_prof.py 20 981 10 > $O/tile_prof.json 2> $O/tile_prof.err || exit 23 ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
   esac
 done
