@@ -2549,6 +2549,9 @@ extern "C" {
 #define C3H_POINT_STAMP 1
 #endif
 constexpr bool kPointStamp = C3H_POINT_STAMP;
+#ifndef C3H_POINT_VOX_PRIO
+#define C3H_POINT_VOX_PRIO 1
+#endif
 // points-in batches: flagged voxels summed exactly and off-cell voxels fixed up in the batch
 // (0: frames with flagged voxels take the single-frame path, as in round 3)
 #ifndef C3H_POINT_EXACT
@@ -2643,7 +2646,16 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
       ENSURE(ctx->pb_vlist, (size_t)max_blk * chunk);
       if (!on_device) ENSURE(ctx->pb_stage, (size_t)max_pts * 4);
     }
-    if (!ctx->pb_vstream) HIPCHK(hipStreamCreateWithFlags(&ctx->pb_vstream, hipStreamNonBlocking));
+    if (!ctx->pb_vstream) {
+      // the voxeliser's stream is the points-in call's critical path (its accumulate runs
+      // beside the tick of the batches before, which has slack): high priority, so its
+      // workgroups are dispatched first as CUs free up (C3H_POINT_VOX_PRIO 0: default)
+      int lo = 0, hi = 0;
+      if (C3H_POINT_VOX_PRIO && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo)
+        HIPCHK(hipStreamCreateWithPriority(&ctx->pb_vstream, hipStreamNonBlocking, hi));
+      else
+        HIPCHK(hipStreamCreateWithFlags(&ctx->pb_vstream, hipStreamNonBlocking));
+    }
     if (!ctx->pb_vox_ev) HIPCHK(hipEventCreateWithFlags(&ctx->pb_vox_ev, hipEventDisableTiming));
     for (hipEvent_t& e : ctx->pb_tick_ev)
       if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));

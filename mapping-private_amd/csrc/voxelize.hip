@@ -1287,6 +1287,16 @@ __global__ __launch_bounds__(kBT) void voxb_bucket_kernel(VoxBatchArgs a, int ni
   __shared__ uint32_t s_key[kVbFlagSlots];
   __shared__ uint16_t s_rec[kVbFlagSlots];
   const int tid = threadIdx.x;
+  // a batch without a flagged voxel in any frame (all synthetic points-in batches): one
+  // load per frame, every block out at once
+  __shared__ int s_any;
+  if (tid < 64) {
+    const bool fl = tid < a.nf && a.xcnt[4 * tid] != 0u;
+    const unsigned long long m = __ballot(fl);
+    if (tid == 0) s_any = m != 0ull;
+  }
+  __syncthreads();
+  if (!s_any) return;
   int f_tab = -1;  // the frame whose flagged keys s_key holds
   for (int w = blockIdx.x; w < nitems; w += gridDim.x) {  // uniform per block
     const int b = w / kBucketSplit, qy = w - b * kBucketSplit;

@@ -48,6 +48,7 @@ def main():
         canvas = (G,) * 3  # frames' extents are G; their min_b differ (x shifts)
         ctx.run_point_frames(frames[:4 * B], leaf, canvas, variant, thr, 10, (2, 2, 2), 100, True, out)
         torch.cuda.synchronize()
+        frames = ctx.prepare_point_frames(frames)  # checked once, outside the timed calls (as bench.py)
         res = {}
         for rep in range(6):  # reps 3-5 without the HIP events around the launches
             timed_events = rep < 3

@@ -62,7 +62,7 @@ def main():
         want = ref.cpu()
         for world in (1, 2, 4, 8):
             mine = list(range(0, n_total, world))
-            fr = [frames[i] for i in mine]
+            fr = ctx.prepare_point_frames([frames[i] for i in mine])
             out = torch.zeros((len(fr), 3 * bench.P_M), dtype=torch.int64, device=dev)
             rates = []
             for rep in range(reps):
