@@ -2068,8 +2068,19 @@ int c3h_clean_max(c3h_ctx* ctx) {
   if (!ctx) return C3H_ERR_ARG;
   QUIESCE(ctx);
   if (ctx->lists.M != std::max(ctx->M, 1) || ctx->lists.rank != ctx->rank) init_lists(ctx);
-  if (!ctx->lists_host_valid && ctx->lists_dev_valid) {  // device copy is authoritative:
-    ctx->pending_clean = true;  // applied by the next replay kernel (or the next download)
+  if (ctx->lists_dev_valid) {
+    // the device copy is current: the next replay kernel applies the clean (or the next
+    // download), so the next search uploads nothing -- the per-callback loop's cleanData
+    // then costs no H2D copy on the frame's critical path (round 6).  A host copy that is
+    // current takes the clean too.
+    ctx->pending_clean = true;
+    if (ctx->lists_host_valid) {
+      auto& L = ctx->lists;
+      std::fill(L.score.begin(), L.score.end(), 0.0);
+      std::fill(L.x.begin(), L.x.end(), 0);
+      std::fill(L.y.begin(), L.y.end(), 0);
+      std::fill(L.z.begin(), L.z.end(), 0);
+    }
     return C3H_OK;
   }
   auto& L = ctx->lists;
