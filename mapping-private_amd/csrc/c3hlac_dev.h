@@ -643,6 +643,19 @@ struct KArgs {
 
 constexpr int kMaxLoads = 4;  // uint4 tile loads per thread kept in flight together
 constexpr int kSegLds = 64;   // segment tables up to 64 segments per axis live in LDS
+#ifndef C3H_TILE_PREFETCH
+#define C3H_TILE_PREFETCH 1  // the next tile's halo into LDS by global_load_lds during this tile's dot4 + epilogue
+#endif
+// 16 zero bytes: the LDS-DMA source of halo words outside the grid (a lane's LDS-DMA
+// destination is fixed by its lane index, so it cannot be skipped, only pointed at zeros)
+static __device__ const uint4 kHaloZero16 = {0u, 0u, 0u, 0u};
+
+// The (vec-path) halo geometry of a tile: its rows of q4 16-byte pieces starting at x = xs
+struct HaloGeo {
+  int y0, z0, ly, TY, q4, n, xs;
+  bool vec;
+};
+__device__ __forceinline__ HaloGeo halo_geo(const KArgs& a, const int32_t* segs, int tile);
 
 // Persistent workgroups.  Phase Z zero-fills the feature rows of the tiles pass 1 left
 // unflagged (direct mode); phase T walks the work list: stage the (lx+2)x(ly+2)x(lz+1)
@@ -650,6 +663,26 @@ constexpr int kSegLds = 64;   // segment tables up to 64 segments per axis live 
 // centres, build the packed dot4 operands and accumulate exactly (see the header).
 #define C3H_PROF(k, cond) \
   if (fprof && tid == 0 && (cond)) fprof[bx * 8 + (k)] = (long long)wall_clock64()
+
+__device__ __forceinline__ HaloGeo halo_geo(const KArgs& a, const int32_t* segs, int tile) {
+  const int ix = tile % a.ns0, iy = (tile / a.ns0) % a.ns1, iz = tile / (a.ns0 * a.ns1);
+  const int32_t* sx = segs + 3 * ix;
+  const int32_t* sy = segs + 3 * (a.seg_stride + iy);
+  const int32_t* sz = segs + 3 * (2 * a.seg_stride + iz);
+  HaloGeo g;
+  const int x0 = sx[0], lx = sx[1];
+  g.y0 = sy[0];
+  g.ly = sy[1];
+  g.z0 = sz[0];
+  const int lz = sz[1];
+  g.vec = (a.gx & 3) == 0 && x0 >= 1 && ((x0 + lx + 1 + 3) & ~3) <= a.gx;
+  g.xs = g.vec ? ((x0 - 1) & ~3) : x0 - 1;
+  const int TX = g.vec ? (((x0 + lx + 1 - g.xs) + 3) & ~3) : lx + 2;
+  g.TY = g.ly + 2;
+  g.q4 = TX >> 2;
+  g.n = g.TY * (lz + 1) * g.q4;
+  return g;
+}
 
 // block bx of gdx for frame fy; smem: c3hlac_lds_bytes(tw_max, list_max) bytes
 __device__ __forceinline__ void c3hlac_tile_body(const KArgs& a, int bx, int fy_, int gdx, uint32_t* smem) {
@@ -718,6 +751,7 @@ __device__ __forceinline__ void c3hlac_tile_body(const KArgs& a, int bx, int fy_
   C3H_PROF(1, true);
 
   if (a.mfma && 2 * nwork >= a.ntiles) return;  // dense frame: c3hlac_mfma_body takes it
+  bool pre = false;  // s_tile already holds this tile's halo (prefetched by the previous tile)
   for (; wi < (a.debug == 4 ? 0 : nwork); wi += G) {
     const int tile = tile_next;
     if (wi + G < nwork) tile_next = fwork[wi + G];
@@ -734,8 +768,11 @@ __device__ __forceinline__ void c3hlac_tile_body(const KArgs& a, int bx, int fy_
     const int nrows = TY * (lz + 1);
     if (tid == 0) s_misc[0] = 0;
 
-    // 1. halo tile; every load of a thread is issued before its first LDS store
-    if (vec) {
+    // 1. halo tile; every load of a thread is issued before its first LDS store (or, when
+    //    the previous tile prefetched it, the LDS-DMA retired here)
+    if (pre) {
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (vec) {
       const int q4 = TX >> 2, n = nrows * q4;
       uint4 w[kMaxLoads];
       int idx[kMaxLoads];
@@ -781,6 +818,7 @@ __device__ __forceinline__ void c3hlac_tile_body(const KArgs& a, int bx, int fy_
       }
     }
     lds_barrier();
+    pre = false;  // consumed; the last chunk below may prefetch the next tile
     C3H_PROF(3, wi == bx - a.zblocks);
     if (a.debug == 1) {
       if (tid == 0 && s_tile[0] == 0xdeadbeefu) fexist[0] = 1;  // keep the loads live
@@ -895,6 +933,41 @@ __device__ __forceinline__ void c3hlac_tile_body(const KArgs& a, int bx, int fy_
       }
       lds_barrier();
       C3H_PROF(2, c0 == 0 && wi == bx - a.zblocks);
+      if (c0 + kChunk >= nlist) {
+        // the last chunk's operands are built: s_tile is free, so the next tile's halo goes
+        // into it by LDS-DMA while this tile's dot4 and epilogue run (round 6; the halo's
+        // global latency was ~2 of ~6.6 us per surface tile).  Retired by the vmcnt wait
+        // at the next tile's phase 1; lds_barrier keeps it in flight (no vmcnt).
+        if (C3H_TILE_PREFETCH && wi + G < nwork) {
+          const HaloGeo g = halo_geo(a, segs, tile_next);
+          if (g.vec && g.n <= kMaxLoads * kBlock) {
+            pre = true;
+            int q = tid / g.q4, r = tid - q * g.q4;
+            const int sq = kBlock / g.q4, sr = kBlock - sq * g.q4;
+#pragma unroll
+            for (int j = 0; j < kMaxLoads; ++j) {
+              const int e = tid + j * kBlock;
+              if (j * kBlock >= g.n) break;  // uniform
+              if (e < g.n) {
+                const int gy = g.y0 - 1 + q % g.TY, gz = g.z0 - 1 + q / g.TY;
+                const uint4* src = ((unsigned)gy < (unsigned)a.gy && (unsigned)gz < (unsigned)a.gz)
+                                       ? reinterpret_cast<const uint4*>(fgrid + ((int64_t)gz * a.gy + gy) * a.gx + g.xs + 4 * r)
+                                       : &kHaloZero16;
+                // wave-uniform LDS base + lane * 16: element e lands at s_tile[4 e]
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                                 reinterpret_cast<void*>(s_tile + 4 * (j * kBlock + (tid & ~63))),
+                                                 16, 0, 0);
+              }
+              q += sq;
+              r += sr;
+              if (r >= g.q4) {
+                r -= g.q4;
+                ++q;
+              }
+            }
+          }
+        }
+      }
       // 4. exact integer accumulation: acc[c] += sum_g dot4(A_c[g], N_{k,n}[g])
       if (tid < 180) {
         const int ng = (min(nlist - c0, kChunk) + 3) >> 2;
