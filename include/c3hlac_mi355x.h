@@ -101,7 +101,11 @@ const char* c3h_last_error(const c3h_ctx* ctx);
  * (c3h_get_downsampled); where a centroid rounds across its cell boundary, the next
  * c3h_extract takes that voxel's subdivision and neighbour base from the centroid, as
  * c3_hlac.cpp:349-377 does.  With on_device = 1, c3h_get_downsampled reads the points
- * again: keep the buffer alive until then. */
+ * again: keep the buffer alive until then.  Any extent whose voxel count fits int32 is
+ * accepted (PCL's check; more: C3H_ERR_RANGE): frames wider than the context's accumulator
+ * budget (2^26 cells, 1.6 GB) are voxelised by a sorted pass with the same results.  An
+ * internal inconsistency of the accumulators (device-side bound checks) fails with
+ * C3H_ERR_HIP without touching memory outside the frame, and the next call starts clean. */
 int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, float leaf,
                  float z_limit, c3h_grid_info* info);
 /* sensor_msgs/PointCloud2 ingestion: pcl::fromROSMsg(*msg, cloud) into PointXYZRGB

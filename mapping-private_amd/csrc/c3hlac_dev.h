@@ -644,7 +644,7 @@ struct KArgs {
 constexpr int kMaxLoads = 4;  // uint4 tile loads per thread kept in flight together
 constexpr int kSegLds = 64;   // segment tables up to 64 segments per axis live in LDS
 #ifndef C3H_TILE_PREFETCH
-#define C3H_TILE_PREFETCH 1  // the next tile's halo into LDS by global_load_lds during this tile's dot4 + epilogue
+#define C3H_TILE_PREFETCH 0  // 1: the next tile's halo into LDS by global_load_lds during this tile's dot4 + epilogue (measured neutral, round 6: DESIGN §8)
 #endif
 // 16 zero bytes: the LDS-DMA source of halo words outside the grid (a lane's LDS-DMA
 // destination is fixed by its lane index, so it cannot be skipped, only pointed at zeros)
