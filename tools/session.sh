@@ -18,6 +18,8 @@
 #                    C3H_TICK_PROF)                         -> tick_roles_points.txt
 #   single           the single-frame block under --kernel-trace --memory-copy-trace
 #                    (tools/single_frame_trace.py)          -> single/
+#   singlephase      the single-frame block with C3H_PROF phase lines (needs VARIANT=diag:
+#                    a -DC3H_DIAG build)                    -> single_phases.txt, single_phase_block.json
 #   config5          BASELINE configs[4] stage times (tools/config5.py --fp16) -> config5.log
 #   real_views       the reference's 126 committed Kinect views (tools/real_views_bench.py) -> real_views.json
 #   tileprof         the dot4 tile body's phases on a points-in frame (tools/tile_prof.py; with
@@ -58,6 +60,8 @@ for step in "$@"; do
         timeout -k 10 300 python -u tools/points_bench.py 128 512 64 > $O/roles_points.jsonl 2> $O/roles.err || exit 19 ;;
     single) prof 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/single -o run --output-format csv -- \
             python3 $R/tools/single_frame_trace.py 40 > $O/single_block.json 2> $O/single.err || exit 20 ;;
+    singlephase) rm -f $O/single_phases.txt
+      C3H_PROF=$O/single_phases.txt timeout -k 10 300 python -u tools/single_frame_trace.py 20 > $O/single_phase_block.json 2> $O/singlephase.err || exit 24 ;;
     config5) timeout -k 10 300 python -u tools/config5.py --fp16 > $O/config5.log 2>&1 || exit 21 ;;
     real_views) timeout -k 10 300 python -u tools/real_views_bench.py tests/golden/kinect_views_126.npz > $O/real_views.json 2> $O/real_views.err || exit 22 ;;
     tileprof) C3H_PROF=$O/tile_prof_phases.txt timeout -k 10 200 python -u tools/tile_prof.py 20 981 10 > $O/tile_prof.json 2> $O/tile_prof.err || exit 23 ;;
