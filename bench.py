@@ -484,7 +484,10 @@ def points_pass(ctx, dev, rank, world, dist, torch, synth, c3hlac, n_total, n_ho
     ctx.run_point_frames(frames[:4 * BATCH], *args[:7], True, out)  # untimed: sizes the buffers
     torch.cuda.synchronize(dev)
 
-    def timed(fr, d_out, gather):
+    def timed(fr, d_out, gather, batch=None):
+        # frames per batch: the binding's choice for the call's frame count (32 from 256
+        # frames up, else 64; Context.point_batch), or the one given
+        ctx.set_batch(batch or ctx.point_batch(len(fr)))
         if dist:
             dist.barrier()
         torch.cuda.synchronize(dev)
@@ -506,6 +509,9 @@ def points_pass(ctx, dev, rank, world, dist, torch, synth, c3hlac, n_total, n_ho
     # timed call runs without HIP events around the launches (they cost ~3 % here); a second
     # call with events gives the voxeliser's per-frame time
     frames = ctx.prepare_point_frames(frames)
+    ctx.set_batch(ctx.point_batch(len(mine)))
+    ctx.run_point_frames(frames, *args[:7], True, out)  # untimed: one whole call at the timed batch size
+    torch.cuda.synchronize(dev)
     el_dev, info = timed(frames, out, True)
     ev_out = torch.zeros_like(out)
     ctx.timing(c3hlac.timing_mask("voxelize", "pipeline"))
@@ -518,6 +524,7 @@ def points_pass(ctx, dev, rank, world, dist, torch, synth, c3hlac, n_total, n_ho
     res = {
         "frames": n_total,
         "frames_per_s_from_points": n_total / el_dev,
+        "batch": ctx.point_batch(len(mine)),
         "note": "configs[3]: %d independent 1M-point frames (128^3, C3-HLAC-981 S=10, 981->100, 1 model x r=20, "
                 "box 2x2x2, rank 1) sharded over %d GPU(s), c3h_run_point_frames per rank (GPU voxeliser + "
                 "pipelined tick, one host sync per call) + RCCL all_gather; points resident in HBM" % (n_total, world),
@@ -544,13 +551,23 @@ def points_pass(ctx, dev, rank, world, dist, torch, synth, c3hlac, n_total, n_ho
                 el_s, _ = timed(s_frames, s_out, False)
                 best = el_s if best is None else min(best, el_s)
             shard[str(len(sel))] = {"frames_per_s": len(sel) / best, "ms_per_call": best * 1e3,
+                                    "batch": ctx.point_batch(len(sel)),
                                     "records_equal_full_run": bool(torch.equal(s_out.cpu(), want[sel]))}
+        # the full run again at the shards' batch of 64: the fill cost of a small shard alone,
+        # without the full run's gain from its smaller batches
+        b64_out = torch.zeros_like(out)
+        el_64, _ = timed(frames, b64_out, False, batch=64)
         res["shard_frames_per_s"] = {k: v["frames_per_s"] for k, v in shard.items()}
         res["shard_over_full"] = {k: v["frames_per_s"] / res["frames_per_s_from_points"] for k, v in shard.items()}
+        res["frames_per_s_from_points_b64"] = len(frames) / el_64
+        res["b64_equals"] = bool(torch.equal(b64_out, out))
+        res["shard_over_full_b64"] = {k: v["frames_per_s"] * el_64 / len(frames) for k, v in shard.items()}
         res["shard"] = shard
         res["shard_note"] = ("rank 0's shard of %d frames at N = 2, 4, 8 (every N-th frame), one c3h_run_point_frames "
-                             "call each on this GPU, best of 3; shard_over_full: per-frame rate against the %d-frame "
-                             "run" % (len(frames), len(frames)))
+                             "call each on this GPU, best of 3, at Context.point_batch's batch (32 from 256 frames up, "
+                             "else 64); shard_over_full: per-frame rate against the %d-frame run; shard_over_full_b64: "
+                             "against the %d-frame run at 64 frames per batch (the fill cost alone)"
+                             % (len(frames), len(frames), len(frames)))
     if n_host > 0:  # H2D included: the frames start in pinned host memory
         hf = [f.cpu().pin_memory() for f in frame_list[:n_host]]
         hout = torch.zeros((len(hf), 3 * P_M), dtype=torch.int64, device=dev)
@@ -677,6 +694,7 @@ def real_views_pass(ctx, dev, torch, synth, c3hlac, reps=10):
     ctx.set_rank(1)
     out = torch.zeros((len(frames), 3 * M), dtype=torch.int64, device=dev)
     args = (0.01, (40, 40, 40), 117, THR, 4, BOX, 4, True, out)
+    ctx.set_batch(64)  # (the views are small: 64 per batch)
     ctx.run_point_frames(frames, *args)  # untimed: sizes the buffers
     torch.cuda.synchronize(dev)
     best = None

@@ -406,6 +406,15 @@ class Context:
         """Frames per pipeline batch / launch in run_frames (1..64)."""
         self._chk(self.lib.c3h_set_batch(self.h, int(n)), "set_batch")
 
+    @staticmethod
+    def point_batch(n_frames):
+        """Batch size for a c3h_run_point_frames call of n_frames 1M-point frames (round 6,
+        measured on MI355X at 128^3, C3-HLAC-981: profiles/r6/shard/): 32 frames per batch
+        from 256 frames up (512 frames: 117k frames/s against 109k at 64), 64 below, where a
+        call has few batches and each tick's fill and drain cost more than the finer
+        overlap of smaller batches gains (64 frames: 85-89k at 64, 80-83k at 32)."""
+        return 32 if n_frames >= 256 else 64
+
     def set_pipeline(self, on):
         """run_frames scheduling: True = pipelined tick launches, False = lanes."""
         self._chk(self.lib.c3h_set_pipeline(self.h, int(bool(on))), "set_pipeline")

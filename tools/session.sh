@@ -10,6 +10,8 @@
 #   bench            the driver's bench command            -> bench.json
 #   prof             the bench under rocprofv3 --kernel-trace --stats, the timed ticks
 #                    against the bench line (tools/tick_trace.py)  -> prof/, tick_trace.json
+#   rehearse=N       bench.py --gpus N with every rank on device 0 over gloo (C3H_BENCH_REHEARSAL=1:
+#                    the multi-rank code path on a one-GPU box; not a measurement) -> rehearse_N.json
 #   pmc              HBM traffic passes of the bench (tools/pmc.sh) -> pmc/summary.json
 #   shard            configs[3]'s per-rank shard at N = 1..8 (tools/points_shard.py) -> shard.jsonl
 #   points[=G,F,B]   points-in rate (tools/points_bench.py, default 128,512,64) -> points.jsonl
@@ -49,6 +51,9 @@ for step in "$@"; do
     prof) prof 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- \
             python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --single-frames 0 > $O/prof_bench.json 2> $O/prof_bench.err || exit 14
           python3 tools/tick_trace.py $O/prof/run_kernel_trace.csv 5 20 $O/prof_bench.json > $O/tick_trace.json || exit 14 ;;
+    rehearse=*) n=${step#rehearse=}
+      C3H_BENCH_REHEARSAL=1 timeout -k 10 600 python -u bench.py --gpus $n --steps 5 --warmup 2 --no-cpu-baseline \
+        > $O/rehearse_$n.json 2> $O/rehearse_$n.err || exit 25 ;;
     pmc) bash tools/pmc.sh $TAG > $O/pmc.log 2>&1 || exit 15 ;;
     shard) timeout -k 10 500 python -u tools/points_shard.py ${SHARD_B:-64,32,16} 3 > $O/shard.jsonl 2> $O/shard.err || exit 16 ;;
     points|points=*) a=${step#points}; a=${a#=}; IFS=, read G F B <<< "${a:-128,512,64}"
