@@ -132,6 +132,7 @@ struct VoxArgs {
   int par;                  // epoch parity of this frame
   int clear_grid;           // clear the grid words the previous frame listed
   int blk0;                 // first accumulate block of this launch (chunked host input)
+  long long* prof;          // diagnostics builds only (C3H_PROF): per-block phase timestamps
 };
 hipError_t launch_voxelize(const VoxArgs& a, hipStream_t s);
 // the accumulate pass over blocks [a.blk0, a.blk0 + nblocks) only (host frames copied in

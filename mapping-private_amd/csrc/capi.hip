@@ -966,8 +966,17 @@ int c3h_voxelize(c3h_ctx* ctx, const float* xyzrgb, int64_t n, int on_device, fl
       }
       HIPCHK(c3h::launch_vox_scatter(a, ctx->stream));
     } else {
-      Timed t(ctx, 0);
-      HIPCHK(c3h::launch_voxelize(a, ctx->stream));
+      int rc = prof_prepare(ctx, std::max(a.nblk, 1), &a.prof);  // diagnostics builds (C3H_PROF)
+      if (rc != C3H_OK) return rc;
+      {
+        Timed t(ctx, 0);
+        HIPCHK(c3h::launch_voxelize(a, ctx->stream));
+      }
+      if (a.prof) {
+        rc = prof_dump(ctx, "vox_accum_kernel", std::max(a.nblk, 1));
+        if (rc != C3H_OK) return rc;
+        a.prof = nullptr;
+      }
     }
     HIPCHK(hipMemcpyAsync(hc, ctx->vcnt.p, c3h::kVcWords * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));

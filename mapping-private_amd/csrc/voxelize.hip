@@ -158,6 +158,14 @@ __device__ __forceinline__ uint32_t vrow_shr(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 | O, 0xf, 0xf, true);
 }
 
+// diagnostics builds: per-block phase timestamps (C3H_PROF; thread 0 of each block)
+#ifdef C3H_DIAG
+#define C3H_VPROF(k) \
+  if (a.prof && threadIdx.x == 0) a.prof[(size_t)blockIdx.x * 8 + (k)] = (long long)wall_clock64()
+#else
+#define C3H_VPROF(k)
+#endif
+
 __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
   __shared__ uint32_t s_key[kLSlots];
   __shared__ unsigned long long s_A[kLSlots];  // count << 40 | sum r
@@ -166,6 +174,7 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
   __shared__ uint32_t s_nnew;                  // list entries of this workgroup
   __shared__ int s_red[kVB / 64][8];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, b = blockIdx.x + a.blk0;
+  C3H_VPROF(0);
   if (b == 0 && tid == 0) {  // totals of an empty frame (the scatter publishes the others)
     for (int ax = 0; ax < 3; ++ax) {
       reinterpret_cast<int32_t*>(a.cnt)[kVcMin + ax] = INT_MAX;
@@ -206,6 +215,7 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
     }
   }
   clear_prev();
+  C3H_VPROF(1);
   for (int s = tid; s < kLSlots; s += kVB) {
     s_key[s] = kNoT;
     s_A[s] = 0;
@@ -214,6 +224,7 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
   }
   if (tid == 0) s_nnew = 0;
   __syncthreads();
+  C3H_VPROF(2);
   uint32_t* sl = a.lists + (size_t)a.par * a.lcap + (size_t)b * kVoxChunk;
   ulonglong2* __restrict__ acc = a.acc;
   uint32_t* __restrict__ mg = a.mg;
@@ -293,6 +304,7 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
     if (!done) add_global(t, A, B, mb);  // LDS table full: straight to the global sums
   }
   __syncthreads();  // every point's LDS update is in
+  C3H_VPROF(3);
   // flush: per (workgroup, voxel) two adds and, near a face only, the margin min (~2 global
   // atomics per pair: 64-bit device atomics run at ~22 G/s chip-wide, tools/atomic_bench.hip,
   // so their count sets the flush's cost).  The returning add detects the voxel's first
@@ -336,6 +348,7 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
     s_red[w][7] = e;
   }
   __syncthreads();
+  C3H_VPROF(4);
   int32_t* pr = a.part + ((size_t)a.par * a.nblk_cap + b) * kPartW;
   if (tid < 8) {
     int v = s_red[0][tid];
@@ -346,6 +359,7 @@ __global__ __launch_bounds__(kVB) void vox_accum_kernel(VoxArgs a) {
     pr[tid < 7 ? tid : kPErr] = v;
   }
   if (tid == 8) pr[kPNew] = (int)s_nnew;
+  C3H_VPROF(5);
 }
 
 // every block reduces the accum blocks' partial records (a few KB, from L2); block 0

@@ -20,6 +20,8 @@
 #                    C3H_TICK_PROF)                         -> tick_roles_points.txt
 #   single           the single-frame block under --kernel-trace --memory-copy-trace
 #                    (tools/single_frame_trace.py)          -> single/
+#   singleblock      the single-frame block alone, no profiler (tools/single_frame_trace.py 40)
+#                    -> single_block_<VARIANT or product>.json
 #   singlephase      the single-frame block with C3H_PROF phase lines (needs VARIANT=diag:
 #                    a -DC3H_DIAG build)                    -> single_phases.txt, single_phase_block.json
 #   config5          BASELINE configs[4] stage times (tools/config5.py --fp16) -> config5.log
@@ -65,6 +67,7 @@ for step in "$@"; do
         timeout -k 10 300 python -u tools/points_bench.py 128 512 64 > $O/roles_points.jsonl 2> $O/roles.err || exit 19 ;;
     single) prof 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/single -o run --output-format csv -- \
             python3 $R/tools/single_frame_trace.py 40 > $O/single_block.json 2> $O/single.err || exit 20 ;;
+    singleblock) timeout -k 10 300 python -u tools/single_frame_trace.py 40 > $O/single_block_${VARIANT:-product}.json 2> $O/singleblock.err || exit 26 ;;
     singlephase) rm -f $O/single_phases.txt
       C3H_PROF=$O/single_phases.txt timeout -k 10 300 python -u tools/single_frame_trace.py 20 > $O/single_phase_block.json 2> $O/singlephase.err || exit 24 ;;
     config5) timeout -k 10 300 python -u tools/config5.py --fp16 > $O/config5.log 2>&1 || exit 21 ;;
