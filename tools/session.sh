@@ -15,7 +15,7 @@
 #   pmc              HBM traffic passes of the bench (tools/pmc.sh) -> pmc/summary.json
 #   shard            configs[3]'s per-rank shard at N = 1..8 (tools/points_shard.py) -> shard.jsonl
 #   points[=G,F,B]   points-in rate (tools/points_bench.py, default 128,512,64) -> points.jsonl
-#   points_prof      the same under rocprofv3 --kernel-trace --stats -> points_prof/
+#   points_prof[=G,F,B] the same under rocprofv3 --kernel-trace --stats -> points_prof_B/, points_timeline_B.txt
 #   roles            points-in tick roles, diagnostics build (lib/variants/diag.so,
 #                    C3H_TICK_PROF)                         -> tick_roles_points.txt
 #   single           the single-frame block under --kernel-trace --memory-copy-trace
@@ -60,8 +60,10 @@ for step in "$@"; do
     shard) timeout -k 10 500 python -u tools/points_shard.py ${SHARD_B:-64,32,16} 3 > $O/shard.jsonl 2> $O/shard.err || exit 16 ;;
     points|points=*) a=${step#points}; a=${a#=}; IFS=, read G F B <<< "${a:-128,512,64}"
       timeout -k 10 300 python -u tools/points_bench.py $G $F $B > $O/points_${G}_${B}.jsonl 2> $O/points.err || exit 17 ;;
-    points_prof) prof 300 rocprofv3 --kernel-trace --stats -d $O/points_prof -o run --output-format csv -- \
-            python3 $R/tools/points_bench.py 128 512 64 > $O/points_prof.jsonl 2> $O/points_prof.err || exit 18 ;;
+    points_prof|points_prof=*) a=${step#points_prof}; a=${a#=}; IFS=, read G F B <<< "${a:-128,512,64}"
+      prof 300 rocprofv3 --kernel-trace --stats -d $O/points_prof_$B -o run --output-format csv -- \
+            python3 $R/tools/points_bench.py $G $F $B > $O/points_prof_$B.jsonl 2> $O/points_prof.err || exit 18
+      python3 tools/points_timeline.py $O/points_prof_$B/run_kernel_trace.csv > $O/points_timeline_$B.txt || exit 18 ;;
     roles) rm -f $O/tick_roles_points.txt
       C3HLAC_LIB=$R/mapping-private_amd/lib/variants/diag.so C3H_TICK_PROF=$O/tick_roles_points.txt \
         timeout -k 10 300 python -u tools/points_bench.py 128 512 64 > $O/roles_points.jsonl 2> $O/roles.err || exit 19 ;;
