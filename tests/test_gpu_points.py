@@ -274,3 +274,30 @@ def test_points_in_256_canvas_overlap_and_repeat(ctx):
         ref, _ = ctx.search(BOX, EXIST)
         assert np.array_equal(ga[i], ref[:, 0]), (i, ga[i], ref[:, 0])
     ctx.set_batch(32)
+
+
+def test_records_do_not_depend_on_batch_size_or_prepared_frames(ctx, bases):
+    """The same 96 frames at 32 and at 64 frames per batch (Context.point_batch's two
+    choices), as a list and as a PointFrames: identical detection records and frame info."""
+    import torch
+    dev = torch.device("cuda", 0)
+    bdev = [torch.from_numpy(b).to(dev) for b in bases]
+    nfr = 96
+    frames = [_variant(torch, bdev[i % 8], 3 + i // 8) for i in range(nfr)]
+    axis_t, var, axis_q = synth.random_bases(981, D, 1, R, seed=synth.BASE_SEED + 31)
+    ctx.search_setup(axis_t, var, axis_q)
+    ctx.set_rank(1)
+    ctx.set_pipeline(True)
+    outs, infos = [], []
+    for batch, prepared in ((32, False), (64, True), (32, True)):
+        ctx.set_batch(batch)
+        d_out = torch.zeros((nfr, 3), dtype=torch.int64, device=dev)
+        fr = ctx.prepare_point_frames(frames) if prepared else frames
+        _, info = ctx.run_point_frames(fr, LEAF, (G,) * 3, 981, THR, S, BOX, EXIST, True, d_out)
+        outs.append(d_out.cpu())
+        infos.append(info)
+    assert (infos[0]["status"] == 0).all()
+    assert (outs[0][:, 0].numpy().view(np.float64) > 0).all()
+    for o, inf in zip(outs[1:], infos[1:]):
+        assert torch.equal(o, outs[0])
+        assert np.array_equal(inf, infos[0])
