@@ -277,6 +277,11 @@ struct PointFixup {
 hipError_t launch_point_fixup(const PointFixup& a, hipStream_t s);
 bool point_fixup_fits(const int lmax[3]);  // the recompute's LDS (tile halo, list, operands) fits a CU
 hipError_t launch_vox_batch(const VoxBatchArgs& a, hipStream_t s);
+// the same in two parts: the accumulate (with the clear of the set's previous words), and the
+// chain that reads the accumulators (reduce, scatter, exact pass); only the chain reads the
+// batch's C3 launch (tile stamps, work lists)
+hipError_t launch_vox_batch_accum(const VoxBatchArgs& a, hipStream_t s);
+hipError_t launch_vox_batch_post(const VoxBatchArgs& a, hipStream_t s);
 
 struct C3Launch {
   const uint32_t* grid[kMaxBatch];  // one grid per frame of the batch
@@ -563,6 +568,8 @@ struct c3h_ctx {
   c3h::DevBuf<uint32_t> tmp_u32;    // leaf-layout block sums
   c3h::DevBuf<int32_t> tmp_i32;     // leaf layout for host copies
   uint32_t* h_small = nullptr;      // pinned host scratch (64 words)
+  c3h::VoxFrameRec* h_recs = nullptr;  // pinned: the frame records a c3h_run_point_frames call reads back
+  size_t h_recs_n = 0;
   bool table_valid = false;         // hash table matches the grid (voxelize path)
 
   // features

@@ -795,6 +795,7 @@ void c3h_destroy(c3h_ctx* ctx) {
     (void)hipEventDestroy(e.second);
   }
   if (ctx->h_small) (void)hipHostFree(ctx->h_small);
+  if (ctx->h_recs) (void)hipHostFree(ctx->h_recs);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
 }
@@ -2778,7 +2779,26 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
         grids[j] = c->pb_grid.p + (size_t)j * cvox;
         outs[j] = d_out + (size_t)(f0 + j) * per_frame;
       }
-      // the batch's launches are captured first: the scatter sets its tile stamps and work
+      // the accumulate needs nothing of the batch's C3 launch, so it starts before the
+      // launch is captured (the capture's host work, ~10 us, then runs beside it: a one-batch
+      // call starts sooner).  The set's grids and gate limits were last read by the tick
+      // pushed two batches ago (tile role: one tick after the batch's own, gate role: two),
+      // so this batch's voxels overlap the previous batch's tick
+      if (ch >= 2) HIPCHK(hipStreamWaitEvent(vs, ctx->pb_tick_ev[(ch - 2) & 3], 0));
+      {
+        Timed t(ctx, 0, nb, vs);
+        HIPCHK(c3h::launch_vox_batch_accum(va, vs));
+      }
+      // until the chain below has run, the accumulators hold this batch's sums: an exit in
+      // between has the next call re-zero them
+      struct PbAccGuard {
+        c3h_ctx* c;
+        bool armed;
+        ~PbAccGuard() {
+          if (armed) c->pb_acc_vox = 0;
+        }
+      } pb_acc_guard{ctx, true};
+      // the batch's launches are captured next: the scatter sets its tile stamps and work
       // lists (the occupancy stream's job), so its first tick carries no occupancy role and
       // no canvas is streamed (128^3: 8.4 MB, 256^3: 67 MB per frame)
       c3h_ctx::PipeBatch fresh{};
@@ -2843,14 +2863,11 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
         HIPCHK(hipEventRecord(ctx->pb_vox_ev, ctx->stream));
         HIPCHK(hipStreamWaitEvent(vs, ctx->pb_vox_ev, 0));
       }
-      // the set's grids and gate limits were last read by the tick pushed two batches ago
-      // (tile role: one tick after the batch's own, gate role: two), so this batch's voxels
-      // overlap the previous batch's tick
-      if (ch >= 2) HIPCHK(hipStreamWaitEvent(vs, ctx->pb_tick_ev[(ch - 2) & 3], 0));
       {
-        Timed t(ctx, 0, nb, vs);
-        HIPCHK(c3h::launch_vox_batch(va, vs));
+        Timed t(ctx, 0, 0, vs);  // (the frames are counted with the accumulate)
+        HIPCHK(c3h::launch_vox_batch_post(va, vs));
       }
+      pb_acc_guard.armed = false;  // the scatter returns every touched accumulator to zero
       HIPCHK(hipEventRecord(ctx->pb_vox_ev, vs));
       c->pb_prev_nf = nb;
       c->pb_prev_total = va.total;
@@ -2876,9 +2893,21 @@ int c3h_run_point_frames(c3h_ctx* ctx, const float* const* pts, const int64_t* n
       ctx->pipe.clear();
       return rc;
     }
-    std::vector<c3h::VoxFrameRec> recs((size_t)nframes);
-    HIPCHK(hipMemcpyAsync(recs.data(), ctx->pb_info.p, recs.size() * sizeof(c3h::VoxFrameRec), hipMemcpyDeviceToHost,
-                          ctx->stream));
+    // the records come back through pinned memory: one asynchronous copy and one stream
+    // synchronisation (a pageable copy blocks, then the stream is synchronised again; ~20 us
+    // of a 64-frame call's ~0.75 ms)
+    if (ctx->h_recs_n < (size_t)nframes) {
+      if (ctx->h_recs) HIPCHK(hipHostFree(ctx->h_recs));
+      ctx->h_recs = nullptr;
+      ctx->h_recs_n = 0;
+      void* hp = nullptr;
+      HIPCHK(hipHostMalloc(&hp, (size_t)nframes * sizeof(c3h::VoxFrameRec)));
+      ctx->h_recs = static_cast<c3h::VoxFrameRec*>(hp);
+      ctx->h_recs_n = (size_t)nframes;
+    }
+    const c3h::VoxFrameRec* recs = ctx->h_recs;
+    HIPCHK(hipMemcpyAsync(ctx->h_recs, ctx->pb_info.p, (size_t)nframes * sizeof(c3h::VoxFrameRec),
+                          hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     for (int i = 0; i < nframes; ++i) {
       const c3h::VoxFrameRec& r = recs[i];

@@ -1487,8 +1487,17 @@ __global__ __launch_bounds__(kBlock) void voxb_exact_kernel(VoxBatchArgs a) {
 int vb_chunk() { return kBChunk; }
 
 hipError_t launch_vox_batch(const VoxBatchArgs& a, hipStream_t s) {
+  const hipError_t e = launch_vox_batch_accum(a, s);
+  return e != hipSuccess ? e : launch_vox_batch_post(a, s);
+}
+
+hipError_t launch_vox_batch_accum(const VoxBatchArgs& a, hipStream_t s) {
   const int g = std::max(a.total, a.prev_total);
   if (g > 0) voxb_accum_kernel<<<(unsigned)g, kBT, 0, s>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_vox_batch_post(const VoxBatchArgs& a, hipStream_t s) {
   if (a.total > 0) {
     voxb_reduce_kernel<<<(unsigned)a.nf, kBlock, 0, s>>>(a);
     voxb_scatter_kernel<<<(unsigned)a.total, kBlock, a.stamp ? 4 * (size_t)((a.ntiles + 31) / 32) : 0, s>>>(a);

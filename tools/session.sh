@@ -16,6 +16,8 @@
 #   shard            configs[3]'s per-rank shard at N = 1..8 (tools/points_shard.py) -> shard.jsonl
 #   points[=G,F,B]   points-in rate (tools/points_bench.py, default 128,512,64) -> points.jsonl
 #   points_prof[=G,F,B] the same under rocprofv3 --kernel-trace --stats -> points_prof_B/, points_timeline_B.txt
+#   hiptrace=G,F,B   points_bench under rocprofv3 --kernel-trace --hip-trace (host API timeline)
+#                    -> hiptrace_B/
 #   roles            points-in tick roles, diagnostics build (lib/variants/diag.so,
 #                    C3H_TICK_PROF)                         -> tick_roles_points.txt
 #   single           the single-frame block under --kernel-trace --memory-copy-trace
@@ -64,6 +66,9 @@ for step in "$@"; do
       prof 300 rocprofv3 --kernel-trace --stats -d $O/points_prof_$B -o run --output-format csv -- \
             python3 $R/tools/points_bench.py $G $F $B > $O/points_prof_$B.jsonl 2> $O/points_prof.err || exit 18
       python3 tools/points_timeline.py $O/points_prof_$B/run_kernel_trace.csv > $O/points_timeline_$B.txt || exit 18 ;;
+    hiptrace=*) a=${step#hiptrace=}; IFS=, read G F B <<< "$a"
+      prof 300 rocprofv3 --kernel-trace --hip-trace -d $O/hiptrace_$B -o run --output-format csv -- \
+            python3 $R/tools/points_bench.py $G $F $B > $O/hiptrace_$B.jsonl 2> $O/hiptrace.err || exit 27 ;;
     roles) rm -f $O/tick_roles_points.txt
       C3HLAC_LIB=$R/mapping-private_amd/lib/variants/diag.so C3H_TICK_PROF=$O/tick_roles_points.txt \
         timeout -k 10 300 python -u tools/points_bench.py 128 512 64 > $O/roles_points.jsonl 2> $O/roles.err || exit 19 ;;
