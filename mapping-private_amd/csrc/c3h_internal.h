@@ -647,6 +647,8 @@ struct c3h_ctx {
   int rank = 1;
   c3h::SearchLists lists;
   std::vector<c3h_det> h_lists;     // host staging of the lists
+  c3h_det* h_dl = nullptr;  // pinned: the lists a search reads back (one async copy + one sync)
+  size_t h_dl_n = 0;
   c3h::DevBuf<c3h_det> d_lists;
   bool lists_host_valid = true;     // host lists are current
   bool lists_dev_valid = false;     // device lists are current

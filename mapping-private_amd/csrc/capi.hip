@@ -299,16 +299,25 @@ int upload_lists(c3h_ctx* ctx) {
 int download_lists(c3h_ctx* ctx) {
   auto& L = ctx->lists;
   const size_t n = (size_t)L.M * L.rank;
-  ctx->h_lists.resize(n);
-  HIPCHK(hipMemcpyAsync(ctx->h_lists.data(), ctx->d_lists.p, n * sizeof(c3h_det),
-                        hipMemcpyDeviceToHost, ctx->stream));
+  // through pinned memory: a pageable read-back blocks in the copy and the stream is then
+  // synchronised a second time (the per-callback loop reads the lists every frame)
+  if (ctx->h_dl_n < n) {
+    if (ctx->h_dl) HIPCHK(hipHostFree(ctx->h_dl));
+    ctx->h_dl = nullptr;
+    ctx->h_dl_n = 0;
+    void* hp = nullptr;
+    HIPCHK(hipHostMalloc(&hp, std::max<size_t>(n, 1) * sizeof(c3h_det)));
+    ctx->h_dl = static_cast<c3h_det*>(hp);
+    ctx->h_dl_n = std::max<size_t>(n, 1);
+  }
+  HIPCHK(hipMemcpyAsync(ctx->h_dl, ctx->d_lists.p, n * sizeof(c3h_det), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   for (size_t i = 0; i < n; ++i) {
-    L.score[i] = ctx->h_lists[i].score;
-    L.x[i] = ctx->h_lists[i].x;
-    L.y[i] = ctx->h_lists[i].y;
-    L.z[i] = ctx->h_lists[i].z;
-    L.mode[i] = ctx->h_lists[i].mode;
+    L.score[i] = ctx->h_dl[i].score;
+    L.x[i] = ctx->h_dl[i].x;
+    L.y[i] = ctx->h_dl[i].y;
+    L.z[i] = ctx->h_dl[i].z;
+    L.mode[i] = ctx->h_dl[i].mode;
   }
   ctx->lists_host_valid = true;
   return C3H_OK;
@@ -796,6 +805,7 @@ void c3h_destroy(c3h_ctx* ctx) {
   }
   if (ctx->h_small) (void)hipHostFree(ctx->h_small);
   if (ctx->h_recs) (void)hipHostFree(ctx->h_recs);
+  if (ctx->h_dl) (void)hipHostFree(ctx->h_dl);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
 }
