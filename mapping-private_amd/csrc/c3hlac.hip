@@ -861,7 +861,10 @@ static int64_t mfma_grid(const C3Launch& l, size_t lds) {
 hipError_t launch_c3hlac(const C3Launch& l, hipStream_t s) {
   if (l.nframes < 1 || l.nframes > kMaxBatch) return hipErrorInvalidValue;
   C3Args c = build_c3_args(l);
-  const bool mf = mfma_ok(l);
+  // a grid stamped from the voxeliser's list is below 1/16 occupancy (extract_frames' rule):
+  // its tiles are sparse whatever their count, so the dot4 body takes them all and the
+  // matrix-core body is not launched (round 6: its early exit cost a launch, ~4.5 us)
+  const bool mf = mfma_ok(l) && !(l.vl_words && l.nframes == 1);
   c.ka.mfma = mf ? 1 : 0;
 #ifndef C3H_OCC_CONTIG
 #define C3H_OCC_CONTIG 1
