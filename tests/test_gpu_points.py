@@ -301,3 +301,32 @@ def test_records_do_not_depend_on_batch_size_or_prepared_frames(ctx, bases):
     for o, inf in zip(outs[1:], infos[1:]):
         assert torch.equal(o, outs[0])
         assert np.array_equal(inf, infos[0])
+
+
+def test_z_limit_in_the_batch(ctx, bases):
+    """limitPoint's depth cut (detect_object.cpp:68-87) inside the batch: 12 frames with
+    z_limit at 60 % of the scene depth give the single-frame path's records and geometry
+    with the same cut, and frame 0's grid geometry and voxel count equal the oracle's."""
+    import torch
+    dev = torch.device("cuda", 0)
+    axis_t, var, axis_q = synth.random_bases(981, D, 1, R, seed=synth.BASE_SEED + 31)
+    ctx.search_setup(axis_t, var, axis_q)
+    ctx.set_rank(1)
+    ctx.set_batch(8)
+    frames = [np.ascontiguousarray(_variant_host(bases[i % 8], i)) for i in range(12)]
+    z = frames[0][:, 2]
+    zl = float(np.float32(np.nanmin(z[np.isfinite(z)]) + 0.6 * (np.nanmax(z[np.isfinite(z)]) -
+                                                                  np.nanmin(z[np.isfinite(z)]))))
+    devf = [torch.from_numpy(f).to(dev) for f in frames]
+    d_out = torch.zeros((len(frames), 3), dtype=torch.int64, device=dev)
+    _, info = ctx.run_point_frames(devf, LEAF, (G,) * 3, 981, THR, S, BOX, EXIST, True, d_out, z_limit=zl)
+    got = d_out.cpu().numpy().view(c3hlac.DET_DTYPE).reshape(len(frames), 1)
+    assert (info["status"] == 0).all(), info["status"]
+    g, layout, _ = po.voxelize(frames[0], LEAF, zl)
+    assert list(info["div_b"][0]) == list(g.div_b) and list(info["min_b"][0]) == list(g.min_b)
+    assert info["n_occ"][0] == (layout >= 0).sum()
+    for i in range(len(frames)):
+        ref = _single(ctx, devf[i], z_limit=zl)
+        assert np.array_equal(got[i], ref[:, 0]), (i, got[i], ref[:, 0])
+        assert list(info["div_b"][i]) == list(ctx.info.div_b), i
+    ctx.set_batch(32)

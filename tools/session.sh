@@ -26,6 +26,7 @@
 #                    -> single_block_<VARIANT or product>.json
 #   singlephase      the single-frame block with C3H_PROF phase lines (needs VARIANT=diag:
 #                    a -DC3H_DIAG build)                    -> single_phases.txt, single_phase_block.json
+#   singlehip        the same with --hip-trace (host API timeline)  -> singlehip/
 #   config5          BASELINE configs[4] stage times (tools/config5.py --fp16) -> config5.log
 #   real_views       the reference's 126 committed Kinect views (tools/real_views_bench.py) -> real_views.json
 #   tileprof         the dot4 tile body's phases on a points-in frame (tools/tile_prof.py; with
@@ -77,6 +78,8 @@ for step in "$@"; do
     singleblock) timeout -k 10 300 python -u tools/single_frame_trace.py 40 > $O/single_block_${VARIANT:-product}.json 2> $O/singleblock.err || exit 26 ;;
     singlephase) rm -f $O/single_phases.txt
       C3H_PROF=$O/single_phases.txt timeout -k 10 300 python -u tools/single_frame_trace.py 20 > $O/single_phase_block.json 2> $O/singlephase.err || exit 24 ;;
+    singlehip) prof 300 rocprofv3 --kernel-trace --memory-copy-trace --hip-trace -d $O/singlehip -o run --output-format csv -- \
+            python3 $R/tools/single_frame_trace.py 40 > $O/singlehip_block.json 2> $O/singlehip.err || exit 28 ;;
     config5) timeout -k 10 300 python -u tools/config5.py --fp16 > $O/config5.log 2>&1 || exit 21 ;;
     real_views) timeout -k 10 300 python -u tools/real_views_bench.py tests/golden/kinect_views_126.npz > $O/real_views.json 2> $O/real_views.err || exit 22 ;;
     tileprof) C3H_PROF=$O/tile_prof_phases.txt timeout -k 10 200 python -u tools/tile_prof.py 20 981 10 > $O/tile_prof.json 2> $O/tile_prof.err || exit 23 ;;
