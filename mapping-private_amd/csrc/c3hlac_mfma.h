@@ -510,6 +510,91 @@ __device__ __forceinline__ void mf_layer_ksteps2u(const uint8_t* pp, const uint8
   }
 }
 
+#ifndef C3H_MF_TR
+#define C3H_MF_TR 1  // two-step layers as a record image read by ds_read_b64_tr_b8 (round 6)
+#endif
+// Record image (round 6).  A two-step layer (pitch 12, 12 rows) is held voxel-major: the
+// voxel at position p = row * 12 + col has the 16-byte record at byte 16 p of the slot,
+// bytes 0..11 = its 12 channel bytes (per colour the setColor table dword {sin, cos, beta,
+// 1 - beta} ^ 0x80, as the planes order them; 0x80 each for an empty voxel) and bytes
+// 12..15 = {0, 0, 0, 1} (the padding rows / columns).  The conversion is then 3 table
+// reads and one ds_write_b128 per voxel, with no byte transpose.  The MFMA operands come
+// back channel-major through ds_read_b64_tr_b8: in each 16-lane group, lane 2q + p
+// supplies the address of record q's bytes 8p .. 8p + 7 (q = 0..7) and lane i receives
+// byte i of the 8 records, i.e. channel i at 8 positions (measured, tools/tr8_probe.hip).
+// Two reads give a lane's 16 K bytes.  K map: byte j of lane group h in K step ks is
+// position 12 + 64 ks + 32 (j >> 3) + 8 h + (j & 7); A, B and the mask use the same
+// bijection, so the integer sums are unchanged.  Groups h and h + 1 (one 32-lane half)
+// read 128-byte runs 8 records apart, i.e. disjoint 32-bank halves: conflict-free, and so
+// is every neighbour offset (it moves all runs together).  The dx shifts stay on the
+// masked centre operand (A_s = centre row read at position + s, masked by the centre mask
+// of position + s), so a layer reads 5 neighbour rows + 3 centre shifts = 32 tr reads.
+// Records 144..151 of a slot (read by the dy = +1 rows beyond the window's centres) are
+// constant padding records.
+constexpr int kMfRecPos = 152;
+typedef int mf_v2i __attribute__((ext_vector_type(2)));
+typedef mf_v2i __attribute__((address_space(3))) * mf_lds_v2i;
+template <int OFF>
+__device__ __forceinline__ mf_v4i mf_trfrag(const uint8_t* base) {
+  const mf_v2i lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((mf_lds_v2i)(base + OFF));
+  const mf_v2i hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((mf_lds_v2i)(base + OFF + 16 * 32));
+  return mf_v4i{lo.x, lo.y, hi.x, hi.y};
+}
+// pp / pc: this lane's read base in the dz = -1 / dz = 0 slot, 16 (12 + 8 h + q) + 8 p - 192
+// bytes past the slot (the -192 keeps every offset a non-negative immediate: the smallest
+// is the dy = -1 row of K step 0); mk[s + 1][ks]: the centre mask of A_s
+template <int D, int KS>
+__device__ __forceinline__ mf_v4i mf_trrow(const uint8_t* b) {
+  return mf_trfrag<16 * (64 * KS + D + 12)>(b);
+}
+__device__ __forceinline__ void mf_layer_ksteps_tr(const uint8_t* pp, const uint8_t* pc, const uint32_t (&mk)[3][2][4],
+                                                   mf_v4i (&acc)[kMfK]) {
+  // the reads are issued one row ahead of the MFMAs that use them (compiler fences keep
+  // the scheduler from hoisting every read of the layer, which spilled)
+  mf_v4i A[3][2], X0[2];
+  {
+    const mf_v4i xm[2] = {mf_trrow<-1, 0>(pc), mf_trrow<-1, 1>(pc)};
+    X0[0] = mf_trrow<0, 0>(pc);
+    X0[1] = mf_trrow<0, 1>(pc);
+    const mf_v4i xp[2] = {mf_trrow<1, 0>(pc), mf_trrow<1, 1>(pc)};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        A[0][ks][i] = (int)(((uint32_t)xm[ks][i] & mk[0][ks][i]) | (0x80808080u & ~mk[0][ks][i]));
+        A[1][ks][i] = (int)(((uint32_t)X0[ks][i] & mk[1][ks][i]) | (0x80808080u & ~mk[1][ks][i]));
+        A[2][ks][i] = (int)(((uint32_t)xp[ks][i] & mk[2][ks][i]) | (0x80808080u & ~mk[2][ks][i]));
+      }
+  }
+  mf_v4i b0[2] = {mf_trrow<-12, 0>(pc), mf_trrow<-12, 1>(pc)};  // dz = 0, dy = -1
+  mf_compiler_fence();
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    acc[13] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1][ks], A[1][ks], acc[13], 0, 0, 0);  // own channels
+    acc[12] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[2][ks], X0[ks], acc[12], 0, 0, 0);    // (-1, 0, 0)
+  }
+  // offset k of a row with dx = -1, 0, +1 uses A_{+1}, A_0, A_{-1}
+#define C3H_MFT3(B, K0, KS)                                                                               \
+  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) {                                                      \
+    acc[K0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[2][ks], B[ks], acc[K0], 0, 0, 0);                  \
+    acc[K0 + KS] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1][ks], B[ks], acc[K0 + KS], 0, 0, 0);       \
+    acc[K0 + 2 * KS] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0][ks], B[ks], acc[K0 + 2 * KS], 0, 0, 0); \
+  }
+  mf_v4i b1[2] = {mf_trrow<-12, 0>(pp), mf_trrow<-12, 1>(pp)};  // dz = -1, dy = -1
+  mf_compiler_fence();
+  C3H_MFT3(b0, 9, 1)  // dz = 0, dy = -1: k = 9 + dx + 1
+  b0[0] = mf_trrow<0, 0>(pp);  // dz = -1, dy = 0
+  b0[1] = mf_trrow<0, 1>(pp);
+  mf_compiler_fence();
+  C3H_MFT3(b1, 0, 3)  // dz = -1, dy = -1: k = 3 (dx + 1)
+  b1[0] = mf_trrow<12, 0>(pp);  // dz = -1, dy = +1
+  b1[1] = mf_trrow<12, 1>(pp);
+  mf_compiler_fence();
+  C3H_MFT3(b0, 1, 3)  // dz = -1, dy = 0
+  C3H_MFT3(b1, 2, 3)  // dz = -1, dy = +1
+#undef C3H_MFT3
+}
+
 // plane p -> (type, reference channel); p >= 12 is padding
 __device__ __forceinline__ int mf_type(int p) { return (p >> 1) & 1; }
 __device__ __forceinline__ int mf_chan(int p) { return 2 * (p >> 2) + (p & 1); }
@@ -595,6 +680,7 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
     const bool two = C3H_MF_TWO && nks == 2 && (PW & 15) == 12;  // mf_layer_ksteps2's layers
     const int gap = two ? C3H_MF_GAP : 0;  // planes 4..11 shifted (banks, see mf_layer_ksteps2)
     uint8_t* mask = wl + kMfSlots * SS;
+    const bool trp = C3H_MF_TR && two;  // record image + transposed reads (mf_layer_ksteps_tr)
     // The tile shape's centre mask and item map (divisions by the pitch: ~300 VALU) are
     // built when the shape differs from this wave's previous tile; S-uniform grids give
     // every interior tile one shape (the mask stays in the wave's LDS region, past the
@@ -602,6 +688,21 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
     const int shape = lx | (ly << 8);
     if (!C3H_MF_SHAPE_CACHE || shape != shape_prev) {
       shape_prev = shape;
+      if (trp) {
+        // record path: per lane group h, 24 mask words (s + 1, ks, i) at mask + 96 h; byte
+        // b of word i: position 12 + 64 ks + 32 (j >> 3) + 8 h + (j & 7) + s, j = 4 i + b
+        for (int d = lane; d < 96; d += 64) {
+          const int gh = d / 24, r = d - 24 * gh, s = r / 8 - 1, ks = (r >> 2) & 1, i = r & 3;
+          uint32_t m = 0;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const int j = 4 * i + b, p = 12 + 64 * ks + 32 * (j >> 3) + 8 * gh + (j & 7) + s;
+            const int row = p / 12, col = p - 12 * row;
+            m |= (row >= 1 && row <= ly && col >= 1 && col <= lx ? 0xffu : 0u) << (8 * b);
+          }
+          reinterpret_cast<uint32_t*>(mask)[d] = m;
+        }
+      } else
       // centre mask of the K positions PW + 4 j + b: rows 1..ly, columns 1..lx
       // (one word more on each side: the shifted centre rows of mf_layer_ksteps2s read them)
       for (int j = lane - 1; j < 16 * nks + 1; j += 64) {
@@ -744,6 +845,90 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
     mf_v4i acc[kMfK];
 #pragma unroll
     for (int k = 0; k < kMfK; ++k) acc[k] = mf_v4i{0, 0, 0, 0};
+    if (trp) {
+      // padding records 144..151 of the three slots (the previous tile's staging overwrote them)
+      mf_compiler_fence();
+      if (lane < 3 * (kMfRecPos - 144))
+        *reinterpret_cast<mf_u4*>(wl + (lane >> 3) * SS + 16 * (144 + (lane & 7))) =
+            mf_u4{0x80808080u, 0x80808080u, 0x80808080u, 0x01000000u};
+      // this lane's masks (lanes n >= 12, the padding rows: everything kept)
+      uint32_t mk[3][2][4];
+      {
+        const mf_u4* mrow = reinterpret_cast<const mf_u4*>(mask + 96 * h4k);
+#pragma unroll
+        for (int s = 0; s < 3; ++s)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            const mf_u4 v = mrow[2 * s + ks];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) mk[s][ks][i] = realk ? v[i] : 0xffffffffu;
+          }
+      }
+      // this lane's voxels of a layer: positions e = lane + 64 i < 144 (row e / 12, column e % 12)
+      // (offsets from the tile's corner word: row * gx + col, -1 outside the tile or the grid)
+      int ro[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int e = lane + 64 * i, row = e / 12, col = e - 12 * row;
+        const int gy = y0 - 1 + row, gx = x0 - 1 + col;
+        const bool v = e < 144 && row < ly + 2 && col < lx + 2 && (unsigned)gy < (unsigned)a.gy && (unsigned)gx < (unsigned)a.gx;
+        ro[i] = v ? row * a.gx + col : -1;
+      }
+      const int64_t zst = (int64_t)a.gy * a.gx;
+      const uint32_t* tbase = fgrid + (((int64_t)(z0 - 1) * a.gy + (y0 - 1)) * a.gx + (x0 - 1));
+      auto load_rec = [&](int L, uint32_t (&w)[3]) {
+        const int gz = z0 - 1 + L;
+        const bool zin = (unsigned)gz < (unsigned)a.gz;
+        const uint32_t* lb = tbase + L * zst;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) w[i] = zin && ro[i] >= 0 ? lb[ro[i]] : 0u;
+      };
+      auto store_rec = [&](int L, const uint32_t (&w)[3]) {
+        uint8_t* slot = wl + (L % kMfSlots) * SS;
+        const uint8_t* tb = reinterpret_cast<const uint8_t*>(s_tab);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const int e = lane + 64 * i;
+          if (i == 2 && e >= 144) continue;
+          uint32_t ar, ag, ab;
+          __asm__("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+                  : "=v"(ar) : "v"(w[i]));
+          __asm__("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+                  : "=v"(ag) : "v"(w[i]));
+          __asm__("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+                  : "=v"(ab) : "v"(w[i]));
+          const uint32_t t0 = *reinterpret_cast<const uint32_t*>(tb + ar);
+          const uint32_t t1 = *reinterpret_cast<const uint32_t*>(tb + 1024 + ag);
+          const uint32_t t2 = *reinterpret_cast<const uint32_t*>(tb + 2048 + ab);
+          const bool occ = (w[i] >> 24) != 0u;
+          *reinterpret_cast<mf_u4*>(slot + 16 * e) =
+              mf_u4{occ ? t0 : 0x80808080u, occ ? t1 : 0x80808080u, occ ? t2 : 0x80808080u, 0x01000000u};
+        }
+      };
+      uint32_t wr[2][3];
+      load_rec(0, wr[0]);
+      load_rec(1, wr[1]);
+      store_rec(0, wr[0]);
+      store_rec(1, wr[1]);
+      if (2 <= lz) load_rec(2, wr[0]);
+      if (3 <= lz) load_rec(3, wr[1]);
+      // lane 2 q + p of group h reads record q's bytes 8 p.. (see mf_layer_ksteps_tr)
+      const int tro = 16 * (12 + 8 * h4k + ((lane & 15) >> 1)) + 8 * (lane & 1) - 192;
+      for (int z = 0; z < lz; ++z) {
+        mf_compiler_fence();
+        mf_layer_ksteps_tr(wl + ((z % kMfSlots) * SS + tro), wl + (((z + 1) % kMfSlots) * SS + tro), mk, acc);
+        mf_compiler_fence();
+        if (z + 2 <= lz) {
+          if (z & 1) {
+            store_rec(z + 2, wr[1]);
+            if (z + 4 <= lz) load_rec(z + 4, wr[1]);
+          } else {
+            store_rec(z + 2, wr[0]);
+            if (z + 4 <= lz) load_rec(z + 4, wr[0]);
+          }
+        }
+      }
+    } else {
     load_layer(0, wv[0]);
     load_layer(1, wv[1]);
     store_layer(0, wv[0]);
@@ -800,6 +985,7 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
         }
       }
     }
+    }  // record path / plane path
     mf_compiler_fence();
     // (the lane's coordinates made opaque per tile, so the bin arithmetic below is not
     // hoisted out of the tile loop and held in registers across it)
