@@ -31,6 +31,10 @@
 // step: 5 plane rows + the mask, 14 MFMAs.  The next layer's grid words are loaded into
 // registers two layers ahead (three layer slots in a ring).  The epilogue corrects and
 // scatters the accumulator tiles from registers (the padding lanes' sums by ds_bpermute).
+// Round 6: tiles of two-step layers (S <= 10, pitch 12: every interior tile of config 5)
+// hold each layer as a voxel-major record image instead of channel planes and read the
+// operands back through ds_read_b64_tr_b8 (mf_layer_ksteps_tr): the conversion needs no
+// byte transpose, and the dx shifts are immediate address offsets.
 #pragma once
 #include "c3hlac_dev.h"
 
@@ -513,6 +517,21 @@ __device__ __forceinline__ void mf_layer_ksteps2u(const uint8_t* pp, const uint8
 #ifndef C3H_MF_TR
 #define C3H_MF_TR 1  // two-step layers as a record image read by ds_read_b64_tr_b8 (round 6)
 #endif
+#ifndef C3H_MF_BFI
+#define C3H_MF_BFI 1  // record path: the centre masks as one v_bfi_b32 per dword
+#endif
+#ifndef C3H_MF_B96
+#define C3H_MF_B96 0  // record path: 12-byte record stores, the padding dword written once per tile (slower: 1.09 vs 1.01 ms)
+#endif
+#ifndef C3H_MF_BUFLD
+#define C3H_MF_BUFLD 1  // record path: branch-free raw buffer loads of the layer words
+#endif
+#ifndef C3H_MF_SRC2
+#define C3H_MF_SRC2 1  // f16 epilogue: the bin -> stage table read as u16 pairs (one LDS read per pair)
+#endif
+#ifndef C3H_MF_UNIWID
+#define C3H_MF_UNIWID 1  // the wave index through readfirstlane (scalar tile loop)
+#endif
 // Record image (round 6).  A two-step layer (pitch 12, 12 rows) is held voxel-major: the
 // voxel at position p = row * 12 + col has the 16-byte record at byte 16 p of the slot,
 // bytes 0..11 = its 12 channel bytes (per colour the setColor table dword {sin, cos, beta,
@@ -532,7 +551,27 @@ __device__ __forceinline__ void mf_layer_ksteps2u(const uint8_t* pp, const uint8
 // Records 144..151 of a slot (read by the dy = +1 rows beyond the window's centres) are
 // constant padding records.
 constexpr int kMfRecPos = 152;
+#ifndef C3H_MF_TRFENCE
+#define C3H_MF_TRFENCE 1  // record K steps: compiler fences hold each row's reads one row ahead
+#endif
+#ifndef C3H_MF_KSMAJOR
+#define C3H_MF_KSMAJOR 1  // record K steps: K step 0's 14 MFMAs, then step 1's (0: row by row, reads one row ahead)
+#endif
+#define C3H_MFT_FENCE() \
+  do {                  \
+    if (C3H_MF_TRFENCE) mf_compiler_fence(); \
+  } while (0)
 typedef int mf_v2i __attribute__((ext_vector_type(2)));
+// (x & m) | (0x80808080 & ~m): one v_bfi_b32 (the compiler split it into two bit ops)
+__device__ __forceinline__ int mf_bfi80(uint32_t m, uint32_t x) {
+#if C3H_MF_BFI
+  uint32_t r;
+  __asm__("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(x), "v"(0x80808080u));
+  return (int)r;
+#else
+  return (int)((x & m) | (0x80808080u & ~m));
+#endif
+}
 typedef mf_v2i __attribute__((address_space(3))) * mf_lds_v2i;
 template <int OFF>
 __device__ __forceinline__ mf_v4i mf_trfrag(const uint8_t* base) {
@@ -561,13 +600,35 @@ __device__ __forceinline__ void mf_layer_ksteps_tr(const uint8_t* pp, const uint
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        A[0][ks][i] = (int)(((uint32_t)xm[ks][i] & mk[0][ks][i]) | (0x80808080u & ~mk[0][ks][i]));
-        A[1][ks][i] = (int)(((uint32_t)X0[ks][i] & mk[1][ks][i]) | (0x80808080u & ~mk[1][ks][i]));
-        A[2][ks][i] = (int)(((uint32_t)xp[ks][i] & mk[2][ks][i]) | (0x80808080u & ~mk[2][ks][i]));
+        A[0][ks][i] = mf_bfi80(mk[0][ks][i], (uint32_t)xm[ks][i]);
+        A[1][ks][i] = mf_bfi80(mk[1][ks][i], (uint32_t)X0[ks][i]);
+        A[2][ks][i] = mf_bfi80(mk[2][ks][i], (uint32_t)xp[ks][i]);
       }
   }
+#if C3H_MF_KSMAJOR
+  // every K step's 14 MFMAs before the next step's: 14 MFMAs between two into one accumulator
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const mf_v4i bcm = ks ? mf_trrow<-12, 1>(pc) : mf_trrow<-12, 0>(pc);
+    const mf_v4i brm = ks ? mf_trrow<-12, 1>(pp) : mf_trrow<-12, 0>(pp);
+    const mf_v4i br0 = ks ? mf_trrow<0, 1>(pp) : mf_trrow<0, 0>(pp);
+    const mf_v4i brp = ks ? mf_trrow<12, 1>(pp) : mf_trrow<12, 0>(pp);
+    acc[13] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1][ks], A[1][ks], acc[13], 0, 0, 0);
+    acc[12] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[2][ks], X0[ks], acc[12], 0, 0, 0);
+#define C3H_MFK(B, K0, KS)                                                                       \
+    acc[K0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[2][ks], B, acc[K0], 0, 0, 0);              \
+    acc[K0 + KS] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1][ks], B, acc[K0 + KS], 0, 0, 0);   \
+    acc[K0 + 2 * KS] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0][ks], B, acc[K0 + 2 * KS], 0, 0, 0);
+    C3H_MFK(bcm, 9, 1)
+    C3H_MFK(brm, 0, 3)
+    C3H_MFK(br0, 1, 3)
+    C3H_MFK(brp, 2, 3)
+#undef C3H_MFK
+  }
+  return;
+#endif
   mf_v4i b0[2] = {mf_trrow<-12, 0>(pc), mf_trrow<-12, 1>(pc)};  // dz = 0, dy = -1
-  mf_compiler_fence();
+  C3H_MFT_FENCE();
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
     acc[13] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1][ks], A[1][ks], acc[13], 0, 0, 0);  // own channels
@@ -581,15 +642,15 @@ __device__ __forceinline__ void mf_layer_ksteps_tr(const uint8_t* pp, const uint
     acc[K0 + 2 * KS] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0][ks], B[ks], acc[K0 + 2 * KS], 0, 0, 0); \
   }
   mf_v4i b1[2] = {mf_trrow<-12, 0>(pp), mf_trrow<-12, 1>(pp)};  // dz = -1, dy = -1
-  mf_compiler_fence();
+  C3H_MFT_FENCE();
   C3H_MFT3(b0, 9, 1)  // dz = 0, dy = -1: k = 9 + dx + 1
   b0[0] = mf_trrow<0, 0>(pp);  // dz = -1, dy = 0
   b0[1] = mf_trrow<0, 1>(pp);
-  mf_compiler_fence();
+  C3H_MFT_FENCE();
   C3H_MFT3(b1, 0, 3)  // dz = -1, dy = -1: k = 3 (dx + 1)
   b1[0] = mf_trrow<12, 0>(pp);  // dz = -1, dy = +1
   b1[1] = mf_trrow<12, 1>(pp);
-  mf_compiler_fence();
+  C3H_MFT_FENCE();
   C3H_MFT3(b0, 1, 3)  // dz = -1, dy = 0
   C3H_MFT3(b1, 2, 3)  // dz = -1, dy = +1
 #undef C3H_MFT3
@@ -605,7 +666,9 @@ template <int LOAD>
 __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int nw, int fy_, uint32_t* s_tab,
                                                  uint32_t* dyn) {
   const int64_t fy = fy_;
-  const int wid = wid_;
+  // the wave index is wave-uniform: the tile loop's loads and the record path's buffer
+  // descriptors stay scalar
+  const int wid = C3H_MF_UNIWID ? __builtin_amdgcn_readfirstlane(wid_) : wid_;
   const uint32_t* __restrict__ fgrid = a.grids[fy];
   float* __restrict__ ffeat = a.feat + fy * a.s_feat;
   int32_t* __restrict__ fexist = a.exist + fy * a.s_h;
@@ -846,8 +909,15 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
 #pragma unroll
     for (int k = 0; k < kMfK; ++k) acc[k] = mf_v4i{0, 0, 0, 0};
     if (trp) {
-      // padding records 144..151 of the three slots (the previous tile's staging overwrote them)
+      // every record's padding dword {0, 0, 0, 1} and the padding records 144..151 of the
+      // three slots (the previous tile's staging overwrote them; the conversion writes only
+      // a record's 12 channel bytes)
       mf_compiler_fence();
+      if (C3H_MF_B96)
+        for (int r = lane; r < kMfSlots * kMfRecPos; r += 64) {
+          const int sl = r / kMfRecPos, p = r - sl * kMfRecPos;
+          *reinterpret_cast<uint32_t*>(wl + sl * SS + 16 * p + 12) = 0x01000000u;
+        }
       if (lane < 3 * (kMfRecPos - 144))
         *reinterpret_cast<mf_u4*>(wl + (lane >> 3) * SS + 16 * (144 + (lane & 7))) =
             mf_u4{0x80808080u, 0x80808080u, 0x80808080u, 0x01000000u};
@@ -876,12 +946,30 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
       }
       const int64_t zst = (int64_t)a.gy * a.gx;
       const uint32_t* tbase = fgrid + (((int64_t)(z0 - 1) * a.gy + (y0 - 1)) * a.gx + (x0 - 1));
+      // branch-free: raw buffer loads off the layer's corner word, an invalid item's offset
+      // (-4) and a layer outside the grid (no records) read 0 from the buffer's range check;
+      // a valid item's word lies in the grid
       auto load_rec = [&](int L, uint32_t (&w)[3]) {
         const int gz = z0 - 1 + L;
         const bool zin = (unsigned)gz < (unsigned)a.gz;
-        const uint32_t* lb = tbase + L * zst;
+        // (the base and the record count are wave-uniform; readfirstlane keeps the descriptor
+        // in SGPRs, where the compiler would otherwise emit a waterfall loop per load)
+        const uint64_t lb = reinterpret_cast<uint64_t>(tbase + L * zst);
+        const uint64_t lbu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(lb >> 32)) << 32) |
+                             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)lb);
+        const int nrec = __builtin_amdgcn_readfirstlane(zin ? 0x7ffffff0 : 0);
+#if C3H_MF_BUFLD
+        const __amdgpu_buffer_rsrc_t r =
+            __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(lbu), (short)0, nrec, 0x00020000);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) w[i] = zin && ro[i] >= 0 ? lb[ro[i]] : 0u;
+        for (int i = 0; i < 3; ++i) w[i] = __builtin_amdgcn_raw_buffer_load_b32(r, 4 * ro[i], 0, 0);
+#else
+        (void)lbu;
+        (void)nrec;
+        const uint32_t* lp = tbase + L * zst;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) w[i] = zin && ro[i] >= 0 ? lp[ro[i]] : 0u;
+#endif
       };
       auto store_rec = [&](int L, const uint32_t (&w)[3]) {
         uint8_t* slot = wl + (L % kMfSlots) * SS;
@@ -901,8 +989,14 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
           const uint32_t t1 = *reinterpret_cast<const uint32_t*>(tb + 1024 + ag);
           const uint32_t t2 = *reinterpret_cast<const uint32_t*>(tb + 2048 + ab);
           const bool occ = (w[i] >> 24) != 0u;
+#if C3H_MF_B96
+          typedef uint32_t mf_u3 __attribute__((ext_vector_type(3)));
+          *reinterpret_cast<mf_u3*>(slot + 16 * e) =
+              mf_u3{occ ? t0 : 0x80808080u, occ ? t1 : 0x80808080u, occ ? t2 : 0x80808080u};
+#else
           *reinterpret_cast<mf_u4*>(slot + 16 * e) =
               mf_u4{occ ? t0 : 0x80808080u, occ ? t1 : 0x80808080u, occ ? t2 : 0x80808080u, 0x01000000u};
+#endif
         }
       };
       uint32_t wr[2][3];
@@ -1050,8 +1144,14 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
         uint32_t* out2 = reinterpret_cast<uint32_t*>(a.feat16 + h * a.f16s);
 #pragma unroll 2
         for (int i = lane; i < (a.f16s >> 1); i += 64) {  // the padding to f16s as zeros
+#if C3H_MF_SRC2
+          const uint32_t sp = 2 * i + 1 < 982 ? reinterpret_cast<const uint32_t*>(s_src)[i] : 0u;
+          const _Float16 lo = 2 * i < 981 ? (_Float16)sf[sp & 0xffffu] : (_Float16)0.0f;
+          const _Float16 hi = 2 * i + 1 < 981 ? (_Float16)sf[sp >> 16] : (_Float16)0.0f;
+#else
           const _Float16 lo = 2 * i < 981 ? (_Float16)sf[s_src[2 * i]] : (_Float16)0.0f;
           const _Float16 hi = 2 * i + 1 < 981 ? (_Float16)sf[s_src[2 * i + 1]] : (_Float16)0.0f;
+#endif
           out2[i] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
         }
         if (wid == 0 && lane == 0) *a.feat16_flag = 1u;
