@@ -526,6 +526,9 @@ __device__ __forceinline__ void mf_layer_ksteps2u(const uint8_t* pp, const uint8
 #ifndef C3H_MF_BUFLD
 #define C3H_MF_BUFLD 1  // record path: branch-free raw buffer loads of the layer words
 #endif
+#ifndef C3H_MF_ST16
+#define C3H_MF_ST16 1  // fp16 rows: the epilogue stages halves (8-byte LDS stores) instead of floats
+#endif
 #ifndef C3H_MF_SRC2
 #define C3H_MF_SRC2 1  // f16 epilogue: the bin -> stage table read as u16 pairs (one LDS read per pair)
 #endif
@@ -1110,6 +1113,55 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
       float* sf = reinterpret_cast<float*>(wl);
       mf_compiler_fence();
       const bool slot = real && h4 < 3;
+#if C3H_MF_ST16
+      if (a.feat16) {  // fp16 rows: every value rounded once (RNE), as the float stage's gather did
+        _Float16* sh = reinterpret_cast<_Float16*>(wl);
+        auto put4 = [&](_Float16* dst, float x, float y, float z, float w) {
+          const uint32_t lo = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)x) |
+                              ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)y) << 16);
+          const uint32_t hi = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)z) |
+                              ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)w) << 16);
+          *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
+        };
+        _Float16* slh = sh + (h4 * 12 + n) * 4;
+        uint32_t base[4];
+        float nrm[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          base[r] = 128u * rs[r] + k2;
+          nrm[r] = mf_type(4 * h4 + r) ? 1.0f : kNorm1;
+        }
+#pragma unroll
+        for (int k = 0; k < kMfK; ++k) {
+          const uint32_t cs = 128u * (uint32_t)__shfl(acc[k][3], 48 + n, 64);
+          if (slot)
+            put4(slh + 144 * k, (float)((uint32_t)acc[k][0] + base[0] + cs) * nrm[0],
+                 (float)((uint32_t)acc[k][1] + base[1] + cs) * nrm[1], (float)((uint32_t)acc[k][2] + base[2] + cs) * nrm[2],
+                 (float)((uint32_t)acc[k][3] + base[3] + cs) * nrm[3]);
+        }
+        if (n == 15 && h4 < 3)
+          put4(sh + 14 * 144 + 4 * h4, (float)(rs[0] + 128u * pos) * (mf_type(4 * h4) ? 1.0f : kNorm0),
+               (float)(rs[1] + 128u * pos) * (mf_type(4 * h4 + 1) ? 1.0f : kNorm0),
+               (float)(rs[2] + 128u * pos) * (mf_type(4 * h4 + 2) ? 1.0f : kNorm0),
+               (float)(rs[3] + 128u * pos) * (mf_type(4 * h4 + 3) ? 1.0f : kNorm0));
+        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's values are in LDS
+        __builtin_amdgcn_wave_barrier();
+        const uint16_t* shu = reinterpret_cast<const uint16_t*>(wl);
+        uint32_t* out2 = reinterpret_cast<uint32_t*>(a.feat16 + h * a.f16s);
+        // (unroll 2: a full unroll with all 8 pairs in flight measured 4 % slower)
+#pragma unroll 2
+        for (int i = lane; i < (a.f16s >> 1); i += 64) {  // the padding to f16s as zeros
+          const uint32_t sp = 2 * i + 1 < 982 ? reinterpret_cast<const uint32_t*>(s_src)[i] : 0u;
+          const uint32_t lo = 2 * i < 981 ? (uint32_t)shu[sp & 0xffffu] : 0u;
+          const uint32_t hi = 2 * i + 1 < 981 ? (uint32_t)shu[sp >> 16] : 0u;
+          out2[i] = lo | (hi << 16);
+        }
+        if (wid == 0 && lane == 0) *a.feat16_flag = 1u;
+        mf_compiler_fence();  // the next tile's layers overwrite the stage after these reads
+        goto staged_done;
+      }
+#endif
+      {
       float* sl = sf + (h4 * 12 + n) * 4;
       uint32_t base[4];
       float nrm[4];
@@ -1161,6 +1213,10 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
         for (int i = lane; i < 981; i += 64) out[i] = sf[s_src[i]];
       }
       mf_compiler_fence();  // the next tile's planes overwrite sf after these reads
+      }
+#if C3H_MF_ST16
+    staged_done:;
+#endif
     } else if (a.atomic || F == 981) {
       float* out = ffeat + h * F;
       unsigned long long* hacc = a.atomic ? facc + h * 981 : nullptr;
