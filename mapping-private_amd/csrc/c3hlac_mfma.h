@@ -526,6 +526,9 @@ __device__ __forceinline__ void mf_layer_ksteps2u(const uint8_t* pp, const uint8
 #ifndef C3H_MF_BUFLD
 #define C3H_MF_BUFLD 1  // record path: branch-free raw buffer loads of the layer words
 #endif
+#ifndef C3H_MF_PLSWAP
+#define C3H_MF_PLSWAP 0  // epilogue: row 15's column sums broadcast by two permlane swaps, not ds_bpermute (correct, measured neutral)
+#endif
 #ifndef C3H_MF_ST16
 #define C3H_MF_ST16 1  // fp16 rows: the epilogue stages halves (8-byte LDS stores) instead of floats
 #endif
@@ -657,6 +660,18 @@ __device__ __forceinline__ void mf_layer_ksteps_tr(const uint8_t* pp, const uint
   C3H_MFT3(b0, 1, 3)  // dz = -1, dy = 0
   C3H_MFT3(b1, 2, 3)  // dz = -1, dy = +1
 #undef C3H_MFT3
+}
+
+// lane l gets x of lane 48 + (l & 15) (the accumulator's row 15 to every lane group); every
+// lane active
+__device__ __forceinline__ uint32_t mf_row3_bcast(uint32_t x) {
+#if C3H_MF_PLSWAP
+  const auto a = __builtin_amdgcn_permlane32_swap(x, x, false, false);     // [1]: rows 2 3 2 3
+  const auto b = __builtin_amdgcn_permlane16_swap(a[1], a[1], false, false);  // [1]: rows 3 3 3 3
+  return b[1];
+#else
+  return (uint32_t)__shfl((int)x, 48 + (int)(threadIdx.x & 15), 64);
+#endif
 }
 
 // plane p -> (type, reference channel); p >= 12 is padding
@@ -1133,7 +1148,7 @@ __device__ __forceinline__ void c3hlac_mfma_body(const KArgs& a, int wid_, int n
         }
 #pragma unroll
         for (int k = 0; k < kMfK; ++k) {
-          const uint32_t cs = 128u * (uint32_t)__shfl(acc[k][3], 48 + n, 64);
+          const uint32_t cs = 128u * mf_row3_bcast((uint32_t)acc[k][3]);
           if (slot)
             put4(slh + 144 * k, (float)((uint32_t)acc[k][0] + base[0] + cs) * nrm[0],
                  (float)((uint32_t)acc[k][1] + base[1] + cs) * nrm[1], (float)((uint32_t)acc[k][2] + base[2] + cs) * nrm[2],
